@@ -1,0 +1,237 @@
+"""Throughput of the ResUNet unified training step on MI355X.
+
+Workload (BASELINE.json metric "images/sec ResUNet fwd+bwd (64x64 GTSRB
+batch)"; config 3 = 14_train_unified_advanced.py unified step, batch 512,
+bf16): one step = ResUNet forward on a 64x64x3 batch, loss = L1 + 0.1 *
+VGG16-features[:16] perceptual (14:238-242), full backward, AdamW(lr 2e-4,
+wd 1e-4) (14:222, 245).  Synthetic GTSRB-shaped data generated on device.
+With --gpus N (launched by torch.distributed.run) every rank runs the same
+per-GPU batch and gradients are all-reduced over RCCL (weak scaling).
+
+Prints ONE JSON line on rank 0 with the driver's fields plus
+  roofline     -- the dominant kernel's algorithmic FLOP rate vs the MFMA peak,
+                  timed with HIP events on the launch stream during the timed
+                  steps;
+  cpu_baseline -- the CPU restatement of the same step (oracle/, the
+                  reference's ATen CPU kernels) on the host cores, bounded
+                  sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.join(REPO, "image-restoration-for-road-sign-recognition-in-autonomous-driving_amd")
+for _p in (PKG_ROOT, REPO):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "images/sec ResUNet fwd+bwd (64x64 GTSRB batch) at 1/2/4/8 MI355X; PSNR parity"
+# hook-counted conv/convT/linear FLOP per image
+FLOP_RESUNET_FWDBWD = 13_698_072_576
+FLOP_STEP_WITH_PERC = 18_270_388_224
+PEAK = {"bf16": 2516.6, "f32": 157.3}          # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=512, help="per-GPU batch")
+    ap.add_argument("--size", type=int, default=64)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-perceptual", action="store_true")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-probe", action="store_true")
+    return ap.parse_args()
+
+
+class KernelProbe:
+    """HIP-event timing of every igemm / wgrad launch, per kernel symbol."""
+
+    def __init__(self):
+        self.rec = []
+
+    def __call__(self, sym, flops, launch):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        launch()
+        e.record()
+        self.rec.append((sym, flops, s, e))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        agg = {}
+        for sym, fl, s, e in self.rec:
+            ms = s.elapsed_time(e)
+            a = agg.setdefault(sym, [0, 0.0, 0.0])
+            a[0] += 1
+            a[1] += fl
+            a[2] += ms
+        return agg
+
+
+def cpu_baseline(seconds, size):
+    """The CPU restatement of the same unified step (oracle, fp32), timed on
+    the host: a bounded sample of the workload (batch 8)."""
+    from oracle import reference_cpu as R
+    from oracle import seeded as S
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    B = 8
+    sd = S.model_state_dict("resunet")
+    p = {k: v.clone().requires_grad_(v.dtype.is_floating_point and "running" not in k)
+         for k, v in sd.items()}
+    perc = S.seeded_state_dict(S.load_manifest("perceptual"), seed=5)
+    clean = S.image_batch(B, size, size, seed=1)
+    bad = S.fog_noise(clean, seed=2)
+    names = [k for k, v in p.items() if v.requires_grad]
+    st = {}
+
+    def step():
+        for k in names:
+            p[k].grad = None
+        loss = R.unified_loss(R.resunet_forward(p, bad, True), clean, perc)
+        loss.backward()
+        with torch.no_grad():
+            R.adamw_step({k: p[k] for k in names}, {k: p[k].grad for k in names}, st, 2e-4,
+                         weight_decay=1e-4)
+
+    step()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        step()
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and n >= 2:
+            break
+    return {"value": round(n * B / el, 3), "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": f"{n} unified steps (ResUNet fwd+bwd + L1 + 0.1*perceptual + AdamW) at "
+                      f"batch {B}, {size}x{size}, fp32, oracle/reference_cpu.py on {threads} "
+                      f"host threads ({el:.1f} s)"}
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import roadrestore as rr
+    from roadrestore import ops
+    from roadrestore.optim import flatten_parameters
+    from roadrestore.parallel import DataParallel
+
+    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    torch.manual_seed(0)
+    model = rr.ResUNet().to(dev)
+    model.compute_dtype = dt
+    model.train()
+    perc = rr.VGGPerceptualLoss().to(dev)
+    perc.compute_dtype = dt
+    flatten_parameters(model)
+    dp = DataParallel(model) if world > 1 else None
+    gscale = dp.grad_scale if dp else 1.0
+    opt = rr.AdamW(model.parameters(), lr=2e-4, weight_decay=1e-4)
+
+    # synthetic GTSRB-shaped batch: clean ~ U{0..255}/255, bad = fog + noise
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    B, H = a.batch, a.size
+    clean = torch.randint(0, 256, (B, 3, H, H), generator=g, device=dev, dtype=torch.uint8).float() / 255
+    noise = torch.randn((B, 3, H, H), generator=g, device=dev) * math.sqrt(0.02)
+    bad = (clean * 0.5 + 0.45 + noise).clamp_(0, 1)
+    w_perc = 0.0 if a.no_perceptual else 0.1
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        out = model(bad)
+        loss = rr.unified_loss(out, clean, perc, w_perc, grad_scale=gscale)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(a.warmup):
+        step()
+    probe = None if a.no_probe else KernelProbe()
+    ops.PROBE = probe
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ops.PROBE = None
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    loss_v = float(loss.item())
+    if not math.isfinite(loss_v):
+        raise RuntimeError(f"non-finite loss {loss_v}")
+
+    roof = None
+    kernels = None
+    if probe is not None:
+        agg = probe.summary()
+        sym, (cnt, fl, ms) = max(agg.items(), key=lambda kv: kv[1][2])
+        ach = fl / (ms * 1e-3) / 1e12
+        pk = PEAK["bf16" if dt == torch.bfloat16 else "f32"]
+        roof = {"bound": "mfma", "kernel": sym, "achieved": round(ach, 2), "peak": pk,
+                "unit": "TFLOP/s", "frac": round(ach / pk, 4), "traffic": None,
+                "launches": cnt, "avg_launch_ms": round(ms / cnt, 4),
+                "flop_per_launch": fl / cnt}
+        tot_fl = sum(v[1] for v in agg.values())
+        tot_ms = sum(v[2] for v in agg.values())
+        kernels = {"conv_gemm_ms_per_step": round(tot_ms / a.steps, 3),
+                   "conv_gemm_tflops": round(tot_fl / (tot_ms * 1e-3) / 1e12, 2)}
+
+    imgs = world * B * a.steps
+    value = imgs / el
+    rec = {
+        "metric": METRIC, "value": round(value, 2), "unit": "images/sec", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "bf16" if dt == torch.bfloat16 else "fp32",
+        "data": "synthetic GTSRB-shaped 64x64x3 (uint8/255 clean, fog t=0.5 + N(0,0.02) noise), "
+                "random-init weights",
+        "config": {"workload": "cfg3: ResUNet unified train step (fwd + L1 + 0.1*VGG16[:16] "
+                               "perceptual + bwd + AdamW), 14_train_unified_advanced.py",
+                   "model": "ResUNet", "global_batch": world * B, "per_gpu_batch": B,
+                   "image": [H, H, 3], "parallelism": f"dp{world}",
+                   "flop_per_image": FLOP_STEP_WITH_PERC if w_perc else FLOP_RESUNET_FWDBWD},
+        "achieved_model_tflops": round(value * (FLOP_STEP_WITH_PERC if w_perc else
+                                                FLOP_RESUNET_FWDBWD) / 1e12, 2),
+        "loss": round(loss_v, 6),
+        "roofline": roof,
+        "kernels": kernels,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        rec["cpu_baseline"] = cpu_baseline(a.cpu_baseline_seconds, H)
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

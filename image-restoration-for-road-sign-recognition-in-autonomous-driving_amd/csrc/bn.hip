@@ -1,0 +1,496 @@
+// bn.hip -- BatchNorm2d / PReLU / residual elementwise kernels (NHWC, gfx950).
+//
+// Replaces the ATen kernels behind the reference's ResidualBlock
+// (14_train_unified_advanced.py:96-115):
+//   nn.BatchNorm2d train fwd (batch stats, running-stat update) / eval fwd /
+//   backward, nn.PReLU fwd / bwd (single alpha), the residual add + ReLU, and
+//   bias-gradient column sums.
+// All of these are HBM-bound: one pass over [P][C] each, 16-B per lane
+// accesses for fp32 (4 channels) and 8-B for bf16, per-channel reductions
+// done as per-workgroup partials followed by a fixed-order finalize
+// (deterministic, no float atomics).
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// finalize of the conv-epilogue statistics -> scale / shift / running stats
+// partial [blocks][C][2] of the pre-bias accumulator.
+// 256 threads = 16 channels x 16 block-slices; double accumulation.
+__global__ void bn_finalize_kernel(int C, int blocks, double count, const float *__restrict__ part,
+                                   const float *bias, const float *gamma, const float *beta,
+                                   float *rmean, float *rvar, float momentum, float eps,
+                                   float *scale, float *shift, float *smean, float *sinv,
+                                   int64_t *nbt) {
+  __shared__ double red[2][16][17];
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
+  const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C) {
+    for (int b = sl; b < blocks; b += 16) {
+      const float *p = part + ((long long)b * C + c) * 2;
+      s1 += p[0];
+      s2 += p[1];
+    }
+  }
+  red[0][sl][cl] = s1;
+  red[1][sl][cl] = s2;
+  __syncthreads();
+  if (sl == 0 && c < C) {
+    for (int k = 1; k < 16; ++k) { s1 += red[0][k][cl]; s2 += red[1][k][cl]; }
+    const double mean_acc = s1 / count;
+    double var = s2 / count - mean_acc * mean_acc;
+    if (var < 0) var = 0;
+    const double mean = mean_acc + (bias ? (double)bias[c] : 0.0);
+    const double inv = 1.0 / sqrt(var + (double)eps);
+    const double g = gamma ? (double)gamma[c] : 1.0;
+    const double bt = beta ? (double)beta[c] : 0.0;
+    scale[c] = (float)(g * inv);
+    shift[c] = (float)(bt - mean * g * inv);
+    if (smean) smean[c] = (float)mean;
+    if (sinv) sinv[c] = (float)inv;
+    if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+    if (rvar) {
+      const double unb = count > 1 ? var * count / (count - 1) : var;
+      rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+    }
+  }
+}
+
+__global__ void bn_eval_kernel(int C, const float *gamma, const float *beta, const float *rm,
+                               const float *rv, float eps, float *scale, float *shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv = 1.0f / sqrtf(rv[c] + eps);
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  scale[c] = g * inv;
+  shift[c] = b - rm[c] * g * inv;
+}
+
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void affine_act_kernel(long long P, int C, const T *__restrict__ x,
+                                  const float *__restrict__ scale, const float *__restrict__ shift,
+                                  const float *alpha, const T *__restrict__ res,
+                                  const float *__restrict__ rs, const float *__restrict__ rb,
+                                  int relu, T *__restrict__ y) {
+  const long long n4 = P * C / 4;
+  const float al = alpha ? alpha[0] : 0.f;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long e = i * 4;
+    const int c = (int)(e % C);
+    f32x4 v = load4<T>(x + e);
+    const f32x4 s = *reinterpret_cast<const f32x4 *>(scale + c);
+    const f32x4 b = *reinterpret_cast<const f32x4 *>(shift + c);
+    v = v * s + b;
+    if (alpha) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = v[k] > 0.f ? v[k] : al * v[k];
+    }
+    if (res) {
+      f32x4 r = load4<T>(res + e);
+      if (rs) r = r * *reinterpret_cast<const f32x4 *>(rs + c) + *reinterpret_cast<const f32x4 *>(rb + c);
+      v += r;
+    }
+    if (relu) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
+    }
+    store4<T>(y + e, v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// BN backward
+struct BnBwd {
+  long long P;
+  int C, mask_kind, nbn;
+  const void *g, *aux;
+  const float *aff_s, *aff_b, *alpha;
+  const void *t0, *t1;
+  const float *mean0, *inv0, *mean1, *inv1;
+};
+
+template <typename T>
+__device__ __forceinline__ f32x4 bwd_gm(const BnBwd &a, long long e, int c, f32x4 &ag) {
+  f32x4 g = load4<T>((const T *)a.g + e);
+  ag = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (a.mask_kind == 1) {
+    const f32x4 m = load4<T>((const T *)a.aux + e);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) g[k] = m[k] > 0.f ? g[k] : 0.f;
+  } else if (a.mask_kind == 2) {
+    const f32x4 t = load4<T>((const T *)a.aux + e);
+    const f32x4 u = t * *reinterpret_cast<const f32x4 *>(a.aff_s + c) +
+                    *reinterpret_cast<const f32x4 *>(a.aff_b + c);
+    const float al = a.alpha[0];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      ag[k] = u[k] > 0.f ? 0.f : g[k] * u[k];
+      g[k] = u[k] > 0.f ? g[k] : al * g[k];
+    }
+  }
+  return g;
+}
+
+// rows of [P][C] handled by one workgroup: TPR = C/4 threads per row
+template <typename T>
+__global__ void bn_bwd_reduce_kernel(BnBwd a, float *__restrict__ part, float *__restrict__ apart,
+                                     long long rows_per_block) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];   // [R][C][3] + [256]
+  const int TPR = a.C / 4;
+  const int R = blockDim.x / TPR;
+  const int tr = threadIdx.x / TPR, tc = threadIdx.x % TPR;
+  const int c = tc * 4;
+  float s[3][4] = {{0.f}};
+  float asum = 0.f;
+  const long long r0 = blockIdx.x * rows_per_block;
+  const long long r1 = min(a.P, r0 + rows_per_block);
+  if (tr < R) {
+    for (long long r = r0 + tr; r < r1; r += R) {
+      const long long e = r * a.C + c;
+      f32x4 ag;
+      const f32x4 gm = bwd_gm<T>(a, e, c, ag);
+      const f32x4 t0 = load4<T>((const T *)a.t0 + e);
+      const f32x4 m0 = *reinterpret_cast<const f32x4 *>(a.mean0 + c);
+      const f32x4 i0 = *reinterpret_cast<const f32x4 *>(a.inv0 + c);
+      f32x4 t1 = {0.f, 0.f, 0.f, 0.f}, m1 = t1, i1 = t1;
+      if (a.nbn == 2) {
+        t1 = load4<T>((const T *)a.t1 + e);
+        m1 = *reinterpret_cast<const f32x4 *>(a.mean1 + c);
+        i1 = *reinterpret_cast<const f32x4 *>(a.inv1 + c);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s[0][k] += gm[k];
+        s[1][k] += gm[k] * ((t0[k] - m0[k]) * i0[k]);
+        s[2][k] += gm[k] * ((t1[k] - m1[k]) * i1[k]);
+        asum += ag[k];
+      }
+    }
+  }
+  float *red = sm;                       // [R][C][3]
+  float *ared = sm + (size_t)R * a.C * 3;
+  if (tr < R) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) red[((size_t)tr * a.C + c + k) * 3 + j] = s[j][k];
+  }
+  ared[threadIdx.x] = asum;
+  __syncthreads();
+  for (int i = threadIdx.x; i < a.C * 3; i += blockDim.x) {
+    float v = 0.f;
+    for (int rr = 0; rr < R; ++rr) v += red[(size_t)rr * a.C * 3 + i];
+    part[(long long)blockIdx.x * a.C * 3 + i] = v;
+  }
+  if (apart && threadIdx.x == 0) {
+    float v = 0.f;
+    for (int i = 0; i < (int)blockDim.x; ++i) v += ared[i];
+    apart[blockIdx.x] = v;
+  }
+}
+
+// coef[C][2][3] = {gamma*invstd, mean(gm), mean(gm*xhat)} per BN
+__global__ void bn_bwd_finalize_kernel(int C, int blocks, double count, int nbn,
+                                       const float *__restrict__ part, const float *apart,
+                                       const float *g0, const float *inv0, const float *g1,
+                                       const float *inv1, float *dg0, float *db0, float *dg1,
+                                       float *db1, float *dalpha, float *coef) {
+  __shared__ double red[3][16][17];
+  const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  double s0 = 0, s1 = 0, s2 = 0;
+  if (c < C) {
+    for (int b = sl; b < blocks; b += 16) {
+      const float *p = part + ((long long)b * C + c) * 3;
+      s0 += p[0]; s1 += p[1]; s2 += p[2];
+    }
+  }
+  red[0][sl][cl] = s0; red[1][sl][cl] = s1; red[2][sl][cl] = s2;
+  __syncthreads();
+  if (sl == 0 && c < C) {
+    for (int k = 1; k < 16; ++k) { s0 += red[0][k][cl]; s1 += red[1][k][cl]; s2 += red[2][k][cl]; }
+    if (db0) db0[c] = (float)s0;
+    if (dg0) dg0[c] = (float)s1;
+    coef[c * 6 + 0] = (g0 ? g0[c] : 1.f) * inv0[c];
+    coef[c * 6 + 1] = (float)(s0 / count);
+    coef[c * 6 + 2] = (float)(s1 / count);
+    if (nbn == 2) {
+      if (db1) db1[c] = (float)s0;
+      if (dg1) dg1[c] = (float)s2;
+      coef[c * 6 + 3] = (g1 ? g1[c] : 1.f) * inv1[c];
+      coef[c * 6 + 4] = (float)(s0 / count);
+      coef[c * 6 + 5] = (float)(s2 / count);
+    }
+  }
+  if (blockIdx.x == 0 && apart && dalpha) {
+    __syncthreads();
+    __shared__ double ar[256];
+    double v = 0;
+    for (int b = threadIdx.x; b < blocks; b += blockDim.x) v += apart[b];
+    ar[threadIdx.x] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0;
+      for (int i = 0; i < (int)blockDim.x; ++i) t += ar[i];
+      dalpha[0] = (float)t;
+    }
+  }
+}
+
+template <typename T>
+__global__ void bn_bwd_apply_kernel(BnBwd a, const float *__restrict__ coef, T *dt0, T *dt1,
+                                    T *gmo) {
+  const long long n4 = a.P * a.C / 4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long e = i * 4;
+    const int c = (int)(e % a.C);
+    f32x4 ag;
+    const f32x4 gm = bwd_gm<T>(a, e, c, ag);
+    if (gmo) store4<T>(gmo + e, gm);
+    {
+      const f32x4 t = load4<T>((const T *)a.t0 + e);
+      f32x4 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float *cf = coef + (c + k) * 6;
+        const float xh = (t[k] - a.mean0[c + k]) * a.inv0[c + k];
+        o[k] = cf[0] * (gm[k] - cf[1] - xh * cf[2]);
+      }
+      store4<T>(dt0 + e, o);
+    }
+    if (a.nbn == 2) {
+      const f32x4 t = load4<T>((const T *)a.t1 + e);
+      f32x4 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float *cf = coef + (c + k) * 6 + 3;
+        const float xh = (t[k] - a.mean1[c + k]) * a.inv1[c + k];
+        o[k] = cf[0] * (gm[k] - cf[1] - xh * cf[2]);
+      }
+      store4<T>(dt1 + e, o);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// column sums (bias grads): partial [blocks][C] then finalize (fixed order)
+template <typename T>
+__global__ void colsum_kernel(long long P, int C, const T *__restrict__ x, float *__restrict__ part,
+                              long long rows_per_block) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int TPR = C / 4;
+  const int R = blockDim.x / TPR;
+  const int tr = threadIdx.x / TPR, tc = threadIdx.x % TPR;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  const long long r0 = blockIdx.x * rows_per_block;
+  const long long r1 = min(P, r0 + rows_per_block);
+  if (tr < R) {
+    for (long long r = r0 + tr; r < r1; r += R) {
+      const f32x4 v = load4<T>(x + r * C + tc * 4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s[k] += v[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sm[(size_t)tr * C + tc * 4 + k] = s[k];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    float v = 0.f;
+    for (int rr = 0; rr < R; ++rr) v += sm[(size_t)rr * C + i];
+    part[(long long)blockIdx.x * C + i] = v;
+  }
+}
+
+__global__ void colsum_finalize(int C, int blocks, const float *__restrict__ part, float *out,
+                                int accumulate) {
+  __shared__ double red[16][17];
+  const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  double s = 0;
+  if (c < C)
+    for (int b = sl; b < blocks; b += 16) s += part[(long long)b * C + c];
+  red[sl][cl] = s;
+  __syncthreads();
+  if (sl == 0 && c < C) {
+    for (int k = 1; k < 16; ++k) s += red[k][cl];
+    out[c] = accumulate ? out[c] + (float)s : (float)s;
+  }
+}
+
+int reduce_blocks(long long P) {
+  long long b = (P + 63) / 64;
+  if (b > 1024) b = 1024;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+
+extern "C" int rr_bn_finalize(int C, int blocks, long long count, const float *part,
+                              const float *bias, const float *gamma, const float *beta,
+                              float *running_mean, float *running_var, float momentum,
+                              float eps, float *scale, float *shift, float *save_mean,
+                              float *save_invstd, int64_t *num_batches_tracked,
+                              rr_stream stream) {
+  if (C <= 0 || blocks <= 0 || count <= 0 || !part || !scale || !shift) return RR_EINVAL;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, (hipStream_t)stream,
+                     C, blocks, (double)count, part, bias, gamma, beta, running_mean,
+                     running_var, momentum, eps, scale, shift, save_mean, save_invstd,
+                     num_batches_tracked);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_bn_eval_affine(int C, const float *gamma, const float *beta,
+                                 const float *running_mean, const float *running_var, float eps,
+                                 float *scale, float *shift, rr_stream stream) {
+  if (C <= 0 || !running_mean || !running_var || !scale || !shift) return RR_EINVAL;
+  hipLaunchKernelGGL(bn_eval_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     C, gamma, beta, running_mean, running_var, eps, scale, shift);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_affine_act(int dtype, long long P, int C, const void *x, const float *scale,
+                             const float *shift, const float *alpha, const void *res,
+                             const float *res_scale, const float *res_shift, int relu, void *y,
+                             rr_stream stream) {
+  if (P <= 0 || C <= 0 || C % 4 || !x || !scale || !shift || !y) return RR_EINVAL;
+  if ((res_scale == nullptr) != (res_shift == nullptr)) return RR_EINVAL;
+  const int grid = rr_grid_cap((P * C / 4 + 255) / 256, 4096);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(affine_act_kernel<bf16_t>, dim3(grid), dim3(256), 0, st, P, C,
+                       (const bf16_t *)x, scale, shift, alpha, (const bf16_t *)res, res_scale,
+                       res_shift, relu, (bf16_t *)y);
+  else
+    hipLaunchKernelGGL(affine_act_kernel<float>, dim3(grid), dim3(256), 0, st, P, C,
+                       (const float *)x, scale, shift, alpha, (const float *)res, res_scale,
+                       res_shift, relu, (float *)y);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_bn_bwd_blocks(const rr_bnbwd_desc *d) {
+  if (!d) return RR_EINVAL;
+  return reduce_blocks(d->P);
+}
+
+static int bnbwd_check(const rr_bnbwd_desc *d) {
+  if (!d || d->P <= 0 || d->C <= 0 || d->C % 4 || d->C / 4 > 256) return RR_EINVAL;
+  if (d->nbn != 1 && d->nbn != 2) return RR_EINVAL;
+  if (d->mask_kind < 0 || d->mask_kind > 2) return RR_EINVAL;
+  return RR_OK;
+}
+
+static BnBwd make_bnbwd(const rr_bnbwd_desc *d, const void *g, const void *aux,
+                        const float *aff_s, const float *aff_b, const float *alpha,
+                        const void *t0, const float *mean0, const float *inv0, const void *t1,
+                        const float *mean1, const float *inv1) {
+  BnBwd a;
+  a.P = d->P; a.C = d->C; a.mask_kind = d->mask_kind; a.nbn = d->nbn;
+  a.g = g; a.aux = aux; a.aff_s = aff_s; a.aff_b = aff_b; a.alpha = alpha;
+  a.t0 = t0; a.t1 = t1; a.mean0 = mean0; a.inv0 = inv0; a.mean1 = mean1; a.inv1 = inv1;
+  return a;
+}
+
+extern "C" int rr_bn_bwd_reduce(const rr_bnbwd_desc *d, const void *g, const void *aux,
+                                const float *aff_s, const float *aff_b, const float *alpha,
+                                const void *t0, const float *mean0, const float *invstd0,
+                                const void *t1, const float *mean1, const float *invstd1,
+                                float *partial, rr_stream stream) {
+  int rc = bnbwd_check(d);
+  if (rc) return rc;
+  if (!g || !t0 || !mean0 || !invstd0 || !partial) return RR_EINVAL;
+  if (d->mask_kind && !aux) return RR_EINVAL;
+  if (d->mask_kind == 2 && (!aff_s || !aff_b || !alpha)) return RR_EINVAL;
+  if (d->nbn == 2 && (!t1 || !mean1 || !invstd1)) return RR_EINVAL;
+  const BnBwd a = make_bnbwd(d, g, aux, aff_s, aff_b, alpha, t0, mean0, invstd0, t1, mean1, invstd1);
+  const int blocks = reduce_blocks(d->P);
+  const long long rpb = (d->P + blocks - 1) / blocks;
+  const int TPR = d->C / 4;
+  const int R = 256 / TPR;
+  const size_t shm = ((size_t)R * d->C * 3 + 256) * sizeof(float);
+  float *apart = partial + (size_t)blocks * d->C * 3;
+  hipStream_t st = (hipStream_t)stream;
+  if (d->dtype == RR_BF16)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st, a, partial,
+                       d->mask_kind == 2 ? apart : nullptr, rpb);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, dim3(blocks), dim3(256), shm, st, a, partial,
+                       d->mask_kind == 2 ? apart : nullptr, rpb);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_bn_bwd_finalize(const rr_bnbwd_desc *d, const float *partial,
+                                  const float *gamma0, const float *invstd0, const float *gamma1,
+                                  const float *invstd1, float *dgamma0, float *dbeta0,
+                                  float *dgamma1, float *dbeta1, float *dalpha, float *coef,
+                                  rr_stream stream) {
+  int rc = bnbwd_check(d);
+  if (rc) return rc;
+  if (!partial || !invstd0 || !coef || (d->nbn == 2 && !invstd1)) return RR_EINVAL;
+  const int blocks = reduce_blocks(d->P);
+  const float *apart = d->mask_kind == 2 ? partial + (size_t)blocks * d->C * 3 : nullptr;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((d->C + 15) / 16), dim3(256), 0,
+                     (hipStream_t)stream, d->C, blocks, (double)d->P, d->nbn, partial, apart,
+                     gamma0, invstd0, gamma1, invstd1, dgamma0, dbeta0, dgamma1, dbeta1, dalpha,
+                     coef);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_bn_bwd_apply(const rr_bnbwd_desc *d, const void *g, const void *aux,
+                               const float *aff_s, const float *aff_b, const float *alpha,
+                               const void *t0, const float *mean0, const float *invstd0,
+                               const void *t1, const float *mean1, const float *invstd1,
+                               const float *coef, void *dt0, void *dt1, void *gm_out,
+                               rr_stream stream) {
+  int rc = bnbwd_check(d);
+  if (rc) return rc;
+  if (!g || !t0 || !coef || !dt0 || (d->nbn == 2 && (!t1 || !dt1))) return RR_EINVAL;
+  const BnBwd a = make_bnbwd(d, g, aux, aff_s, aff_b, alpha, t0, mean0, invstd0, t1, mean1, invstd1);
+  const int grid = rr_grid_cap((d->P * d->C / 4 + 255) / 256, 4096);
+  hipStream_t st = (hipStream_t)stream;
+  if (d->dtype == RR_BF16)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, dim3(grid), dim3(256), 0, st, a, coef,
+                       (bf16_t *)dt0, (bf16_t *)dt1, (bf16_t *)gm_out);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(grid), dim3(256), 0, st, a, coef,
+                       (float *)dt0, (float *)dt1, (float *)gm_out);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" size_t rr_channel_sum_workspace(long long P, int C) {
+  return (size_t)reduce_blocks(P) * C * sizeof(float);
+}
+
+extern "C" int rr_channel_sum(int dtype, long long P, int C, const void *x, float *out,
+                              int accumulate, void *ws, size_t ws_bytes, rr_stream stream) {
+  if (P <= 0 || C <= 0 || C % 4 || C / 4 > 256 || !x || !out) return RR_EINVAL;
+  const int blocks = reduce_blocks(P);
+  if (!ws || ws_bytes < (size_t)blocks * C * sizeof(float)) return RR_EWORKSPACE;
+  const long long rpb = (P + blocks - 1) / blocks;
+  const int R = 256 / (C / 4);
+  const size_t shm = (size_t)R * C * sizeof(float);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st, P, C,
+                       (const bf16_t *)x, (float *)ws, rpb);
+  else
+    hipLaunchKernelGGL(colsum_kernel<float>, dim3(blocks), dim3(256), shm, st, P, C,
+                       (const float *)x, (float *)ws, rpb);
+  RR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(colsum_finalize, dim3((C + 15) / 16), dim3(256), 0, st, C, blocks,
+                     (const float *)ws, out, accumulate);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}

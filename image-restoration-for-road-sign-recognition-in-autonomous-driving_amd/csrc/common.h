@@ -1,0 +1,111 @@
+// common.h -- shared device helpers for the gfx950 kernels (CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/roadrestore.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+typedef u16 u16x4 __attribute__((ext_vector_type(4)));
+typedef u16 u16x8 __attribute__((ext_vector_type(8)));
+
+#define LDS_PTR(p) ((__attribute__((address_space(3))) void *)(p))
+
+// bf16 storage type: raw 16-bit pattern.
+struct bf16_t {
+  u16 v;
+};
+
+__device__ __forceinline__ float bf16_to_f32(u16 b) {
+  return __uint_as_float(((uint32_t)b) << 16);
+}
+// round-to-nearest-even (NaN-preserving enough for activations)
+__device__ __forceinline__ u16 f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (u16)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (u16)(u >> 16);
+}
+
+// Element traits: storage <-> fp32
+template <typename T> struct Elt;
+template <> struct Elt<float> {
+  static constexpr int size = 4;
+  static constexpr int dtype = RR_F32;
+  __device__ __forceinline__ static float load(const float *p, long long i) { return p[i]; }
+  __device__ __forceinline__ static void store(float *p, long long i, float v) { p[i] = v; }
+};
+template <> struct Elt<bf16_t> {
+  static constexpr int size = 2;
+  static constexpr int dtype = RR_BF16;
+  __device__ __forceinline__ static float load(const bf16_t *p, long long i) {
+    return bf16_to_f32(p[i].v);
+  }
+  __device__ __forceinline__ static void store(bf16_t *p, long long i, float v) {
+    p[i].v = f32_to_bf16(v);
+  }
+};
+
+// 4 consecutive elements <-> float4
+template <typename T> __device__ __forceinline__ f32x4 load4(const T *p);
+template <> __device__ __forceinline__ f32x4 load4<float>(const float *p) {
+  return *reinterpret_cast<const f32x4 *>(p);
+}
+template <> __device__ __forceinline__ f32x4 load4<bf16_t>(const bf16_t *p) {
+  u16x4 r = *reinterpret_cast<const u16x4 *>(p);
+  f32x4 o;
+  o[0] = bf16_to_f32(r[0]); o[1] = bf16_to_f32(r[1]);
+  o[2] = bf16_to_f32(r[2]); o[3] = bf16_to_f32(r[3]);
+  return o;
+}
+template <typename T> __device__ __forceinline__ void store4(T *p, f32x4 v);
+template <> __device__ __forceinline__ void store4<float>(float *p, f32x4 v) {
+  *reinterpret_cast<f32x4 *>(p) = v;
+}
+template <> __device__ __forceinline__ void store4<bf16_t>(bf16_t *p, f32x4 v) {
+  u16x4 r;
+  r[0] = f32_to_bf16(v[0]); r[1] = f32_to_bf16(v[1]);
+  r[2] = f32_to_bf16(v[2]); r[3] = f32_to_bf16(v[3]);
+  *reinterpret_cast<u16x4 *>(p) = r;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+#define RR_CHECK_LAUNCH()                                   \
+  do {                                                      \
+    if (hipGetLastError() != hipSuccess) return RR_ELAUNCH; \
+  } while (0)
+
+static inline int rr_grid_cap(long long want, int cap = 2048) {
+  if (want < 1) return 1;
+  return (int)(want < cap ? want : cap);
+}
+
+// 256 zero bytes: out-of-bounds rows of an implicit-GEMM gather load from here.
+static __device__ __attribute__((aligned(16))) const char rr_zero_page[256] = {0};
+
+// Fast unsigned division by a runtime-invariant divisor (n < 2^31, d >= 1):
+// q = (mulhi(n, m) + n) >> s with s = ceil(log2 d), m = floor(2^32 (2^s - d) / d) + 1.
+struct FastDiv {
+  uint32_t d, m, s;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f) {
+  const uint32_t t = __umulhi(n, f.m);
+  return (t + n) >> f.s;
+}

@@ -1,0 +1,400 @@
+// igemm.hip -- implicit-GEMM convolution on CDNA4 MFMA (gfx950).
+//
+// Replaces the ATen convolution kernels the reference dispatches from
+//   nn.Conv2d(k=3, p=1) fwd / dgrad     07:78-96, 14:100-104, VGG16 features
+//   nn.Conv2d(k=1) fwd / dgrad          14:111 (shortcut), 07:96 / 14:149 final
+//   nn.ConvTranspose2d(k=2, s=2) fwd / dgrad   07:88,92, 14:143-149
+//   nn.Linear (h = w = 1)               VGG16 classifier (18:58-61)
+//
+// GEMM view (NHWC activations, channels contiguous):
+//   D[c][p] = sum_k W[c][k] * X[p][k]
+//     c : GEMM column = output channel (weights row)       -> MFMA "A" rows
+//     p : GEMM row    = output pixel (activation row)      -> MFMA "B" cols
+//     k : tap * Cin + ci; X[p][k] gathered from the source pixel of tap
+//
+// Tile: BC x BP per 256-thread workgroup (4 waves in 2x2), one 128-byte
+// k-stage per LDS buffer (bf16: 64 k, f32: 32 k), double buffered.  Both
+// operand tiles are filled by global_load_lds_dwordx4 (LDS-DMA): each
+// wave-instruction moves 8 rows x 128 B; the per-lane SOURCE address does the
+// implicit-GEMM gather (halo taps, concat sources, convT 2x2) and points
+// out-of-image rows at a zero page.  The 16-B chunk order inside a row is
+// XOR-swizzled on the source side (chunk ^ ((row>>1)&7)) and undone on the
+// ds_read_b128 fragment reads, which makes those reads bank-conflict-free.
+//
+// MFMA: bf16 v_mfma_f32_16x16x32_bf16 (one per 16-B fragment pair);
+//       f32  v_mfma_f32_16x16x4_f32 (exact fp32, four per fragment pair).
+// Accumulator lane map: pixel = lane&15, channels (lane>>4)*4 .. +3, so each
+// lane stores 4 consecutive NHWC channels of one pixel.
+//
+// Epilogue (fused): per-column partial BN statistics of the pre-bias
+// accumulator, + bias, accumulate into the destination, ReLU, multiply by a
+// (mask > 0) relu-backward mask, split of the columns over two destinations
+// (the grads of a torch.cat's two halves), convT 2x2 pixel scatter.
+#include "common.h"
+
+namespace {
+
+struct IgemmArgs {
+  const char *x1, *x2, *wt;
+  const float *bias;
+  char *y1, *y2;
+  const char *mask;
+  float *stats;
+  int n, h, w;        // GEMM row grid
+  int c1, c2, cin;    // K-side channels
+  int cout;           // GEMM columns
+  int split;          // column split (0: none)
+  int act, accumulate, has_mask;
+  int taps, K;
+  int P;              // n*h*w
+  int ncblk;
+  int cout_t;         // convT_up: channels per tap
+};
+
+template <typename T> struct Frag;
+template <> struct Frag<bf16_t> {
+  using type = bf16x8;
+  __device__ __forceinline__ static void mma(f32x4 &acc, const type &a, const type &b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+  }
+};
+template <> struct Frag<float> {
+  using type = f32x4;
+  __device__ __forceinline__ static void mma(f32x4 &acc, const type &a, const type &b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], acc, 0, 0, 0);
+  }
+};
+
+__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
+
+constexpr int ROWB = 128;  // bytes of k per row per stage
+
+template <typename T, int BC, int BP, int MODE>
+__global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs a) {
+  constexpr int ES = sizeof(T);
+  constexpr int BK = ROWB / ES;                 // k elements per stage
+  constexpr int NROWS = BC + BP;
+  constexpr int NINST = NROWS / 8;              // glds wave-instructions per stage
+  static_assert(NINST % 4 == 0, "rows per stage must be a multiple of 32");
+  constexpr int IPW = NINST / 4;                // per wave
+  constexpr int STAGE_BYTES = NROWS * ROWB;
+  constexpr int MC = BC / 32, MP = BP / 32;     // 16x16 subtiles per wave
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = tid >> 6;
+  const int wc = wv & 1, wp = wv >> 1;
+  const int cblk = blockIdx.x % a.ncblk;
+  const int pblk = blockIdx.x / a.ncblk;
+  const int c0 = cblk * BC;
+  const int p0 = pblk * BP;
+
+  // ---- per-lane load descriptors --------------------------------------
+  // instruction j = wv + 4*i covers tile rows [8j, 8j+8); lane -> row 8j + lane/8
+  const int lrow = lane >> 3;
+  const int pchunk = lane & 7;
+  const char *wrow[IPW];     // weight row base (or zero page) for A instructions
+  int prow_pix[IPW];         // pixel index or -1 for B instructions
+  int prow_h[IPW], prow_w[IPW];
+  int lchunk[IPW];
+  bool isA[IPW];
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int j = wv + 4 * i;
+    const int r = 8 * j + lrow;
+    isA[i] = (8 * j) < BC;
+    int tr = isA[i] ? r : r - BC;
+    lchunk[i] = pchunk ^ swz(tr);
+    if (isA[i]) {
+      const int c = c0 + tr;
+      wrow[i] = (c < a.cout) ? a.wt + ((long long)c * a.K) * ES : nullptr;
+      prow_pix[i] = -1; prow_h[i] = 0; prow_w[i] = 0;
+    } else {
+      const int p = p0 + tr;
+      wrow[i] = nullptr;
+      if (p < a.P) {
+        prow_pix[i] = p;
+        const int hw = a.h * a.w;
+        const int rem = p % hw;
+        prow_h[i] = rem / a.w;
+        prow_w[i] = rem % a.w;
+      } else {
+        prow_pix[i] = -1; prow_h[i] = 0; prow_w[i] = 0;
+      }
+    }
+  }
+
+  const int kchunks = a.cin / BK;   // stages per tap
+  const int nstage = a.taps * kchunks;
+
+  auto issue = [&](int s, int buf) {
+    const int tap = s / kchunks;
+    const int ci0 = (s - tap * kchunks) * BK;
+    char *sbase = smem + buf * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const int j = wv + 4 * i;
+      const char *src = rr_zero_page;
+      if (isA[i]) {
+        if (wrow[i]) src = wrow[i] + ((long long)s * BK) * ES + lchunk[i] * 16;
+      } else if (prow_pix[i] >= 0) {
+        long long sp = -1;
+        if (MODE == RR_CONV3X3) {
+          const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+          const int hh = prow_h[i] + dy, ww = prow_w[i] + dx;
+          if (hh >= 0 && hh < a.h && ww >= 0 && ww < a.w) sp = prow_pix[i] + dy * a.w + dx;
+        } else if (MODE == RR_CONV1X1 || MODE == RR_CONVT_UP) {
+          sp = prow_pix[i];
+        } else {  // RR_CONVT_DOWN: source grid is (2h, 2w)
+          const int nn = prow_pix[i] / (a.h * a.w);
+          const int ky = tap >> 1, kx = tap & 1;
+          sp = ((long long)nn * 2 * a.h + 2 * prow_h[i] + ky) * (2 * a.w) + 2 * prow_w[i] + kx;
+        }
+        if (sp >= 0) {
+          if (ci0 < a.c1)
+            src = a.x1 + (sp * a.c1 + ci0) * ES + lchunk[i] * 16;
+          else
+            src = a.x2 + (sp * a.c2 + (ci0 - a.c1)) * ES + lchunk[i] * 16;
+        }
+      }
+      __builtin_amdgcn_global_load_lds((const void *)src, LDS_PTR(sbase + j * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[MC][MP];
+#pragma unroll
+  for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < MP; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  using FT = typename Frag<T>::type;
+  const int frow = lane & 15;
+  const int fq = lane >> 4;
+
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int s = 0; s < nstage; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nstage) issue(s + 1, buf ^ 1);
+    const char *sA = smem + buf * STAGE_BYTES;
+    const char *sB = sA + BC * ROWB;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      FT fa[MC], fb[MP];
+#pragma unroll
+      for (int mi = 0; mi < MC; ++mi) {
+        const int r = wc * (BC / 2) + mi * 16 + frow;
+        const int ch = (kk * 4 + fq) ^ swz(r);
+        fa[mi] = *reinterpret_cast<const FT *>(sA + r * ROWB + ch * 16);
+      }
+#pragma unroll
+      for (int ni = 0; ni < MP; ++ni) {
+        const int r = wp * (BP / 2) + ni * 16 + frow;
+        const int ch = (kk * 4 + fq) ^ swz(r);
+        fb[ni] = *reinterpret_cast<const FT *>(sB + r * ROWB + ch * 16);
+      }
+#pragma unroll
+      for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < MP; ++ni) Frag<T>::mma(acc[mi][ni], fa[mi], fb[ni]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue --------------------------------------------------------
+  float s1[MC][4], s2[MC][4];
+#pragma unroll
+  for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { s1[mi][i] = 0.f; s2[mi][i] = 0.f; }
+
+#pragma unroll
+  for (int ni = 0; ni < MP; ++ni) {
+    const int p = p0 + wp * (BP / 2) + ni * 16 + frow;
+    if (p >= a.P) continue;
+    long long outpix = p;   // convT_up: recomputed per column (depends on tap)
+    int nn = 0, hh = 0, ww = 0;
+    if (MODE == RR_CONVT_UP) {
+      const int hw = a.h * a.w;
+      nn = p / hw;
+      const int rem = p - nn * hw;
+      hh = rem / a.w;
+      ww = rem - hh * a.w;
+    }
+#pragma unroll
+    for (int mi = 0; mi < MC; ++mi) {
+      const int cb = c0 + wc * (BC / 2) + mi * 16 + fq * 4;
+      if (cb >= a.cout) continue;
+      f32x4 v = acc[mi][ni];
+      if (a.stats) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { s1[mi][i] += v[i]; s2[mi][i] += v[i] * v[i]; }
+      }
+      T *dst;
+      const T *msk = nullptr;
+      int cc = cb;
+      if (MODE == RR_CONVT_UP) {
+        const int tap = cb / a.cout_t;
+        cc = cb - tap * a.cout_t;
+        outpix = ((long long)nn * 2 * a.h + 2 * hh + (tap >> 1)) * (2 * a.w) + 2 * ww + (tap & 1);
+        dst = reinterpret_cast<T *>(a.y1) + outpix * a.cout_t + cc;
+      } else if (a.split > 0 && cb >= a.split) {
+        cc = cb - a.split;
+        dst = reinterpret_cast<T *>(a.y2) + outpix * (a.cout - a.split) + cc;
+      } else {
+        const int ld = a.split > 0 ? a.split : a.cout;
+        dst = reinterpret_cast<T *>(a.y1) + outpix * ld + cb;
+        if (a.has_mask) msk = reinterpret_cast<const T *>(a.mask) + outpix * ld + cb;
+      }
+      const bool full = (cb + 3 < a.cout);
+      if (full) {
+        if (a.bias) v += *reinterpret_cast<const f32x4 *>(a.bias + cb);
+        if (a.accumulate) v += load4<T>(dst);
+        if (a.act == RR_ACT_RELU) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], 0.f);
+        }
+        if (msk) {
+          const f32x4 m = load4<T>(msk);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = m[i] > 0.f ? v[i] : 0.f;
+        }
+        store4<T>(dst, v);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (cb + i >= a.cout) break;
+          float x = v[i];
+          if (a.bias) x += a.bias[cb + i];
+          if (a.accumulate) x += Elt<T>::load(dst, i);
+          if (a.act == RR_ACT_RELU) x = fmaxf(x, 0.f);
+          if (msk && !(Elt<T>::load(msk, i) > 0.f)) x = 0.f;
+          Elt<T>::store(dst, i, x);
+        }
+      }
+    }
+  }
+
+  if (a.stats) {
+    // reduce over the 16 pixel lanes that share (lane>>4), then over wp.
+#pragma unroll
+    for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float x = s1[mi][i], y = s2[mi][i];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          x += __shfl_xor(x, o, 64);
+          y += __shfl_xor(y, o, 64);
+        }
+        s1[mi][i] = x; s2[mi][i] = y;
+      }
+    float *red = reinterpret_cast<float *>(smem);   // [2 wp][BC][2]
+    // (the K loop ended with a barrier; smem is free)
+    if (frow == 0) {
+#pragma unroll
+      for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int cl = wc * (BC / 2) + mi * 16 + fq * 4 + i;
+          red[(wp * BC + cl) * 2 + 0] = s1[mi][i];
+          red[(wp * BC + cl) * 2 + 1] = s2[mi][i];
+        }
+    }
+    __syncthreads();
+    for (int cl = tid; cl < BC; cl += 256) {
+      const int c = c0 + cl;
+      if (c < a.cout) {
+        const float x = red[cl * 2 + 0] + red[(BC + cl) * 2 + 0];
+        const float y = red[cl * 2 + 1] + red[(BC + cl) * 2 + 1];
+        a.stats[((long long)pblk * a.cout + c) * 2 + 0] = x;
+        a.stats[((long long)pblk * a.cout + c) * 2 + 1] = y;
+      }
+    }
+  }
+}
+
+template <typename T, int BC, int BP>
+int launch_mode(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
+  a.ncblk = (a.cout + BC - 1) / BC;
+  const long long npblk = ((long long)a.P + BP - 1) / BP;
+  const long long nblk = npblk * a.ncblk;
+  if (nblk > 0x7fffffffLL) return RR_EUNSUPPORTED;
+  dim3 grid((unsigned)nblk), block(256);
+  switch (d->mode) {
+    case RR_CONV3X3: hipLaunchKernelGGL((igemm_kernel<T, BC, BP, RR_CONV3X3>), grid, block, 0, st, a); break;
+    case RR_CONV1X1: hipLaunchKernelGGL((igemm_kernel<T, BC, BP, RR_CONV1X1>), grid, block, 0, st, a); break;
+    case RR_CONVT_UP: hipLaunchKernelGGL((igemm_kernel<T, BC, BP, RR_CONVT_UP>), grid, block, 0, st, a); break;
+    case RR_CONVT_DOWN: hipLaunchKernelGGL((igemm_kernel<T, BC, BP, RR_CONVT_DOWN>), grid, block, 0, st, a); break;
+    default: return RR_EINVAL;
+  }
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+constexpr int kBP = 128;
+
+int pick_bc(const rr_igemm_desc *d) {
+  // 128-wide column tiles when the columns fill them and the pixel grid gives
+  // enough workgroups to cover 256 CUs twice over; otherwise 64.
+  const long long P = (long long)d->n * d->h * d->w;
+  const long long pb = (P + kBP - 1) / kBP;
+  if (d->c_out % 128 == 0 && pb * (d->c_out / 128) >= 512 &&
+      (d->out_split == 0 || d->out_split % 128 == 0))
+    return 128;
+  return 64;
+}
+
+template <typename T>
+int dispatch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
+  if (pick_bc(d) == 128) return launch_mode<T, 128, kBP>(d, a, st);
+  return launch_mode<T, 64, kBP>(d, a, st);
+}
+
+}  // namespace
+
+extern "C" int rr_igemm_stat_blocks(const rr_igemm_desc *d) {
+  if (!d) return RR_EINVAL;
+  const long long P = (long long)d->n * d->h * d->w;
+  return (int)((P + kBP - 1) / kBP);
+}
+
+extern "C" int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
+                        const void *w, const float *bias, void *y1, void *y2,
+                        const void *mask, float *stats_partial, rr_stream stream) {
+  if (!d || !x1 || !w || !y1) return RR_EINVAL;
+  if (d->dtype != RR_F32 && d->dtype != RR_BF16) return RR_EINVAL;
+  const int bk = d->dtype == RR_F32 ? 32 : 64;
+  if (d->n <= 0 || d->h <= 0 || d->w <= 0 || d->c_out <= 0 || d->c_in1 <= 0) return RR_EINVAL;
+  if (d->c_in1 % bk || d->c_in2 % bk) return RR_EUNSUPPORTED;
+  if (d->c_in2 > 0 && !x2) return RR_EINVAL;
+  if (d->out_split > 0 && (!y2 || d->out_split % 64 || d->out_split >= d->c_out)) return RR_EUNSUPPORTED;
+  if (d->mode == RR_CONVT_UP && (d->c_out % 4 || (d->c_out / 4) % 64 || d->out_split || d->want_stats))
+    return RR_EUNSUPPORTED;
+  if (d->has_mask && (!mask || d->out_split)) return RR_EINVAL;
+  if (d->want_stats && !stats_partial) return RR_EINVAL;
+  const long long P = (long long)d->n * d->h * d->w;
+  if (P > 0x7fffffffLL / 4) return RR_EUNSUPPORTED;
+  IgemmArgs a;
+  a.x1 = (const char *)x1; a.x2 = (const char *)x2; a.wt = (const char *)w;
+  a.bias = bias; a.y1 = (char *)y1; a.y2 = (char *)y2; a.mask = (const char *)mask;
+  a.stats = d->want_stats ? stats_partial : nullptr;
+  a.n = d->n; a.h = d->h; a.w = d->w;
+  a.c1 = d->c_in1; a.c2 = d->c_in2; a.cin = d->c_in1 + d->c_in2;
+  a.cout = d->c_out; a.split = d->out_split;
+  a.act = d->act; a.accumulate = d->accumulate; a.has_mask = d->has_mask;
+  a.taps = d->mode == RR_CONV3X3 ? 9 : (d->mode == RR_CONVT_DOWN ? 4 : 1);
+  a.K = a.taps * a.cin;
+  a.P = (int)P;
+  a.cout_t = d->mode == RR_CONVT_UP ? d->c_out / 4 : d->c_out;
+  a.ncblk = 1;
+  hipStream_t st = (hipStream_t)stream;
+  if (d->dtype == RR_BF16) return dispatch<bf16_t>(d, a, st);
+  return dispatch<float>(d, a, st);
+}

@@ -1,0 +1,977 @@
+// misc.hip -- the remaining ops of the hot path (gfx950, NHWC).
+//
+//  * weight packing fp32 torch layout -> compute layout / dtype
+//  * first layer conv3x3 3->64 straight from the NCHW fp32 image
+//    (07:78 enc1.0, 14:122 enc1, VGG16 features.0) fwd / wgrad / dgrad
+//  * last layer conv1x1 64->3 into NCHW fp32 (07:96, 14:149) fwd / bwd
+//  * MaxPool2d(2, 2) fwd with 1-byte argmax, gather-form bwd (07:81, 14:125)
+//  * PReLU backward for the enc1 activation (14:122)
+//  * layout conversion NCHW fp32 <-> NHWC
+//  * L1 / MSE / perceptual-MSE losses (14:219, 07:142, 14:196)
+//  * fused Adam / AdamW over flat fp32 buffers (14:222, 07:143)
+//  * clamp -> x255 -> uint8 truncation (17:84-92), PSNR (08:123),
+//    argmax (18:47), AdaptiveAvgPool2d(7) + flatten (VGG16 classifier input)
+#include "common.h"
+
+namespace {
+
+template <typename T>
+__global__ void pack_conv_kernel(int co_n, int ci_n, int k, const float *__restrict__ w,
+                                 T *__restrict__ wf, T *__restrict__ wd) {
+  const int kk = k * k;
+  const long long total = (long long)co_n * ci_n * kk;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int t = (int)(i % kk);
+    const long long r = i / kk;
+    const int ci = (int)(r % ci_n);
+    const int co = (int)(r / ci_n);
+    const float v = w[i];
+    if (wf) Elt<T>::store(wf, ((long long)co * kk + t) * ci_n + ci, v);
+    if (wd) {
+      const int ky = t / k, kx = t % k;
+      const int tf = (k - 1 - ky) * k + (k - 1 - kx);
+      Elt<T>::store(wd, ((long long)ci * kk + tf) * co_n + co, v);
+    }
+  }
+}
+
+template <typename T>
+__global__ void pack_convT_kernel(int ci_n, int co_n, const float *__restrict__ w,
+                                  T *__restrict__ wu, T *__restrict__ wdn) {
+  const long long total = (long long)ci_n * co_n * 4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int t = (int)(i & 3);
+    const long long r = i >> 2;
+    const int co = (int)(r % co_n);
+    const int ci = (int)(r / co_n);
+    const float v = w[i];
+    if (wu) Elt<T>::store(wu, ((long long)t * co_n + co) * ci_n + ci, v);
+    if (wdn) Elt<T>::store(wdn, ((long long)ci * 4 + t) * co_n + co, v);
+  }
+}
+
+__global__ void bias_tile4_kernel(int co_n, const float *b, float *b4) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 4 * co_n) b4[i] = b[i % co_n];
+}
+
+// ---------------------------------------------------------------------------
+// first layer: thread = (pixel, 4 output channels); channel groups fastest
+template <typename T>
+__global__ void conv_in_fwd_kernel(int n, int h, int w, int cin, int cout,
+                                   const float *__restrict__ x, const float *__restrict__ wt,
+                                   const float *__restrict__ b, int act, const float *alpha,
+                                   T *__restrict__ y) {
+  extern __shared__ __attribute__((aligned(16))) float sw[];   // [cin*9][cout] + bias
+  const int kk = cin * 9;
+  for (int i = threadIdx.x; i < kk * cout; i += blockDim.x) {
+    const int co = i % cout, j = i / cout;     // j = ci*9 + t
+    sw[i] = wt[(long long)co * kk + j];
+  }
+  for (int i = threadIdx.x; i < cout; i += blockDim.x) sw[kk * cout + i] = b ? b[i] : 0.f;
+  __syncthreads();
+  const int G = cout / 4;
+  const long long P = (long long)n * h * w;
+  const float al = alpha ? alpha[0] : 0.f;
+  for (long long id = blockIdx.x * (long long)blockDim.x + threadIdx.x; id < P * G;
+       id += (long long)gridDim.x * blockDim.x) {
+    const int g = (int)(id % G);
+    const long long p = id / G;
+    const int ww = (int)(p % w);
+    const long long nh = p / w;
+    const int hh = (int)(nh % h);
+    const int nn = (int)(nh / h);
+    f32x4 acc = *reinterpret_cast<const f32x4 *>(sw + kk * cout + g * 4);
+    for (int ci = 0; ci < cin; ++ci) {
+      const float *xp = x + ((long long)nn * cin + ci) * h * w;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int y2 = hh + t / 3 - 1, x2 = ww + t % 3 - 1;
+        if (y2 < 0 || y2 >= h || x2 < 0 || x2 >= w) continue;
+        const float v = xp[(long long)y2 * w + x2];
+        acc += v * *reinterpret_cast<const f32x4 *>(sw + (ci * 9 + t) * cout + g * 4);
+      }
+    }
+    if (act == 1) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] = fmaxf(acc[k], 0.f);
+    } else if (act == 2) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] = acc[k] > 0.f ? acc[k] : al * acc[k];
+    }
+    store4<T>(y + p * cout + g * 4, acc);
+  }
+}
+
+// wgrad of the first layer: dW[co][j] (j = ci*9+t, padded to 32 with j=kk the
+// bias "ones" column).  One workgroup = a pixel range; stage 64 pixels of dy
+// [64][cout] and of the im2col patch [64][32] in LDS as fp32.
+template <typename T>
+__global__ void conv_in_wgrad_kernel(int n, int h, int w, int cin, int cout,
+                                     const float *__restrict__ x, const T *__restrict__ dy,
+                                     float *__restrict__ part, long long px_per_block) {
+  __shared__ __attribute__((aligned(16))) float sdy[64][65];
+  __shared__ __attribute__((aligned(16))) float spt[64][32];
+  const int kk = cin * 9;
+  const long long P = (long long)n * h * w;
+  const long long pb = blockIdx.x * px_per_block;
+  const long long pe = min(P, pb + px_per_block);
+  // thread -> (co, jgroup of 8): cout*4 threads active (cout <= 64)
+  const int co = threadIdx.x & 63, jg = threadIdx.x >> 6;
+  // per-stage fp32 sums folded into fp64 accumulators: the bias column is a
+  // sum of signed gradients with heavy cancellation (pairwise-like accuracy)
+  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (long long p0 = pb; p0 < pe; p0 += 64) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) {
+      const int r = i >> 6, c = i & 63;
+      const long long p = p0 + r;
+      sdy[r][c] = (p < pe && c < cout) ? Elt<T>::load(dy, p * cout + c) : 0.f;
+    }
+    for (int i = threadIdx.x; i < 64 * 32; i += blockDim.x) {
+      const int r = i >> 5, j = i & 31;
+      const long long p = p0 + r;
+      float v = 0.f;
+      if (p < pe) {
+        if (j < kk) {
+          const int ci = j / 9, t = j % 9;
+          const int ww = (int)(p % w);
+          const long long nh = p / w;
+          const int hh = (int)(nh % h);
+          const int nn = (int)(nh / h);
+          const int y2 = hh + t / 3 - 1, x2 = ww + t % 3 - 1;
+          if (y2 >= 0 && y2 < h && x2 >= 0 && x2 < w)
+            v = x[(((long long)nn * cin + ci) * h + y2) * w + x2];
+        } else if (j == kk) {
+          v = 1.f;
+        }
+      }
+      spt[r][j] = v;
+    }
+    __syncthreads();
+    if (co < cout) {
+      float st[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int r = 0; r < 64; ++r) {
+        const float d = sdy[r][co];
+        const f32x4 a0 = *reinterpret_cast<const f32x4 *>(&spt[r][jg * 8]);
+        const f32x4 a1 = *reinterpret_cast<const f32x4 *>(&spt[r][jg * 8 + 4]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { st[k] += d * a0[k]; st[4 + k] += d * a1[k]; }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += st[k];
+    }
+  }
+  if (co < cout) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) part[((long long)blockIdx.x * cout + co) * 32 + jg * 8 + k] = (float)acc[k];
+  }
+}
+
+__global__ void conv_in_wgrad_finalize(int cout, int kk, int blocks, const float *__restrict__ part,
+                                       float *dw, float *db) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over cout*32
+  if (i >= cout * 32) return;
+  const int co = i / 32, j = i % 32;
+  if (j > kk) return;
+  double s = 0;
+  for (int b = 0; b < blocks; ++b) s += part[(long long)b * cout * 32 + i];
+  if (j < kk) dw[(long long)co * kk + j] = (float)s;
+  else if (db) db[co] = (float)s;
+}
+
+// dgrad of the first layer into the NCHW fp32 image grad: thread = pixel
+template <typename T>
+__global__ void conv_in_dgrad_kernel(int n, int h, int w, int cin, int cout,
+                                     const T *__restrict__ dy, const float *__restrict__ wt,
+                                     float *__restrict__ dx, int accumulate) {
+  extern __shared__ __attribute__((aligned(16))) float sw[];  // [t][ci][cout]
+  const int kk = cin * 9;
+  for (int i = threadIdx.x; i < kk * cout; i += blockDim.x) {
+    const int co = i % cout, j = i / cout;   // j = t*cin + ci
+    const int t = j / cin, ci = j % cin;
+    sw[i] = wt[((long long)co * cin + ci) * 9 + t];
+  }
+  __syncthreads();
+  const long long P = (long long)n * h * w;
+  for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < P;
+       p += (long long)gridDim.x * blockDim.x) {
+    const int ww = (int)(p % w);
+    const long long nh = p / w;
+    const int hh = (int)(nh % h);
+    const int nn = (int)(nh / h);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 9; ++t) {
+      // output pixel o with o + (ky-1, kx-1) = this pixel
+      const int ky = t / 3, kx = t % 3;
+      const int y2 = hh - ky + 1, x2 = ww - kx + 1;
+      if (y2 < 0 || y2 >= h || x2 < 0 || x2 >= w) continue;
+      const T *dp = dy + (((long long)nn * h + y2) * w + x2) * cout;
+      for (int c = 0; c < cout; c += 4) {
+        const f32x4 d = load4<T>(dp + c);
+        for (int ci = 0; ci < cin && ci < 4; ++ci) {
+          const f32x4 wv = *reinterpret_cast<const f32x4 *>(sw + (t * cin + ci) * cout + c);
+          acc[ci] += d[0] * wv[0] + d[1] * wv[1] + d[2] * wv[2] + d[3] * wv[3];
+        }
+      }
+    }
+    for (int ci = 0; ci < cin && ci < 4; ++ci) {
+      const long long o = (((long long)nn * cin + ci) * h + hh) * w + ww;
+      dx[o] = accumulate ? dx[o] + acc[ci] : acc[ci];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// last layer: y[n][co][h][w] = b[co] + sum_ci x[p][ci] w[co][ci]; thread = pixel
+template <typename T>
+__global__ void conv_out_fwd_kernel(int n, int h, int w, int cin, int cout, const T *__restrict__ x,
+                                    const float *__restrict__ wt, const float *__restrict__ b,
+                                    float *__restrict__ y) {
+  extern __shared__ __attribute__((aligned(16))) float sw[];   // [cout][cin]
+  for (int i = threadIdx.x; i < cin * cout; i += blockDim.x) sw[i] = wt[i];
+  __syncthreads();
+  const long long P = (long long)n * h * w;
+  const long long hw = (long long)h * w;
+  for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < P;
+       p += (long long)gridDim.x * blockDim.x) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    const T *xp = x + p * cin;
+    for (int c = 0; c < cin; c += 4) {
+      const f32x4 v = load4<T>(xp + c);
+      for (int co = 0; co < cout && co < 4; ++co) {
+        const f32x4 wv = *reinterpret_cast<const f32x4 *>(sw + co * cin + c);
+        acc[co] += v[0] * wv[0] + v[1] * wv[1] + v[2] * wv[2] + v[3] * wv[3];
+      }
+    }
+    const long long nn = p / hw, r = p % hw;
+    for (int co = 0; co < cout && co < 4; ++co)
+      y[(nn * cout + co) * hw + r] = acc[co] + (b ? b[co] : 0.f);
+  }
+}
+
+// last layer backward (cin <= 64, cout <= 4).  dx[p][ci] = sum_co dy[n][co][p]
+// w[co][ci] (optionally masked by x > 0); per-workgroup partial dW / db sums.
+// block: 256 threads = 4 pixel rows x 64 channel lanes
+template <typename T>
+__global__ void conv_out_bwd_kernel(int n, int h, int w, int cin, int cout,
+                                    const float *__restrict__ dy, const T *__restrict__ x,
+                                    const float *__restrict__ wt, T *__restrict__ dx, int mask_relu,
+                                    float *__restrict__ part, long long px_per_block) {
+  __shared__ float red[4][64][4];
+  __shared__ float redb[4][4];
+  const int ci = threadIdx.x & 63, row = threadIdx.x >> 6;
+  const long long hw = (long long)h * w;
+  const long long P = (long long)n * hw;
+  const long long pb = blockIdx.x * px_per_block;
+  const long long pe = min(P, pb + px_per_block);
+  float wv[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int co = 0; co < cout; ++co) wv[co] = ci < cin ? wt[co * cin + ci] : 0.f;
+  float sw[4] = {0.f, 0.f, 0.f, 0.f}, sb[4] = {0.f, 0.f, 0.f, 0.f};
+  for (long long p = pb + row; p < pe; p += 4) {
+    const long long nn = p / hw, r = p - nn * hw;
+    float d[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int co = 0; co < cout; ++co) d[co] = dy[(nn * cout + co) * hw + r];
+    if (ci < cin) {
+      const float xv = Elt<T>::load(x, p * cin + ci);
+      float g = 0.f;
+      for (int co = 0; co < cout; ++co) {
+        g += d[co] * wv[co];
+        sw[co] += d[co] * xv;
+      }
+      if (mask_relu && !(xv > 0.f)) g = 0.f;
+      if (dx) Elt<T>::store(dx, p * cin + ci, g);
+    }
+    for (int co = 0; co < cout; ++co) sb[co] += d[co];
+  }
+  for (int co = 0; co < 4; ++co) red[row][ci][co] = sw[co];
+  if (ci == 0)
+    for (int co = 0; co < 4; ++co) redb[row][co] = sb[co];
+  __syncthreads();
+  if (row == 0 && ci < cin)
+    for (int co = 0; co < cout; ++co)
+      part[((long long)blockIdx.x * (cout + 1) + co) * cin + ci] =
+          red[0][ci][co] + red[1][ci][co] + red[2][ci][co] + red[3][ci][co];
+  if (threadIdx.x < cout) {
+    const int co = threadIdx.x;
+    part[((long long)blockIdx.x * (cout + 1) + cout) * cin + co] =
+        redb[0][co] + redb[1][co] + redb[2][co] + redb[3][co];
+  }
+}
+
+__global__ void conv_out_bwd_finalize(int cin, int cout, int blocks, const float *__restrict__ part,
+                                      float *dw, float *db) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over cout*cin + cout
+  if (i >= cout * cin + cout) return;
+  double s = 0;
+  if (i < cout * cin) {
+    for (int b = 0; b < blocks; ++b) s += part[(long long)b * (cout + 1) * cin + i];
+    if (dw) dw[i] = (float)s;
+  } else {
+    const int co = i - cout * cin;
+    for (int b = 0; b < blocks; ++b) s += part[((long long)b * (cout + 1) + cout) * cin + co];
+    if (db) db[co] = (float)s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void maxpool_fwd_kernel(int n, int h, int w, int C, const T *__restrict__ x,
+                                   T *__restrict__ y, uint8_t *__restrict__ idx) {
+  const int ho = h / 2, wo = w / 2;
+  const int G = C / 4;
+  const long long total = (long long)n * ho * wo * G;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int g = (int)(i % G);
+    const long long op = i / G;
+    const int ox = (int)(op % wo);
+    const long long t = op / wo;
+    const int oy = (int)(t % ho);
+    const int nn = (int)(t / ho);
+    const long long base = (((long long)nn * h + 2 * oy) * w + 2 * ox) * C + g * 4;
+    f32x4 m = load4<T>(x + base);
+    uint8_t id[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const long long off = base + ((long long)(k >> 1) * w + (k & 1)) * C;
+      const f32x4 v = load4<T>(x + off);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (v[c] > m[c] || (v[c] != v[c] && m[c] == m[c])) { m[c] = v[c]; id[c] = (uint8_t)k; }
+    }
+    store4<T>(y + op * C + g * 4, m);
+    *reinterpret_cast<uchar4 *>(idx + op * C + g * 4) = make_uchar4(id[0], id[1], id[2], id[3]);
+  }
+}
+
+template <typename T>
+__global__ void maxpool_bwd_kernel(int n, int h, int w, int C, const T *__restrict__ dy,
+                                   const uint8_t *__restrict__ idx, T *__restrict__ dx,
+                                   int accumulate, const T *__restrict__ mask) {
+  const int ho = h / 2, wo = w / 2;
+  const int G = C / 4;
+  const long long total = (long long)n * h * w * G;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int g = (int)(i % G);
+    const long long p = i / G;
+    const int xx = (int)(p % w);
+    const long long t = p / w;
+    const int yy = (int)(t % h);
+    const int nn = (int)(t / h);
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    const int oy = yy >> 1, ox = xx >> 1;
+    if (oy < ho && ox < wo) {
+      const long long op = ((long long)nn * ho + oy) * wo + ox;
+      const uchar4 id = *reinterpret_cast<const uchar4 *>(idx + op * C + g * 4);
+      const uint8_t k = (uint8_t)((yy & 1) * 2 + (xx & 1));
+      const f32x4 d = load4<T>(dy + op * C + g * 4);
+      v[0] = id.x == k ? d[0] : 0.f;
+      v[1] = id.y == k ? d[1] : 0.f;
+      v[2] = id.z == k ? d[2] : 0.f;
+      v[3] = id.w == k ? d[3] : 0.f;
+    }
+    const long long e = p * C + g * 4;
+    if (accumulate) v += load4<T>(dx + e);
+    if (mask) {
+      const f32x4 m = load4<T>(mask + e);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = m[c] > 0.f ? v[c] : 0.f;
+    }
+    store4<T>(dx + e, v);
+  }
+}
+
+// PReLU backward on an NHWC tensor (count elements): dx = dy*(y>0 ? 1 : a);
+// alpha partial per block of sum(dy*y_pre*(y_pre<=0)).
+template <typename T>
+__global__ void prelu_bwd_kernel(long long count, const T *__restrict__ dy, const T *__restrict__ yp,
+                                 const float *alpha, T *__restrict__ dx, float *__restrict__ apart) {
+  __shared__ float red[256];
+  const float a = alpha[0];
+  float s = 0.f;
+  const long long n4 = count / 4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
+       i += (long long)gridDim.x * blockDim.x) {
+    const f32x4 d = load4<T>(dy + i * 4);
+    const f32x4 u = load4<T>(yp + i * 4);
+    f32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o[k] = u[k] > 0.f ? d[k] : a * d[k];
+      s += u[k] > 0.f ? 0.f : d[k] * u[k];
+    }
+    store4<T>(dx + i * 4, o);
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) apart[blockIdx.x] = red[0];
+}
+
+__global__ void sum_partials(int n, const float *__restrict__ part, float *out, int accumulate) {
+  __shared__ double red[256];
+  double s = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += part[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = accumulate ? out[0] + (float)red[0] : (float)red[0];
+}
+
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void nchw_to_nhwc_kernel(int n, int c, int h, int w, const float *__restrict__ x,
+                                    T *__restrict__ y) {
+  const long long total = (long long)n * c * h * w;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % c);
+    const long long p = i / c;
+    const long long hw = (long long)h * w;
+    const long long nn = p / hw, r = p % hw;
+    Elt<T>::store(y, i, x[(nn * c + cc) * hw + r]);
+  }
+}
+
+template <typename T>
+__global__ void nhwc_to_nchw_kernel(int n, int c, int h, int w, const T *__restrict__ x,
+                                    float *__restrict__ y) {
+  const long long total = (long long)n * c * h * w;
+  const long long hw = (long long)h * w;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i % hw;
+    const long long t = i / hw;
+    const int cc = (int)(t % c);
+    const long long nn = t / c;
+    y[i] = Elt<T>::load(x, (nn * hw + r) * c + cc);
+  }
+}
+
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void loss_partial_kernel(int kind, long long count, const T *__restrict__ a,
+                                    const T *__restrict__ b, float *__restrict__ part) {
+  __shared__ double red[256];
+  double s = 0;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < count;
+       i += (long long)gridDim.x * blockDim.x) {
+    const float d = Elt<T>::load(a, i) - Elt<T>::load(b, i);
+    s += kind == 0 ? fabsf(d) : d * d;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = (float)red[0];
+}
+
+__global__ void loss_finalize(int blocks, const float *__restrict__ part, float *out, double scale,
+                              int accumulate) {
+  __shared__ double red[256];
+  double s = 0;
+  for (int i = threadIdx.x; i < blocks; i += blockDim.x) s += part[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = (accumulate ? out[0] : 0.f) + (float)(red[0] * scale);
+}
+
+template <typename T>
+__global__ void loss_bwd_kernel(int kind, long long count, const T *__restrict__ a,
+                                const T *__restrict__ b, const float *gs, float scale,
+                                T *__restrict__ ga, T *__restrict__ gb, int accumulate,
+                                int mask_a_pos) {
+  const float g = (gs ? gs[0] : 1.f) * scale;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < count;
+       i += (long long)gridDim.x * blockDim.x) {
+    const float av = Elt<T>::load(a, i);
+    const float d = av - Elt<T>::load(b, i);
+    float v = kind == 0 ? (d > 0.f ? g : (d < 0.f ? -g : 0.f)) : 2.f * g * d;
+    if (mask_a_pos && !(av > 0.f)) v = 0.f;
+    if (ga) Elt<T>::store(ga, i, accumulate ? Elt<T>::load(ga, i) + v : v);
+    if (gb) Elt<T>::store(gb, i, accumulate ? Elt<T>::load(gb, i) - v : -v);
+  }
+}
+
+__global__ void adamw_kernel(long long count, float *__restrict__ p, const float *__restrict__ g,
+                             float *__restrict__ m, float *__restrict__ v, float lr, float b1,
+                             float b2, float eps, float wd, int decoupled, float bc1, float sbc2) {
+  const float step = lr / bc1;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < count;
+       i += (long long)gridDim.x * blockDim.x) {
+    float pv = p[i];
+    float gv = g[i];
+    if (decoupled) pv *= (1.f - lr * wd);
+    else if (wd != 0.f) gv += wd * pv;
+    float mv = m[i];
+    mv = mv + (1.f - b1) * (gv - mv);          // lerp_(g, 1-b1)
+    float vv = v[i] * b2 + (1.f - b2) * gv * gv;
+    const float denom = sqrtf(vv) / sbc2 + eps;
+    pv = pv - step * (mv / denom);
+    p[i] = pv; m[i] = mv; v[i] = vv;
+  }
+}
+
+__global__ void to_u8_kernel(int n, int c, int h, int w, const float *__restrict__ x,
+                             uint8_t *__restrict__ out, int bgr) {
+  const long long total = (long long)n * h * w * c;
+  const long long hw = (long long)h * w;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % c);
+    const long long p = i / c;
+    const long long nn = p / hw, r = p % hw;
+    const int sc = bgr ? (c - 1 - cc) : cc;
+    float v = x[(nn * c + sc) * hw + r];
+    v = fminf(fmaxf(v, 0.f), 1.f);           // torch.clamp(0, 1)
+    out[i] = (uint8_t)(v * 255.f);            // astype(uint8): truncation
+  }
+}
+
+__global__ void psnr_kernel(long long per, const uint8_t *__restrict__ a, const uint8_t *__restrict__ b,
+                            double *out) {
+  __shared__ double red[256];
+  const uint8_t *pa = a + blockIdx.x * per, *pb = b + blockIdx.x * per;
+  double s = 0;
+  for (long long i = threadIdx.x; i < per; i += blockDim.x) {
+    const double d = (double)pa[i] - (double)pb[i];
+    s += d * d;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double mse = red[0] / (double)per;
+    out[blockIdx.x] = mse == 0 ? __builtin_inf() : 10.0 * log10(255.0 * 255.0 / mse);
+  }
+}
+
+__global__ void argmax_kernel(int n, int k, const float *__restrict__ x, int64_t *out) {
+  const int row = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  const int lane = threadIdx.x & 63;
+  if (row >= n) return;
+  float best = -__builtin_inff();
+  int bi = 0x7fffffff;
+  for (int j = lane; j < k; j += 64) {
+    const float v = x[(long long)row * k + j];
+    if (v > best || (v != v && best == best)) { best = v; bi = j; }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    const bool onan = ov != ov, bnan = best != best;
+    bool take;
+    if (onan != bnan) take = onan;
+    else take = (ov > best) || (ov == best && oi < bi) || (onan && oi < bi);
+    if (take) { best = ov; bi = oi; }
+  }
+  if (lane == 0) out[row] = bi == 0x7fffffff ? 0 : bi;
+}
+
+// AdaptiveAvgPool2d((oh, ow)) on NHWC input -> [n][C*oh*ow] in NCHW flatten order
+template <typename T>
+__global__ void adaptive_avgpool_kernel(int n, int h, int w, int C, int oh, int ow,
+                                        const T *__restrict__ x, T *__restrict__ y) {
+  const long long total = (long long)n * C * oh * ow;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int ox = (int)(i % ow);
+    long long t = i / ow;
+    const int oy = (int)(t % oh);
+    t /= oh;
+    const int c = (int)(t % C);
+    const int nn = (int)(t / C);
+    // torch: start = floor(o*in/out), end = ceil((o+1)*in/out)
+    const int y0 = (oy * h) / oh, y1 = ((oy + 1) * h + oh - 1) / oh;
+    const int x0 = (ox * w) / ow, x1 = ((ox + 1) * w + ow - 1) / ow;
+    float s = 0.f;
+    for (int yy = y0; yy < y1; ++yy)
+      for (int xx = x0; xx < x1; ++xx) s += Elt<T>::load(x, (((long long)nn * h + yy) * w + xx) * C + c);
+    Elt<T>::store(y, i, s / (float)((y1 - y0) * (x1 - x0)));
+  }
+}
+
+}  // namespace
+
+#define DT_LAUNCH(dtype, kern, grid, block, shm, st, ...)                                 \
+  do {                                                                                    \
+    if ((dtype) == RR_BF16)                                                               \
+      hipLaunchKernelGGL(kern<bf16_t>, grid, block, shm, st, __VA_ARGS__);                \
+    else                                                                                  \
+      hipLaunchKernelGGL(kern<float>, grid, block, shm, st, __VA_ARGS__);                 \
+  } while (0)
+
+// dtype-generic pointer casts inside the macro are done by the callers below.
+
+extern "C" int rr_pack_conv(int dtype, int c_out, int c_in, int k, const float *w, void *w_fwd,
+                            void *w_dgrad, rr_stream stream) {
+  if (!w || c_out <= 0 || c_in <= 0 || (k != 1 && k != 3)) return RR_EINVAL;
+  const long long total = (long long)c_out * c_in * k * k;
+  dim3 g(rr_grid_cap((total + 255) / 256)), b(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(pack_conv_kernel<bf16_t>, g, b, 0, st, c_out, c_in, k, w, (bf16_t *)w_fwd,
+                       (bf16_t *)w_dgrad);
+  else
+    hipLaunchKernelGGL(pack_conv_kernel<float>, g, b, 0, st, c_out, c_in, k, w, (float *)w_fwd,
+                       (float *)w_dgrad);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_pack_convT(int dtype, int c_in, int c_out, const float *w, void *w_up,
+                             void *w_down, rr_stream stream) {
+  if (!w || c_out <= 0 || c_in <= 0) return RR_EINVAL;
+  const long long total = (long long)c_out * c_in * 4;
+  dim3 g(rr_grid_cap((total + 255) / 256)), b(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(pack_convT_kernel<bf16_t>, g, b, 0, st, c_in, c_out, w, (bf16_t *)w_up,
+                       (bf16_t *)w_down);
+  else
+    hipLaunchKernelGGL(pack_convT_kernel<float>, g, b, 0, st, c_in, c_out, w, (float *)w_up,
+                       (float *)w_down);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_bias_tile4(int c_out, const float *b, float *b4, rr_stream stream) {
+  if (!b || !b4 || c_out <= 0) return RR_EINVAL;
+  hipLaunchKernelGGL(bias_tile4_kernel, dim3((4 * c_out + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, c_out, b, b4);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_conv_in_fwd(int dtype, int n, int h, int w, int cin, int cout, const float *x,
+                              const float *wt, const float *b, int act, const float *alpha,
+                              void *y, rr_stream stream) {
+  if (!x || !wt || !y || n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cin > 4 || cout % 4 ||
+      cout > 128 || (act == 2 && !alpha))
+    return RR_EINVAL;
+  const long long work = (long long)n * h * w * (cout / 4);
+  const size_t shm = ((size_t)cin * 9 * cout + cout) * sizeof(float);
+  dim3 g(rr_grid_cap((work + 255) / 256, 8192)), bl(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(conv_in_fwd_kernel<bf16_t>, g, bl, shm, st, n, h, w, cin, cout, x, wt, b,
+                       act, alpha, (bf16_t *)y);
+  else
+    hipLaunchKernelGGL(conv_in_fwd_kernel<float>, g, bl, shm, st, n, h, w, cin, cout, x, wt, b,
+                       act, alpha, (float *)y);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+static int conv_in_wgrad_blocks(int n, int h, int w) {
+  const long long P = (long long)n * h * w;
+  long long b = (P + 2047) / 2048;
+  if (b > 1024) b = 1024;
+  return (int)(b < 1 ? 1 : b);
+}
+
+extern "C" size_t rr_conv_in_wgrad_workspace(int n, int h, int w, int cin, int cout) {
+  (void)cin;
+  return (size_t)conv_in_wgrad_blocks(n, h, w) * cout * 32 * sizeof(float);
+}
+
+extern "C" int rr_conv_in_wgrad(int dtype, int n, int h, int w, int cin, int cout, const float *x,
+                                const void *dy, float *dw, float *db, void *ws, size_t ws_bytes,
+                                rr_stream stream) {
+  if (!x || !dy || !dw || cin * 9 >= 32 || cout > 64 || cout <= 0) return RR_EINVAL;
+  const int blocks = conv_in_wgrad_blocks(n, h, w);
+  if (!ws || ws_bytes < (size_t)blocks * cout * 32 * sizeof(float)) return RR_EWORKSPACE;
+  const long long P = (long long)n * h * w;
+  long long ppb = (P + blocks - 1) / blocks;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(conv_in_wgrad_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, n, h, w, cin,
+                       cout, x, (const bf16_t *)dy, (float *)ws, ppb);
+  else
+    hipLaunchKernelGGL(conv_in_wgrad_kernel<float>, dim3(blocks), dim3(256), 0, st, n, h, w, cin,
+                       cout, x, (const float *)dy, (float *)ws, ppb);
+  RR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(conv_in_wgrad_finalize, dim3((cout * 32 + 255) / 256), dim3(256), 0, st, cout,
+                     cin * 9, blocks, (const float *)ws, dw, db);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_conv_in_dgrad(int dtype, int n, int h, int w, int cin, int cout, const void *dy,
+                                const float *wt, float *dx, int accumulate, rr_stream stream) {
+  if (!dy || !wt || !dx || cin > 4 || cout % 4) return RR_EINVAL;
+  const long long P = (long long)n * h * w;
+  const size_t shm = (size_t)cin * 9 * cout * sizeof(float);
+  dim3 g(rr_grid_cap((P + 255) / 256, 8192)), b(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(conv_in_dgrad_kernel<bf16_t>, g, b, shm, st, n, h, w, cin, cout,
+                       (const bf16_t *)dy, wt, dx, accumulate);
+  else
+    hipLaunchKernelGGL(conv_in_dgrad_kernel<float>, g, b, shm, st, n, h, w, cin, cout,
+                       (const float *)dy, wt, dx, accumulate);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_prelu_bwd(int dtype, long long count, const void *dy, const void *y_pre,
+                            const float *alpha, void *dx, float *alpha_partial, int blocks,
+                            float *dalpha, rr_stream stream) {
+  if (!dy || !y_pre || !alpha || !dx || !alpha_partial || !dalpha || count % 4 || blocks <= 0 ||
+      blocks > 4096)
+    return RR_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(prelu_bwd_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, count,
+                       (const bf16_t *)dy, (const bf16_t *)y_pre, alpha, (bf16_t *)dx, alpha_partial);
+  else
+    hipLaunchKernelGGL(prelu_bwd_kernel<float>, dim3(blocks), dim3(256), 0, st, count,
+                       (const float *)dy, (const float *)y_pre, alpha, (float *)dx, alpha_partial);
+  RR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sum_partials, dim3(1), dim3(256), 0, st, blocks, alpha_partial, dalpha, 0);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_conv_out_fwd(int dtype, int n, int h, int w, int cin, int cout, const void *x,
+                               const float *wt, const float *b, float *y, rr_stream stream) {
+  if (!x || !wt || !y || cout > 4 || cout <= 0 || cin % 4) return RR_EINVAL;
+  const long long P = (long long)n * h * w;
+  dim3 g(rr_grid_cap((P + 255) / 256, 8192)), bl(256);
+  const size_t shm = (size_t)cin * cout * sizeof(float);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(conv_out_fwd_kernel<bf16_t>, g, bl, shm, st, n, h, w, cin, cout,
+                       (const bf16_t *)x, wt, b, y);
+  else
+    hipLaunchKernelGGL(conv_out_fwd_kernel<float>, g, bl, shm, st, n, h, w, cin, cout,
+                       (const float *)x, wt, b, y);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+static int conv_out_blocks(int n, int h, int w) {
+  const long long P = (long long)n * h * w;
+  long long b = (P + 1023) / 1024;
+  if (b > 2048) b = 2048;
+  return (int)(b < 1 ? 1 : b);
+}
+
+extern "C" size_t rr_conv_out_bwd_workspace(int n, int h, int w, int cin, int cout) {
+  return (size_t)conv_out_blocks(n, h, w) * (cout + 1) * cin * sizeof(float);
+}
+
+extern "C" int rr_conv_out_bwd(int dtype, int n, int h, int w, int cin, int cout, const float *dy,
+                               const void *x, const float *wt, void *dx, int mask_relu, float *dw,
+                               float *db, void *ws, size_t ws_bytes, rr_stream stream) {
+  if (!dy || !x || !wt || cout > 4 || cout <= 0 || cin > 64) return RR_EINVAL;
+  const int blocks = conv_out_blocks(n, h, w);
+  if (!ws || ws_bytes < (size_t)blocks * (cout + 1) * cin * sizeof(float)) return RR_EWORKSPACE;
+  const long long P = (long long)n * h * w;
+  const long long ppb = (P + blocks - 1) / blocks;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(conv_out_bwd_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, n, h, w, cin,
+                       cout, dy, (const bf16_t *)x, wt, (bf16_t *)dx, mask_relu, (float *)ws, ppb);
+  else
+    hipLaunchKernelGGL(conv_out_bwd_kernel<float>, dim3(blocks), dim3(256), 0, st, n, h, w, cin,
+                       cout, dy, (const float *)x, wt, (float *)dx, mask_relu, (float *)ws, ppb);
+  RR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(conv_out_bwd_finalize, dim3((cout * cin + cout + 255) / 256), dim3(256), 0,
+                     st, cin, cout, blocks, (const float *)ws, dw, db);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_maxpool2_fwd(int dtype, int n, int h, int w, int C, const void *x, void *y,
+                               uint8_t *idx, rr_stream stream) {
+  if (!x || !y || !idx || C % 4 || h < 2 || w < 2) return RR_EINVAL;
+  const long long total = (long long)n * (h / 2) * (w / 2) * (C / 4);
+  dim3 g(rr_grid_cap((total + 255) / 256, 8192)), b(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<bf16_t>, g, b, 0, st, n, h, w, C, (const bf16_t *)x,
+                       (bf16_t *)y, idx);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, g, b, 0, st, n, h, w, C, (const float *)x,
+                       (float *)y, idx);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_maxpool2_bwd(int dtype, int n, int h, int w, int C, const void *dy,
+                               const uint8_t *idx, void *dx, int accumulate, const void *mask,
+                               rr_stream stream) {
+  if (!dy || !idx || !dx || C % 4) return RR_EINVAL;
+  const long long total = (long long)n * h * w * (C / 4);
+  dim3 g(rr_grid_cap((total + 255) / 256, 8192)), b(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, g, b, 0, st, n, h, w, C, (const bf16_t *)dy, idx,
+                       (bf16_t *)dx, accumulate, (const bf16_t *)mask);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, g, b, 0, st, n, h, w, C, (const float *)dy, idx,
+                       (float *)dx, accumulate, (const float *)mask);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_nchw_to_nhwc(int dtype, int n, int c, int h, int w, const float *x, void *y,
+                               rr_stream stream) {
+  if (!x || !y) return RR_EINVAL;
+  const long long total = (long long)n * c * h * w;
+  dim3 g(rr_grid_cap((total + 255) / 256, 8192)), b(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16_t>, g, b, 0, st, n, c, h, w, x, (bf16_t *)y);
+  else
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, g, b, 0, st, n, c, h, w, x, (float *)y);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_nhwc_to_nchw(int dtype, int n, int c, int h, int w, const void *x, float *y,
+                               rr_stream stream) {
+  if (!x || !y) return RR_EINVAL;
+  const long long total = (long long)n * c * h * w;
+  dim3 g(rr_grid_cap((total + 255) / 256, 8192)), b(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<bf16_t>, g, b, 0, st, n, c, h, w, (const bf16_t *)x, y);
+  else
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<float>, g, b, 0, st, n, c, h, w, (const float *)x, y);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+static int loss_blocks(long long count) {
+  long long b = (count + 4095) / 4096;
+  if (b > 1024) b = 1024;
+  return (int)(b < 1 ? 1 : b);
+}
+
+extern "C" size_t rr_loss_workspace(long long count) {
+  return (size_t)loss_blocks(count) * sizeof(float);
+}
+
+extern "C" int rr_loss_fwd(int kind, int dtype, long long count, const void *a, const void *b,
+                           float *out_scalar, float scale, int accumulate, void *ws,
+                           size_t ws_bytes, rr_stream stream) {
+  if (!a || !b || !out_scalar || count <= 0 || (kind != 0 && kind != 1)) return RR_EINVAL;
+  const int blocks = loss_blocks(count);
+  if (!ws || ws_bytes < (size_t)blocks * sizeof(float)) return RR_EWORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(loss_partial_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, kind, count,
+                       (const bf16_t *)a, (const bf16_t *)b, (float *)ws);
+  else
+    hipLaunchKernelGGL(loss_partial_kernel<float>, dim3(blocks), dim3(256), 0, st, kind, count,
+                       (const float *)a, (const float *)b, (float *)ws);
+  RR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(loss_finalize, dim3(1), dim3(256), 0, st, blocks, (const float *)ws,
+                     out_scalar, (double)scale / (double)count, accumulate);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_loss_bwd(int kind, int dtype, long long count, const void *a, const void *b,
+                           const float *gscale_dev, float scale, void *ga, void *gb, int accumulate,
+                           int mask_a_pos, rr_stream stream) {
+  if (!a || !b || count <= 0 || (kind != 0 && kind != 1)) return RR_EINVAL;
+  dim3 g(rr_grid_cap((count + 255) / 256, 8192)), bl(256);
+  const float sc = scale / (float)count;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(loss_bwd_kernel<bf16_t>, g, bl, 0, st, kind, count, (const bf16_t *)a,
+                       (const bf16_t *)b, gscale_dev, sc, (bf16_t *)ga, (bf16_t *)gb, accumulate,
+                       mask_a_pos);
+  else
+    hipLaunchKernelGGL(loss_bwd_kernel<float>, g, bl, 0, st, kind, count, (const float *)a,
+                       (const float *)b, gscale_dev, sc, (float *)ga, (float *)gb, accumulate,
+                       mask_a_pos);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_adamw(long long count, float *param, const float *grad, float *m, float *v,
+                        float lr, float beta1, float beta2, float eps, float weight_decay,
+                        int decoupled, int step, rr_stream stream) {
+  if (!param || !grad || !m || !v || count <= 0 || step < 1) return RR_EINVAL;
+  const double bc1 = 1.0 - pow((double)beta1, step);
+  const double bc2 = 1.0 - pow((double)beta2, step);
+  dim3 g(rr_grid_cap((count + 255) / 256, 8192)), b(256);
+  hipLaunchKernelGGL(adamw_kernel, g, b, 0, (hipStream_t)stream, count, param, grad, m, v, lr,
+                     beta1, beta2, eps, weight_decay, decoupled, (float)bc1, (float)sqrt(bc2));
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_to_uint8_hwc(int n, int c, int h, int w, const float *x, uint8_t *out, int bgr,
+                               rr_stream stream) {
+  if (!x || !out) return RR_EINVAL;
+  const long long total = (long long)n * c * h * w;
+  dim3 g(rr_grid_cap((total + 255) / 256, 8192)), b(256);
+  hipLaunchKernelGGL(to_u8_kernel, g, b, 0, (hipStream_t)stream, n, c, h, w, x, out, bgr);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_psnr_u8(int n, long long per_image, const uint8_t *a, const uint8_t *b,
+                          double *out, rr_stream stream) {
+  if (!a || !b || !out || n <= 0 || per_image <= 0) return RR_EINVAL;
+  hipLaunchKernelGGL(psnr_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream, per_image, a, b, out);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_argmax_rows(int n, int k, const float *logits, int64_t *out, rr_stream stream) {
+  if (!logits || !out || n <= 0 || k <= 0) return RR_EINVAL;
+  hipLaunchKernelGGL(argmax_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, n, k,
+                     logits, out);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_adaptive_avgpool_flatten(int dtype, int n, int h, int w, int C, int oh, int ow,
+                                           const void *x, void *y, rr_stream stream) {
+  if (!x || !y || oh <= 0 || ow <= 0) return RR_EINVAL;
+  const long long total = (long long)n * C * oh * ow;
+  dim3 g(rr_grid_cap((total + 255) / 256, 8192)), b(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(adaptive_avgpool_kernel<bf16_t>, g, b, 0, st, n, h, w, C, oh, ow,
+                       (const bf16_t *)x, (bf16_t *)y);
+  else
+    hipLaunchKernelGGL(adaptive_avgpool_kernel<float>, g, b, 0, st, n, h, w, C, oh, ow,
+                       (const float *)x, (float *)y);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_zero(void *p, size_t bytes, rr_stream stream) {
+  if (!p) return RR_EINVAL;
+  if (hipMemsetAsync(p, 0, bytes, (hipStream_t)stream) != hipSuccess) return RR_ELAUNCH;
+  return RR_OK;
+}
+
+extern "C" const char *rr_version(void) { return "roadrestore-gfx950 0.1"; }

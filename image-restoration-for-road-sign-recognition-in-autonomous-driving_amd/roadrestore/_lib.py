@@ -1,0 +1,123 @@
+"""ctypes binding of the gfx950 C-ABI library (include/roadrestore.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (csrc/Makefile) and
+loaded from this directory.  There is no fallback: if the library is missing
+or a GPU is absent, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libroadrestore.so")
+
+RR_F32, RR_BF16 = 0, 1
+RR_CONV3X3, RR_CONV1X1, RR_CONVT_UP, RR_CONVT_DOWN = 0, 1, 2, 3
+RR_ACT_NONE, RR_ACT_RELU = 0, 1
+
+_STATUS = {0: "ok", -1: "EINVAL", -2: "EUNSUPPORTED", -3: "ELAUNCH", -4: "EWORKSPACE"}
+
+
+class IgemmDesc(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in (
+        "dtype", "mode", "n", "h", "w", "c_in1", "c_in2", "c_out", "out_split", "act",
+        "accumulate", "has_bias", "has_mask", "want_stats")]
+
+
+class WgradDesc(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in (
+        "dtype", "mode", "n", "h", "w", "c_in1", "c_in2", "c_out", "accumulate")]
+
+
+class BnBwdDesc(C.Structure):
+    _fields_ = [("dtype", C.c_int32), ("P", C.c_int64), ("C", C.c_int32),
+                ("mask_kind", C.c_int32), ("nbn", C.c_int32)]
+
+
+P_ = C.c_void_p
+I_ = C.c_int
+L_ = C.c_longlong
+F_ = C.c_float
+S_ = C.c_size_t
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "rr_igemm": (I_, [C.POINTER(IgemmDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_]),
+    "rr_igemm_stat_blocks": (I_, [C.POINTER(IgemmDesc)]),
+    "rr_wgrad_workspace": (S_, [C.POINTER(WgradDesc)]),
+    "rr_wgrad": (I_, [C.POINTER(WgradDesc), P_, P_, P_, P_, P_, S_, P_]),
+    "rr_pack_conv": (I_, [I_, I_, I_, I_, P_, P_, P_, P_]),
+    "rr_pack_convT": (I_, [I_, I_, I_, P_, P_, P_, P_]),
+    "rr_bias_tile4": (I_, [I_, P_, P_, P_]),
+    "rr_bn_finalize": (I_, [I_, I_, L_, P_, P_, P_, P_, P_, P_, F_, F_, P_, P_, P_, P_, P_, P_]),
+    "rr_bn_eval_affine": (I_, [I_, P_, P_, P_, P_, F_, P_, P_, P_]),
+    "rr_affine_act": (I_, [I_, L_, I_, P_, P_, P_, P_, P_, P_, P_, I_, P_, P_]),
+    "rr_bn_bwd_blocks": (I_, [C.POINTER(BnBwdDesc)]),
+    "rr_bn_bwd_reduce": (I_, [C.POINTER(BnBwdDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_, P_, P_,
+                              P_, P_]),
+    "rr_bn_bwd_finalize": (I_, [C.POINTER(BnBwdDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_, P_,
+                                P_, P_]),
+    "rr_bn_bwd_apply": (I_, [C.POINTER(BnBwdDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_, P_, P_,
+                             P_, P_, P_, P_, P_]),
+    "rr_channel_sum": (I_, [I_, L_, I_, P_, P_, I_, P_, S_, P_]),
+    "rr_channel_sum_workspace": (S_, [L_, I_]),
+    "rr_maxpool2_fwd": (I_, [I_, I_, I_, I_, I_, P_, P_, P_, P_]),
+    "rr_maxpool2_bwd": (I_, [I_, I_, I_, I_, I_, P_, P_, P_, I_, P_, P_]),
+    "rr_conv_in_fwd": (I_, [I_, I_, I_, I_, I_, I_, P_, P_, P_, I_, P_, P_, P_]),
+    "rr_conv_in_wgrad": (I_, [I_, I_, I_, I_, I_, I_, P_, P_, P_, P_, P_, S_, P_]),
+    "rr_conv_in_wgrad_workspace": (S_, [I_, I_, I_, I_, I_]),
+    "rr_conv_in_dgrad": (I_, [I_, I_, I_, I_, I_, I_, P_, P_, P_, I_, P_]),
+    "rr_prelu_bwd": (I_, [I_, L_, P_, P_, P_, P_, P_, I_, P_, P_]),
+    "rr_conv_out_fwd": (I_, [I_, I_, I_, I_, I_, I_, P_, P_, P_, P_, P_]),
+    "rr_conv_out_bwd": (I_, [I_, I_, I_, I_, I_, I_, P_, P_, P_, P_, I_, P_, P_, P_, S_, P_]),
+    "rr_conv_out_bwd_workspace": (S_, [I_, I_, I_, I_, I_]),
+    "rr_nchw_to_nhwc": (I_, [I_, I_, I_, I_, I_, P_, P_, P_]),
+    "rr_nhwc_to_nchw": (I_, [I_, I_, I_, I_, I_, P_, P_, P_]),
+    "rr_loss_fwd": (I_, [I_, I_, L_, P_, P_, P_, F_, I_, P_, S_, P_]),
+    "rr_loss_workspace": (S_, [L_]),
+    "rr_loss_bwd": (I_, [I_, I_, L_, P_, P_, P_, F_, P_, P_, I_, I_, P_]),
+    "rr_adamw": (I_, [L_, P_, P_, P_, P_, F_, F_, F_, F_, F_, I_, I_, P_]),
+    "rr_to_uint8_hwc": (I_, [I_, I_, I_, I_, P_, P_, I_, P_]),
+    "rr_psnr_u8": (I_, [I_, L_, P_, P_, P_, P_]),
+    "rr_argmax_rows": (I_, [I_, I_, P_, P_, P_]),
+    "rr_adaptive_avgpool_flatten": (I_, [I_, I_, I_, I_, I_, I_, I_, P_, P_, P_]),
+    "rr_zero": (I_, [P_, S_, P_]),
+    "rr_version": (C.c_char_p, []),
+}
+
+EXPORTED = tuple(_SIGS)
+
+
+class Lib:
+    """Loaded library with typed entry points; ``check`` turns status codes
+    into RuntimeError (the reference's ATen ops raise RuntimeError too)."""
+
+    def __init__(self, path=LIB_PATH):
+        if not os.path.exists(path):
+            raise RuntimeError(
+                f"roadrestore HIP library not built: {path} is missing "
+                "(run __graft_entry__.build())")
+        self.path = path
+        self.dll = C.CDLL(path)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(self.dll, name)
+            fn.restype = res
+            fn.argtypes = args
+            setattr(self, name, fn)
+
+    @staticmethod
+    def check(rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed: {_STATUS.get(rc, rc)} ({rc})")
+        return rc
+
+
+_LIB = None
+
+
+def lib() -> Lib:
+    global _LIB
+    if _LIB is None:
+        _LIB = Lib()
+    return _LIB

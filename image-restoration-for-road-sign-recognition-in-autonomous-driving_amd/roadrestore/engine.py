@@ -1,0 +1,514 @@
+"""Network executors: forward schedules and hand-written backward schedules.
+
+Each reference network is run as one autograd node whose forward issues the
+fused HIP kernels in order (NHWC activations kept resident in HBM, saved for
+backward) and whose backward issues the reverse schedule: BN/PReLU/ReLU
+backward reductions, dgrad implicit GEMMs and split-K wgrad GEMMs.  Parameter
+gradients are written straight into one flat fp32 buffer laid out in the
+order they become final (``GradSink``), so a data-parallel wrapper can
+all-reduce finished buckets while the rest of the backward still runs, and a
+fused optimizer can update every parameter with one launch.
+
+Reference schedules mirrored (file:line in the reference repo):
+  SimpleUNet.forward        07_train_restoration.py:99-120
+  ResidualBlock.forward     14_train_unified_advanced.py:114-115
+  ResUNet.forward           14_train_unified_advanced.py:151-186
+  VGGPerceptualLoss.forward 14_train_unified_advanced.py:195-196
+  VGG16 classifier          18_test_unified_benchmark.py:46 (torchvision cfg D)
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+from ._lib import RR_CONV1X1, RR_CONV3X3, RR_CONVT_DOWN, RR_CONVT_UP
+
+RELU = 1
+
+
+class Bag(dict):
+    __getattr__ = dict.__getitem__
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+
+# ---------------------------------------------------------------------------
+# packed weights
+
+class WeightCache:
+    """Packed (compute layout / dtype) copies of fp32 weights, re-packed when
+    the parameter's version counter moves (every optimizer step) and always
+    while a HIP graph is being captured (so replays re-pack)."""
+
+    def __init__(self):
+        self._c = {}
+
+    def _get(self, w, dtype, kind, fn):
+        cap = torch.cuda.is_current_stream_capturing()
+        key = (id(w), dtype, kind)
+        ver = (w.data_ptr(), w._version)
+        e = None if cap else self._c.get(key)
+        if e is not None and e[0] == ver:
+            return e[1]
+        v = fn()
+        if not cap:
+            self._c[key] = (ver, v)
+        return v
+
+    def conv(self, w, dtype, dgrad):
+        kind = "conv+d" if dgrad else "conv"
+        return self._get(w, dtype, kind, lambda: ops.pack_conv(w, dtype, True, dgrad))
+
+    def convT(self, w, dtype, down):
+        kind = "convT+d" if down else "convT"
+        return self._get(w, dtype, kind, lambda: ops.pack_convT(w, dtype, True, down))
+
+    def linear(self, w, dtype):
+        return self._get(w, dtype, "linear", lambda: ops.pack_conv(
+            w.view(w.shape[0], w.shape[1], 1, 1), dtype, True, False))
+
+    def bias4(self, b):
+        return self._get(b, torch.float32, "b4", lambda: ops.bias_tile4(b))
+
+    def clear(self):
+        self._c.clear()
+
+
+# ---------------------------------------------------------------------------
+# gradient sink
+
+class GradSink:
+    """Flat fp32 gradient buffer over ``params`` (in readiness order).
+
+    ``zero_params`` are parameters whose gradient is exactly zero (a conv bias
+    feeding a train-mode BatchNorm: the BN subtracts the batch mean, so
+    d(loss)/d(bias) = sum_p dt_p = 0); they sit first and are cleared with one
+    memset.  ``hook(sink, params)`` is called as groups become final.
+    """
+
+    def __init__(self, params, device, zero_params=(), hook=None):
+        zp = [p for p in params if id(p) in {id(z) for z in zero_params}]
+        rest = [p for p in params if id(p) not in {id(z) for z in zero_params}]
+        self.order = zp + rest
+        total = sum(p.numel() for p in self.order)
+        self.flat = torch.empty(total, dtype=torch.float32, device=device)
+        self.view = {}
+        self.offset = {}
+        off = 0
+        for p in self.order:
+            self.view[id(p)] = self.flat[off:off + p.numel()].view(p.shape)
+            self.offset[id(p)] = off
+            off += p.numel()
+        nz = sum(p.numel() for p in zp)
+        if nz:
+            ops.zero_(self.flat[:nz])
+        self.zero_count = nz
+        self.hook = hook
+
+    def __getitem__(self, p):
+        return self.view[id(p)]
+
+    def ready(self, params):
+        if self.hook is not None:
+            self.hook(self, params)
+
+    def release(self):
+        """Hand the per-parameter views over (the autograd engine then adopts
+        them as .grad without a copy) and drop our references."""
+        out = {k: v for k, v in self.view.items()}
+        self.view = {}
+        return out
+
+
+def _params(*mods):
+    out = []
+    for m in mods:
+        out.extend(m.parameters())
+    return out
+
+
+# ---------------------------------------------------------------------------
+# SimpleUNet (07:75-120)
+
+def _conv3(wc, dt, conv, x1, x2, n, h, w, act, need_bwd, stats=False):
+    pk = wc.conv(conv.weight, dt, dgrad=need_bwd)
+    y, _, st = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, pk[0], conv.weight.shape[0],
+                         bias=conv.bias, act=act, stats=stats)
+    return y, pk, st
+
+
+def _convT_up(wc, dt, conv, x, n, h, w, need_bwd):
+    pk = wc.convT(conv.weight, dt, down=need_bwd)
+    cout = conv.weight.shape[1]
+    y, _, _ = ops.igemm(RR_CONVT_UP, x, None, n, h, w, pk[0], 4 * cout, bias=wc.bias4(conv.bias))
+    return y, pk
+
+
+def simple_unet_forward(m, x, wc, dt, need_bwd):
+    n, _, H, W = x.shape
+    S = Bag(n=n, H=H, W=W, x=x)
+    e1a = ops.conv_in_fwd(x, m.enc1[0].weight, m.enc1[0].bias, dt, act=RELU)
+    e1, pk12, _ = _conv3(wc, dt, m.enc1[2], e1a, None, n, H, W, RELU, need_bwd)
+    p1, i1 = ops.maxpool2_fwd(e1)
+    H2, W2 = H // 2, W // 2
+    e2a, pk20, _ = _conv3(wc, dt, m.enc2[0], p1, None, n, H2, W2, RELU, need_bwd)
+    e2, pk22, _ = _conv3(wc, dt, m.enc2[2], e2a, None, n, H2, W2, RELU, need_bwd)
+    p2, i2 = ops.maxpool2_fwd(e2)
+    H4, W4 = H2 // 2, W2 // 2
+    ba, pkb0, _ = _conv3(wc, dt, m.bottleneck[0], p2, None, n, H4, W4, RELU, need_bwd)
+    b, pkb2, _ = _conv3(wc, dt, m.bottleneck[2], ba, None, n, H4, W4, RELU, need_bwd)
+    u2, pku2 = _convT_up(wc, dt, m.up2, b, n, H4, W4, need_bwd)
+    d2a, pkd20, _ = _conv3(wc, dt, m.dec2[0], u2, e2, n, H2, W2, RELU, need_bwd)   # cat(up, skip)
+    d2, pkd22, _ = _conv3(wc, dt, m.dec2[2], d2a, None, n, H2, W2, RELU, need_bwd)
+    u1, pku1 = _convT_up(wc, dt, m.up1, d2, n, H2, W2, need_bwd)
+    d1a, pkd10, _ = _conv3(wc, dt, m.dec1[0], u1, e1, n, H, W, RELU, need_bwd)
+    d1, pkd12, _ = _conv3(wc, dt, m.dec1[2], d1a, None, n, H, W, RELU, need_bwd)
+    out = ops.conv_out_fwd(d1, m.final.weight, m.final.bias)
+    if need_bwd:
+        S.update(e1a=e1a, e1=e1, p1=p1, i1=i1, e2a=e2a, e2=e2, p2=p2, i2=i2, ba=ba, b=b, u2=u2,
+                 d2a=d2a, d2=d2, u1=u1, d1a=d1a, d1=d1, pk12=pk12, pk20=pk20, pk22=pk22,
+                 pkb0=pkb0, pkb2=pkb2, pku2=pku2, pkd20=pkd20, pkd22=pkd22, pku1=pku1,
+                 pkd10=pkd10, pkd12=pkd12)
+    return out, S
+
+
+def simple_unet_grad_order(m):
+    return _params(m.final, m.dec1, m.up1, m.dec2, m.up2, m.bottleneck, m.enc2, m.enc1)
+
+
+def _conv3_bwd(conv, pk, gpre, xin1, xin2, n, h, w, sink, mask=None, want_dx=True, split=0):
+    """grads of a 3x3 conv given the pre-activation grad: dW, db, dx."""
+    cout = conv.weight.shape[0]
+    ops.wgrad(RR_CONV3X3, gpre, xin1, xin2, n, h, w, cout, dw=sink[conv.weight])
+    ops.channel_sum(gpre, out=sink[conv.bias])
+    if not want_dx:
+        return None, None
+    cin = conv.weight.shape[1]
+    y1, y2, _ = ops.igemm(RR_CONV3X3, gpre, None, n, h, w, pk[1], cin, mask=mask, split=split)
+    return y1, y2
+
+
+def _convT_bwd(conv, pk, gu, xin, n, h, w, sink, mask=None):
+    """ConvTranspose2d(k2,s2) backward: gu on the (2h, 2w) grid; xin [n,h,w,cin]."""
+    cin, cout = conv.weight.shape[0], conv.weight.shape[1]
+    ops.wgrad(RR_CONVT_UP, gu, xin, None, n, h, w, cout, dw=sink[conv.weight])
+    ops.channel_sum(gu, out=sink[conv.bias])
+    gx, _, _ = ops.igemm(RR_CONVT_DOWN, gu, None, n, h, w, pk[1], cin, mask=mask)
+    return gx
+
+
+def simple_unet_backward(m, S, g_out, sink):
+    n, H, W = S.n, S.H, S.W
+    H2, W2, H4, W4 = H // 2, W // 2, H // 4, W // 4
+    g_d1, _, _ = ops.conv_out_bwd(g_out, S.d1, m.final.weight, mask_relu=True,
+                                  dw=sink[m.final.weight], db=sink[m.final.bias])
+    sink.ready(_params(m.final))
+    g_d1a, _ = _conv3_bwd(m.dec1[2], S.pkd12, g_d1, S.d1a, None, n, H, W, sink, mask=S.d1a)
+    g_u1, g_e1 = _conv3_bwd(m.dec1[0], S.pkd10, g_d1a, S.u1, S.e1, n, H, W, sink,
+                            split=m.dec1[0].weight.shape[1] // 2)
+    sink.ready(_params(m.dec1))
+    g_d2 = _convT_bwd(m.up1, S.pku1, g_u1, S.d2, n, H2, W2, sink, mask=S.d2)
+    sink.ready(_params(m.up1))
+    g_d2a, _ = _conv3_bwd(m.dec2[2], S.pkd22, g_d2, S.d2a, None, n, H2, W2, sink, mask=S.d2a)
+    g_u2, g_e2 = _conv3_bwd(m.dec2[0], S.pkd20, g_d2a, S.u2, S.e2, n, H2, W2, sink,
+                            split=m.dec2[0].weight.shape[1] // 2)
+    sink.ready(_params(m.dec2))
+    g_b = _convT_bwd(m.up2, S.pku2, g_u2, S.b, n, H4, W4, sink, mask=S.b)
+    sink.ready(_params(m.up2))
+    g_ba, _ = _conv3_bwd(m.bottleneck[2], S.pkb2, g_b, S.ba, None, n, H4, W4, sink, mask=S.ba)
+    g_p2, _ = _conv3_bwd(m.bottleneck[0], S.pkb0, g_ba, S.p2, None, n, H4, W4, sink)
+    sink.ready(_params(m.bottleneck))
+    ops.maxpool2_bwd(g_p2, S.i2, H2, W2, out=g_e2, accumulate=True, mask=S.e2)
+    g_e2a, _ = _conv3_bwd(m.enc2[2], S.pk22, g_e2, S.e2a, None, n, H2, W2, sink, mask=S.e2a)
+    g_p1, _ = _conv3_bwd(m.enc2[0], S.pk20, g_e2a, S.p1, None, n, H2, W2, sink)
+    sink.ready(_params(m.enc2))
+    ops.maxpool2_bwd(g_p1, S.i1, H, W, out=g_e1, accumulate=True, mask=S.e1)
+    g_e1a, _ = _conv3_bwd(m.enc1[2], S.pk12, g_e1, S.e1a, None, n, H, W, sink, mask=S.e1a)
+    ops.conv_in_wgrad(S.x, g_e1a, dw=sink[m.enc1[0].weight], db=sink[m.enc1[0].bias])
+    sink.ready(_params(m.enc1))
+
+
+# ---------------------------------------------------------------------------
+# ResidualBlock (14:96-115) and ResUNet (14:117-186)
+
+def _bn_affine(bn, st, bias, count, training):
+    if training:
+        if bn.momentum is None:
+            raise NotImplementedError("BatchNorm2d(momentum=None) is not supported")
+        return ops.bn_finalize(st, count, bias, bn.weight, bn.bias, bn.running_mean,
+                               bn.running_var, bn.momentum, bn.eps, bn.num_batches_tracked)
+    s, b = ops.bn_eval_affine(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
+    return s, b, None, None
+
+
+def block_has_shortcut(blk):
+    return len(blk.shortcut) > 0
+
+
+def resblock_forward(blk, x1, x2, n, h, w, wc, dt, training, need_bwd):
+    cb = blk.conv_block
+    c1, bn1, pr, c2, bn2 = cb[0], cb[1], cb[2], cb[3], cb[4]
+    cout = c1.weight.shape[0]
+    P = n * h * w
+    pk1 = wc.conv(c1.weight, dt, dgrad=need_bwd)
+    t1, _, st1 = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, pk1[0], cout, bias=c1.bias, stats=training)
+    s1, sh1, m1, i1 = _bn_affine(bn1, st1, c1.bias, P, training)
+    a1 = ops.affine_act(t1, s1, sh1, alpha=pr.weight)
+    pk2 = wc.conv(c2.weight, dt, dgrad=need_bwd)
+    t2, _, st2 = ops.igemm(RR_CONV3X3, a1, None, n, h, w, pk2[0], cout, bias=c2.bias, stats=training)
+    s2, sh2, m2, i2 = _bn_affine(bn2, st2, c2.bias, P, training)
+    S = Bag(x1=x1, x2=x2, n=n, h=h, w=w)
+    if block_has_shortcut(blk):
+        sc0, sc1 = blk.shortcut[0], blk.shortcut[1]
+        pks = wc.conv(sc0.weight, dt, dgrad=need_bwd)
+        s, _, sts = ops.igemm(RR_CONV1X1, x1, x2, n, h, w, pks[0], cout, bias=sc0.bias,
+                              stats=training)
+        ss, shs, ms, is_ = _bn_affine(sc1, sts, sc0.bias, P, training)
+        out = ops.affine_act(t2, s2, sh2, res=s, res_scale=ss, res_shift=shs, relu=True)
+        if need_bwd:
+            S.update(s=s, ms=ms, is_=is_, pks=pks)
+    else:
+        if x2 is not None:
+            raise RuntimeError("identity shortcut with a concatenated input")
+        out = ops.affine_act(t2, s2, sh2, res=x1, relu=True)
+    if need_bwd:
+        S.update(t1=t1, a1=a1, t2=t2, out=out, s1=s1, sh1=sh1, m1=m1, i1=i1, m2=m2, i2=i2,
+                 pk1=pk1, pk2=pk2)
+    return out, S
+
+
+def resblock_zero_grad_params(blk):
+    """conv biases followed by a train-mode BN: exactly-zero gradients."""
+    z = [blk.conv_block[0].bias, blk.conv_block[3].bias]
+    if block_has_shortcut(blk):
+        z.append(blk.shortcut[0].bias)
+    return z
+
+
+def resblock_backward(blk, S, g_out, sink):
+    cb = blk.conv_block
+    c1, bn1, pr, c2, bn2 = cb[0], cb[1], cb[2], cb[3], cb[4]
+    n, h, w = S.n, S.h, S.w
+    cout = c1.weight.shape[0]
+    x1, x2 = S.x1, S.x2
+    c_in1 = x1.shape[-1]
+    c_in2 = x2.shape[-1] if x2 is not None else 0
+    cin = c_in1 + c_in2
+    has_sc = block_has_shortcut(blk)
+    gx1 = gx2 = None
+    if has_sc:
+        sc0, sc1 = blk.shortcut[0], blk.shortcut[1]
+        r = ops.bn_backward(g_out, S.t2, S.m2, S.i2, bn2.weight, mask_kind=1, aux=S.out,
+                            t1=S.s, mean1=S.ms, inv1=S.is_, gamma1=sc1.weight,
+                            outs=dict(dgamma0=sink[bn2.weight], dbeta0=sink[bn2.bias],
+                                      dgamma1=sink[sc1.weight], dbeta1=sink[sc1.bias]))
+        dt2, ds = r["dt0"], r["dt1"]
+    else:
+        gx1 = torch.empty_like(x1)
+        r = ops.bn_backward(g_out, S.t2, S.m2, S.i2, bn2.weight, mask_kind=1, aux=S.out,
+                            want_gm=True, gm_out=gx1,
+                            outs=dict(dgamma0=sink[bn2.weight], dbeta0=sink[bn2.bias]))
+        dt2 = r["dt0"]
+    ops.wgrad(RR_CONV3X3, dt2, S.a1, None, n, h, w, cout, dw=sink[c2.weight])
+    da1, _, _ = ops.igemm(RR_CONV3X3, dt2, None, n, h, w, S.pk2[1], cout)
+    r1 = ops.bn_backward(da1, S.t1, S.m1, S.i1, bn1.weight, mask_kind=2, aux=S.t1, aff_s=S.s1,
+                         aff_b=S.sh1, alpha=pr.weight,
+                         outs=dict(dgamma0=sink[bn1.weight], dbeta0=sink[bn1.bias],
+                                   dalpha=sink[pr.weight]))
+    dt1 = r1["dt0"]
+    ops.wgrad(RR_CONV3X3, dt1, x1, x2, n, h, w, cout, dw=sink[c1.weight])
+    split = c_in1 if c_in2 else 0
+    if has_sc:
+        ops.wgrad(RR_CONV1X1, ds, x1, x2, n, h, w, cout, dw=sink[sc0.weight])
+        gx1, gx2, _ = ops.igemm(RR_CONV3X3, dt1, None, n, h, w, S.pk1[1], cin, split=split)
+        ops.igemm(RR_CONV1X1, ds, None, n, h, w, S.pks[1], cin, out=gx1, out2=gx2, split=split,
+                  accumulate=True)
+    else:
+        ops.igemm(RR_CONV3X3, dt1, None, n, h, w, S.pk1[1], cin, out=gx1, accumulate=True)
+    sink.ready(_params(blk))
+    return gx1, gx2
+
+
+def resunet_block_names():
+    return ["res1", "res2", "res3", "bottleneck.0", "bottleneck.1", "bottleneck.2", "dec3", "dec2",
+            "dec1"]
+
+
+def resunet_forward(m, x, wc, dt, training, need_bwd):
+    n, _, H, W = x.shape
+    if H % 8 or W % 8:
+        raise NotImplementedError(
+            "ResUNet input sizes must be multiples of 8 (the reference's F.interpolate "
+            "alignment branch, 14:169-182, is not implemented on this path)")
+    S = Bag(n=n, H=H, W=W, x=x)
+    pr = m.enc1[1]
+    if need_bwd:
+        e1pre = ops.conv_in_fwd(x, m.enc1[0].weight, m.enc1[0].bias, dt, act=0)
+        one, zero = _unit_affine(64, x.device)
+        e1 = ops.affine_act(e1pre, one, zero, alpha=pr.weight)
+        S.e1pre = e1pre
+    else:
+        e1 = ops.conv_in_fwd(x, m.enc1[0].weight, m.enc1[0].bias, dt, act=2, alpha=pr.weight)
+    r1, S.res1 = resblock_forward(m.res1, e1, None, n, H, W, wc, dt, training, need_bwd)
+    p1, i1 = ops.maxpool2_fwd(r1)
+    r2, S.res2 = resblock_forward(m.res2, p1, None, n, H // 2, W // 2, wc, dt, training, need_bwd)
+    p2, i2 = ops.maxpool2_fwd(r2)
+    r3, S.res3 = resblock_forward(m.res3, p2, None, n, H // 4, W // 4, wc, dt, training, need_bwd)
+    p3, i3 = ops.maxpool2_fwd(r3)
+    b = p3
+    for i in range(3):
+        b, S[f"bottleneck.{i}"] = resblock_forward(m.bottleneck[i], b, None, n, H // 8, W // 8, wc,
+                                                   dt, training, need_bwd)
+    u3, pku3 = _convT_up(wc, dt, m.up3, b, n, H // 8, W // 8, need_bwd)
+    d3, S.dec3 = resblock_forward(m.dec3, u3, r3, n, H // 4, W // 4, wc, dt, training, need_bwd)
+    u2, pku2 = _convT_up(wc, dt, m.up2, d3, n, H // 4, W // 4, need_bwd)
+    d2, S.dec2 = resblock_forward(m.dec2, u2, r2, n, H // 2, W // 2, wc, dt, training, need_bwd)
+    u1, pku1 = _convT_up(wc, dt, m.up1, d2, n, H // 2, W // 2, need_bwd)
+    d1, S.dec1 = resblock_forward(m.dec1, u1, r1, n, H, W, wc, dt, training, need_bwd)
+    out = ops.conv_out_fwd(d1, m.final.weight, m.final.bias)
+    if need_bwd:
+        S.update(e1=e1, r1=r1, r2=r2, r3=r3, i1=i1, i2=i2, i3=i3, b=b, d3=d3, d2=d2, d1=d1,
+                 pku3=pku3, pku2=pku2, pku1=pku1)
+    return out, S
+
+
+_UNIT = {}
+
+
+def _unit_affine(C, device):
+    key = (C, str(device))
+    if key not in _UNIT:
+        _UNIT[key] = (torch.ones(C, device=device), torch.zeros(C, device=device))
+    return _UNIT[key]
+
+
+def resunet_grad_order(m):
+    return _params(m.final, m.dec1, m.up1, m.dec2, m.up2, m.dec3, m.up3, m.bottleneck[2],
+                   m.bottleneck[1], m.bottleneck[0], m.res3, m.res2, m.res1, m.enc1)
+
+
+def resunet_zero_grad_params(m):
+    z = []
+    for name in resunet_block_names():
+        z.extend(resblock_zero_grad_params(m.get_submodule(name)))
+    return z
+
+
+def resunet_backward(m, S, g_out, sink):
+    n, H, W = S.n, S.H, S.W
+    g_d1, _, _ = ops.conv_out_bwd(g_out, S.d1, m.final.weight, mask_relu=False,
+                                  dw=sink[m.final.weight], db=sink[m.final.bias])
+    sink.ready(_params(m.final))
+    g_u1, g_r1 = resblock_backward(m.dec1, S.dec1, g_d1, sink)
+    g_d2 = _convT_bwd(m.up1, S.pku1, g_u1, S.d2, n, H // 2, W // 2, sink)
+    sink.ready(_params(m.up1))
+    g_u2, g_r2 = resblock_backward(m.dec2, S.dec2, g_d2, sink)
+    g_d3 = _convT_bwd(m.up2, S.pku2, g_u2, S.d3, n, H // 4, W // 4, sink)
+    sink.ready(_params(m.up2))
+    g_u3, g_r3 = resblock_backward(m.dec3, S.dec3, g_d3, sink)
+    g_b = _convT_bwd(m.up3, S.pku3, g_u3, S.b, n, H // 8, W // 8, sink)
+    sink.ready(_params(m.up3))
+    for i in (2, 1, 0):
+        g_b, _ = resblock_backward(m.bottleneck[i], S[f"bottleneck.{i}"], g_b, sink)
+    ops.maxpool2_bwd(g_b, S.i3, H // 4, W // 4, out=g_r3, accumulate=True)
+    g_p2, _ = resblock_backward(m.res3, S.res3, g_r3, sink)
+    ops.maxpool2_bwd(g_p2, S.i2, H // 2, W // 2, out=g_r2, accumulate=True)
+    g_p1, _ = resblock_backward(m.res2, S.res2, g_r2, sink)
+    ops.maxpool2_bwd(g_p1, S.i1, H, W, out=g_r1, accumulate=True)
+    g_e1, _ = resblock_backward(m.res1, S.res1, g_r1, sink)
+    pr = m.enc1[1]
+    g_e1pre, _ = ops.prelu_bwd(g_e1, S.e1pre, pr.weight, dalpha=sink[pr.weight])
+    ops.conv_in_wgrad(S.x, g_e1pre, dw=sink[m.enc1[0].weight], db=sink[m.enc1[0].bias])
+    sink.ready(_params(m.enc1))
+
+
+# ---------------------------------------------------------------------------
+# VGG16 features (torchvision cfg D) -- perceptual slice and classifier trunk
+
+def vgg_layers(features, upto=None):
+    """[(kind, module)] of features[:upto]; ReLU after each conv is fused."""
+    mods = list(features)
+    if upto is not None:
+        mods = mods[:upto]
+    out = []
+    for mod in mods:
+        name = type(mod).__name__
+        if name == "Conv2d":
+            out.append(("conv", mod))
+        elif name == "MaxPool2d":
+            out.append(("pool", mod))
+        elif name == "ReLU":
+            if not out or out[-1][0] != "conv":
+                raise RuntimeError("unsupported VGG layer order")
+            out[-1] = ("conv_relu", out[-1][1])
+        else:
+            raise RuntimeError(f"unsupported VGG feature layer {name}")
+    return out
+
+
+def vgg_features_forward(features, x, wc, dt, upto=None, need_bwd=False):
+    """x: NCHW fp32 image.  Returns NHWC features and the saved state."""
+    n, _, H, W = x.shape
+    layers = vgg_layers(features, upto)
+    S = Bag(n=n, H=H, W=W, acts=[], layers=layers)
+    h, w = H, W
+    cur = None
+    for li, (kind, mod) in enumerate(layers):
+        if kind in ("conv", "conv_relu"):
+            act = RELU if kind == "conv_relu" else 0
+            if cur is None:
+                y = ops.conv_in_fwd(x, mod.weight, mod.bias, dt, act=act)
+                pk = None
+            else:
+                pk = wc.conv(mod.weight, dt, dgrad=need_bwd)
+                y, _, _ = ops.igemm(RR_CONV3X3, cur, None, n, h, w, pk[0], mod.weight.shape[0],
+                                    bias=mod.bias, act=act)
+            S.acts.append((kind, mod, cur, pk, h, w, None))
+            cur = y
+        else:
+            y, idx = ops.maxpool2_fwd(cur)
+            S.acts.append((kind, mod, cur, None, h, w, idx))
+            h, w = h // 2, w // 2
+            cur = y
+    S.out = cur
+    return cur, S
+
+
+def vgg_features_backward_input(S, g_pre_last, x_grad_out=None, accumulate=False):
+    """Input (image) gradient of the frozen features: dgrad only, no wgrad.
+
+    g_pre_last is the gradient at the PRE-activation of the last layer if it is
+    a conv_relu (the caller folds the last ReLU mask in).  Returns the NCHW
+    fp32 image grad (accumulated into x_grad_out if given)."""
+    g = g_pre_last
+    acts = S.acts
+    for li in range(len(acts) - 1, -1, -1):
+        kind, mod, xin, pk, h, w, idx = acts[li]
+        if kind == "pool":
+            # input of the pool is the previous layer's (relu) output
+            prev_relu = li > 0 and acts[li - 1][0] == "conv_relu"
+            g = ops.maxpool2_bwd(g, idx, h, w, mask=xin if prev_relu else None)
+            continue
+        if xin is None:   # first layer: image grad
+            cin = mod.weight.shape[1]
+            return ops.conv_in_dgrad(g, mod.weight, cin, out=x_grad_out, accumulate=accumulate)
+        prev_relu = acts[li - 1][0] == "conv_relu"
+        g, _, _ = ops.igemm(RR_CONV3X3, g, None, S.n, h, w, pk[1], mod.weight.shape[1],
+                            mask=xin if prev_relu else None)
+    raise RuntimeError("unreachable")
+
+
+def vgg_classifier_forward(vgg, x, wc, dt):
+    """Eval-mode VGG16 logits (Dropout = identity): 18:46."""
+    f, _ = vgg_features_forward(vgg.features, x, wc, dt)
+    n = x.shape[0]
+    pooled = ops.adaptive_avgpool_flatten(f, 7, 7)        # [n, 25088] (NCHW flatten)
+    h = pooled.view(n, 1, 1, -1)
+    cls = [m for m in vgg.classifier if type(m).__name__ == "Linear"]
+    for i, lin in enumerate(cls):
+        pk = wc.linear(lin.weight, dt)
+        last = i == len(cls) - 1
+        h, _, _ = ops.igemm(RR_CONV1X1, h, None, n, 1, 1, pk[0], lin.weight.shape[0],
+                            bias=lin.bias, act=0 if last else RELU)
+    return h.view(n, -1)

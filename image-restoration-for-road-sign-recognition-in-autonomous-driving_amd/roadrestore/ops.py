@@ -1,0 +1,450 @@
+"""Tensor-level wrappers over the C ABI (one launch each, current HIP stream).
+
+Activations are NHWC tensors ([N, H, W, C] contiguous) in the compute dtype
+(torch.float32 or torch.bfloat16).  Every wrapper allocates its outputs from
+the PyTorch caching allocator (PyTorch is plumbing here: device memory and
+streams) and launches exactly one C-ABI entry point.  No op has a PyTorch or
+CPU fallback: a missing library or device raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from ._lib import (RR_BF16, RR_F32, RR_CONV1X1, RR_CONV3X3, RR_CONVT_DOWN, RR_CONVT_UP,
+                   BnBwdDesc, IgemmDesc, WgradDesc, lib)
+
+__all__ = [
+    "rr_dtype", "stream", "pack_conv", "pack_convT", "bias_tile4", "igemm", "wgrad",
+    "bn_finalize", "bn_eval_affine", "affine_act", "bn_backward", "channel_sum",
+    "maxpool2_fwd", "maxpool2_bwd", "conv_in_fwd", "conv_in_wgrad", "conv_in_dgrad",
+    "prelu_bwd", "conv_out_fwd", "conv_out_bwd", "nchw_to_nhwc", "nhwc_to_nchw",
+    "loss_fwd", "loss_bwd", "adamw_", "to_uint8_hwc", "psnr_u8", "argmax_rows",
+    "adaptive_avgpool_flatten", "zero_",
+]
+
+
+def rr_dtype(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return RR_F32
+    if dt == torch.bfloat16:
+        return RR_BF16
+    raise TypeError(f"unsupported compute dtype {dt}")
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _need_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("roadrestore ops need device tensors (no CPU fallback)")
+
+
+# Optional launch probe (bench.py): probe(kernel_symbol, algorithmic_flops, launch_fn)
+PROBE = None
+
+
+def _kpick_bc(mode, n, h, w, cout, split):
+    """Mirror of csrc/igemm.hip pick_bc (for naming the template instance)."""
+    P = n * h * w
+    pb = (P + 127) // 128
+    if cout % 128 == 0 and pb * (cout // 128) >= 512 and (split == 0 or split % 128 == 0):
+        return 128
+    return 64
+
+
+def _ws(nbytes, device):
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+# ---------------------------------------------------------------------------
+# weights
+
+def pack_conv(w: torch.Tensor, dtype: torch.dtype, fwd=True, dgrad=True):
+    """fp32 [co][ci][k][k] -> (fwd [co][k*k][ci], dgrad [ci][k*k flipped][co])."""
+    _need_cuda(w)
+    co, ci, k, _ = w.shape
+    wf = torch.empty(co * k * k * ci, dtype=dtype, device=w.device) if fwd else None
+    wd = torch.empty(co * k * k * ci, dtype=dtype, device=w.device) if dgrad else None
+    lib().check(lib().rr_pack_conv(rr_dtype(dtype), co, ci, k, _p(w.contiguous()), _p(wf),
+                                   _p(wd), stream()), "rr_pack_conv")
+    return wf, wd
+
+
+def pack_convT(w: torch.Tensor, dtype: torch.dtype, up=True, down=True):
+    """fp32 [ci][co][2][2] -> (up [tap*co][ci], down [ci][tap][co])."""
+    _need_cuda(w)
+    ci, co = w.shape[0], w.shape[1]
+    wu = torch.empty(4 * co * ci, dtype=dtype, device=w.device) if up else None
+    wd = torch.empty(4 * co * ci, dtype=dtype, device=w.device) if down else None
+    lib().check(lib().rr_pack_convT(rr_dtype(dtype), ci, co, _p(w.contiguous()), _p(wu), _p(wd),
+                                    stream()), "rr_pack_convT")
+    return wu, wd
+
+
+def bias_tile4(b: torch.Tensor):
+    out = torch.empty(4 * b.numel(), dtype=torch.float32, device=b.device)
+    lib().check(lib().rr_bias_tile4(b.numel(), _p(b), _p(out), stream()), "rr_bias_tile4")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# implicit GEMM
+
+def igemm(mode, x1, x2, n, h, w, wpack, cout, bias=None, act=0, out=None, out2=None,
+          split=0, accumulate=False, mask=None, stats=False):
+    """Run rr_igemm.  Returns (y1, y2, stats_partial_or_None).
+
+    mode RR_CONV3X3 / RR_CONV1X1: y [n, h, w, cout]
+    mode RR_CONVT_UP: GEMM columns 4*cout_t, y [n, 2h, 2w, cout/4]
+    mode RR_CONVT_DOWN: x1 on the (2h, 2w) grid, y [n, h, w, cout]
+    """
+    _need_cuda(x1, wpack)
+    dt = x1.dtype
+    c1 = x1.shape[-1]
+    c2 = x2.shape[-1] if x2 is not None else 0
+    d = IgemmDesc(rr_dtype(dt), mode, n, h, w, c1, c2, cout, split, act, int(accumulate),
+                  int(bias is not None), int(mask is not None), int(stats))
+    dev = x1.device
+    if out is None:
+        if mode == RR_CONVT_UP:
+            out = torch.empty((n, 2 * h, 2 * w, cout // 4), dtype=dt, device=dev)
+        elif split:
+            out = torch.empty((n, h, w, split), dtype=dt, device=dev)
+        else:
+            out = torch.empty((n, h, w, cout), dtype=dt, device=dev)
+    if split and out2 is None:
+        out2 = torch.empty((n, h, w, cout - split), dtype=dt, device=dev)
+    st = None
+    if stats:
+        blocks = lib().rr_igemm_stat_blocks(C.byref(d))
+        st = torch.empty((blocks, cout, 2), dtype=torch.float32, device=dev)
+    def launch():
+        lib().check(lib().rr_igemm(C.byref(d), _p(x1), _p(x2), _p(wpack), _p(bias), _p(out),
+                                   _p(out2), _p(mask), _p(st), stream()), "rr_igemm")
+    if PROBE is None:
+        launch()
+    else:
+        taps = 9 if mode == RR_CONV3X3 else (4 if mode == RR_CONVT_DOWN else 1)
+        bc = _kpick_bc(mode, n, h, w, cout, split)
+        sym = f"igemm_kernel<{'bf16' if dt == torch.bfloat16 else 'f32'},{bc},128,mode{mode}>"
+        PROBE(sym, 2.0 * n * h * w * cout * taps * (c1 + c2), launch)
+    return out, out2, st
+
+
+def wgrad(mode, dy, x1, x2, n, h, w, cout, dw=None, accumulate=False, dw_shape=None):
+    """Weight grad (fp32, torch layout) of a conv / convT; see rr_wgrad."""
+    _need_cuda(dy, x1)
+    c1 = x1.shape[-1]
+    c2 = x2.shape[-1] if x2 is not None else 0
+    d = WgradDesc(rr_dtype(dy.dtype), mode, n, h, w, c1, c2, cout, int(accumulate))
+    if dw is None:
+        dw = torch.empty(dw_shape, dtype=torch.float32, device=dy.device)
+    need = lib().rr_wgrad_workspace(C.byref(d))
+    ws = _ws(need, dy.device)
+
+    def launch():
+        lib().check(lib().rr_wgrad(C.byref(d), _p(dy), _p(x1), _p(x2), _p(dw), _p(ws),
+                                   ws.numel(), stream()), "rr_wgrad")
+    if PROBE is None:
+        launch()
+    else:
+        taps = 9 if mode == RR_CONV3X3 else (4 if mode == RR_CONVT_UP else 1)
+        convT = mode == RR_CONVT_UP
+        CA = c1 if convT else cout
+        CB = cout if convT else c1 + c2
+        ba = 128 if CA % 128 == 0 else 64
+        bb = 128 if (CB % 128 == 0 and (cout if convT else c1) % 128 == 0 and c2 % 128 == 0) else 64
+        sym = f"wgrad_kernel<{'bf16' if dy.dtype == torch.bfloat16 else 'f32'},{ba},{bb},mode{mode}>"
+        PROBE(sym, 2.0 * CA * CB * taps * n * h * w, launch)
+    return dw
+
+
+# ---------------------------------------------------------------------------
+# batch norm
+
+def bn_finalize(st, count, bias, gamma, beta, running_mean, running_var, momentum=0.1,
+                eps=1e-5, num_batches_tracked=None):
+    blocks, Cc = st.shape[0], st.shape[1]
+    dev = st.device
+    scale = torch.empty(Cc, dtype=torch.float32, device=dev)
+    shift = torch.empty_like(scale)
+    mean = torch.empty_like(scale)
+    inv = torch.empty_like(scale)
+    lib().check(lib().rr_bn_finalize(Cc, blocks, int(count), _p(st), _p(bias), _p(gamma), _p(beta),
+                                     _p(running_mean), _p(running_var), float(momentum),
+                                     float(eps), _p(scale), _p(shift), _p(mean), _p(inv),
+                                     _p(num_batches_tracked), stream()), "rr_bn_finalize")
+    return scale, shift, mean, inv
+
+
+def bn_eval_affine(gamma, beta, running_mean, running_var, eps=1e-5):
+    Cc = running_mean.numel()
+    scale = torch.empty(Cc, dtype=torch.float32, device=running_mean.device)
+    shift = torch.empty_like(scale)
+    lib().check(lib().rr_bn_eval_affine(Cc, _p(gamma), _p(beta), _p(running_mean),
+                                        _p(running_var), float(eps), _p(scale), _p(shift),
+                                        stream()), "rr_bn_eval_affine")
+    return scale, shift
+
+
+def affine_act(x, scale, shift, alpha=None, res=None, res_scale=None, res_shift=None, relu=False,
+               out=None):
+    _need_cuda(x)
+    Cc = x.shape[-1]
+    P = x.numel() // Cc
+    if out is None:
+        out = torch.empty_like(x)
+    lib().check(lib().rr_affine_act(rr_dtype(x.dtype), P, Cc, _p(x), _p(scale), _p(shift),
+                                    _p(alpha), _p(res), _p(res_scale), _p(res_shift), int(relu),
+                                    _p(out), stream()), "rr_affine_act")
+    return out
+
+
+def bn_backward(g, t0, mean0, inv0, gamma0, *, mask_kind=0, aux=None, aff_s=None, aff_b=None,
+                alpha=None, t1=None, mean1=None, inv1=None, gamma1=None, want_gm=False,
+                gm_out=None, outs=None):
+    """Full BN backward (reduce + finalize + apply) for one or two BNs that
+    share the upstream gradient.  Returns dict with dt0, dt1, gm, dgamma0,
+    dbeta0, dgamma1, dbeta1, dalpha."""
+    Cc = g.shape[-1]
+    P = g.numel() // Cc
+    nbn = 2 if t1 is not None else 1
+    dev = g.device
+    d = BnBwdDesc(rr_dtype(g.dtype), P, Cc, mask_kind, nbn)
+    blocks = lib().rr_bn_bwd_blocks(C.byref(d))
+    part = torch.empty(blocks * Cc * 3 + blocks, dtype=torch.float32, device=dev)
+    s = stream()
+    lib().check(lib().rr_bn_bwd_reduce(C.byref(d), _p(g), _p(aux), _p(aff_s), _p(aff_b), _p(alpha),
+                                       _p(t0), _p(mean0), _p(inv0), _p(t1), _p(mean1), _p(inv1),
+                                       _p(part), s), "rr_bn_bwd_reduce")
+    o = outs or {}
+    dg0 = o.get("dgamma0")
+    if dg0 is None:
+        dg0 = torch.empty(Cc, dtype=torch.float32, device=dev)
+    db0 = o.get("dbeta0")
+    if db0 is None:
+        db0 = torch.empty_like(dg0)
+    dg1 = o.get("dgamma1")
+    if dg1 is None and nbn == 2:
+        dg1 = torch.empty_like(dg0)
+    db1 = o.get("dbeta1")
+    if db1 is None and nbn == 2:
+        db1 = torch.empty_like(dg0)
+    dal = o.get("dalpha")
+    if dal is None and mask_kind == 2:
+        dal = torch.empty(1, dtype=torch.float32, device=dev)
+    coef = torch.empty(Cc * 6, dtype=torch.float32, device=dev)
+    lib().check(lib().rr_bn_bwd_finalize(C.byref(d), _p(part), _p(gamma0), _p(inv0), _p(gamma1),
+                                         _p(inv1), _p(dg0), _p(db0), _p(dg1), _p(db1), _p(dal),
+                                         _p(coef), s), "rr_bn_bwd_finalize")
+    dt0 = torch.empty_like(g)
+    dt1 = torch.empty_like(g) if nbn == 2 else None
+    if want_gm and gm_out is None:
+        gm_out = torch.empty_like(g)
+    lib().check(lib().rr_bn_bwd_apply(C.byref(d), _p(g), _p(aux), _p(aff_s), _p(aff_b), _p(alpha),
+                                      _p(t0), _p(mean0), _p(inv0), _p(t1), _p(mean1), _p(inv1),
+                                      _p(coef), _p(dt0), _p(dt1), _p(gm_out), s),
+                "rr_bn_bwd_apply")
+    return dict(dt0=dt0, dt1=dt1, gm=gm_out, dgamma0=dg0, dbeta0=db0, dgamma1=dg1, dbeta1=db1,
+                dalpha=dal)
+
+
+def channel_sum(x, out=None, accumulate=False):
+    Cc = x.shape[-1]
+    P = x.numel() // Cc
+    if out is None:
+        out = torch.empty(Cc, dtype=torch.float32, device=x.device)
+    ws = _ws(lib().rr_channel_sum_workspace(P, Cc), x.device)
+    lib().check(lib().rr_channel_sum(rr_dtype(x.dtype), P, Cc, _p(x), _p(out), int(accumulate),
+                                     _p(ws), ws.numel(), stream()), "rr_channel_sum")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# pooling, first / last layers, layout
+
+def maxpool2_fwd(x):
+    n, h, w, Cc = x.shape
+    y = torch.empty((n, h // 2, w // 2, Cc), dtype=x.dtype, device=x.device)
+    idx = torch.empty((n, h // 2, w // 2, Cc), dtype=torch.uint8, device=x.device)
+    lib().check(lib().rr_maxpool2_fwd(rr_dtype(x.dtype), n, h, w, Cc, _p(x), _p(y), _p(idx),
+                                      stream()), "rr_maxpool2_fwd")
+    return y, idx
+
+
+def maxpool2_bwd(dy, idx, h, w, out=None, accumulate=False, mask=None):
+    n, _, _, Cc = dy.shape
+    if out is None:
+        out = torch.empty((n, h, w, Cc), dtype=dy.dtype, device=dy.device)
+    lib().check(lib().rr_maxpool2_bwd(rr_dtype(dy.dtype), n, h, w, Cc, _p(dy), _p(idx), _p(out),
+                                      int(accumulate), _p(mask), stream()), "rr_maxpool2_bwd")
+    return out
+
+
+def conv_in_fwd(x_nchw, wt, b, dtype, act=0, alpha=None):
+    n, cin, h, w = x_nchw.shape
+    cout = wt.shape[0]
+    y = torch.empty((n, h, w, cout), dtype=dtype, device=x_nchw.device)
+    lib().check(lib().rr_conv_in_fwd(rr_dtype(dtype), n, h, w, cin, cout, _p(x_nchw), _p(wt),
+                                     _p(b), act, _p(alpha), _p(y), stream()), "rr_conv_in_fwd")
+    return y
+
+
+def conv_in_wgrad(x_nchw, dy, dw_shape=None, dw=None, db=None):
+    n, cin, h, w = x_nchw.shape
+    cout = dy.shape[-1]
+    if dw is None:
+        dw = torch.empty(dw_shape, dtype=torch.float32, device=dy.device)
+    if db is None:
+        db = torch.empty(cout, dtype=torch.float32, device=dy.device)
+    ws = _ws(lib().rr_conv_in_wgrad_workspace(n, h, w, cin, cout), dy.device)
+    lib().check(lib().rr_conv_in_wgrad(rr_dtype(dy.dtype), n, h, w, cin, cout, _p(x_nchw), _p(dy),
+                                       _p(dw), _p(db), _p(ws), ws.numel(), stream()),
+                "rr_conv_in_wgrad")
+    return dw, db
+
+
+def conv_in_dgrad(dy, wt, cin, out=None, accumulate=False):
+    n, h, w, cout = dy.shape
+    if out is None:
+        out = torch.empty((n, cin, h, w), dtype=torch.float32, device=dy.device)
+    lib().check(lib().rr_conv_in_dgrad(rr_dtype(dy.dtype), n, h, w, cin, cout, _p(dy), _p(wt),
+                                       _p(out), int(accumulate), stream()), "rr_conv_in_dgrad")
+    return out
+
+
+def prelu_bwd(dy, y_pre, alpha, dalpha=None):
+    count = dy.numel()
+    blocks = max(1, min(1024, (count + 4095) // 4096))
+    dx = torch.empty_like(dy)
+    part = torch.empty(blocks, dtype=torch.float32, device=dy.device)
+    if dalpha is None:
+        dalpha = torch.empty(1, dtype=torch.float32, device=dy.device)
+    lib().check(lib().rr_prelu_bwd(rr_dtype(dy.dtype), count, _p(dy), _p(y_pre), _p(alpha),
+                                   _p(dx), _p(part), blocks, _p(dalpha), stream()),
+                "rr_prelu_bwd")
+    return dx, dalpha
+
+
+def conv_out_fwd(x, wt, b):
+    n, h, w, cin = x.shape
+    cout = wt.shape[0]
+    y = torch.empty((n, cout, h, w), dtype=torch.float32, device=x.device)
+    lib().check(lib().rr_conv_out_fwd(rr_dtype(x.dtype), n, h, w, cin, cout, _p(x),
+                                      _p(wt.reshape(cout, cin)), _p(b), _p(y), stream()),
+                "rr_conv_out_fwd")
+    return y
+
+
+def conv_out_bwd(dy_nchw, x, wt, mask_relu=False, want_dx=True, dw=None, db=None):
+    n, h, w, cin = x.shape
+    cout = wt.shape[0]
+    dx = torch.empty_like(x) if want_dx else None
+    if dw is None:
+        dw = torch.empty(wt.shape, dtype=torch.float32, device=x.device)
+    if db is None:
+        db = torch.empty(cout, dtype=torch.float32, device=x.device)
+    ws = _ws(lib().rr_conv_out_bwd_workspace(n, h, w, cin, cout), x.device)
+    lib().check(lib().rr_conv_out_bwd(rr_dtype(x.dtype), n, h, w, cin, cout,
+                                      _p(dy_nchw.contiguous()), _p(x), _p(wt.reshape(cout, cin)),
+                                      _p(dx), int(mask_relu), _p(dw), _p(db), _p(ws), ws.numel(),
+                                      stream()), "rr_conv_out_bwd")
+    return dx, dw, db
+
+
+def nchw_to_nhwc(x, dtype):
+    n, c, h, w = x.shape
+    y = torch.empty((n, h, w, c), dtype=dtype, device=x.device)
+    lib().check(lib().rr_nchw_to_nhwc(rr_dtype(dtype), n, c, h, w, _p(x.contiguous()), _p(y),
+                                      stream()), "rr_nchw_to_nhwc")
+    return y
+
+
+def nhwc_to_nchw(x):
+    n, h, w, c = x.shape
+    y = torch.empty((n, c, h, w), dtype=torch.float32, device=x.device)
+    lib().check(lib().rr_nhwc_to_nchw(rr_dtype(x.dtype), n, c, h, w, _p(x), _p(y), stream()),
+                "rr_nhwc_to_nchw")
+    return y
+
+
+# ---------------------------------------------------------------------------
+# losses / optimiser / post-processing
+
+L1, MSE = 0, 1
+
+
+def loss_fwd(kind, a, b, scale=1.0, out=None, accumulate=False):
+    count = a.numel()
+    if out is None:
+        out = torch.empty((), dtype=torch.float32, device=a.device)
+    ws = _ws(lib().rr_loss_workspace(count), a.device)
+    lib().check(lib().rr_loss_fwd(kind, rr_dtype(a.dtype), count, _p(a), _p(b), _p(out),
+                                  float(scale), int(accumulate), _p(ws), ws.numel(), stream()),
+                "rr_loss_fwd")
+    return out
+
+
+def loss_bwd(kind, a, b, gscale=None, scale=1.0, ga=None, accumulate=False, mask_a_pos=False):
+    if ga is None:
+        ga = torch.empty_like(a)
+    lib().check(lib().rr_loss_bwd(kind, rr_dtype(a.dtype), a.numel(), _p(a), _p(b), _p(gscale),
+                                  float(scale), _p(ga), None, int(accumulate), int(mask_a_pos),
+                                  stream()), "rr_loss_bwd")
+    return ga
+
+
+def adamw_(param, grad, m, v, lr, beta1, beta2, eps, weight_decay, decoupled, step):
+    lib().check(lib().rr_adamw(param.numel(), _p(param), _p(grad), _p(m), _p(v), float(lr),
+                               float(beta1), float(beta2), float(eps), float(weight_decay),
+                               int(decoupled), int(step), stream()), "rr_adamw")
+
+
+def to_uint8_hwc(x_nchw, bgr=False):
+    n, c, h, w = x_nchw.shape
+    out = torch.empty((n, h, w, c), dtype=torch.uint8, device=x_nchw.device)
+    lib().check(lib().rr_to_uint8_hwc(n, c, h, w, _p(x_nchw.contiguous()), _p(out), int(bgr),
+                                      stream()), "rr_to_uint8_hwc")
+    return out
+
+
+def psnr_u8(a, b):
+    n = a.shape[0]
+    per = a.numel() // n
+    out = torch.empty(n, dtype=torch.float64, device=a.device)
+    lib().check(lib().rr_psnr_u8(n, per, _p(a.contiguous()), _p(b.contiguous()), _p(out),
+                                 stream()), "rr_psnr_u8")
+    return out
+
+
+def argmax_rows(logits):
+    n, k = logits.shape
+    out = torch.empty(n, dtype=torch.int64, device=logits.device)
+    lib().check(lib().rr_argmax_rows(n, k, _p(logits.contiguous()), _p(out), stream()),
+                "rr_argmax_rows")
+    return out
+
+
+def adaptive_avgpool_flatten(x, oh=7, ow=7):
+    n, h, w, Cc = x.shape
+    y = torch.empty((n, Cc * oh * ow), dtype=x.dtype, device=x.device)
+    lib().check(lib().rr_adaptive_avgpool_flatten(rr_dtype(x.dtype), n, h, w, Cc, oh, ow, _p(x),
+                                                  _p(y), stream()), "rr_adaptive_avgpool_flatten")
+    return y
+
+
+def zero_(t):
+    lib().check(lib().rr_zero(_p(t), t.numel() * t.element_size(), stream()), "rr_zero")
+    return t
+
+
+MODES = dict(conv3x3=RR_CONV3X3, conv1x1=RR_CONV1X1, convT_up=RR_CONVT_UP,
+             convT_down=RR_CONVT_DOWN)

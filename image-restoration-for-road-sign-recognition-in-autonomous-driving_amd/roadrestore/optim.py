@@ -1,0 +1,134 @@
+"""Fused Adam / AdamW (one HIP launch per contiguous parameter span).
+
+Update rule = torch.optim.Adam / AdamW (the reference's optimisers, 07:143 and
+14:222): decoupled weight decay p *= 1 - lr*wd (AdamW), m.lerp_(g, 1-b1),
+v = b2 v + (1-b2) g^2, p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps).
+
+When the parameters (``flatten_parameters``) and their gradients (written by
+the network's backward into one flat buffer in the same order) each tile one
+contiguous span, a step is a single kernel over every parameter; otherwise
+one launch per parameter.  The learning-rate schedule is host arithmetic:
+torch.optim.lr_scheduler.CosineAnnealingLR works unchanged (14:223, 248).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+from ._lib import lib
+
+CosineAnnealingLR = torch.optim.lr_scheduler.CosineAnnealingLR
+
+
+def flatten_parameters(model, order=None):
+    """Re-home ``model``'s parameters into one contiguous fp32 buffer laid out
+    in ``order`` (default: the network's gradient layout), so the fused
+    optimiser updates all of them with one launch.  Values are preserved."""
+    if order is None:
+        order = model.grad_layout() if hasattr(model, "grad_layout") else list(model.parameters())
+    total = sum(p.numel() for p in order)
+    dev = order[0].device
+    flat = torch.empty(total, dtype=torch.float32, device=dev)
+    off = 0
+    with torch.no_grad():
+        for p in order:
+            n = p.numel()
+            flat[off:off + n].copy_(p.detach().reshape(-1))
+            p.data = flat[off:off + n].view(p.shape)
+            off += n
+    model._rr_flat_params = flat
+    return flat
+
+
+def _span(tensors):
+    """Sorted [(ptr, tensor)] if the tensors tile one contiguous fp32 span."""
+    if not tensors:
+        return None
+    items = sorted(((t.data_ptr(), i) for i, t in enumerate(tensors)))
+    exp = items[0][0]
+    for ptr, i in items:
+        t = tensors[i]
+        if ptr != exp or not t.is_contiguous() or t.dtype != torch.float32:
+            return None
+        exp += t.numel() * 4
+    return items
+
+
+class _FusedAdamBase(torch.optim.Optimizer):
+    decoupled = True
+
+    def __init__(self, params, lr, betas, eps, weight_decay):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        super().__init__(params, defaults)
+        self._gstate = {}
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            ps = [p for p in group["params"] if p.grad is not None]
+            if not ps:
+                continue
+            if any(not p.is_cuda for p in ps):
+                raise RuntimeError("fused Adam/AdamW runs on the GPU only")
+            b1, b2 = group["betas"]
+            gstate = self._gstate.setdefault(self.param_groups.index(group), {})
+            gstate["step"] = gstate.get("step", 0) + 1
+            step = gstate["step"]
+            pspan = _span([p.data for p in ps])
+            gspan = _span([p.grad for p in ps]) if pspan is not None else None
+            flat_ok = (pspan is not None and gspan is not None and
+                       [i for _, i in pspan] == [i for _, i in gspan])
+            if flat_ok:
+                key = tuple(id(ps[i]) for _, i in pspan)
+                if gstate.get("key") != key:
+                    total = sum(p.numel() for p in ps)
+                    gstate["m"] = torch.zeros(total, dtype=torch.float32, device=ps[0].device)
+                    gstate["v"] = torch.zeros_like(gstate["m"])
+                    gstate["key"] = key
+                    off = 0
+                    for _, i in pspan:
+                        p = ps[i]
+                        st = self.state.setdefault(p, {})
+                        st["exp_avg"] = gstate["m"][off:off + p.numel()].view(p.shape)
+                        st["exp_avg_sq"] = gstate["v"][off:off + p.numel()].view(p.shape)
+                        off += p.numel()
+                total = gstate["m"].numel()
+                lib().check(lib().rr_adamw(total, pspan[0][0], gspan[0][0], gstate["m"].data_ptr(),
+                                           gstate["v"].data_ptr(), float(group["lr"]), float(b1),
+                                           float(b2), float(group["eps"]),
+                                           float(group["weight_decay"]), int(self.decoupled), step,
+                                           ops.stream()), "rr_adamw")
+            else:
+                for p in ps:
+                    st = self.state.setdefault(p, {})
+                    if "exp_avg" not in st:
+                        st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                        st["exp_avg_sq"] = torch.zeros_like(st["exp_avg"])
+                    ops.adamw_(p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"],
+                               group["lr"], b1, b2, group["eps"], group["weight_decay"],
+                               self.decoupled, step)
+            for p in ps:
+                self.state.setdefault(p, {})["step"] = step
+        return loss
+
+
+class AdamW(_FusedAdamBase):
+    """torch.optim.AdamW semantics (14:222: lr 2e-4, wd 1e-4)."""
+
+    decoupled = True
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        super().__init__(params, lr, betas, eps, weight_decay)
+
+
+class Adam(_FusedAdamBase):
+    """torch.optim.Adam semantics (07:143: lr 1e-3, L2 weight decay folded into g)."""
+
+    decoupled = False
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        super().__init__(params, lr, betas, eps, weight_decay)

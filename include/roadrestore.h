@@ -1,0 +1,278 @@
+/*
+ * roadrestore.h -- C ABI of the MI355X (gfx950) hot path of the road-sign
+ * restoration pipeline.
+ *
+ * The reference (LordTARN1SHED/Image-Restoration-for-Road-Sign-Recognition-in-
+ * Autonomous-Driving) has no FFI: its hot path is torch.nn.Module.forward +
+ * autograd dispatching ATen conv / BN / PReLU / pool / convT / cat kernels
+ * (SURVEY.md §2.3, §8b).  Each entry point below replaces one of those ATen
+ * calls as issued by the reference modules; the reference call site is cited
+ * on every declaration.  The Python host side (roadrestore/, ctypes) binds
+ * exactly these symbols -- see INTEGRATION.md.
+ *
+ * Conventions
+ *  - Activations are NHWC (channels contiguous), dtype RR_F32 or RR_BF16.
+ *    Model inputs/outputs at the module boundary are NCHW fp32.
+ *  - All buffers are device pointers owned by the caller; the library never
+ *    allocates device memory.  Scratch comes from a caller workspace whose size
+ *    is reported by the matching *_workspace() query.
+ *  - Every launcher is asynchronous on `stream` (a hipStream_t) and returns an
+ *    rr_status: 0 ok, <0 error (bad descriptor, unsupported shape, launch
+ *    failure).  No C++ exception crosses the ABI.
+ */
+#ifndef ROADRESTORE_H
+#define ROADRESTORE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *rr_stream;   /* hipStream_t */
+
+enum rr_status {
+  RR_OK = 0,
+  RR_EINVAL = -1,        /* malformed descriptor / null pointer            */
+  RR_EUNSUPPORTED = -2,  /* shape outside what the kernels implement       */
+  RR_ELAUNCH = -3,       /* hipLaunchKernel / runtime error                */
+  RR_EWORKSPACE = -4     /* workspace smaller than *_workspace() reported  */
+};
+
+enum rr_dtype { RR_F32 = 0, RR_BF16 = 1 };
+
+/* implicit-GEMM geometry (how the activation operand is gathered) */
+enum rr_igemm_mode {
+  RR_CONV3X3 = 0,   /* 3x3, stride 1, pad 1: fwd conv and its dgrad        */
+  RR_CONV1X1 = 1,   /* 1x1 conv, shortcut conv, Linear (h = w = 1)         */
+  RR_CONVT_UP = 2,  /* ConvTranspose2d(k2,s2) fwd: GEMM + 2x2 pixel scatter */
+  RR_CONVT_DOWN = 3 /* ConvTranspose2d(k2,s2) dgrad: gather 2x2 -> GEMM     */
+};
+
+enum rr_act { RR_ACT_NONE = 0, RR_ACT_RELU = 1 };
+
+/*
+ * Implicit-GEMM convolution: y[p, c] = sum_k W[c, k] * X[p, k] (+ epilogue).
+ *   p runs over the n*h*w pixels of the GEMM's row grid, c over c_out
+ *   GEMM columns (RR_CONVT_UP: c_out = 4*Cout, column = tap*Cout + co),
+ *   k over taps x (c_in1 + c_in2) input channels (two NHWC sources = the
+ *   reference's torch.cat((up, skip), 1) read in place, 07:112, 14:174).
+ */
+typedef struct {
+  int32_t dtype;       /* rr_dtype of x1, x2, w, y                          */
+  int32_t mode;        /* rr_igemm_mode                                     */
+  int32_t n, h, w;     /* GEMM row grid (output pixels; convT_up: input px)  */
+  int32_t c_in1;       /* channels of source 1 (the "up" half of a cat)      */
+  int32_t c_in2;       /* channels of source 2 (skip half) or 0              */
+  int32_t c_out;       /* GEMM columns                                       */
+  int32_t out_split;   /* columns [0,out_split) -> y1, rest -> y2; 0 = all y1 */
+  int32_t act;         /* rr_act applied after bias                          */
+  int32_t accumulate;  /* 1: y = y_old + result (before act/mask)            */
+  int32_t has_bias;    /* bias[c] (fp32) added                               */
+  int32_t has_mask;    /* result *= (mask[p, c] > 0); mask has y's layout    */
+  int32_t want_stats;  /* per-(row-block, column) partial sum / sum of squares */
+} rr_igemm_desc;
+
+/* packed weights: w[c_out][taps][c_in1+c_in2] in dtype (see rr_pack_*). */
+int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
+             const void *w, const float *bias, void *y1, void *y2,
+             const void *mask, float *stats_partial, rr_stream stream);
+/* number of row blocks the partial stats buffer holds: [blocks][c_out][2] */
+int rr_igemm_stat_blocks(const rr_igemm_desc *d);
+
+/*
+ * Weight-gradient GEMM (split over pixels):
+ *  RR_CONV3X3 / RR_CONV1X1:  dW[co][ci][ky][kx] = sum_p dy[p,co] x[p+tap,ci]
+ *  RR_CONVT_UP:              dW[ci][co][ky][kx] = sum_p x[p,ci] dy[2p+tap,co]
+ *  (nn.Conv2d / nn.ConvTranspose2d weight grads of the reference modules).
+ *  dw is fp32 in torch's layout; accumulate adds into it.
+ */
+typedef struct {
+  int32_t dtype;
+  int32_t mode;        /* RR_CONV3X3, RR_CONV1X1 or RR_CONVT_UP              */
+  int32_t n, h, w;     /* conv: output grid (= input grid); convT: input grid */
+  int32_t c_in1, c_in2;/* x channels (two sources for a cat input)           */
+  int32_t c_out;       /* dy channels                                        */
+  int32_t accumulate;
+} rr_wgrad_desc;
+
+size_t rr_wgrad_workspace(const rr_wgrad_desc *d);
+int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
+             const void *x2, float *dw, void *ws, size_t ws_bytes,
+             rr_stream stream);
+
+/* weight packing (fp32 torch layout -> compute layout/dtype) */
+/* conv [co][ci][k][k] -> fwd [co][k*k][ci] and dgrad [ci][k*k flipped][co] */
+int rr_pack_conv(int dtype, int c_out, int c_in, int k, const float *w,
+                 void *w_fwd, void *w_dgrad, rr_stream stream);
+/* convT [ci][co][2][2] -> up [tap*co][ci] and down [ci][tap][co] */
+int rr_pack_convT(int dtype, int c_in, int c_out, const float *w,
+                  void *w_up, void *w_down, rr_stream stream);
+/* replicate bias over the 4 taps of a convT: b4[tap*co] = b[co] */
+int rr_bias_tile4(int c_out, const float *b, float *b4, rr_stream stream);
+
+/*
+ * BatchNorm2d (14:101-112; eps, momentum as given).  stats_partial is the
+ * [blocks][C][2] output of rr_igemm(want_stats) over the PRE-BIAS accumulator;
+ * bias is that conv's bias (may be NULL).  Writes scale/shift (the affine the
+ * apply kernels use), save_mean / save_invstd (for backward) and updates the
+ * running stats in place (unbiased var), like F.batch_norm(training=True).
+ */
+int rr_bn_finalize(int C, int blocks, long long count, const float *stats_partial,
+                   const float *bias, const float *gamma, const float *beta,
+                   float *running_mean, float *running_var, float momentum,
+                   float eps, float *scale, float *shift, float *save_mean,
+                   float *save_invstd, int64_t *num_batches_tracked,
+                   rr_stream stream);
+/* eval mode: scale/shift from running stats (17:64 model.eval()) */
+int rr_bn_eval_affine(int C, const float *gamma, const float *beta,
+                      const float *running_mean, const float *running_var,
+                      float eps, float *scale, float *shift, rr_stream stream);
+
+/*
+ * Fused elementwise forward over NHWC [P][C]:
+ *   u = x*scale[c] + shift[c];  u = prelu(u, alpha) if alpha != NULL
+ *   if res != NULL: u += (res_scale ? res*res_scale[c]+res_shift[c] : res)
+ *   if relu: u = max(u, 0)
+ * (PReLU(BN(conv)) 14:101-103 and relu(BN(conv) + shortcut) 14:115.)
+ */
+int rr_affine_act(int dtype, long long P, int C, const void *x, const float *scale,
+                  const float *shift, const float *alpha, const void *res,
+                  const float *res_scale, const float *res_shift, int relu,
+                  void *y, rr_stream stream);
+
+/*
+ * BatchNorm backward, reduction half.  Upstream grad g on the BN output side:
+ *   mask_kind 0: gm = g
+ *   mask_kind 1: gm = g * (aux > 0)                  (relu after the add, 14:115)
+ *   mask_kind 2: u = aux*aff_s[c]+aff_b[c]; gm = g*(u>0 ? 1 : alpha)
+ *                and alpha_grad partial += g*u*(u<=0)   (PReLU, 14:103)
+ * For up to two BNs fed by the same gm (BN2 and the shortcut BN) it produces
+ * per-row-block partials of sum(gm) and sum(gm * xhat_i), xhat_i = (t_i -
+ * mean_i) * invstd_i.  partial layout [blocks][C][3] (+ alpha partial).
+ */
+typedef struct {
+  int32_t dtype;
+  int64_t P;
+  int32_t C;
+  int32_t mask_kind;
+  int32_t nbn;          /* 1 or 2 */
+} rr_bnbwd_desc;
+int rr_bn_bwd_blocks(const rr_bnbwd_desc *d);
+int rr_bn_bwd_reduce(const rr_bnbwd_desc *d, const void *g, const void *aux,
+                     const float *aff_s, const float *aff_b, const float *alpha,
+                     const void *t0, const float *mean0, const float *invstd0,
+                     const void *t1, const float *mean1, const float *invstd1,
+                     float *partial, rr_stream stream);
+/* finalize: dgamma/dbeta (fp32, written) and the per-channel coefficients */
+int rr_bn_bwd_finalize(const rr_bnbwd_desc *d, const float *partial,
+                       const float *gamma0, const float *invstd0,
+                       const float *gamma1, const float *invstd1,
+                       float *dgamma0, float *dbeta0, float *dgamma1, float *dbeta1,
+                       float *dalpha, float *coef, rr_stream stream);
+/* apply: dt_i = coef_a[c]*(gm - coef_b[c] - xhat_i*coef_c[c]); optional gm out */
+int rr_bn_bwd_apply(const rr_bnbwd_desc *d, const void *g, const void *aux,
+                    const float *aff_s, const float *aff_b, const float *alpha,
+                    const void *t0, const float *mean0, const float *invstd0,
+                    const void *t1, const float *mean1, const float *invstd1,
+                    const float *coef, void *dt0, void *dt1, void *gm_out,
+                    rr_stream stream);
+
+/* per-channel column sums of an NHWC [P][C] tensor (bias grads), fp32 out */
+int rr_channel_sum(int dtype, long long P, int C, const void *x, float *out,
+                   int accumulate, void *ws, size_t ws_bytes, rr_stream stream);
+size_t rr_channel_sum_workspace(long long P, int C);
+
+/* MaxPool2d(2,2) floor mode (07:82, 14:125): y and 1-byte argmax (0..3) */
+int rr_maxpool2_fwd(int dtype, int n, int h, int w, int C, const void *x,
+                    void *y, uint8_t *idx, rr_stream stream);
+/* gather-form backward: dx = (accumulate ? dx : 0) + scatter(dy by idx);
+ * then dx *= (mask > 0) if mask (relu of the pooled activation, 07:81) */
+int rr_maxpool2_bwd(int dtype, int n, int h, int w, int C, const void *dy,
+                    const uint8_t *idx, void *dx, int accumulate,
+                    const void *mask, rr_stream stream);
+
+/* first layer: conv3x3 p1 from NCHW fp32 [n][cin][h][w] into NHWC dtype,
+ * + bias, act: 0 none, 1 relu, 2 prelu(alpha)  (07:78 enc1.0, 14:122 enc1) */
+int rr_conv_in_fwd(int dtype, int n, int h, int w, int cin, int cout,
+                   const float *x, const float *wt, const float *b,
+                   int act, const float *alpha, void *y, rr_stream stream);
+/* its weight/bias grads given dy (NHWC, pre-activation grad) */
+int rr_conv_in_wgrad(int dtype, int n, int h, int w, int cin, int cout,
+                     const float *x, const void *dy, float *dw, float *db,
+                     void *ws, size_t ws_bytes, rr_stream stream);
+size_t rr_conv_in_wgrad_workspace(int n, int h, int w, int cin, int cout);
+/* input grad of that conv (VGG perceptual slice dgrad reaching the image) */
+int rr_conv_in_dgrad(int dtype, int n, int h, int w, int cin, int cout,
+                     const void *dy, const float *wt, float *dx, int accumulate,
+                     rr_stream stream);
+/* PReLU backward on an NHWC tensor (14:122 enc1's PReLU): dx = dy*(y_pre>0 ?
+ * 1 : alpha); alpha_partial holds `blocks` per-workgroup partials and the
+ * alpha gradient (their fixed-order sum) is written to *dalpha. */
+int rr_prelu_bwd(int dtype, long long count, const void *dy, const void *y_pre,
+                 const float *alpha, void *dx, float *alpha_partial, int blocks,
+                 float *dalpha, rr_stream stream);
+
+/* last layer: conv1x1 cin->cout (cout small) NHWC dtype -> NCHW fp32 (07:119) */
+int rr_conv_out_fwd(int dtype, int n, int h, int w, int cin, int cout,
+                    const void *x, const float *wt, const float *b, float *y,
+                    rr_stream stream);
+/* grads of the last layer: dx (NHWC dtype, optional mask by x>0),
+ * dw / db (fp32, need workspace) from dy (NCHW fp32) */
+int rr_conv_out_bwd(int dtype, int n, int h, int w, int cin, int cout,
+                    const float *dy, const void *x, const float *wt,
+                    void *dx, int mask_relu, float *dw, float *db, void *ws,
+                    size_t ws_bytes, rr_stream stream);
+size_t rr_conv_out_bwd_workspace(int n, int h, int w, int cin, int cout);
+
+/* layout: NCHW fp32 <-> NHWC dtype */
+int rr_nchw_to_nhwc(int dtype, int n, int c, int h, int w, const float *x,
+                    void *y, rr_stream stream);
+int rr_nhwc_to_nchw(int dtype, int n, int c, int h, int w, const void *x,
+                    float *y, rr_stream stream);
+
+/* mean losses (nn.L1Loss 14:219, nn.MSELoss 07:142, the perceptual
+ * mean((F(x)-F(y))^2) 14:196): *out = (accumulate ? *out : 0) + scale *
+ * mean(|a-b| or (a-b)^2), per-workgroup partials then a fixed-order sum. */
+int rr_loss_fwd(int kind /*0 l1, 1 mse*/, int dtype, long long count,
+                const void *a, const void *b, float *out_scalar, float scale,
+                int accumulate, void *ws, size_t ws_bytes, rr_stream stream);
+size_t rr_loss_workspace(long long count);
+/* grad wrt a: g*scale/count * sign(a-b) (l1) or *2(a-b) (mse), g = *gscale_dev
+ * (autograd's incoming grad, device scalar) or 1; optional grad wrt b;
+ * mask_a_pos: the grad is zeroed where a <= 0 (a is a ReLU output: the
+ * perceptual slice ends in relu3_3, 14:192). */
+int rr_loss_bwd(int kind, int dtype, long long count, const void *a,
+                const void *b, const float *gscale_dev, float scale, void *ga,
+                void *gb, int accumulate, int mask_a_pos, rr_stream stream);
+
+/* fused multi-tensor Adam/AdamW (14:222, 07:143) over a flat fp32 buffer */
+int rr_adamw(long long count, float *param, const float *grad, float *m,
+             float *v, float lr, float beta1, float beta2, float eps,
+             float weight_decay, int decoupled, int step, rr_stream stream);
+
+/* inference post-processing (17:84-92): clamp(0,1)*255 -> uint8 HWC */
+int rr_to_uint8_hwc(int n, int c, int h, int w, const float *x, uint8_t *out,
+                    int bgr, rr_stream stream);
+/* per-image PSNR between uint8 images (08:123, data_range 255), fp64 out */
+int rr_psnr_u8(int n, long long per_image, const uint8_t *a, const uint8_t *b,
+               double *out, rr_stream stream);
+/* argmax over rows of [n][k] fp32 logits, first max on ties (18:47) */
+int rr_argmax_rows(int n, int k, const float *logits, int64_t *out,
+                   rr_stream stream);
+/* AdaptiveAvgPool2d((oh,ow)) on NHWC -> NCHW-flatten order fp32-or-dtype
+ * rows for the classifier (torch.flatten(x, 1) of NCHW) */
+int rr_adaptive_avgpool_flatten(int dtype, int n, int h, int w, int C, int oh,
+                                int ow, const void *x, void *y, rr_stream stream);
+
+/* async memset of a device buffer (zero_grad of the flat buffers) */
+int rr_zero(void *p, size_t bytes, rr_stream stream);
+
+/* library version string */
+const char *rr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ROADRESTORE_H */

@@ -1,0 +1,249 @@
+"""Generate tests/golden/* by importing the REFERENCE scripts -- TEST INFRA ONLY.
+
+Run here (the survey container, where /root/reference exists):
+
+    python oracle/gen_golden.py
+
+The reference is a set of digit-prefixed scripts whose third-party imports
+(torchvision, cv2, skimage) are not installed; those are replaced by empty
+stub modules before each script is loaded with importlib.
+``torchvision.models.vgg16`` is stubbed with the restated torchvision cfg-D
+module (oracle.reference_cpu.TorchvisionVGG16) because the ImageNet weights are
+a network download; the reference's own ``VGGPerceptualLoss`` slicing /
+freezing / loss code then runs unchanged on seeded weights.
+
+Every fixture is produced by the reference classes themselves; the functional
+restatement (oracle/reference_cpu.py) is checked against them here and the
+check is re-run from the committed fixtures by tests/test_oracle.py.
+The reference itself never travels: only the .npz/.json data land in
+tests/golden/.
+"""
+from __future__ import annotations
+
+import importlib.util
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, REPO)
+
+from oracle import reference_cpu as R          # noqa: E402
+from oracle import seeded as S                 # noqa: E402
+
+REF = os.environ.get("RR_REFERENCE", "/root/reference")
+OUT = os.path.join(REPO, "tests", "golden")
+
+
+def _install_stubs():
+    tv = types.ModuleType("torchvision")
+    for sub in ("transforms", "models", "datasets"):
+        m = types.ModuleType("torchvision." + sub)
+        setattr(tv, sub, m)
+        sys.modules["torchvision." + sub] = m
+    sys.modules["torchvision"] = tv
+    tv.models.vgg16 = lambda weights=None, **kw: R.TorchvisionVGG16(num_classes=1000)
+    sys.modules["cv2"] = types.ModuleType("cv2")
+    sk = types.ModuleType("skimage")
+    skm = types.ModuleType("skimage.metrics")
+    skm.peak_signal_noise_ratio = None
+    skm.structural_similarity = None
+    sk.metrics = skm
+    sys.modules["skimage"] = sk
+    sys.modules["skimage.metrics"] = skm
+
+
+def _load(fname, modname):
+    spec = importlib.util.spec_from_file_location(modname, os.path.join(REF, fname))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def manifest(module):
+    return [[k, list(v.shape)] for k, v in module.state_dict().items()]
+
+
+def digest(named, idx_seed=123, n_samples=8):
+    """Per-tensor (sum, L2 norm, sampled elements at fixed flat indices)."""
+    out = {}
+    for i, (k, t) in enumerate(named.items()):
+        t = t.detach().double().reshape(-1)
+        rng = np.random.Generator(np.random.PCG64([idx_seed, i]))
+        idx = rng.integers(0, t.numel(), size=n_samples)
+        out[k + "|sum"] = np.array([t.sum().item()])
+        out[k + "|norm"] = np.array([t.norm().item()])
+        out[k + "|idx"] = idx.astype(np.int64)
+        out[k + "|val"] = t[idx].numpy()
+    return out
+
+
+def save(name, **arrays):
+    path = os.path.join(OUT, name)
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, os.path.getsize(path + ("" if path.endswith(".npz") else ".npz")))
+
+
+def _close(a, b, tol=0.0):
+    d = (a - b).abs().max().item()
+    assert d <= tol, d
+    return d
+
+
+def main():
+    torch.set_num_threads(8)
+    torch.use_deterministic_algorithms(True)
+    os.makedirs(OUT, exist_ok=True)
+    _install_stubs()
+    m07 = _load("07_train_restoration.py", "ref07")
+    m14 = _load("14_train_unified_advanced.py", "ref14")
+    m17 = _load("17_run_unified_inference.py", "ref17")
+    m08 = _load("08_run_inference.py", "ref08")
+
+    # ---- manifests (reference key trees) ----------------------------------
+    su, ru = m07.SimpleUNet(), m14.ResUNet()
+    assert manifest(su) == manifest(m08.SimpleUNet())        # 08:19-46 copy
+    assert manifest(ru) == manifest(m17.ResUNet())           # 17:29-55 copy
+    perc = m14.VGGPerceptualLoss()
+    mans = {"simpleunet": manifest(su), "resunet": manifest(ru),
+            "vgg16": manifest(R.TorchvisionVGG16(43)), "perceptual": manifest(perc)}
+    for n, man in mans.items():
+        with open(os.path.join(OUT, f"manifest_{n}.json"), "w") as f:
+            json.dump(man, f)
+        print(n, len(man), "keys")
+
+    # ---- SimpleUNet: fwd + MSE train step (07:151-160) ---------------------
+    for H, B, tag in ((64, 2, "64"), (224, 1, "224")):
+        sd = S.model_state_dict("simpleunet", seed=0)
+        clean = S.image_batch(B, H, H, seed=10 + H)
+        bad = S.fog_noise(clean, seed=20 + H)
+        m = m07.SimpleUNet()
+        m.load_state_dict(sd)
+        out = m(bad)
+        p = {k: v.clone() for k, v in sd.items()}
+        _close(R.simple_unet_forward(p, bad), out.detach())
+        arrays = dict(bad=bad.numpy(), clean=clean.numpy(), out=out.detach().numpy())
+        if H == 64:
+            opt = torch.optim.Adam(m.parameters(), lr=1e-3)          # 07:143
+            opt.zero_grad()
+            loss = torch.nn.MSELoss()(m(bad), clean)                  # 07:154-156
+            loss.backward()
+            grads = {k: v.grad for k, v in m.named_parameters()}
+            opt.step()
+            arrays["loss"] = np.array([loss.item()])
+            arrays.update({"grad:" + k: v for k, v in digest(grads).items()})
+            arrays.update({"post:" + k: v for k, v in
+                           digest(dict(m.named_parameters())).items()})
+        if H == 224:
+            arrays["bad_sum"] = np.array([bad.double().sum().item()])
+            del arrays["bad"], arrays["clean"]
+        save(f"simpleunet_{tag}.npz", **arrays)
+
+    # ---- ResUNet ------------------------------------------------------------
+    # Seeded running stats do not match the seeded conv statistics, so eval-mode
+    # activations would grow through 10 blocks.  Calibrate them the way a
+    # trained model's are (cumulative batch statistics of a calibration batch,
+    # momentum=None) and commit them: S.model_state_dict("resunet") applies them.
+    cal = m14.ResUNet()
+    cal.load_state_dict(S.seeded_state_dict(mans["resunet"], 0, S.convT_prefixes(mans["resunet"])))
+    for mod in cal.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.momentum = None
+            mod.reset_running_stats()
+    cal.train()
+    with torch.no_grad():
+        cal(S.fog_noise(S.image_batch(4, 64, 64, seed=99), seed=98))
+    run = {k: v for k, v in cal.state_dict().items()
+           if k.endswith("running_mean") or k.endswith("running_var")}
+    save("resunet_calib.npz", keys=np.array(list(run)),
+         vals=np.concatenate([v.numpy().ravel() for v in run.values()]))
+    perc_sd = S.seeded_state_dict(mans["perceptual"], seed=5)
+    perc.slice.load_state_dict({k[len("slice."):]: v for k, v in perc_sd.items()})
+    for H, B, tag in ((64, 2, "64"), (224, 1, "224")):
+        sd = S.model_state_dict("resunet", seed=0)
+        clean = S.image_batch(B, H, H, seed=30 + H)
+        bad = S.fog_noise(clean, seed=40 + H)
+        m = m14.ResUNet()
+        m.load_state_dict(sd)
+        m.eval()
+        with torch.no_grad():
+            out_eval = m(bad)                       # 17:84-86 (running stats)
+        p = {k: v.clone() for k, v in sd.items()}
+        _close(R.resunet_forward(p, bad, training=False), out_eval)
+        arrays = dict(bad=bad.numpy(), clean=clean.numpy(), out_eval=out_eval.numpy())
+        u8 = R.to_uint8_image(out_eval)
+        cu8 = R.to_uint8_image(clean)
+        arrays["out_u8"] = u8
+        arrays["clean_u8"] = cu8
+        arrays["psnr"] = np.array([R.psnr_u8(cu8[i], u8[i]) for i in range(B)])
+        if H == 64:
+            m.train()
+            out_train = m(bad)                      # 14:236 (batch stats)
+            p = {k: v.clone() for k, v in sd.items()}
+            _close(R.resunet_forward(p, bad, training=True), out_train.detach(), 0.0)
+            arrays["out_train"] = out_train.detach().numpy()
+            run = {k: v for k, v in m.state_dict().items()
+                   if k.endswith("running_mean") or k.endswith("running_var")}
+            arrays["running_keys"] = np.array(sorted(run))
+            arrays["running_vals"] = np.concatenate(
+                [run[k].numpy().ravel() for k in sorted(run)])
+            # one unified train step (14:235-245) from the seeded state
+            m.load_state_dict(sd)
+            m.train()
+            opt = torch.optim.AdamW(m.parameters(), lr=2e-4, weight_decay=1e-4)  # 14:222
+            crit_l1 = torch.nn.L1Loss()
+            opt.zero_grad()
+            out = m(bad)
+            l_pix = crit_l1(out, clean)
+            l_perc = perc(out, clean)
+            loss = l_pix + 0.1 * l_perc
+            loss.backward()
+            grads = {k: v.grad for k, v in m.named_parameters()}
+            # restatement check of the loss and a couple of grads
+            p = {k: v.clone().requires_grad_(not ("running" in k or "num_batches" in k)) for k, v in sd.items()}
+            lr_ = R.unified_loss(R.resunet_forward(p, bad, True), clean, perc_sd)
+            lr_.backward()
+            assert abs(lr_.item() - loss.item()) < 1e-6, (lr_.item(), loss.item())
+            for k in ("enc1.0.weight", "res1.conv_block.0.weight", "final.bias"):
+                _close(p[k].grad, grads[k], 1e-5)
+            opt.step()
+            arrays["loss"] = np.array([loss.item()])
+            arrays["l_pix"] = np.array([l_pix.item()])
+            arrays["l_perc"] = np.array([l_perc.item()])
+            arrays.update({"grad:" + k: v for k, v in digest(grads).items()})
+            arrays.update({"post:" + k: v for k, v in
+                           digest(dict(m.named_parameters())).items()})
+            # perceptual loss alone on (bad, clean)
+            with torch.no_grad():
+                arrays["perc_bad_clean"] = np.array([perc(bad, clean).item()])
+                _close(R.perceptual_loss(perc_sd, bad, clean),
+                       perc(bad, clean), 1e-6)
+        if H == 224:   # regenerated from the seeded generator; keep a checksum
+            arrays["bad_sum"] = np.array([bad.double().sum().item()])
+            del arrays["bad"], arrays["clean"]
+        save(f"resunet_{tag}.npz", **arrays)
+
+    # ---- VGG16 classifier (18:43-49) ------------------------------------
+    vsd = S.seeded_state_dict(mans["vgg16"], seed=3)
+    vgg = R.TorchvisionVGG16(43)
+    vgg.load_state_dict(vsd)
+    vgg.eval()
+    for H, B in ((224, 8), (64, 8)):
+        x = S.classifier_batch(B, H, seed=50 + H)
+        with torch.no_grad():
+            logits = vgg(x)
+        _close(R.vgg16_forward(vsd, x), logits, 0.0)
+        top2 = torch.topk(logits, 2, dim=1).values
+        xin = dict(x=x.numpy()) if H == 64 else dict(x_sum=np.array([x.double().sum().item()]))
+        save(f"vgg16_{H}.npz", **xin, logits=logits.numpy(),
+             pred=R.top1(logits).numpy(), margin=(top2[:, 0] - top2[:, 1]).numpy())
+    print("done")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,272 @@
+"""Per-op parity of the HIP kernels against the CPU oracle (ATen fp32 ops the
+reference dispatches), small shapes.  fp32 path: tight tolerances (the f32
+MFMA is an exact fp32 FMA chain; only the summation order differs); bf16:
+relative tolerances of bf16 storage."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+TOL = {torch.float32: (2e-4, 2e-5), torch.bfloat16: (3e-2, 3e-2)}
+
+
+def nhwc(x, dev, dt):
+    return x.permute(0, 2, 3, 1).contiguous().to(dev, dt)
+
+
+def nchw(y):
+    return y.float().permute(0, 3, 1, 2).contiguous().cpu()
+
+
+def close(a, b, dt, scale=None):
+    """fp32: max-abs error relative to the tensor scale.  bf16: relative L2
+    error (bf16 storage flips a few ReLU/PReLU masks near 0, so a max-abs
+    bound would test the rounding of single elements, not the kernel)."""
+    a = a.float().cpu()
+    b = b.float()
+    if dt == torch.float32:
+        rtol, atol = TOL[dt]
+        s = scale if scale is not None else max(1.0, b.abs().max().item())
+        err = (a - b).abs().max().item()
+        assert err <= atol * s, (err, s)
+    else:
+        rel = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+        assert rel <= 5e-2, rel
+
+
+def rnd(*shape, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,h,w,cin,cout", [(2, 8, 8, 64, 64), (1, 5, 7, 128, 64), (2, 16, 16, 64, 256),
+                                            (3, 9, 4, 192, 128)])
+def test_conv3x3_fwd(dev, dt, n, h, w, cin, cout):
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    x = rnd(n, cin, h, w, seed=1)
+    wt = rnd(cout, cin, 3, 3, seed=2) * 0.05
+    b = rnd(cout, seed=3)
+    if dt == torch.bfloat16:
+        x, wt = x.bfloat16().float(), wt.bfloat16().float()
+    ref = F.relu(F.conv2d(x, wt, b, padding=1))
+    wf, wd = rr.ops.pack_conv(wt.to(dev), dt)
+    y, _, st = rr.ops.igemm(RR_CONV3X3, nhwc(x, dev, dt), None, n, h, w, wf, cout,
+                            bias=b.to(dev), act=1, stats=True)
+    close(nchw(y), ref, dt)
+    # stats of the pre-bias accumulator
+    pre = F.conv2d(x, wt, None, padding=1)
+    s = st.cpu().double().sum(0)
+    mag = pre.abs().sum((0, 2, 3)).max().item()
+    tol = (1e-5 if dt == torch.float32 else 1e-2) * mag
+    assert (s[:, 0] - pre.double().sum((0, 2, 3))).abs().max().item() <= tol
+    assert (s[:, 1] - (pre.double() ** 2).sum((0, 2, 3))).abs().max().item() <= \
+        tol * pre.abs().max().item() * 2
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_conv3x3_concat_dgrad_split(dev, dt):
+    """cat((up, skip), 1) read in place (07:112) and the dgrad split."""
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    n, h, w, c1, c2, cout = 2, 8, 8, 128, 64, 64
+    x1, x2 = rnd(n, c1, h, w, seed=4), rnd(n, c2, h, w, seed=5)
+    wt = rnd(cout, c1 + c2, 3, 3, seed=6) * 0.05
+    if dt == torch.bfloat16:
+        x1, x2, wt = x1.bfloat16().float(), x2.bfloat16().float(), wt.bfloat16().float()
+    xc = torch.cat((x1, x2), 1).requires_grad_(True)
+    ref = F.conv2d(xc, wt, None, padding=1)
+    g = rnd(*ref.shape, seed=7)
+    if dt == torch.bfloat16:
+        g = g.bfloat16().float()
+    ref.backward(g)
+    wf, wd = rr.ops.pack_conv(wt.to(dev), dt)
+    y, _, _ = rr.ops.igemm(RR_CONV3X3, nhwc(x1, dev, dt), nhwc(x2, dev, dt), n, h, w, wf, cout)
+    close(nchw(y), ref.detach(), dt)
+    g1, g2, _ = rr.ops.igemm(RR_CONV3X3, nhwc(g, dev, dt), None, n, h, w, wd, c1 + c2, split=c1)
+    close(nchw(g1), xc.grad[:, :c1], dt)
+    close(nchw(g2), xc.grad[:, c1:], dt)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("k", [3, 1])
+def test_wgrad(dev, dt, k):
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV1X1, RR_CONV3X3
+    n, h, w, cin, cout = 3, 12, 10, 128, 64
+    x = rnd(n, cin, h, w, seed=8)
+    g = rnd(n, cout, h, w, seed=9)
+    if dt == torch.bfloat16:
+        x, g = x.bfloat16().float(), g.bfloat16().float()
+    wt = torch.zeros(cout, cin, k, k, requires_grad=True)
+    F.conv2d(x, wt, None, padding=k // 2).backward(g)
+    dw = rr.ops.wgrad(RR_CONV3X3 if k == 3 else RR_CONV1X1, nhwc(g, dev, dt), nhwc(x, dev, dt),
+                      None, n, h, w, cout, dw_shape=(cout, cin, k, k))
+    close(dw.cpu(), wt.grad, dt, scale=wt.grad.abs().max().item())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_convT(dev, dt):
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONVT_DOWN, RR_CONVT_UP
+    n, h, w, cin, cout = 2, 4, 6, 128, 64
+    x = rnd(n, cin, h, w, seed=10).requires_grad_(True)
+    wt = (rnd(cin, cout, 2, 2, seed=11) * 0.05).requires_grad_(True)
+    b = rnd(cout, seed=12)
+    if dt == torch.bfloat16:
+        with torch.no_grad():
+            x.copy_(x.bfloat16().float()); wt.copy_(wt.bfloat16().float())
+    ref = F.conv_transpose2d(x, wt, b, stride=2)
+    g = rnd(*ref.shape, seed=13)
+    if dt == torch.bfloat16:
+        g = g.bfloat16().float()
+    ref.backward(g)
+    wu, wdn = rr.ops.pack_convT(wt.detach().to(dev), dt)
+    y, _, _ = rr.ops.igemm(RR_CONVT_UP, nhwc(x.detach(), dev, dt), None, n, h, w, wu, 4 * cout,
+                           bias=rr.ops.bias_tile4(b.to(dev)))
+    close(nchw(y), ref.detach(), dt)
+    gx, _, _ = rr.ops.igemm(RR_CONVT_DOWN, nhwc(g, dev, dt), None, n, h, w, wdn, cin)
+    close(nchw(gx), x.grad, dt)
+    dw = rr.ops.wgrad(RR_CONVT_UP, nhwc(g, dev, dt), nhwc(x.detach(), dev, dt), None, n, h, w,
+                      cout, dw_shape=(cin, cout, 2, 2))
+    close(dw.cpu(), wt.grad, dt, scale=wt.grad.abs().max().item())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_bn_train_fwd_bwd(dev, dt):
+    """BatchNorm2d train fwd (batch stats, running update) + PReLU, and the
+    fused backward (mask kinds 1 and 2)."""
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    n, h, w, cin, C = 4, 8, 8, 64, 64
+    x = rnd(n, cin, h, w, seed=14)
+    wt = rnd(C, cin, 3, 3, seed=15) * 0.05
+    b = rnd(C, seed=16)
+    gamma, beta = rnd(C, seed=17).abs() + 0.5, rnd(C, seed=18) * 0.1
+    alpha = torch.tensor([0.25])
+    if dt == torch.bfloat16:
+        x, wt = x.bfloat16().float(), wt.bfloat16().float()
+    t = F.conv2d(x, wt, b, padding=1)
+    tr = t.detach().requires_grad_(True)
+    gam, bet, alp = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True), alpha.clone().requires_grad_(True)
+    rm, rv = torch.zeros(C), torch.ones(C)
+    u = F.batch_norm(tr, rm, rv, gam, bet, True, 0.1, 1e-5)
+    a = F.prelu(u, alp)
+    g = rnd(*a.shape, seed=19)
+    a.backward(g)
+    wf, _ = rr.ops.pack_conv(wt.to(dev), dt)
+    tt, _, st = rr.ops.igemm(RR_CONV3X3, nhwc(x, dev, dt), None, n, h, w, wf, C, bias=b.to(dev), stats=True)
+    rmd, rvd = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    nbt = torch.zeros((), dtype=torch.long, device=dev)
+    scale, shift, mean, inv = rr.ops.bn_finalize(st, n * h * w, b.to(dev), gamma.to(dev), beta.to(dev),
+                                                 rmd, rvd, 0.1, 1e-5, nbt)
+    aa = rr.ops.affine_act(tt, scale, shift, alpha=alpha.to(dev))
+    close(nchw(aa), a.detach(), dt)
+    torch.testing.assert_close(rmd.cpu(), rm, rtol=1e-4 if dt == torch.float32 else 3e-2, atol=1e-4)
+    torch.testing.assert_close(rvd.cpu(), rv, rtol=1e-4 if dt == torch.float32 else 3e-2, atol=1e-4)
+    assert nbt.item() == 1
+    gd = nhwc(g, dev, dt)
+    r = rr.ops.bn_backward(gd, tt, mean, inv, gamma.to(dev), mask_kind=2, aux=tt, aff_s=scale,
+                           aff_b=shift, alpha=alpha.to(dev))
+    close(nchw(r["dt0"]), tr.grad, dt)
+    close(r["dgamma0"].cpu(), gam.grad, dt, scale=gam.grad.abs().max().item())
+    close(r["dbeta0"].cpu(), bet.grad, dt, scale=bet.grad.abs().max().item())
+    close(r["dalpha"].cpu(), alp.grad, dt, scale=alp.grad.abs().max().item())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_maxpool(dev, dt):
+    import roadrestore as rr
+    n, C, h, w = 2, 64, 8, 10
+    x = F.relu(rnd(n, C, h, w, seed=20))          # many exact-zero ties after ReLU
+    x[0, 0, 0, :4] = 1.0                            # explicit ties inside a window
+    if dt == torch.bfloat16:
+        x = x.bfloat16().float()
+    xr = x.clone().requires_grad_(True)
+    y = F.max_pool2d(xr, 2, 2)
+    g = rnd(*y.shape, seed=21)
+    if dt == torch.bfloat16:
+        g = g.bfloat16().float()
+    y.backward(g)
+    yd, idx = rr.ops.maxpool2_fwd(nhwc(x, dev, dt))
+    close(nchw(yd), y.detach(), dt)
+    gx = rr.ops.maxpool2_bwd(nhwc(g, dev, dt), idx, h, w)
+    assert torch.equal(nchw(gx) != 0, xr.grad != 0)
+    close(nchw(gx), xr.grad, dt)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_first_last_layers(dev, dt):
+    import roadrestore as rr
+    n, h, w = 2, 12, 8
+    x = torch.rand(n, 3, h, w)
+    w0 = (rnd(64, 3, 3, 3, seed=22) * 0.2).requires_grad_(True)
+    b0 = rnd(64, seed=23).requires_grad_(True)
+    xr = x.clone().requires_grad_(True)
+    y0 = F.conv2d(xr, w0, b0, padding=1)
+    y = rr.ops.conv_in_fwd(x.to(dev), w0.detach().to(dev), b0.detach().to(dev), dt, act=0)
+    close(nchw(y), y0.detach(), dt)
+    g = rnd(*y0.shape, seed=24)
+    if dt == torch.bfloat16:
+        g = g.bfloat16().float()
+    y0.backward(g)
+    dw, db = rr.ops.conv_in_wgrad(x.to(dev), nhwc(g, dev, dt), dw_shape=(64, 3, 3, 3))
+    close(dw.cpu(), w0.grad, dt, scale=w0.grad.abs().max().item())
+    close(db.cpu(), b0.grad, dt, scale=b0.grad.abs().max().item())
+    gx = rr.ops.conv_in_dgrad(nhwc(g, dev, dt), w0.detach().to(dev), 3)
+    close(gx.cpu(), xr.grad, dt, scale=xr.grad.abs().max().item())
+    # last layer 64 -> 3 (1x1)
+    a = F.relu(rnd(n, 64, h, w, seed=25))
+    if dt == torch.bfloat16:
+        a = a.bfloat16().float()
+    ar = a.clone().requires_grad_(True)
+    wl = (rnd(3, 64, 1, 1, seed=26) * 0.1).requires_grad_(True)
+    bl = rnd(3, seed=27).requires_grad_(True)
+    o = F.conv2d(ar, wl, bl)
+    od = rr.ops.conv_out_fwd(nhwc(a, dev, dt), wl.detach().to(dev), bl.detach().to(dev))
+    close(od.cpu(), o.detach(), dt)
+    go = rnd(*o.shape, seed=28)
+    o.backward(go)
+    dx, dwl, dbl = rr.ops.conv_out_bwd(go.to(dev), nhwc(a, dev, dt), wl.detach().to(dev), mask_relu=True)
+    close(nchw(dx), ar.grad * (a > 0), dt)
+    close(dwl.cpu(), wl.grad, dt, scale=wl.grad.abs().max().item())
+    close(dbl.cpu(), bl.grad, dt, scale=bl.grad.abs().max().item())
+
+
+def test_losses_adamw_postproc(dev):
+    import numpy as np
+    import roadrestore as rr
+    from oracle import reference_cpu as R
+    a, b = torch.rand(2, 3, 16, 16), torch.rand(2, 3, 16, 16)
+    l1 = rr.ops.loss_fwd(rr.ops.L1, a.to(dev), b.to(dev))
+    mse = rr.ops.loss_fwd(rr.ops.MSE, a.to(dev), b.to(dev))
+    assert abs(l1.item() - R.l1_loss(a, b).item()) < 1e-6
+    assert abs(mse.item() - R.mse_loss(a, b).item()) < 1e-6
+    ar = a.clone().requires_grad_(True)
+    R.l1_loss(ar, b).backward()
+    g = rr.ops.loss_bwd(rr.ops.L1, a.to(dev), b.to(dev))
+    torch.testing.assert_close(g.cpu(), ar.grad)
+    # AdamW vs the restated torch update order
+    p = rnd(1000, seed=30)
+    gr = rnd(1000, seed=31)
+    pd, gd = p.to(dev), gr.to(dev)
+    m, v = torch.zeros_like(pd), torch.zeros_like(pd)
+    st = {}
+    ref = {"p": p.clone()}
+    for step in (1, 2, 3):
+        rr.ops.adamw_(pd, gd, m, v, 2e-4, 0.9, 0.999, 1e-8, 1e-4, True, step)
+        R.adamw_step(ref, {"p": gr}, st, 2e-4, weight_decay=1e-4)
+    torch.testing.assert_close(pd.cpu(), ref["p"], rtol=1e-6, atol=1e-7)
+    # uint8 truncation + PSNR (17:89-92, 08:123)
+    o = torch.rand(2, 3, 16, 16) * 1.2 - 0.1
+    u8 = rr.ops.to_uint8_hwc(o.to(dev)).cpu().numpy()
+    assert np.array_equal(u8, R.to_uint8_image(o))
+    c8 = R.to_uint8_image(torch.rand(2, 3, 16, 16))
+    ps = rr.ops.psnr_u8(torch.from_numpy(u8).to(dev), torch.from_numpy(c8).to(dev)).cpu().numpy()
+    for i in range(2):
+        assert abs(ps[i] - R.psnr_u8(c8[i], u8[i])) < 1e-9
+    lg = rnd(9, 43, seed=32)
+    lg[3, 5] = lg[3, 7] = lg[3].max() + 1       # tie: first index wins (18:47)
+    assert torch.equal(rr.ops.argmax_rows(lg.to(dev)).cpu(), R.top1(lg))
