@@ -17,7 +17,7 @@ namespace {
 // finalize of the conv-epilogue statistics -> scale / shift / running stats
 // partial [blocks][C][2] of the pre-bias accumulator.
 // 256 threads = 16 channels x 16 block-slices; double accumulation.
-__global__ void bn_finalize_kernel(int C, int blocks, double count, const float *__restrict__ part,
+__global__ void bn_finalize_kernel(int C, int blocks, double count, const double *__restrict__ part,
                                    const float *bias, const float *gamma, const float *beta,
                                    float *rmean, float *rvar, float momentum, float eps,
                                    float *scale, float *shift, float *smean, float *sinv,
@@ -29,7 +29,7 @@ __global__ void bn_finalize_kernel(int C, int blocks, double count, const float 
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
     for (int b = sl; b < blocks; b += 16) {
-      const float *p = part + ((long long)b * C + c) * 2;
+      const double *p = part + ((long long)b * C + c) * 2;
       s1 += p[0];
       s2 += p[1];
     }
@@ -332,15 +332,23 @@ int reduce_blocks(long long P) {
 
 }  // namespace
 
+extern "C" size_t rr_bn_finalize_workspace(int C, int blocks) {
+  return rr_colreduce_bytes(blocks, C * 2);
+}
+
 extern "C" int rr_bn_finalize(int C, int blocks, long long count, const float *part,
                               const float *bias, const float *gamma, const float *beta,
                               float *running_mean, float *running_var, float momentum,
                               float eps, float *scale, float *shift, float *save_mean,
-                              float *save_invstd, int64_t *num_batches_tracked,
-                              rr_stream stream) {
+                              float *save_invstd, int64_t *num_batches_tracked, void *ws,
+                              size_t ws_bytes, rr_stream stream) {
   if (C <= 0 || blocks <= 0 || count <= 0 || !part || !scale || !shift) return RR_EINVAL;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, (hipStream_t)stream,
-                     C, blocks, (double)count, part, bias, gamma, beta, running_mean,
+  if (!ws || ws_bytes < rr_colreduce_bytes(blocks, C * 2)) return RR_EWORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int chunks = rr_colreduce(part, blocks, C * 2, (double *)ws, st);
+  if (chunks < 0) return RR_ELAUNCH;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st,
+                     C, chunks, (double)count, (const double *)ws, bias, gamma, beta, running_mean,
                      running_var, momentum, eps, scale, shift, save_mean, save_invstd,
                      num_batches_tracked);
   RR_CHECK_LAUNCH();

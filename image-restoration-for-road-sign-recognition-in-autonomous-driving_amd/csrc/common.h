@@ -109,3 +109,34 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f) {
   const uint32_t t = __umulhi(n, f.m);
   return (t + n) >> f.s;
 }
+
+// Deterministic column reduction of fp32 partials: in [rows][cols] ->
+// out [chunks][cols] in fp64 (fixed order).  grid (ceil(cols/64), chunks),
+// 256 threads = 64 columns x 4 row lanes.  Feeds the finalize kernels so
+// their sequential part is at most `chunks` rows.
+__global__ static void rr_colreduce_kernel(const float *__restrict__ in, int rows, int cols,
+                                           int rows_per_chunk, double *__restrict__ out) {
+  __shared__ double red[4][64];
+  const int tc = threadIdx.x & 63, l = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tc;
+  const long long r0 = (long long)blockIdx.y * rows_per_chunk;
+  const long long r1 = min((long long)rows, r0 + rows_per_chunk);
+  double s = 0.0;
+  if (c < cols)
+    for (long long r = r0 + l; r < r1; r += 4) s += in[r * cols + c];
+  red[l][tc] = s;
+  __syncthreads();
+  if (l == 0 && c < cols) out[(long long)blockIdx.y * cols + c] = red[0][tc] + red[1][tc] + red[2][tc] + red[3][tc];
+}
+
+static inline int rr_colreduce_chunks(int rows) { return rows < 64 ? (rows < 1 ? 1 : rows) : 64; }
+static inline size_t rr_colreduce_bytes(int rows, int cols) {
+  return (size_t)rr_colreduce_chunks(rows) * cols * sizeof(double);
+}
+static inline int rr_colreduce(const float *in, int rows, int cols, double *out, hipStream_t st) {
+  const int chunks = rr_colreduce_chunks(rows);
+  const int rpc = (rows + chunks - 1) / chunks;
+  hipLaunchKernelGGL(rr_colreduce_kernel, dim3((cols + 63) / 64, chunks), dim3(256), 0, st, in, rows,
+                     cols, rpc, out);
+  return hipGetLastError() == hipSuccess ? chunks : -1;
+}

@@ -49,6 +49,7 @@ struct IgemmArgs {
   int P;              // n*h*w
   int ncblk;
   int cout_t;         // convT_up: channels per tap
+  int out_nchw;       // y1 = fp32 NCHW
 };
 
 template <typename T> struct Frag;
@@ -236,6 +237,24 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) { s1[mi][i] += v[i]; s2[mi][i] += v[i] * v[i]; }
       }
+      if (a.out_nchw) {
+        // model-boundary epilogue: fp32 NCHW (16 lanes = 16 consecutive pixels
+        // of one channel plane -> 64-B coalesced per register)
+        const int hw = a.h * a.w;
+        const int nn2 = p / hw, rem = p - nn2 * hw;
+        float *yo = reinterpret_cast<float *>(a.y1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = cb + i;
+          if (c >= a.cout) break;
+          float x = v[i] + (a.bias ? a.bias[c] : 0.f);
+          const long long o = ((long long)nn2 * a.cout + c) * hw + rem;
+          if (a.accumulate) x += yo[o];
+          if (a.act == RR_ACT_RELU) x = fmaxf(x, 0.f);
+          yo[o] = x;
+        }
+        continue;
+      }
       T *dst;
       const T *msk = nullptr;
       int cc = cb;
@@ -378,6 +397,7 @@ extern "C" int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
   if (d->mode == RR_CONVT_UP && (d->c_out % 4 || (d->c_out / 4) % 64 || d->out_split || d->want_stats))
     return RR_EUNSUPPORTED;
   if (d->has_mask && (!mask || d->out_split)) return RR_EINVAL;
+  if (d->out_nchw && (d->out_split || d->has_mask || d->mode == RR_CONVT_UP)) return RR_EINVAL;
   if (d->want_stats && !stats_partial) return RR_EINVAL;
   const long long P = (long long)d->n * d->h * d->w;
   if (P > 0x7fffffffLL / 4) return RR_EUNSUPPORTED;
@@ -393,6 +413,7 @@ extern "C" int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
   a.K = a.taps * a.cin;
   a.P = (int)P;
   a.cout_t = d->mode == RR_CONVT_UP ? d->c_out / 4 : d->c_out;
+  a.out_nchw = d->out_nchw;
   a.ncblk = 1;
   hipStream_t st = (hipStream_t)stream;
   if (d->dtype == RR_BF16) return dispatch<bf16_t>(d, a, st);

@@ -171,7 +171,7 @@ __global__ void conv_in_wgrad_kernel(int n, int h, int w, int cin, int cout,
   }
 }
 
-__global__ void conv_in_wgrad_finalize(int cout, int kk, int blocks, const float *__restrict__ part,
+__global__ void conv_in_wgrad_finalize(int cout, int kk, int blocks, const double *__restrict__ part,
                                        float *dw, float *db) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over cout*32
   if (i >= cout * 32) return;
@@ -302,7 +302,7 @@ __global__ void conv_out_bwd_kernel(int n, int h, int w, int cin, int cout,
   }
 }
 
-__global__ void conv_out_bwd_finalize(int cin, int cout, int blocks, const float *__restrict__ part,
+__global__ void conv_out_bwd_finalize(int cin, int cout, int blocks, const double *__restrict__ part,
                                       float *dw, float *db) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over cout*cin + cout
   if (i >= cout * cin + cout) return;
@@ -692,7 +692,8 @@ static int conv_in_wgrad_blocks(int n, int h, int w) {
 
 extern "C" size_t rr_conv_in_wgrad_workspace(int n, int h, int w, int cin, int cout) {
   (void)cin;
-  return (size_t)conv_in_wgrad_blocks(n, h, w) * cout * 32 * sizeof(float);
+  const int blocks = conv_in_wgrad_blocks(n, h, w);
+  return (size_t)blocks * cout * 32 * sizeof(float) + rr_colreduce_bytes(blocks, cout * 32);
 }
 
 extern "C" int rr_conv_in_wgrad(int dtype, int n, int h, int w, int cin, int cout, const float *x,
@@ -700,7 +701,8 @@ extern "C" int rr_conv_in_wgrad(int dtype, int n, int h, int w, int cin, int cou
                                 rr_stream stream) {
   if (!x || !dy || !dw || cin * 9 >= 32 || cout > 64 || cout <= 0) return RR_EINVAL;
   const int blocks = conv_in_wgrad_blocks(n, h, w);
-  if (!ws || ws_bytes < (size_t)blocks * cout * 32 * sizeof(float)) return RR_EWORKSPACE;
+  const size_t pbytes = (size_t)blocks * cout * 32 * sizeof(float);
+  if (!ws || ws_bytes < pbytes + rr_colreduce_bytes(blocks, cout * 32)) return RR_EWORKSPACE;
   const long long P = (long long)n * h * w;
   long long ppb = (P + blocks - 1) / blocks;
   hipStream_t st = (hipStream_t)stream;
@@ -711,8 +713,11 @@ extern "C" int rr_conv_in_wgrad(int dtype, int n, int h, int w, int cin, int cou
     hipLaunchKernelGGL(conv_in_wgrad_kernel<float>, dim3(blocks), dim3(256), 0, st, n, h, w, cin,
                        cout, x, (const float *)dy, (float *)ws, ppb);
   RR_CHECK_LAUNCH();
+  double *red = (double *)((char *)ws + pbytes);
+  const int chunks = rr_colreduce((const float *)ws, blocks, cout * 32, red, st);
+  if (chunks < 0) return RR_ELAUNCH;
   hipLaunchKernelGGL(conv_in_wgrad_finalize, dim3((cout * 32 + 255) / 256), dim3(256), 0, st, cout,
-                     cin * 9, blocks, (const float *)ws, dw, db);
+                     cin * 9, chunks, (const double *)red, dw, db);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }
@@ -778,7 +783,9 @@ static int conv_out_blocks(int n, int h, int w) {
 }
 
 extern "C" size_t rr_conv_out_bwd_workspace(int n, int h, int w, int cin, int cout) {
-  return (size_t)conv_out_blocks(n, h, w) * (cout + 1) * cin * sizeof(float);
+  const int blocks = conv_out_blocks(n, h, w);
+  return (size_t)blocks * (cout + 1) * cin * sizeof(float) +
+         rr_colreduce_bytes(blocks, (cout + 1) * cin);
 }
 
 extern "C" int rr_conv_out_bwd(int dtype, int n, int h, int w, int cin, int cout, const float *dy,
@@ -786,7 +793,8 @@ extern "C" int rr_conv_out_bwd(int dtype, int n, int h, int w, int cin, int cout
                                float *db, void *ws, size_t ws_bytes, rr_stream stream) {
   if (!dy || !x || !wt || cout > 4 || cout <= 0 || cin > 64) return RR_EINVAL;
   const int blocks = conv_out_blocks(n, h, w);
-  if (!ws || ws_bytes < (size_t)blocks * (cout + 1) * cin * sizeof(float)) return RR_EWORKSPACE;
+  const size_t pbytes = (size_t)blocks * (cout + 1) * cin * sizeof(float);
+  if (!ws || ws_bytes < pbytes + rr_colreduce_bytes(blocks, (cout + 1) * cin)) return RR_EWORKSPACE;
   const long long P = (long long)n * h * w;
   const long long ppb = (P + blocks - 1) / blocks;
   hipStream_t st = (hipStream_t)stream;
@@ -797,8 +805,11 @@ extern "C" int rr_conv_out_bwd(int dtype, int n, int h, int w, int cin, int cout
     hipLaunchKernelGGL(conv_out_bwd_kernel<float>, dim3(blocks), dim3(256), 0, st, n, h, w, cin,
                        cout, dy, (const float *)x, wt, (float *)dx, mask_relu, (float *)ws, ppb);
   RR_CHECK_LAUNCH();
+  double *red = (double *)((char *)ws + pbytes);
+  const int chunks = rr_colreduce((const float *)ws, blocks, (cout + 1) * cin, red, st);
+  if (chunks < 0) return RR_ELAUNCH;
   hipLaunchKernelGGL(conv_out_bwd_finalize, dim3((cout * cin + cout + 255) / 256), dim3(256), 0,
-                     st, cin, cout, blocks, (const float *)ws, dw, db);
+                     st, cin, cout, chunks, (const double *)red, dw, db);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

@@ -251,20 +251,27 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs a) {
     }
 }
 
-// dw[(a*CB + b)*taps + t] (+)= sum_s partial[s][a][t][b]
+// dw[(a*CB + b)*taps + t] (+)= sum_s partial[s][a][t][b]   (fixed order, 4 chains)
 __global__ void wgrad_reduce(const float *__restrict__ partial, float *__restrict__ dw,
                              int CA, int CB, int taps, int nsplit, int accumulate) {
   const long long total = (long long)CA * CB * taps;
   const long long slab = total;
   for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < total;
        o += (long long)gridDim.x * blockDim.x) {
-    // o indexes partial order (a, t, b)
     const int b = (int)(o % CB);
     const long long at = o / CB;
     const int t = (int)(at % taps);
     const int ar = (int)(at / taps);
-    float s = 0.f;
-    for (int sp = 0; sp < nsplit; ++sp) s += partial[sp * slab + o];
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int sp = 0;
+    for (; sp + 4 <= nsplit; sp += 4) {
+      s0 += partial[(sp + 0) * slab + o];
+      s1 += partial[(sp + 1) * slab + o];
+      s2 += partial[(sp + 2) * slab + o];
+      s3 += partial[(sp + 3) * slab + o];
+    }
+    for (; sp < nsplit; ++sp) s0 += partial[sp * slab + o];
+    const float s = (s0 + s1) + (s2 + s3);
     const long long di = ((long long)ar * CB + b) * taps + t;
     dw[di] = accumulate ? dw[di] + s : s;
   }
@@ -361,7 +368,7 @@ extern "C" int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
   int rc = d->dtype == RR_BF16 ? launch_t<bf16_t>(d, pl, a, st) : launch_t<float>(d, pl, a, st);
   if (rc) return rc;
   const long long total = (long long)pl.CA * pl.CB * pl.taps;
-  hipLaunchKernelGGL(wgrad_reduce, dim3(rr_grid_cap((total + 255) / 256)), dim3(256), 0, st,
+  hipLaunchKernelGGL(wgrad_reduce, dim3(rr_grid_cap((total + 255) / 256, 8192)), dim3(256), 0, st,
                      (const float *)ws, dw, pl.CA, pl.CB, pl.taps, pl.nsplit, d->accumulate);
   RR_CHECK_LAUNCH();
   return RR_OK;

@@ -22,7 +22,7 @@ _STATUS = {0: "ok", -1: "EINVAL", -2: "EUNSUPPORTED", -3: "ELAUNCH", -4: "EWORKS
 class IgemmDesc(C.Structure):
     _fields_ = [(n, C.c_int32) for n in (
         "dtype", "mode", "n", "h", "w", "c_in1", "c_in2", "c_out", "out_split", "act",
-        "accumulate", "has_bias", "has_mask", "want_stats")]
+        "accumulate", "has_bias", "has_mask", "want_stats", "out_nchw")]
 
 
 class WgradDesc(C.Structure):
@@ -50,7 +50,9 @@ _SIGS = {
     "rr_pack_conv": (I_, [I_, I_, I_, I_, P_, P_, P_, P_]),
     "rr_pack_convT": (I_, [I_, I_, I_, P_, P_, P_, P_]),
     "rr_bias_tile4": (I_, [I_, P_, P_, P_]),
-    "rr_bn_finalize": (I_, [I_, I_, L_, P_, P_, P_, P_, P_, P_, F_, F_, P_, P_, P_, P_, P_, P_]),
+    "rr_bn_finalize": (I_, [I_, I_, L_, P_, P_, P_, P_, P_, P_, F_, F_, P_, P_, P_, P_, P_, P_,
+                            S_, P_]),
+    "rr_bn_finalize_workspace": (S_, [I_, I_]),
     "rr_bn_eval_affine": (I_, [I_, P_, P_, P_, P_, F_, P_, P_, P_]),
     "rr_affine_act": (I_, [I_, L_, I_, P_, P_, P_, P_, P_, P_, P_, I_, P_, P_]),
     "rr_bn_bwd_blocks": (I_, [C.POINTER(BnBwdDesc)]),

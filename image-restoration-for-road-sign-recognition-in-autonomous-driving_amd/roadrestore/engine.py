@@ -164,7 +164,8 @@ def simple_unet_forward(m, x, wc, dt, need_bwd):
     u1, pku1 = _convT_up(wc, dt, m.up1, d2, n, H2, W2, need_bwd)
     d1a, pkd10, _ = _conv3(wc, dt, m.dec1[0], u1, e1, n, H, W, RELU, need_bwd)
     d1, pkd12, _ = _conv3(wc, dt, m.dec1[2], d1a, None, n, H, W, RELU, need_bwd)
-    out = ops.conv_out_fwd(d1, m.final.weight, m.final.bias)
+    out = ops.conv_out_fwd(d1, m.final.weight, m.final.bias,
+                           wpack=wc.conv(m.final.weight, dt, dgrad=False)[0])
     if need_bwd:
         S.update(e1a=e1a, e1=e1, p1=p1, i1=i1, e2a=e2a, e2=e2, p2=p2, i2=i2, ba=ba, b=b, u2=u2,
                  d2a=d2a, d2=d2, u1=u1, d1a=d1a, d1=d1, pk12=pk12, pk20=pk20, pk22=pk22,
@@ -366,7 +367,8 @@ def resunet_forward(m, x, wc, dt, training, need_bwd):
     d2, S.dec2 = resblock_forward(m.dec2, u2, r2, n, H // 2, W // 2, wc, dt, training, need_bwd)
     u1, pku1 = _convT_up(wc, dt, m.up1, d2, n, H // 2, W // 2, need_bwd)
     d1, S.dec1 = resblock_forward(m.dec1, u1, r1, n, H, W, wc, dt, training, need_bwd)
-    out = ops.conv_out_fwd(d1, m.final.weight, m.final.bias)
+    out = ops.conv_out_fwd(d1, m.final.weight, m.final.bias,
+                           wpack=wc.conv(m.final.weight, dt, dgrad=False)[0])
     if need_bwd:
         S.update(e1=e1, r1=r1, r2=r2, r3=r3, i1=i1, i2=i2, i3=i3, b=b, d3=d3, d2=d2, d1=d1,
                  pku3=pku3, pku2=pku2, pku1=pku1)
@@ -459,7 +461,7 @@ def vgg_features_forward(features, x, wc, dt, upto=None, need_bwd=False):
             act = RELU if kind == "conv_relu" else 0
             if cur is None:
                 y = ops.conv_in_fwd(x, mod.weight, mod.bias, dt, act=act)
-                pk = None
+                pk = wc.conv(mod.weight, dt, dgrad=True) if need_bwd else None
             else:
                 pk = wc.conv(mod.weight, dt, dgrad=need_bwd)
                 y, _, _ = ops.igemm(RR_CONV3X3, cur, None, n, h, w, pk[0], mod.weight.shape[0],
@@ -492,7 +494,8 @@ def vgg_features_backward_input(S, g_pre_last, x_grad_out=None, accumulate=False
             continue
         if xin is None:   # first layer: image grad
             cin = mod.weight.shape[1]
-            return ops.conv_in_dgrad(g, mod.weight, cin, out=x_grad_out, accumulate=accumulate)
+            return ops.conv_in_dgrad(g, mod.weight, cin, out=x_grad_out, accumulate=accumulate,
+                                     wpack_dgrad=pk[1] if pk is not None else None)
         prev_relu = acts[li - 1][0] == "conv_relu"
         g, _, _ = ops.igemm(RR_CONV3X3, g, None, S.n, h, w, pk[1], mod.weight.shape[1],
                             mask=xin if prev_relu else None)

@@ -99,7 +99,7 @@ def bias_tile4(b: torch.Tensor):
 # implicit GEMM
 
 def igemm(mode, x1, x2, n, h, w, wpack, cout, bias=None, act=0, out=None, out2=None,
-          split=0, accumulate=False, mask=None, stats=False):
+          split=0, accumulate=False, mask=None, stats=False, out_nchw=False):
     """Run rr_igemm.  Returns (y1, y2, stats_partial_or_None).
 
     mode RR_CONV3X3 / RR_CONV1X1: y [n, h, w, cout]
@@ -111,10 +111,12 @@ def igemm(mode, x1, x2, n, h, w, wpack, cout, bias=None, act=0, out=None, out2=N
     c1 = x1.shape[-1]
     c2 = x2.shape[-1] if x2 is not None else 0
     d = IgemmDesc(rr_dtype(dt), mode, n, h, w, c1, c2, cout, split, act, int(accumulate),
-                  int(bias is not None), int(mask is not None), int(stats))
+                  int(bias is not None), int(mask is not None), int(stats), int(out_nchw))
     dev = x1.device
     if out is None:
-        if mode == RR_CONVT_UP:
+        if out_nchw:
+            out = torch.empty((n, cout, h, w), dtype=torch.float32, device=dev)
+        elif mode == RR_CONVT_UP:
             out = torch.empty((n, 2 * h, 2 * w, cout // 4), dtype=dt, device=dev)
         elif split:
             out = torch.empty((n, h, w, split), dtype=dt, device=dev)
@@ -178,10 +180,12 @@ def bn_finalize(st, count, bias, gamma, beta, running_mean, running_var, momentu
     shift = torch.empty_like(scale)
     mean = torch.empty_like(scale)
     inv = torch.empty_like(scale)
+    ws = _ws(lib().rr_bn_finalize_workspace(Cc, blocks), dev)
     lib().check(lib().rr_bn_finalize(Cc, blocks, int(count), _p(st), _p(bias), _p(gamma), _p(beta),
                                      _p(running_mean), _p(running_var), float(momentum),
                                      float(eps), _p(scale), _p(shift), _p(mean), _p(inv),
-                                     _p(num_batches_tracked), stream()), "rr_bn_finalize")
+                                     _p(num_batches_tracked), _p(ws), ws.numel(), stream()),
+                "rr_bn_finalize")
     return scale, shift, mean, inv
 
 
@@ -312,8 +316,15 @@ def conv_in_wgrad(x_nchw, dy, dw_shape=None, dw=None, db=None):
     return dw, db
 
 
-def conv_in_dgrad(dy, wt, cin, out=None, accumulate=False):
+def conv_in_dgrad(dy, wt, cin, out=None, accumulate=False, wpack_dgrad=None):
+    """Image grad of the first 3x3 conv (cin = 3): an implicit GEMM with K =
+    9*cout and cin GEMM columns, written straight into NCHW fp32.  Without
+    a packed dgrad weight it uses the VALU kernel rr_conv_in_dgrad."""
     n, h, w, cout = dy.shape
+    if wpack_dgrad is not None and cout % 64 == 0:
+        y, _, _ = igemm(RR_CONV3X3, dy, None, n, h, w, wpack_dgrad, cin, out=out,
+                        accumulate=accumulate, out_nchw=True)
+        return y
     if out is None:
         out = torch.empty((n, cin, h, w), dtype=torch.float32, device=dy.device)
     lib().check(lib().rr_conv_in_dgrad(rr_dtype(dy.dtype), n, h, w, cin, cout, _p(dy), _p(wt),
@@ -334,9 +345,14 @@ def prelu_bwd(dy, y_pre, alpha, dalpha=None):
     return dx, dalpha
 
 
-def conv_out_fwd(x, wt, b):
+def conv_out_fwd(x, wt, b, wpack=None):
+    """Final 1x1 conv cin -> cout (3) into NCHW fp32: implicit GEMM with the
+    NCHW epilogue when a packed weight is given, else the VALU kernel."""
     n, h, w, cin = x.shape
     cout = wt.shape[0]
+    if wpack is not None and cin % 64 == 0:
+        y, _, _ = igemm(RR_CONV1X1, x, None, n, h, w, wpack, cout, bias=b, out_nchw=True)
+        return y
     y = torch.empty((n, cout, h, w), dtype=torch.float32, device=x.device)
     lib().check(lib().rr_conv_out_fwd(rr_dtype(x.dtype), n, h, w, cin, cout, _p(x),
                                       _p(wt.reshape(cout, cin)), _p(b), _p(y), stream()),

@@ -72,6 +72,9 @@ typedef struct {
   int32_t has_bias;    /* bias[c] (fp32) added                               */
   int32_t has_mask;    /* result *= (mask[p, c] > 0); mask has y's layout    */
   int32_t want_stats;  /* per-(row-block, column) partial sum / sum of squares */
+  int32_t out_nchw;    /* y1 is fp32 NCHW [n][c_out][h][w] (model boundary:
+                          the 64->3 final conv 07:96 / 14:149, and the image
+                          grad of the perceptual slice's conv1_1, 14:196) */
 } rr_igemm_desc;
 
 /* packed weights: w[c_out][taps][c_in1+c_in2] in dtype (see rr_pack_*). */
@@ -123,8 +126,11 @@ int rr_bn_finalize(int C, int blocks, long long count, const float *stats_partia
                    const float *bias, const float *gamma, const float *beta,
                    float *running_mean, float *running_var, float momentum,
                    float eps, float *scale, float *shift, float *save_mean,
-                   float *save_invstd, int64_t *num_batches_tracked,
-                   rr_stream stream);
+                   float *save_invstd, int64_t *num_batches_tracked, void *ws,
+                   size_t ws_bytes, rr_stream stream);
+/* workspace of rr_bn_finalize: the [blocks][C][2] partials are first folded to
+ * <= 64 fp64 rows by a parallel fixed-order column reduction */
+size_t rr_bn_finalize_workspace(int C, int blocks);
 /* eval mode: scale/shift from running stats (17:64 model.eval()) */
 int rr_bn_eval_affine(int C, const float *gamma, const float *beta,
                       const float *running_mean, const float *running_var,

@@ -1,0 +1,83 @@
+"""The C ABI: the library loads without a GPU and exports every entry point
+include/roadrestore.h declares; descriptors match the header layout; the
+module trees match the reference's state_dict manifests.  No compute calls."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from oracle import seeded as S
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    txt = open(os.path.join(REPO, "include", "roadrestore.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(rr_[A-Za-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    import roadrestore
+    lib = roadrestore.lib()
+    declared = header_functions()
+    assert len(declared) >= 30
+    missing = [n for n in declared if not hasattr(lib.dll, n)]
+    assert not missing, missing
+    assert set(declared) == set(roadrestore.EXPORTED)
+    assert lib.rr_version().startswith(b"roadrestore")
+
+
+def test_descriptor_layouts():
+    from roadrestore._lib import BnBwdDesc, IgemmDesc, WgradDesc
+    assert ctypes.sizeof(IgemmDesc) == 15 * 4
+    assert ctypes.sizeof(WgradDesc) == 9 * 4
+    assert ctypes.sizeof(BnBwdDesc) == 32     # int32, pad, int64, 3 x int32, pad (C layout)
+
+
+def test_status_codes_raise():
+    from roadrestore._lib import Lib
+    with pytest.raises(RuntimeError, match="EINVAL"):
+        Lib.check(-1, "x")
+
+
+def test_invalid_descriptor_rejected_without_gpu():
+    """Validation happens before any launch: a bad descriptor returns EINVAL."""
+    import roadrestore
+    from roadrestore._lib import IgemmDesc
+    lib = roadrestore.lib()
+    d = IgemmDesc(0, 0, 0, 8, 8, 64, 0, 64, 0, 0, 0, 0, 0, 0, 0)   # n = 0
+    assert lib.rr_igemm(ctypes.byref(d), None, None, None, None, None, None, None, None, None) == -1
+    d = IgemmDesc(1, 0, 1, 8, 8, 48, 0, 64, 0, 0, 0, 0, 0, 0, 0)   # c_in not a multiple of 64
+    assert lib.rr_igemm(ctypes.byref(d), 1, None, 1, None, 1, None, None, None, None) == -2
+
+
+@pytest.mark.parametrize("name,cls", [("simpleunet", "SimpleUNet"), ("resunet", "ResUNet")])
+def test_module_trees_match_reference(name, cls):
+    import roadrestore as rr
+    m = getattr(rr, cls)()
+    got = [[k, list(v.shape)] for k, v in m.state_dict().items()]
+    assert got == S.load_manifest(name)
+
+
+def test_vgg_trees_match_reference():
+    import roadrestore as rr
+    got = [[k, list(v.shape)] for k, v in rr.VGGPerceptualLoss().state_dict().items()]
+    assert got == S.load_manifest("perceptual")
+    got = [[k, list(v.shape)] for k, v in rr.vgg16(num_classes=43).state_dict().items()]
+    assert got == S.load_manifest("vgg16")
+
+
+def test_reference_state_dict_loads():
+    import roadrestore as rr
+    m = rr.ResUNet()
+    m.load_state_dict(S.model_state_dict("resunet"))     # strict: every key and shape
+
+
+def test_cpu_tensors_rejected():
+    import torch
+    import roadrestore as rr
+    m = rr.ResUNet()
+    with pytest.raises(RuntimeError, match="GPU"):
+        m(torch.zeros(1, 3, 64, 64))

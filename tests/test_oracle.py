@@ -1,0 +1,109 @@
+"""The CPU oracle (oracle/reference_cpu.py) against the golden fixtures the
+REFERENCE classes produced (oracle/gen_golden.py).  Runs without a GPU."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import reference_cpu as R
+from oracle import seeded as S
+
+
+def gold(name):
+    return np.load(os.path.join(S.GOLDEN_DIR, name + ".npz"))
+
+
+def test_seeded_inputs_reproduce_fixtures():
+    z = gold("resunet_64")
+    clean = S.image_batch(2, 64, 64, seed=30 + 64)
+    assert torch.equal(clean, torch.from_numpy(z["clean"]))
+    assert torch.equal(S.fog_noise(clean, seed=40 + 64), torch.from_numpy(z["bad"]))
+    z = gold("resunet_224")
+    bad = S.fog_noise(S.image_batch(1, 224, 224, seed=30 + 224), seed=40 + 224)
+    assert abs(bad.double().sum().item() - z["bad_sum"][0]) < 1e-6
+
+
+def test_simpleunet_oracle_bitwise():
+    z = gold("simpleunet_64")
+    p = S.model_state_dict("simpleunet")
+    out = R.simple_unet_forward(p, torch.from_numpy(z["bad"]))
+    assert torch.equal(out, torch.from_numpy(z["out"]))
+
+
+def test_resunet_oracle_eval_and_train():
+    z = gold("resunet_64")
+    sd = S.model_state_dict("resunet")
+    bad = torch.from_numpy(z["bad"])
+    with torch.no_grad():
+        out = R.resunet_forward({k: v.clone() for k, v in sd.items()}, bad, training=False)
+    assert torch.equal(out, torch.from_numpy(z["out_eval"]))
+    p = {k: v.clone() for k, v in sd.items()}
+    with torch.no_grad():
+        out = R.resunet_forward(p, bad, training=True)
+    assert torch.equal(out, torch.from_numpy(z["out_train"]))
+    keys = [str(k) for k in z["running_keys"]]
+    got = torch.cat([p[k].reshape(-1) for k in keys]).numpy()
+    assert np.array_equal(got, z["running_vals"])
+    assert p["res1.conv_block.1.num_batches_tracked"].item() == 1
+
+
+def test_unified_loss_oracle():
+    z = gold("resunet_64")
+    sd = S.model_state_dict("resunet")
+    perc = S.seeded_state_dict(S.load_manifest("perceptual"), seed=5)
+    bad, clean = torch.from_numpy(z["bad"]), torch.from_numpy(z["clean"])
+    with torch.no_grad():
+        out = R.resunet_forward({k: v.clone() for k, v in sd.items()}, bad, True)
+        assert abs(R.l1_loss(out, clean).item() - z["l_pix"][0]) == 0
+        assert abs(R.perceptual_loss(perc, out, clean).item() - z["l_perc"][0]) <= 1e-6 * z["l_perc"][0]
+        assert abs(R.perceptual_loss(perc, bad, clean).item() - z["perc_bad_clean"][0]) <= 1e-6
+
+
+def test_postprocess_psnr_oracle():
+    z = gold("resunet_64")
+    u8 = R.to_uint8_image(torch.from_numpy(z["out_eval"]))
+    assert np.array_equal(u8, z["out_u8"])
+    for i in range(2):
+        assert abs(R.psnr_u8(z["clean_u8"][i], z["out_u8"][i]) - z["psnr"][i]) < 1e-12
+    a = np.zeros((4, 4, 3), np.uint8)
+    assert R.psnr_u8(a, a) == float("inf")
+
+
+@pytest.mark.parametrize("H", [64])
+def test_vgg16_oracle_logits(H):
+    z = gold(f"vgg16_{H}")
+    sd = S.seeded_state_dict(S.load_manifest("vgg16"), seed=3)
+    x = S.classifier_batch(8, H, seed=50 + H)
+    assert torch.equal(x, torch.from_numpy(z["x"]))
+    with torch.no_grad():
+        lg = R.vgg16_forward(sd, x)
+    assert torch.equal(lg, torch.from_numpy(z["logits"]))
+    assert np.array_equal(R.top1(lg).numpy(), z["pred"])
+
+
+def test_adamw_restatement_matches_torch():
+    p = torch.randn(100)
+    g = torch.randn(100)
+    ref = p.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([ref], lr=2e-4, weight_decay=1e-4)
+    st = {}
+    mine = {"p": p.clone()}
+    for _ in range(3):
+        ref.grad = g.clone()
+        opt.step()
+        R.adamw_step(mine, {"p": g}, st, 2e-4, weight_decay=1e-4)
+    assert torch.equal(mine["p"], ref.detach())
+
+
+def test_cosine_schedule():
+    sch_lr = []
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.AdamW([p], lr=2e-4)
+    sch = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=25)
+    for e in range(25):
+        sch_lr.append(opt.param_groups[0]["lr"])
+        opt.step()
+        sch.step()
+    for e, lr in enumerate(sch_lr):
+        assert abs(lr - R.cosine_lr(2e-4, e, 25)) < 1e-12
