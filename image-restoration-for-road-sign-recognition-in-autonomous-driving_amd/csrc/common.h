@@ -72,6 +72,19 @@ template <> __device__ __forceinline__ void store4<bf16_t>(bf16_t *p, f32x4 v) {
   *reinterpret_cast<u16x4 *>(p) = r;
 }
 
+// 8 consecutive elements (one 16-B bf16 store / two 16-B fp32 stores)
+template <typename T> __device__ __forceinline__ void store8(T *p, f32x4 a, f32x4 b);
+template <> __device__ __forceinline__ void store8<float>(float *p, f32x4 a, f32x4 b) {
+  *reinterpret_cast<f32x4 *>(p) = a;
+  *reinterpret_cast<f32x4 *>(p + 4) = b;
+}
+template <> __device__ __forceinline__ void store8<bf16_t>(bf16_t *p, f32x4 a, f32x4 b) {
+  u16x8 r;
+  r[0] = f32_to_bf16(a[0]); r[1] = f32_to_bf16(a[1]); r[2] = f32_to_bf16(a[2]); r[3] = f32_to_bf16(a[3]);
+  r[4] = f32_to_bf16(b[0]); r[5] = f32_to_bf16(b[1]); r[6] = f32_to_bf16(b[2]); r[7] = f32_to_bf16(b[3]);
+  *reinterpret_cast<u16x8 *>(p) = r;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

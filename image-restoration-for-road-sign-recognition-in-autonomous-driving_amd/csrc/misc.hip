@@ -226,6 +226,68 @@ __global__ void conv_in_dgrad_kernel(int n, int h, int w, int cin, int cout,
 }
 
 // ---------------------------------------------------------------------------
+// im2col of the first 3x3 conv straight from the NCHW fp32 image:
+// col[p][j] = x[n][ci][h+ky-1][w+kx-1] for j = ci*9 + ky*3 + kx < 9*cin,
+// col[p][9*cin] = 1 (the bias column: its wgrad column is the bias grad),
+// 0 up to kpad.  The first conv then runs as a K = kpad implicit GEMM.
+template <typename T>
+__global__ void im2col3_kernel(int n, int h, int w, int cin, int kpad, const float *__restrict__ x,
+                               T *__restrict__ col) {
+  const int G = kpad / 4;
+  const long long total = (long long)n * h * w * G;
+  const int kk = cin * 9;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int g = (int)(i % G);
+    const long long p = i / G;
+    const int ww = (int)(p % w);
+    const long long nh = p / w;
+    const int hh = (int)(nh % h);
+    const int nn = (int)(nh / h);
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = g * 4 + e;
+      float val = 0.f;
+      if (j < kk) {
+        const int ci = j / 9, t = j - (j / 9) * 9;
+        const int y2 = hh + t / 3 - 1, x2 = ww + t % 3 - 1;
+        if (y2 >= 0 && y2 < h && x2 >= 0 && x2 < w)
+          val = x[(((long long)nn * cin + ci) * h + y2) * w + x2];
+      } else if (j == kk) {
+        val = 1.f;
+      }
+      v[e] = val;
+    }
+    store4<T>(col + p * kpad + g * 4, v);
+  }
+}
+
+// first-layer weights [co][ci][3][3] (+ bias) -> [co][kpad] GEMM layout
+template <typename T>
+__global__ void pack_in_kernel(int cout, int cin, int kpad, const float *__restrict__ w,
+                               const float *__restrict__ b, T *__restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cout * kpad) return;
+  const int co = i / kpad, j = i % kpad, kk = cin * 9;
+  float v = 0.f;
+  if (j < kk) v = w[(long long)co * kk + j];
+  else if (j == kk && b) v = b[co];
+  Elt<T>::store(out, i, v);
+}
+
+__global__ void unpack_in_grad_kernel(int cout, int cin, int kpad, const float *__restrict__ g,
+                                      float *dw, float *db) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int kk = cin * 9;
+  if (i >= cout * (kk + 1)) return;
+  const int co = i / (kk + 1), j = i % (kk + 1);
+  const float v = g[(long long)co * kpad + j];
+  if (j < kk) dw[(long long)co * kk + j] = v;
+  else if (db) db[co] = v;
+}
+
+// ---------------------------------------------------------------------------
 // last layer: y[n][co][h][w] = b[co] + sum_ci x[p][ci] w[co][ci]; thread = pixel
 template <typename T>
 __global__ void conv_out_fwd_kernel(int n, int h, int w, int cin, int cout, const T *__restrict__ x,
@@ -659,6 +721,42 @@ extern "C" int rr_bias_tile4(int c_out, const float *b, float *b4, rr_stream str
   if (!b || !b4 || c_out <= 0) return RR_EINVAL;
   hipLaunchKernelGGL(bias_tile4_kernel, dim3((4 * c_out + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, c_out, b, b4);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_im2col3(int dtype, int n, int h, int w, int cin, int kpad, const float *x,
+                          void *col, rr_stream stream) {
+  if (!x || !col || cin <= 0 || kpad % 4 || kpad < 9 * cin + 1) return RR_EINVAL;
+  const long long total = (long long)n * h * w * (kpad / 4);
+  dim3 g(rr_grid_cap((total + 255) / 256, 8192)), b(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(im2col3_kernel<bf16_t>, g, b, 0, st, n, h, w, cin, kpad, x, (bf16_t *)col);
+  else
+    hipLaunchKernelGGL(im2col3_kernel<float>, g, b, 0, st, n, h, w, cin, kpad, x, (float *)col);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_pack_conv_in(int dtype, int cout, int cin, int kpad, const float *w,
+                               const float *b, void *out, rr_stream stream) {
+  if (!w || !out || kpad < 9 * cin + 1) return RR_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 g((cout * kpad + 255) / 256), bl(256);
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(pack_in_kernel<bf16_t>, g, bl, 0, st, cout, cin, kpad, w, b, (bf16_t *)out);
+  else
+    hipLaunchKernelGGL(pack_in_kernel<float>, g, bl, 0, st, cout, cin, kpad, w, b, (float *)out);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_unpack_conv_in_grad(int cout, int cin, int kpad, const float *g, float *dw,
+                                      float *db, rr_stream stream) {
+  if (!g || !dw || kpad < 9 * cin + 1) return RR_EINVAL;
+  hipLaunchKernelGGL(unpack_in_grad_kernel, dim3((cout * (9 * cin + 1) + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, cout, cin, kpad, g, dw, db);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

@@ -44,10 +44,12 @@ class WeightCache:
     def __init__(self):
         self._c = {}
 
-    def _get(self, w, dtype, kind, fn):
+    def _get(self, w, dtype, kind, fn, also=None):
+        from .optim import GENERATION
         cap = torch.cuda.is_current_stream_capturing()
         key = (id(w), dtype, kind)
-        ver = (w.data_ptr(), w._version)
+        ver = (w.data_ptr(), w._version, GENERATION[0],
+               None if also is None else (also.data_ptr(), also._version))
         e = None if cap else self._c.get(key)
         if e is not None and e[0] == ver:
             return e[1]
@@ -67,6 +69,9 @@ class WeightCache:
     def linear(self, w, dtype):
         return self._get(w, dtype, "linear", lambda: ops.pack_conv(
             w.view(w.shape[0], w.shape[1], 1, 1), dtype, True, False))
+
+    def conv_in(self, w, b, dtype):
+        return self._get(w, dtype, "conv_in", lambda: ops.pack_conv_in(w, b, dtype), also=b)
 
     def bias4(self, b):
         return self._get(b, torch.float32, "b4", lambda: ops.bias_tile4(b))
@@ -148,7 +153,9 @@ def _convT_up(wc, dt, conv, x, n, h, w, need_bwd):
 def simple_unet_forward(m, x, wc, dt, need_bwd):
     n, _, H, W = x.shape
     S = Bag(n=n, H=H, W=W, x=x)
-    e1a = ops.conv_in_fwd(x, m.enc1[0].weight, m.enc1[0].bias, dt, act=RELU)
+    e1a, col = ops.first_conv_fwd(x, m.enc1[0].weight, m.enc1[0].bias, dt,
+                                  wc.conv_in(m.enc1[0].weight, m.enc1[0].bias, dt), act=RELU)
+    S.col = col
     e1, pk12, _ = _conv3(wc, dt, m.enc1[2], e1a, None, n, H, W, RELU, need_bwd)
     p1, i1 = ops.maxpool2_fwd(e1)
     H2, W2 = H // 2, W // 2
@@ -226,7 +233,7 @@ def simple_unet_backward(m, S, g_out, sink):
     sink.ready(_params(m.enc2))
     ops.maxpool2_bwd(g_p1, S.i1, H, W, out=g_e1, accumulate=True, mask=S.e1)
     g_e1a, _ = _conv3_bwd(m.enc1[2], S.pk12, g_e1, S.e1a, None, n, H, W, sink, mask=S.e1a)
-    ops.conv_in_wgrad(S.x, g_e1a, dw=sink[m.enc1[0].weight], db=sink[m.enc1[0].bias])
+    ops.first_conv_wgrad(S.col, g_e1a, sink[m.enc1[0].weight], sink[m.enc1[0].bias])
     sink.ready(_params(m.enc1))
 
 
@@ -344,13 +351,12 @@ def resunet_forward(m, x, wc, dt, training, need_bwd):
             "alignment branch, 14:169-182, is not implemented on this path)")
     S = Bag(n=n, H=H, W=W, x=x)
     pr = m.enc1[1]
+    e1pre, col = ops.first_conv_fwd(x, m.enc1[0].weight, m.enc1[0].bias, dt,
+                                    wc.conv_in(m.enc1[0].weight, m.enc1[0].bias, dt))
+    one, zero = _unit_affine(m.enc1[0].weight.shape[0], x.device)
+    e1 = ops.affine_act(e1pre, one, zero, alpha=pr.weight)
     if need_bwd:
-        e1pre = ops.conv_in_fwd(x, m.enc1[0].weight, m.enc1[0].bias, dt, act=0)
-        one, zero = _unit_affine(64, x.device)
-        e1 = ops.affine_act(e1pre, one, zero, alpha=pr.weight)
-        S.e1pre = e1pre
-    else:
-        e1 = ops.conv_in_fwd(x, m.enc1[0].weight, m.enc1[0].bias, dt, act=2, alpha=pr.weight)
+        S.e1pre, S.col = e1pre, col
     r1, S.res1 = resblock_forward(m.res1, e1, None, n, H, W, wc, dt, training, need_bwd)
     p1, i1 = ops.maxpool2_fwd(r1)
     r2, S.res2 = resblock_forward(m.res2, p1, None, n, H // 2, W // 2, wc, dt, training, need_bwd)
@@ -421,7 +427,7 @@ def resunet_backward(m, S, g_out, sink):
     g_e1, _ = resblock_backward(m.res1, S.res1, g_r1, sink)
     pr = m.enc1[1]
     g_e1pre, _ = ops.prelu_bwd(g_e1, S.e1pre, pr.weight, dalpha=sink[pr.weight])
-    ops.conv_in_wgrad(S.x, g_e1pre, dw=sink[m.enc1[0].weight], db=sink[m.enc1[0].bias])
+    ops.first_conv_wgrad(S.col, g_e1pre, sink[m.enc1[0].weight], sink[m.enc1[0].bias])
     sink.ready(_params(m.enc1))
 
 
@@ -460,7 +466,8 @@ def vgg_features_forward(features, x, wc, dt, upto=None, need_bwd=False):
         if kind in ("conv", "conv_relu"):
             act = RELU if kind == "conv_relu" else 0
             if cur is None:
-                y = ops.conv_in_fwd(x, mod.weight, mod.bias, dt, act=act)
+                y, _ = ops.first_conv_fwd(x, mod.weight, mod.bias, dt,
+                                          wc.conv_in(mod.weight, mod.bias, dt), act=act)
                 pk = wc.conv(mod.weight, dt, dgrad=True) if need_bwd else None
             else:
                 pk = wc.conv(mod.weight, dt, dgrad=need_bwd)

@@ -51,13 +51,14 @@ def _need_cuda(*ts):
 PROBE = None
 
 
-def _kpick_bc(mode, n, h, w, cout, split):
-    """Mirror of csrc/igemm.hip pick_bc (for naming the template instance)."""
+def _kpick_tile(mode, n, h, w, cout, split):
+    """Mirror of csrc/igemm.hip pick_tile (names the template instance)."""
     P = n * h * w
-    pb = (P + 127) // 128
-    if cout % 128 == 0 and pb * (cout // 128) >= 512 and (split == 0 or split % 128 == 0):
-        return 128
-    return 64
+    if cout % 128 == 0 and (split == 0 or split % 128 == 0) and ((P + 127) // 128) * (cout // 128) >= 512:
+        return 128, 128, 2
+    if cout <= 64 and (P + 255) // 256 >= 512:
+        return 64, 256, 1
+    return 64, 128, 2
 
 
 def _ws(nbytes, device):
@@ -135,8 +136,8 @@ def igemm(mode, x1, x2, n, h, w, wpack, cout, bias=None, act=0, out=None, out2=N
         launch()
     else:
         taps = 9 if mode == RR_CONV3X3 else (4 if mode == RR_CONVT_DOWN else 1)
-        bc = _kpick_bc(mode, n, h, w, cout, split)
-        sym = f"igemm_kernel<{'bf16' if dt == torch.bfloat16 else 'f32'},{bc},128,mode{mode}>"
+        bc, bp, wc = _kpick_tile(mode, n, h, w, cout, split)
+        sym = f"igemm_kernel<{'bf16' if dt == torch.bfloat16 else 'f32'},{bc},{bp},{wc},mode{mode}>"
         PROBE(sym, 2.0 * n * h * w * cout * taps * (c1 + c2), launch)
     return out, out2, st
 
@@ -291,6 +292,45 @@ def maxpool2_bwd(dy, idx, h, w, out=None, accumulate=False, mask=None):
     lib().check(lib().rr_maxpool2_bwd(rr_dtype(dy.dtype), n, h, w, Cc, _p(dy), _p(idx), _p(out),
                                       int(accumulate), _p(mask), stream()), "rr_maxpool2_bwd")
     return out
+
+
+KPAD_IN = 64      # K of the first-layer GEMM: 27 taps x channels + bias column, padded
+
+
+def im2col3(x_nchw, dtype, kpad=KPAD_IN):
+    n, cin, h, w = x_nchw.shape
+    col = torch.empty((n, h, w, kpad), dtype=dtype, device=x_nchw.device)
+    lib().check(lib().rr_im2col3(rr_dtype(dtype), n, h, w, cin, kpad, _p(x_nchw.contiguous()),
+                                 _p(col), stream()), "rr_im2col3")
+    return col
+
+
+def pack_conv_in(wt, b, dtype, kpad=KPAD_IN):
+    cout, cin = wt.shape[0], wt.shape[1]
+    out = torch.empty(cout * kpad, dtype=dtype, device=wt.device)
+    lib().check(lib().rr_pack_conv_in(rr_dtype(dtype), cout, cin, kpad, _p(wt.contiguous()), _p(b),
+                                      _p(out), stream()), "rr_pack_conv_in")
+    return out
+
+
+def first_conv_fwd(x_nchw, wt, b, dtype, wpack, act=0):
+    """First 3x3 conv (cin = 3) as im2col + K=64 implicit GEMM (bias in the
+    GEMM).  Returns (y NHWC, col) -- col is kept for the weight gradient."""
+    n, cin, h, w = x_nchw.shape
+    col = im2col3(x_nchw, dtype)
+    y, _, _ = igemm(RR_CONV1X1, col, None, n, h, w, wpack, wt.shape[0], act=act)
+    return y, col
+
+
+def first_conv_wgrad(col, dy, dw, db):
+    """Weight + bias grad of the first conv from its im2col matrix."""
+    n, h, w, kpad = col.shape
+    cout = dy.shape[-1]
+    cin = dw.shape[1]
+    g = wgrad(RR_CONV1X1, dy, col, None, n, h, w, cout, dw_shape=(cout, kpad, 1, 1))
+    lib().check(lib().rr_unpack_conv_in_grad(cout, cin, kpad, _p(g), _p(dw), _p(db), stream()),
+                "rr_unpack_conv_in_grad")
+    return dw, db
 
 
 def conv_in_fwd(x_nchw, wt, b, dtype, act=0, alpha=None):

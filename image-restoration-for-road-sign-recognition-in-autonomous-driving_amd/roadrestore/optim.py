@@ -19,6 +19,17 @@ from ._lib import lib
 
 CosineAnnealingLR = torch.optim.lr_scheduler.CosineAnnealingLR
 
+# global parameter generation: incremented by every fused optimizer step
+# (engine.WeightCache keys on it in addition to the tensor version counters)
+GENERATION = [0]
+
+
+def _bump_versions(tensors):
+    GENERATION[0] += 1
+    inc = getattr(torch.autograd.graph, "increment_version", None)
+    if inc is not None:
+        inc(tensors)
+
 
 def flatten_parameters(model, order=None):
     """Re-home ``model``'s parameters into one contiguous fp32 buffer laid out
@@ -113,6 +124,10 @@ class _FusedAdamBase(torch.optim.Optimizer):
                                self.decoupled, step)
             for p in ps:
                 self.state.setdefault(p, {})["step"] = step
+            # the fused kernel wrote through raw pointers: bump the version
+            # counters so packed-weight caches (engine.WeightCache) and autograd
+            # see the in-place update
+            _bump_versions([p.data for p in ps])
         return loss
 
 

@@ -204,6 +204,19 @@ int rr_maxpool2_bwd(int dtype, int n, int h, int w, int C, const void *dy,
 int rr_conv_in_fwd(int dtype, int n, int h, int w, int cin, int cout,
                    const float *x, const float *wt, const float *b,
                    int act, const float *alpha, void *y, rr_stream stream);
+/* MFMA form of the first conv: im2col of the NCHW fp32 image into an NHWC
+ * [P][kpad] matrix (j = ci*9+ky*3+kx, column 9*cin = 1.0 carries the bias,
+ * zero-padded to kpad, a multiple of the GEMM K step), and the matching
+ * [cout][kpad] weight pack (bias in column 9*cin).  The conv is then
+ * rr_igemm(RR_CONV1X1, c_in1 = kpad) and its weight+bias grad is
+ * rr_wgrad(RR_CONV1X1) on the same im2col matrix. */
+int rr_im2col3(int dtype, int n, int h, int w, int cin, int kpad, const float *x,
+               void *col, rr_stream stream);
+int rr_pack_conv_in(int dtype, int cout, int cin, int kpad, const float *wt,
+                    const float *b, void *out, rr_stream stream);
+/* [cout][kpad] fp32 wgrad of that GEMM -> torch-layout dW [cout][cin][3][3], db */
+int rr_unpack_conv_in_grad(int cout, int cin, int kpad, const float *g, float *dw,
+                           float *db, rr_stream stream);
 /* its weight/bias grads given dy (NHWC, pre-activation grad) */
 int rr_conv_in_wgrad(int dtype, int n, int h, int w, int cin, int cout,
                      const float *x, const void *dy, float *dw, float *db,

@@ -254,3 +254,42 @@ def test_vgg16_top1_golden(dev):
         assert _rel(lg.cpu(), ref) <= 1e-3 * max(1, ref.abs().max().item())
         pred = rr.ops.argmax_rows(lg).cpu().numpy()
         assert np.array_equal(pred, z["pred"])
+
+
+def test_multi_step_training_matches_oracle(dev):
+    """Three SimpleUNet Adam steps (07:151-160): weights updated by the fused
+    optimizer must be the ones the next forward packs (version bump)."""
+    import roadrestore as rr
+    from roadrestore.optim import flatten_parameters
+    from oracle import reference_cpu as R
+    from oracle import seeded as S
+    z = gold("simpleunet_64")
+    sd = S.model_state_dict("simpleunet")
+    m = rr.SimpleUNet().to(dev)
+    m.load_state_dict(sd)
+    flatten_parameters(m)
+    opt = rr.Adam(m.parameters(), lr=1e-3)
+    bad, clean = torch.from_numpy(z["bad"]), torch.from_numpy(z["clean"])
+    p = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    st = {}
+    for it in range(3):
+        opt.zero_grad()
+        loss = rr.MSELoss()(m(bad.to(dev)), clean.to(dev))
+        loss.backward()
+        opt.step()
+        for v in p.values():
+            v.grad = None
+        rl = R.mse_loss(R.simple_unet_forward(p, bad), clean)
+        rl.backward()
+        with torch.no_grad():
+            R.adamw_step(p, {k: v.grad for k, v in p.items()}, st, 1e-4, weight_decay=0.0,
+                         decoupled=False)
+        print(it, loss.item(), rl.item())
+        assert abs(loss.item() - rl.item()) <= 1e-5 * abs(rl.item()), (it, loss.item(), rl.item())
+    # Adam steps ~lr*sign(g): elements with noise-level grads may step apart
+    # (see _check_post), so after several steps the bound is looser than the
+    # single-forward 1e-4; stale weights would already break the loss check.
+    with torch.no_grad():
+        out = m(bad.to(dev)).cpu()
+        ref = R.simple_unet_forward(p, bad)
+    assert (out - ref).abs().mean().item() <= 1e-3
