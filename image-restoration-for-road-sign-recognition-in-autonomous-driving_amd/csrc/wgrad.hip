@@ -23,6 +23,8 @@
 //   f32 : ds_read_b32 per fragment, 16x16x4 f32 MFMA (exact fp32)
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 struct WgradArgs {
@@ -251,6 +253,176 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// 3x3 bf16 weight grad with an LDS halo: one workgroup owns a 64 x 64
+// (a = dy channel, b = x channel) tile for ALL 9 taps.  A K stage is 64
+// pixels = R = 64/W whole image rows of one image; it stages dy[64 px][64 ch]
+// and the zero-padded x halo [(R+2) rows][(W+2) cols][64 ch] once, and every
+// tap reads its B fragments at a shifted halo row (padding = the conv's zero
+// padding, so no masking).  Per stage per wave: 36 MFMAs (2 x 2 x 9) for
+// 4 + 36 ds_read_b64_tr_b16; global traffic ~4x lower than per-tap tiles.
+struct Halo3Args {
+  const char *A;           // dy [P][CA]
+  const char *B1, *B2;     // x sources [P][c1], [P][c2]
+  float *partial;          // [nsplit][CA][9][CB]
+  int CA, CB, c1, c2;
+  int n, h, w, lw;         // lw = log2(w)
+  int stages;              // total 64-pixel stages (P / 64)
+  int split_stages;        // stages per split
+  int nablk, nbblk;
+};
+
+template <int W>
+__global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
+  constexpr int R = 64 / W;                    // image rows per stage
+  constexpr int HW2 = W + 2;
+  constexpr int HROWS = (R + 2) * HW2;         // halo pixel rows
+  // 64 bf16 channels per row, padded 128 -> 136 B: the 8 rows one
+  // ds_read_b64_tr_b16 half-wave touches ({0..3, 8..11} or {0..3, 10..13}
+  // plus any base) start 34 banks apart and never overlap, and every tap's
+  // address is the lane's base + a compile-time offset
+  constexpr int RS = 136;
+  constexpr int A_BYTES = 64 * RS;
+  constexpr int B_BYTES = ((HROWS * RS + 15) / 16) * 16;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int LA = 64 * 8 / 256;             // 16-B pieces per thread (A)
+  constexpr int LB = (HROWS * 8 + 255) / 256;  // (B halo)
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wa = wv & 1, wb = wv >> 1;
+  int bid = blockIdx.x;
+  const int ablk = bid % a.nablk; bid /= a.nablk;
+  const int bblk = bid % a.nbblk; bid /= a.nbblk;
+  const int split = bid;
+  const int a0 = ablk * 64, b0 = bblk * 64;
+  const int sbeg = split * a.split_stages;
+  const int send = min(a.stages, sbeg + a.split_stages);
+  const char *Bsrc;
+  int ldb, bc0;
+  if (b0 < a.c1) { Bsrc = a.B1; ldb = a.c1; bc0 = b0; }
+  else { Bsrc = a.B2; ldb = a.c2; bc0 = b0 - a.c1; }
+  const int hw = a.h * a.w;
+
+  typedef uint4 V;
+  V ra[LA], rb[LB];
+  auto gload = [&](int st) {
+    const int p0 = st * 64;                    // first pixel of the stage
+    const int nn = p0 / hw;
+    const int h0 = (p0 - nn * hw) >> a.lw;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int idx = tid + 256 * i;
+      const int r = idx >> 3, pc = idx & 7;
+      ra[i] = *reinterpret_cast<const V *>(a.A + ((long long)(p0 + r) * a.CA + a0) * 2 + pc * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int idx = tid + 256 * i;
+      const int r = idx >> 3, pc = idx & 7;
+      V v = {0, 0, 0, 0};
+      if (r < HROWS) {
+        const int hy = r / HW2, hx = r - (r / HW2) * HW2;
+        const int yy = h0 - 1 + hy, xx = hx - 1;
+        if (yy >= 0 && yy < a.h && xx >= 0 && xx < a.w) {
+          const long long sp = ((long long)nn * a.h + yy) * a.w + xx;
+          v = *reinterpret_cast<const V *>(Bsrc + (sp * ldb + bc0) * 2 + pc * 16);
+        }
+      }
+      rb[i] = v;
+    }
+  };
+  auto swrite = [&](int buf) {
+    char *sA = smem + buf * STAGE;
+    char *sB = sA + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int idx = tid + 256 * i;
+      uint2 *d = reinterpret_cast<uint2 *>(sA + (idx >> 3) * RS + (idx & 7) * 16);
+      d[0] = uint2{ra[i].x, ra[i].y};
+      d[1] = uint2{ra[i].z, ra[i].w};
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int idx = tid + 256 * i;
+      if ((idx >> 3) < HROWS) {
+        uint2 *d = reinterpret_cast<uint2 *>(sB + (idx >> 3) * RS + (idx & 7) * 16);
+        d[0] = uint2{rb[i].x, rb[i].y};
+        d[1] = uint2{rb[i].z, rb[i].w};
+      }
+    }
+  };
+
+  f32x4 acc[2][2][9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) acc[i][j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, gi = lane & 15;
+  const int q = gi >> 2, pp = gi & 3;
+  const int nst = send - sbeg;
+  if (nst > 0) {
+    gload(sbeg);
+    swrite(0);
+    __syncthreads();
+  }
+  for (int s = 0; s < nst; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nst) gload(sbeg + s + 1);
+    const char *sA = smem + buf * STAGE;
+    const char *sB = sA + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int k0 = kk * 32 + 8 * g + q, k1 = k0 + 4;      // this lane's address rows
+      bf16x8 fa[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int col = wa * 32 + i * 16;
+        fa[i] = tr_frag(sA + k0 * RS + col * 2 + pp * 8, sA + k1 * RS + col * 2 + pp * 8);
+      }
+      // halo rows of the pixels k0 / k1 at tap (0, 0)
+      const int hr0 = (k0 / W) * HW2 + (k0 & (W - 1));
+      const int hr1 = (k1 / W) * HW2 + (k1 & (W - 1));
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int toff = (t / 3) * HW2 + (t % 3);
+        bf16x8 fb[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int col = wb * 32 + j * 16;
+          fb[j] = tr_frag(sB + (hr0 + toff) * RS + col * 2 + pp * 8,
+                          sB + (hr1 + toff) * RS + col * 2 + pp * 8);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j][t], 0, 0, 0);
+      }
+    }
+    if (s + 1 < nst) swrite(buf ^ 1);
+    __syncthreads();
+  }
+
+  // partial[split][a][tap][b]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int b = b0 + wb * 32 + j * 16 + gi;
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int ar = a0 + wa * 32 + i * 16 + g * 4 + e;
+          a.partial[(((long long)split * a.CA + ar) * 9 + t) * a.CB + b] = acc[i][j][t][e];
+        }
+    }
+}
+
 // dw[(a*CB + b)*taps + t] (+)= sum_s partial[s][a][t][b]   (fixed order, 4 chains)
 __global__ void wgrad_reduce(const float *__restrict__ partial, float *__restrict__ dw,
                              int CA, int CB, int taps, int nsplit, int accumulate) {
@@ -274,6 +446,77 @@ __global__ void wgrad_reduce(const float *__restrict__ partial, float *__restric
     const float s = (s0 + s1) + (s2 + s3);
     const long long di = ((long long)ar * CB + b) * taps + t;
     dw[di] = accumulate ? dw[di] + s : s;
+  }
+}
+
+// Split-parallel variant: G split groups x (256/G) float4 output columns per
+// block; group g sums splits g, g+G, ... and the groups are combined in LDS in
+// fixed order (deterministic).  Needs slab % 4 == 0.
+template <int G>
+__global__ __launch_bounds__(256) void wgrad_reduce_g(const float *__restrict__ partial,
+                                                       float *__restrict__ dw, int CA, int CB,
+                                                       int taps, int nsplit, int accumulate) {
+  constexpr int NC = 256 / G;                  // float4 columns per block
+  __shared__ float4 red[G][NC];
+  const long long slab = (long long)CA * CB * taps;
+  const int col = threadIdx.x % NC, g = threadIdx.x / NC;
+  const long long o4 = (long long)blockIdx.x * NC + col;
+  const bool live = o4 * 4 < slab;
+  const float4 *p4 = reinterpret_cast<const float4 *>(partial);
+  const long long s4 = slab / 4;
+  float4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
+  if (live) {
+    int sp = g;
+    for (; sp + G < nsplit; sp += 2 * G) {
+      const float4 u = p4[sp * s4 + o4], v = p4[(sp + G) * s4 + o4];
+      s0.x += u.x; s0.y += u.y; s0.z += u.z; s0.w += u.w;
+      s1.x += v.x; s1.y += v.y; s1.z += v.z; s1.w += v.w;
+    }
+    if (sp < nsplit) {
+      const float4 u = p4[sp * s4 + o4];
+      s0.x += u.x; s0.y += u.y; s0.z += u.z; s0.w += u.w;
+    }
+  }
+  red[g][col] = float4{s0.x + s1.x, s0.y + s1.y, s0.z + s1.z, s0.w + s1.w};
+  __syncthreads();
+  if (g != 0 || !live) return;
+  float4 s = red[0][col];
+#pragma unroll
+  for (int i = 1; i < G; ++i) {
+    const float4 u = red[i][col];
+    s.x += u.x; s.y += u.y; s.z += u.z; s.w += u.w;
+  }
+  const float v[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const long long o = o4 * 4 + e;
+    const int b = (int)(o % CB);
+    const long long at = o / CB;
+    const int t = (int)(at % taps);
+    const int ar = (int)(at / taps);
+    const long long di = ((long long)ar * CB + b) * taps + t;
+    dw[di] = accumulate ? dw[di] + v[e] : v[e];
+  }
+}
+
+static void launch_reduce(const float *ws, float *dw, int CA, int CB, int taps, int nsplit,
+                          int accumulate, hipStream_t st) {
+  const long long total = (long long)CA * CB * taps;
+  if (total % 4) {
+    hipLaunchKernelGGL(wgrad_reduce, dim3(rr_grid_cap((total + 255) / 256, 8192)), dim3(256), 0, st,
+                       ws, dw, CA, CB, taps, nsplit, accumulate);
+    return;
+  }
+  // smallest G (fewest LDS combines) that still gives >= ~1024 blocks
+  int G = 1;
+  while (G < 16 && G * 2 <= nsplit && (total / 4 + 256 / G - 1) / (256 / G) < 1024) G *= 2;
+  const unsigned nb = (unsigned)((total / 4 + 256 / G - 1) / (256 / G));
+  switch (G) {
+    case 1: hipLaunchKernelGGL(wgrad_reduce_g<1>, dim3(nb), dim3(256), 0, st, ws, dw, CA, CB, taps, nsplit, accumulate); break;
+    case 2: hipLaunchKernelGGL(wgrad_reduce_g<2>, dim3(nb), dim3(256), 0, st, ws, dw, CA, CB, taps, nsplit, accumulate); break;
+    case 4: hipLaunchKernelGGL(wgrad_reduce_g<4>, dim3(nb), dim3(256), 0, st, ws, dw, CA, CB, taps, nsplit, accumulate); break;
+    case 8: hipLaunchKernelGGL(wgrad_reduce_g<8>, dim3(nb), dim3(256), 0, st, ws, dw, CA, CB, taps, nsplit, accumulate); break;
+    default: hipLaunchKernelGGL(wgrad_reduce_g<16>, dim3(nb), dim3(256), 0, st, ws, dw, CA, CB, taps, nsplit, accumulate); break;
   }
 }
 
@@ -330,8 +573,41 @@ int launch_t(const rr_wgrad_desc *d, const Plan &pl, WgradArgs &a, hipStream_t s
 
 }  // namespace
 
+static bool halo_ok(const rr_wgrad_desc *d) {
+  if (d->dtype != RR_BF16 || d->mode != RR_CONV3X3) return false;
+  if (!(d->w == 8 || d->w == 16 || d->w == 32 || d->w == 64)) return false;
+  if (d->h % (64 / d->w)) return false;
+  if (d->c_out % 64 || d->c_in1 % 64 || d->c_in2 % 64) return false;
+  const char *e = getenv("RR_WGRAD_NOHALO");
+  return !(e && atoi(e));
+}
+
+struct HaloPlan { int stages, split_stages, nsplit; };
+
+static HaloPlan halo_plan(const rr_wgrad_desc *d) {
+  HaloPlan p;
+  const long long P = (long long)d->n * d->h * d->w;
+  p.stages = (int)(P / 64);
+  const int tiles = (d->c_out / 64) * ((d->c_in1 + d->c_in2) / 64);
+  static const int target = [] {
+    const char *e = getenv("RR_WGRAD_HALO_WGS");
+    return e ? atoi(e) : 512;
+  }();
+  int want = (target + tiles - 1) / tiles;          // ~target workgroups (512 = one full wave at 2 blocks/CU, measured best)
+  int maxs = (p.stages + 3) / 4;                    // >= 4 stages per split
+  int ns = want < maxs ? want : maxs;
+  if (ns < 1) ns = 1;
+  p.split_stages = (p.stages + ns - 1) / ns;
+  p.nsplit = (p.stages + p.split_stages - 1) / p.split_stages;
+  return p;
+}
+
 extern "C" size_t rr_wgrad_workspace(const rr_wgrad_desc *d) {
   if (!d) return 0;
+  if (halo_ok(d)) {
+    const HaloPlan hp = halo_plan(d);
+    return (size_t)hp.nsplit * d->c_out * 9 * (d->c_in1 + d->c_in2) * sizeof(float);
+  }
   const Plan p = plan_of(d);
   return (size_t)p.nsplit * p.CA * p.taps * p.CB * sizeof(float);
 }
@@ -346,7 +622,7 @@ extern "C" int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
   const long long P = (long long)d->n * d->h * d->w;
   if (P <= 0 || P * 4 > 0x7fffffffLL) return RR_EUNSUPPORTED;
   const Plan pl = plan_of(d);
-  const size_t need = (size_t)pl.nsplit * pl.CA * pl.taps * pl.CB * sizeof(float);
+  const size_t need = rr_wgrad_workspace(d);
   if (!ws || ws_bytes < need) return RR_EWORKSPACE;
   WgradArgs a;
   const bool convT = d->mode == RR_CONVT_UP;
@@ -365,11 +641,31 @@ extern "C" int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
   a.fd_w = make_fastdiv((uint32_t)d->w);
   a.fd_hw = make_fastdiv((uint32_t)(d->h * d->w));
   hipStream_t st = (hipStream_t)stream;
+  if (halo_ok(d)) {
+    const HaloPlan hp = halo_plan(d);
+    Halo3Args ha;
+    ha.A = (const char *)dy; ha.B1 = (const char *)x1; ha.B2 = (const char *)x2;
+    ha.partial = (float *)ws;
+    ha.CA = d->c_out; ha.CB = d->c_in1 + d->c_in2; ha.c1 = d->c_in1; ha.c2 = d->c_in2;
+    ha.n = d->n; ha.h = d->h; ha.w = d->w;
+    ha.lw = __builtin_ctz((unsigned)d->w);
+    ha.stages = hp.stages; ha.split_stages = hp.split_stages;
+    ha.nablk = ha.CA / 64; ha.nbblk = ha.CB / 64;
+    const dim3 grid((unsigned)(ha.nablk * ha.nbblk * hp.nsplit)), block(256);
+    switch (d->w) {
+      case 64: hipLaunchKernelGGL(wgrad3_halo_kernel<64>, grid, block, 0, st, ha); break;
+      case 32: hipLaunchKernelGGL(wgrad3_halo_kernel<32>, grid, block, 0, st, ha); break;
+      case 16: hipLaunchKernelGGL(wgrad3_halo_kernel<16>, grid, block, 0, st, ha); break;
+      default: hipLaunchKernelGGL(wgrad3_halo_kernel<8>, grid, block, 0, st, ha); break;
+    }
+    RR_CHECK_LAUNCH();
+    launch_reduce((const float *)ws, dw, ha.CA, ha.CB, 9, hp.nsplit, d->accumulate, st);
+    RR_CHECK_LAUNCH();
+    return RR_OK;
+  }
   int rc = d->dtype == RR_BF16 ? launch_t<bf16_t>(d, pl, a, st) : launch_t<float>(d, pl, a, st);
   if (rc) return rc;
-  const long long total = (long long)pl.CA * pl.CB * pl.taps;
-  hipLaunchKernelGGL(wgrad_reduce, dim3(rr_grid_cap((total + 255) / 256, 8192)), dim3(256), 0, st,
-                     (const float *)ws, dw, pl.CA, pl.CB, pl.taps, pl.nsplit, d->accumulate);
+  launch_reduce((const float *)ws, dw, pl.CA, pl.CB, pl.taps, pl.nsplit, d->accumulate, st);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

@@ -268,7 +268,7 @@ def test_multi_step_training_matches_oracle(dev):
     m = rr.SimpleUNet().to(dev)
     m.load_state_dict(sd)
     flatten_parameters(m)
-    opt = rr.Adam(m.parameters(), lr=1e-3)
+    opt = rr.Adam(m.parameters(), lr=1e-4)
     bad, clean = torch.from_numpy(z["bad"]), torch.from_numpy(z["clean"])
     p = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
     st = {}

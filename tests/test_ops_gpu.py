@@ -107,6 +107,30 @@ def test_wgrad(dev, dt, k):
     close(dw.cpu(), wt.grad, dt, scale=wt.grad.abs().max().item())
 
 
+@pytest.mark.parametrize("hw", [(8, 8), (16, 16), (12, 32), (2, 64)])
+@pytest.mark.parametrize("halo", [True, False])
+def test_wgrad3_halo(dev, hw, halo, monkeypatch):
+    """bf16 3x3 weight grad through the LDS-halo kernel (64-pixel stages of
+    whole image rows, zero-padded halo) and through the per-tap kernel, with a
+    concat second source (dec*.c1 shape), vs fp32 torch."""
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    monkeypatch.setenv("RR_WGRAD_NOHALO", "0" if halo else "1")
+    h, w = hw
+    n, c1, c2, cout = 5, 64, 128, 128
+    x = rnd(n, c1 + c2, h, w, seed=30).bfloat16().float()
+    g = rnd(n, cout, h, w, seed=31).bfloat16().float()
+    wt = torch.zeros(cout, c1 + c2, 3, 3, requires_grad=True)
+    F.conv2d(x, wt, None, padding=1).backward(g)
+    dw = rr.ops.wgrad(RR_CONV3X3, nhwc(g, dev, torch.bfloat16), nhwc(x[:, :c1], dev, torch.bfloat16),
+                      nhwc(x[:, c1:], dev, torch.bfloat16), n, h, w, cout,
+                      dw_shape=(cout, c1 + c2, 3, 3))
+    # inputs are bf16-exact and products are exact in fp32: only the
+    # summation order differs from torch
+    rel = ((dw.cpu() - wt.grad).norm() / wt.grad.norm()).item()
+    assert rel < 2e-5, rel
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_convT(dev, dt):
     import roadrestore as rr
