@@ -195,8 +195,9 @@ __global__ void bn_bwd_reduce_kernel(BnBwd a, float *__restrict__ part, float *_
 }
 
 // coef[C][2][3] = {gamma*invstd, mean(gm), mean(gm*xhat)} per BN
+template <typename PT>
 __global__ void bn_bwd_finalize_kernel(int C, int blocks, double count, int nbn,
-                                       const float *__restrict__ part, const float *apart,
+                                       const PT *__restrict__ part, int ablocks, const float *apart,
                                        const float *g0, const float *inv0, const float *g1,
                                        const float *inv1, float *dg0, float *db0, float *dg1,
                                        float *db1, float *dalpha, float *coef) {
@@ -206,7 +207,7 @@ __global__ void bn_bwd_finalize_kernel(int C, int blocks, double count, int nbn,
   double s0 = 0, s1 = 0, s2 = 0;
   if (c < C) {
     for (int b = sl; b < blocks; b += 16) {
-      const float *p = part + ((long long)b * C + c) * 3;
+      const PT *p = part + ((long long)b * C + c) * 3;
       s0 += p[0]; s1 += p[1]; s2 += p[2];
     }
   }
@@ -231,7 +232,7 @@ __global__ void bn_bwd_finalize_kernel(int C, int blocks, double count, int nbn,
     __syncthreads();
     __shared__ double ar[256];
     double v = 0;
-    for (int b = threadIdx.x; b < blocks; b += blockDim.x) v += apart[b];
+    for (int b = threadIdx.x; b < ablocks; b += blockDim.x) v += apart[b];
     ar[threadIdx.x] = v;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -447,8 +448,8 @@ extern "C" int rr_bn_bwd_finalize(const rr_bnbwd_desc *d, const float *partial,
   if (!partial || !invstd0 || !coef || (d->nbn == 2 && !invstd1)) return RR_EINVAL;
   const int blocks = reduce_blocks(d->P);
   const float *apart = d->mask_kind == 2 ? partial + (size_t)blocks * d->C * 3 : nullptr;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((d->C + 15) / 16), dim3(256), 0,
-                     (hipStream_t)stream, d->C, blocks, (double)d->P, d->nbn, partial, apart,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3((d->C + 15) / 16), dim3(256), 0,
+                     (hipStream_t)stream, d->C, blocks, (double)d->P, d->nbn, partial, blocks, apart,
                      gamma0, invstd0, gamma1, invstd1, dgamma0, dbeta0, dgamma1, dbeta1, dalpha,
                      coef);
   RR_CHECK_LAUNCH();
@@ -499,6 +500,30 @@ extern "C" int rr_channel_sum(int dtype, long long P, int C, const void *x, floa
   RR_CHECK_LAUNCH();
   hipLaunchKernelGGL(colsum_finalize, dim3((C + 15) / 16), dim3(256), 0, st, C, blocks,
                      (const float *)ws, out, accumulate);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" size_t rr_bn_bwd_finalize_rows_workspace(int C, int rows) {
+  return rr_colreduce_bytes(rows, C * 3);
+}
+
+extern "C" int rr_bn_bwd_finalize_rows(const rr_bnbwd_desc *d, int rows, const float *partial,
+                                       int arows, const float *apartial, const float *gamma0,
+                                       const float *invstd0, float *dgamma0, float *dbeta0,
+                                       float *dalpha, float *coef, void *ws, size_t ws_bytes,
+                                       rr_stream stream) {
+  int rc = bnbwd_check(d);
+  if (rc) return rc;
+  if (d->nbn != 1 || rows <= 0 || !partial || !invstd0 || !coef) return RR_EINVAL;
+  if ((arows > 0) != (apartial != nullptr)) return RR_EINVAL;
+  if (!ws || ws_bytes < rr_colreduce_bytes(rows, d->C * 3)) return RR_EWORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int chunks = rr_colreduce(partial, rows, d->C * 3, (double *)ws, st);
+  if (chunks < 0) return RR_ELAUNCH;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<double>, dim3((d->C + 15) / 16), dim3(256), 0, st,
+                     d->C, chunks, (double)d->P, 1, (const double *)ws, arows, apartial, gamma0,
+                     invstd0, nullptr, nullptr, dgamma0, dbeta0, nullptr, nullptr, dalpha, coef);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

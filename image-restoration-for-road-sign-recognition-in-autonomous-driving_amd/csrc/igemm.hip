@@ -33,6 +33,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -52,6 +53,12 @@ struct IgemmArgs {
   int ncblk;
   int cout_t;         // convT_up: channels per tap
   int out_nchw;       // y1 = fp32 NCHW
+  // BN-backward fusion (rr_igemm_bnbwd): the accumulator is dL/d(PReLU out)
+  // of a BN -> PReLU pair; the epilogue writes gm = dL/d(BN out) and the
+  // per-channel partials of sum(gm), sum(gm * xhat) and the PReLU alpha grad
+  const char *bt;                              // pre-BN activation t [P][cout]
+  const float *bmean, *binv, *baff_s, *baff_b, *balpha;
+  float *bpart, *bapart;                       // [npblk][cout][3], [npblk][cout/64]
   int dbg;            // diagnostics (RR_IGEMM_DBG): bit0 skip epilogue, bit1 K loop x2
 };
 
@@ -76,6 +83,188 @@ __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
 constexpr int ROWB = 128;  // bytes of k per row per stage
 
+// BN-backward fused epilogue (see IgemmArgs::bpart).  Thread -> fixed
+// 8-channel chunk cc; per-thread sums reduced over the lanes sharing cc
+// (xor shuffles), then over the waves in LDS (fixed order).
+template <typename T, int BC, int BP, int NT>
+__device__ __forceinline__ void store_staged_bnbwd(const IgemmArgs &a, float *stg, int c0, int p0,
+                                                   int pblk, int tid, int nvalid) {
+  constexpr int SROW = BC + 4;
+  constexpr int CPR = BC / 8;
+  constexpr int NCH = BP * CPR / NT;
+  constexpr int NW = NT / 64;
+  const int cc = (tid % CPR) * 8;
+  const int c = c0 + cc;
+  float ms[8], iv[8], as[8], ab[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ms[j] = a.bmean[c + j]; iv[j] = a.binv[c + j];
+    as[j] = a.baff_s[c + j]; ab[j] = a.baff_b[c + j];
+  }
+  const float al = a.balpha[0];
+  float s0[8], s1[8], sa = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s0[j] = 0.f; s1[j] = 0.f; }
+#pragma unroll 2
+  for (int i = 0; i < NCH; ++i) {
+    const int q = tid + NT * i;
+    const int r = q / CPR;
+    if (r >= nvalid) continue;
+    const long long e = (long long)(p0 + r) * a.cout + c;
+    const f32x4 g0 = *reinterpret_cast<const f32x4 *>(stg + r * SROW + cc);
+    const f32x4 g1 = *reinterpret_cast<const f32x4 *>(stg + r * SROW + cc + 4);
+    const f32x4 t0 = load4<T>(reinterpret_cast<const T *>(a.bt) + e);
+    const f32x4 t1 = load4<T>(reinterpret_cast<const T *>(a.bt) + e + 4);
+    const float g[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+    const float t[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+    float gm[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float u = t[j] * as[j] + ab[j];            // BN output (PReLU input)
+      sa += u > 0.f ? 0.f : g[j] * u;
+      gm[j] = u > 0.f ? g[j] : al * g[j];
+      s0[j] += gm[j];
+      s1[j] += gm[j] * ((t[j] - ms[j]) * iv[j]);
+    }
+    store8<T>(reinterpret_cast<T *>(a.y1) + e, f32x4{gm[0], gm[1], gm[2], gm[3]},
+              f32x4{gm[4], gm[5], gm[6], gm[7]});
+  }
+#pragma unroll
+  for (int o = CPR; o < 64; o <<= 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s0[j] += __shfl_xor(s0[j], o, 64);
+      s1[j] += __shfl_xor(s1[j], o, 64);
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) sa += __shfl_xor(sa, o, 64);
+  __syncthreads();                             // stg reads done before red is written
+  float *red = stg + BP * SROW;                // [NW][BC][2] + [NW]
+  const int lane = tid & 63, wv = tid >> 6;
+  if (lane < CPR) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[(wv * BC + cc + j) * 2 + 0] = s0[j];
+      red[(wv * BC + cc + j) * 2 + 1] = s1[j];
+    }
+  }
+  if (lane == 0) red[NW * BC * 2 + wv] = sa;
+  __syncthreads();
+  for (int cl = tid; cl < BC; cl += NT) {
+    float x = 0.f, y = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      x += red[(q * BC + cl) * 2 + 0];
+      y += red[(q * BC + cl) * 2 + 1];
+    }
+    float *pp = a.bpart + ((long long)pblk * a.cout + c0 + cl) * 3;
+    pp[0] = x; pp[1] = y; pp[2] = 0.f;
+  }
+  if (tid == 0) {
+    float x = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) x += red[NW * BC * 2 + q];
+    // layout [npblk][cout / 64] (independent of BC): this tile's sum in its
+    // first 64-channel slot, zeros in the rest
+    float *ap = a.bapart + (long long)pblk * (a.cout / 64) + c0 / 64;
+#pragma unroll
+    for (int k = 0; k < BC / 64; ++k) ap[k] = k == 0 ? x : 0.f;
+  }
+}
+
+// Staged epilogue: the fp32 tile sits in LDS as stg[BP][BC + 4] (pre-bias
+// accumulators, after a barrier).  Column-wise BN partial statistics from
+// LDS, then 8-channel chunks (16-B bf16 / 32-B f32 stores, row-contiguous per
+// wave) with bias, accumulate, ReLU, relu-backward mask, column split and the
+// convT 2x2 pixel scatter.  NT threads; needs BC | (the column count).
+template <typename T, int BC, int BP, int NT, int MODE>
+__device__ __forceinline__ void store_staged(const IgemmArgs &a, float *stg, int c0, int p0,
+                                             int pblk, int tid) {
+  constexpr int SROW = BC + 4;
+  const int nvalid = min(BP, a.P - p0);
+  if (a.bpart) {
+    store_staged_bnbwd<T, BC, BP, NT>(a, stg, c0, p0, pblk, tid, nvalid);
+    return;
+  }
+  if (a.stats) {
+    constexpr int TPC = NT / BC;            // threads per channel column
+    float *red = stg + BP * SROW;            // [TPC][BC][2]
+    const int c = tid % BC, sl = tid / BC;
+    float x = 0.f, y = 0.f;
+    for (int r = sl; r < nvalid; r += TPC) {
+      const float v = stg[r * SROW + c];
+      x += v;
+      y += v * v;
+    }
+    red[(sl * BC + c) * 2 + 0] = x;
+    red[(sl * BC + c) * 2 + 1] = y;
+    __syncthreads();
+    if (tid < BC) {
+      float sx = 0.f, sy = 0.f;
+#pragma unroll
+      for (int q = 0; q < TPC; ++q) {
+        sx += red[(q * BC + tid) * 2 + 0];
+        sy += red[(q * BC + tid) * 2 + 1];
+      }
+      a.stats[((long long)pblk * a.cout + c0 + tid) * 2 + 0] = sx;
+      a.stats[((long long)pblk * a.cout + c0 + tid) * 2 + 1] = sy;
+    }
+  }
+  constexpr int CPR = BC / 8;                // 8-channel chunks per pixel row
+  constexpr int NCH = BP * CPR / NT;        // chunks per thread
+#pragma unroll 2
+  for (int i = 0; i < NCH; ++i) {
+    const int q = tid + NT * i;
+    const int r = q / CPR;
+    const int cc = (q - r * CPR) * 8;
+    if (r >= nvalid) continue;
+    const int p = p0 + r;
+    const int c = c0 + cc;
+    f32x4 v0 = *reinterpret_cast<const f32x4 *>(stg + r * SROW + cc);
+    f32x4 v1 = *reinterpret_cast<const f32x4 *>(stg + r * SROW + cc + 4);
+    if (a.bias) {
+      v0 += *reinterpret_cast<const f32x4 *>(a.bias + c);
+      v1 += *reinterpret_cast<const f32x4 *>(a.bias + c + 4);
+    }
+    T *dst;
+    const T *msk = nullptr;
+    if (MODE == RR_CONVT_UP) {
+      const int tap = c / a.cout_t;
+      const int co = c - tap * a.cout_t;
+      const int hw = a.h * a.w;
+      const int nn = p / hw;
+      const int rem = p - nn * hw;
+      const int hh = rem / a.w, ww = rem - (rem / a.w) * a.w;
+      const long long op = ((long long)nn * 2 * a.h + 2 * hh + (tap >> 1)) * (2 * a.w) + 2 * ww + (tap & 1);
+      dst = reinterpret_cast<T *>(a.y1) + op * a.cout_t + co;
+    } else if (a.split > 0 && c >= a.split) {
+      dst = reinterpret_cast<T *>(a.y2) + (long long)p * (a.cout - a.split) + (c - a.split);
+    } else {
+      const int ld = a.split > 0 ? a.split : a.cout;
+      dst = reinterpret_cast<T *>(a.y1) + (long long)p * ld + c;
+      if (a.has_mask) msk = reinterpret_cast<const T *>(a.mask) + (long long)p * ld + c;
+    }
+    if (a.accumulate) {
+      v0 += load4<T>(dst);
+      v1 += load4<T>(dst + 4);
+    }
+    if (a.act == RR_ACT_RELU) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { v0[k] = fmaxf(v0[k], 0.f); v1[k] = fmaxf(v1[k], 0.f); }
+    }
+    if (msk) {
+      const f32x4 m0 = load4<T>(msk), m1 = load4<T>(msk + 4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v0[k] = m0[k] > 0.f ? v0[k] : 0.f;
+        v1[k] = m1[k] > 0.f ? v1[k] : 0.f;
+      }
+    }
+    store8<T>(dst, v0, v1);
+  }
+}
+
 template <typename T, int BC, int BP, int WC, int MODE>
 __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs a) {
   constexpr int ES = sizeof(T);
@@ -85,7 +274,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs a) {
   constexpr int STAGE_BYTES = (BC + BP) * ROWB;
   constexpr int MC = BC / WC / 16, MP = BP / WP / 16;   // 16x16 subtiles per wave
   constexpr int SROW = BC + 4;                   // fp32 staging row (floats), padded
-  constexpr int STG_BYTES = BP * SROW * 4 + 2 * 256 * 4 * 2;
+  constexpr int STG_BYTES = BP * SROW * 4 + 2 * 256 * 4 * 2 + 256;
   constexpr int SMEM = (2 * STAGE_BYTES > STG_BYTES) ? 2 * STAGE_BYTES : STG_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
@@ -246,83 +435,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs a) {
         *reinterpret_cast<f32x4 *>(stg + r * SROW + col) = acc[mi][ni];
       }
     __syncthreads();
-    const int nvalid = min(BP, a.P - p0);
-    if (a.stats) {
-      constexpr int TPC = 256 / BC;            // threads per channel column
-      float *red = stg + BP * SROW;            // [TPC][BC][2]
-      const int c = tid % BC, sl = tid / BC;
-      float x = 0.f, y = 0.f;
-      for (int r = sl; r < nvalid; r += TPC) {
-        const float v = stg[r * SROW + c];
-        x += v;
-        y += v * v;
-      }
-      red[(sl * BC + c) * 2 + 0] = x;
-      red[(sl * BC + c) * 2 + 1] = y;
-      __syncthreads();
-      if (tid < BC) {
-        float sx = 0.f, sy = 0.f;
-#pragma unroll
-        for (int q = 0; q < TPC; ++q) {
-          sx += red[(q * BC + tid) * 2 + 0];
-          sy += red[(q * BC + tid) * 2 + 1];
-        }
-        a.stats[((long long)pblk * a.cout + c0 + tid) * 2 + 0] = sx;
-        a.stats[((long long)pblk * a.cout + c0 + tid) * 2 + 1] = sy;
-      }
-    }
-    constexpr int CPR = BC / 8;                // 8-channel chunks per pixel row
-    constexpr int NCH = BP * CPR / 256;        // chunks per thread
-#pragma unroll 2
-    for (int i = 0; i < NCH; ++i) {
-      const int q = tid + 256 * i;
-      const int r = q / CPR;
-      const int cc = (q - r * CPR) * 8;
-      if (r >= nvalid) continue;
-      const int p = p0 + r;
-      const int c = c0 + cc;
-      f32x4 v0 = *reinterpret_cast<const f32x4 *>(stg + r * SROW + cc);
-      f32x4 v1 = *reinterpret_cast<const f32x4 *>(stg + r * SROW + cc + 4);
-      if (a.bias) {
-        v0 += *reinterpret_cast<const f32x4 *>(a.bias + c);
-        v1 += *reinterpret_cast<const f32x4 *>(a.bias + c + 4);
-      }
-      T *dst;
-      const T *msk = nullptr;
-      if (MODE == RR_CONVT_UP) {
-        const int tap = c / a.cout_t;
-        const int co = c - tap * a.cout_t;
-        const int hw = a.h * a.w;
-        const int nn = p / hw;
-        const int rem = p - nn * hw;
-        const int hh = rem / a.w, ww = rem - (rem / a.w) * a.w;
-        const long long op = ((long long)nn * 2 * a.h + 2 * hh + (tap >> 1)) * (2 * a.w) + 2 * ww + (tap & 1);
-        dst = reinterpret_cast<T *>(a.y1) + op * a.cout_t + co;
-      } else if (a.split > 0 && c >= a.split) {
-        dst = reinterpret_cast<T *>(a.y2) + (long long)p * (a.cout - a.split) + (c - a.split);
-      } else {
-        const int ld = a.split > 0 ? a.split : a.cout;
-        dst = reinterpret_cast<T *>(a.y1) + (long long)p * ld + c;
-        if (a.has_mask) msk = reinterpret_cast<const T *>(a.mask) + (long long)p * ld + c;
-      }
-      if (a.accumulate) {
-        v0 += load4<T>(dst);
-        v1 += load4<T>(dst + 4);
-      }
-      if (a.act == RR_ACT_RELU) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) { v0[k] = fmaxf(v0[k], 0.f); v1[k] = fmaxf(v1[k], 0.f); }
-      }
-      if (msk) {
-        const f32x4 m0 = load4<T>(msk), m1 = load4<T>(msk + 4);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          v0[k] = m0[k] > 0.f ? v0[k] : 0.f;
-          v1[k] = m1[k] > 0.f ? v1[k] : 0.f;
-        }
-      }
-      store8<T>(dst, v0, v1);
-    }
+    store_staged<T, BC, BP, 256, MODE>(a, stg, c0, p0, pblk, tid);
     return;
   }
 
@@ -460,6 +573,268 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// 3x3 bf16 conv (fwd or dgrad) with an LDS halo.  A tile is BP = 256 output
+// pixels = R = 256/W whole image rows (or R/H whole images when R > H) x BC
+// output channels, 512 threads (8 waves, wave tile 64 ch x 256/WP px).  Per
+// 64-channel K chunk the zero-padded input halo -- (Hs+2) x (W+2) rows per
+// image, Hs = min(R, H) -- is staged ONCE and serves all 9 taps; the weights
+// stream per (chunk, tap).  So the activation is read ~1.3x instead of 9x.
+//
+// LDS image ("k-planes"): plane j (16-B channel chunk j of the 64) holds the
+// rows contiguously, 16 B per row.  A ds_read_b128 16-lane group reads rows
+// {0-3,12-15} at chunk q and rows {4-11} at chunk q+1 (MFMA fragment map);
+// with plane size = 0 mod 256 B those 16 rows hit 16 distinct 16-B bank
+// slots for ANY base row, so every tap's shifted read is conflict-free and
+// its address is the lane's base + tap * 16 B.  Fills are register-staged:
+// piece idx -> chunk (idx >> 3) & 7, row 8 * (idx >> 6) + (idx & 7): a wave
+// instruction reads 8 full 128-B lines and writes 8 x 128 contiguous bytes.
+//
+// Pipeline: one barrier per (chunk, tap) stage; weights prefetched 2 stages
+// ahead in registers, the next chunk's halo loaded at tap 0 and written at
+// tap 8.
+template <int W> struct HaloGeom {
+  static constexpr int R = 256 / W;
+  // worst case over H >= 8 with H | R or R | H: R/Hs images of (Hs+2) rows
+  static constexpr int HMAX = (R <= 8 ? (R + 2) : (R / 8) * 10) * (W + 2);
+  static constexpr int PLANE = ((HMAX * 16 + 255) / 256) * 256;
+  static constexpr int HBYTES = 8 * PLANE;
+  static constexpr int LH = (HMAX * 8 + 511) / 512;           // pieces per thread
+};
+
+// BC = 64 keeps ONE halo buffer (the next chunk's halo is written after an
+// extra barrier at tap 8), so LDS <= 78 KB and VGPRs <= 128: 2 workgroups
+// per CU, one tile's prologue / epilogue overlapping the other's MFMA loop.
+// BC = 128 double-buffers the halo, 1 workgroup per CU.
+template <int BC> struct HaloCfg {
+  static constexpr int HB = BC == 64 ? 1 : 2;
+  static constexpr int OCC = BC == 64 ? 4 : 2;   // min waves per SIMD (launch bound)
+};
+
+template <int BC, int W, int MODE>
+__global__ __launch_bounds__(512, HaloCfg<BC>::OCC) void igemm3_halo_kernel(IgemmArgs a) {
+  using T = bf16_t;
+  using G = HaloGeom<W>;
+  constexpr int HB = HaloCfg<BC>::HB;
+  constexpr int BP = 256, NT = 512;
+  constexpr int WC = BC / 64, WP = 8 / WC;
+  constexpr int MC = 4, MP = BP / WP / 16;
+  constexpr int WPLANE = BC * 16;                               // weight planes: BC rows
+  constexpr int WBYTES = 8 * WPLANE;
+  constexpr int LW = BC * 8 / NT;                               // weight pieces per thread
+  constexpr int MAIN = HB * G::HBYTES + 2 * WBYTES;
+  constexpr int SROW = BC + 4;
+  constexpr int STG = BP * SROW * 4 + 2 * 512 * 4 * 2 + 256;
+  constexpr int SMEM = MAIN > STG ? MAIN : STG;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  char *const hbuf = smem;                                      // [HB][HBYTES]
+  char *const wbuf = smem + HB * G::HBYTES;                     // [2][WBYTES]
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wc = wv % WC, wp = wv / WC;
+  const int cblk = blockIdx.x % a.ncblk, pblk = blockIdx.x / a.ncblk;
+  const int c0 = cblk * BC, p0 = pblk * BP;
+
+  // ---- tile geometry (uniform) ----
+  const int hw = a.h * a.w;
+  const int n0 = p0 / hw;
+  const int y0 = (p0 - n0 * hw) / W;
+  const int Hs = G::R < a.h ? G::R : a.h;
+  const int himg = (Hs + 2) * (W + 2);                          // halo rows per image
+  const int hrows = (G::R / Hs) * himg;
+
+  // ---- per-piece halo source pixel (-1: zero padding), fixed for the tile ----
+  int hpix[G::LH];
+#pragma unroll
+  for (int i = 0; i < G::LH; ++i) {
+    const int idx = tid + NT * i;
+    const int r = 8 * (idx >> 6) + (idx & 7);
+    int pix = -1;
+    if (r < hrows) {
+      const int im = r / himg, rem = r - (r / himg) * himg;
+      const int hy = rem / (W + 2), hx = rem - (rem / (W + 2)) * (W + 2);
+      const int yy = y0 - 1 + hy, xx = hx - 1;
+      if (yy >= 0 && yy < a.h && xx >= 0 && xx < W) pix = ((n0 + im) * a.h + yy) * W + xx;
+    }
+    hpix[i] = pix;
+  }
+  const int pj = ((tid >> 3) & 7) * 16;                         // this thread's 16-B chunk
+  // ---- weight rows ----
+  const char *wrow[LW];
+#pragma unroll
+  for (int i = 0; i < LW; ++i) {
+    const int idx = tid + NT * i;
+    const int r = 8 * (idx >> 6) + (idx & 7);
+    wrow[i] = a.wt + ((long long)(c0 + r) * a.K) * 2 + pj;
+  }
+
+  // ---- per-lane fragment bases ----
+  const int frow = lane & 15, fq = lane >> 4;
+  int abase[MC], bbase[MP];
+#pragma unroll
+  for (int mi = 0; mi < MC; ++mi) abase[mi] = fq * WPLANE + (wc * 64 + mi * 16 + frow) * 16;
+#pragma unroll
+  for (int ni = 0; ni < MP; ++ni) {
+    const int q = wp * (BP / WP) + ni * 16 + frow;              // pixel within the tile
+    const int r = q / W, x = q % W;
+    const int im = r / Hs, rr = r - (r / Hs) * Hs;
+    bbase[ni] = fq * G::PLANE + (im * himg + rr * (W + 2) + x) * 16;   // tap (dy,dx) = (-1,-1)
+  }
+
+  const int kch = a.cin / 64;
+  const int nst = kch * 9;
+  typedef uint4 V;
+  V hreg[G::LH];
+  V wr0[LW], wr1[LW];                    // weight register sets (stage parity)
+
+  auto load_halo = [&](int ch) __attribute__((always_inline)) {
+    const int ci0 = ch * 64;
+    const bool first = ci0 < a.c1;
+    const char *base = first ? a.x1 : a.x2;
+    const long long cs = first ? a.c1 : a.c2;
+    const char *src0 = base + (long long)(first ? ci0 : ci0 - a.c1) * 2 + pj;
+#pragma unroll
+    for (int i = 0; i < G::LH; ++i) {
+      // padding pieces load pixel 0 (valid, L2-hot) and are zeroed by a
+      // select: no divergent branch, no pointer merge across address spaces
+      const bool ok = hpix[i] >= 0;
+      V v = *reinterpret_cast<const V *>(src0 + (long long)(ok ? hpix[i] : 0) * cs * 2);
+      v.x = ok ? v.x : 0u; v.y = ok ? v.y : 0u; v.z = ok ? v.z : 0u; v.w = ok ? v.w : 0u;
+      hreg[i] = v;
+    }
+  };
+  auto store_halo = [&](int buf) __attribute__((always_inline)) {
+    char *d = hbuf + buf * G::HBYTES;
+#pragma unroll
+    for (int i = 0; i < G::LH; ++i) {
+      const int idx = tid + NT * i;
+      const int r = 8 * (idx >> 6) + (idx & 7);
+      if (r < hrows) *reinterpret_cast<V *>(d + ((idx >> 3) & 7) * G::PLANE + r * 16) = hreg[i];
+    }
+  };
+  auto load_w = [&](int s, auto setc) __attribute__((always_inline)) {
+    const int ch = s / 9, tap = s - (s / 9) * 9;
+    const long long off = ((long long)tap * a.cin + ch * 64) * 2;
+#pragma unroll
+    for (int i = 0; i < LW; ++i) {
+      const V v = *reinterpret_cast<const V *>(wrow[i] + off);
+      if constexpr (decltype(setc)::value == 0) wr0[i] = v; else wr1[i] = v;
+    }
+  };
+  auto store_w = [&](auto setc) __attribute__((always_inline)) {
+    constexpr int SET = decltype(setc)::value;
+    char *d = wbuf + SET * WBYTES;
+#pragma unroll
+    for (int i = 0; i < LW; ++i) {
+      const int idx = tid + NT * i;
+      const int r = 8 * (idx >> 6) + (idx & 7);
+      *reinterpret_cast<V *>(d + ((idx >> 3) & 7) * WPLANE + r * 16) = SET == 0 ? wr0[i] : wr1[i];
+    }
+  };
+
+  f32x4 acc[MC][MP];
+#pragma unroll
+  for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < MP; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: halo(0), weights(0) into LDS; weights(1) in flight
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  load_halo(0);
+  load_w(0, I0{});
+  load_w(nst > 1 ? 1 : 0, I1{});
+  store_halo(0);
+  store_w(I0{});
+  __syncthreads();
+
+  // One (chunk, tap) stage s = 9 ch + TAP.  weights(k) live in register set
+  // k & 1: stage s loads weights(s + 2) into set s & 1 (freed when weights(s)
+  // was stored) and stores weights(s + 1) from set (s + 1) & 1.  Every load
+  // is unconditional (indices clamped at the tail) so no register is a
+  // branch merge and the compiler can keep the loads in flight.
+  auto stage = [&](int ch, auto tapc, auto setc) __attribute__((always_inline)) {
+    constexpr int TAP = decltype(tapc)::value;
+    constexpr int SET = decltype(setc)::value;        // == s & 1
+    const int s = ch * 9 + TAP;
+    load_w(s + 2 < nst ? s + 2 : nst - 1, setc);
+    if constexpr (TAP == 0) {
+      if constexpr (HB == 2) load_halo(ch + 1 < kch ? ch + 1 : ch);
+      else if (kch > 1) load_halo(ch + 1 < kch ? ch + 1 : ch);   // uniform: kch per launch
+    }
+    const char *sA = wbuf + SET * WBYTES;
+    const char *sB = hbuf + (HB == 2 ? (ch & 1) * G::HBYTES : 0) + ((TAP / 3) * (W + 2) + TAP % 3) * 16;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[MC], fb[MP];
+#pragma unroll
+      for (int mi = 0; mi < MC; ++mi)
+        fa[mi] = *reinterpret_cast<const bf16x8 *>(sA + abase[mi] + kk * 4 * WPLANE);
+#pragma unroll
+      for (int ni = 0; ni < MP; ++ni)
+        fb[ni] = *reinterpret_cast<const bf16x8 *>(sB + bbase[ni] + kk * 4 * G::PLANE);
+#pragma unroll
+      for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < MP; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi], fb[ni], acc[mi][ni], 0, 0, 0);
+    }
+    if (s + 1 < nst) store_w(std::integral_constant<int, SET ^ 1>{});
+    if constexpr (TAP == 8) {
+      if (ch + 1 < kch) {
+        if constexpr (HB == 1) {
+          __syncthreads();                   // every wave is done reading this chunk's halo
+          store_halo(0);
+        } else {
+          store_halo((ch + 1) & 1);
+        }
+      }
+    }
+    __syncthreads();
+  };
+  auto chunk_even = [&](int ch) __attribute__((always_inline)) {          // 9 ch even: s & 1 == TAP & 1
+    stage(ch, std::integral_constant<int, 0>{}, I0{});
+    stage(ch, std::integral_constant<int, 1>{}, I1{});
+    stage(ch, std::integral_constant<int, 2>{}, I0{});
+    stage(ch, std::integral_constant<int, 3>{}, I1{});
+    stage(ch, std::integral_constant<int, 4>{}, I0{});
+    stage(ch, std::integral_constant<int, 5>{}, I1{});
+    stage(ch, std::integral_constant<int, 6>{}, I0{});
+    stage(ch, std::integral_constant<int, 7>{}, I1{});
+    stage(ch, std::integral_constant<int, 8>{}, I0{});
+  };
+  auto chunk_odd = [&](int ch) __attribute__((always_inline)) {           // 9 ch odd: s & 1 == (TAP + 1) & 1
+    stage(ch, std::integral_constant<int, 0>{}, I1{});
+    stage(ch, std::integral_constant<int, 1>{}, I0{});
+    stage(ch, std::integral_constant<int, 2>{}, I1{});
+    stage(ch, std::integral_constant<int, 3>{}, I0{});
+    stage(ch, std::integral_constant<int, 4>{}, I1{});
+    stage(ch, std::integral_constant<int, 5>{}, I0{});
+    stage(ch, std::integral_constant<int, 6>{}, I1{});
+    stage(ch, std::integral_constant<int, 7>{}, I0{});
+    stage(ch, std::integral_constant<int, 8>{}, I1{});
+  };
+  int ch = 0;
+  for (; ch + 2 <= kch; ch += 2) {
+    chunk_even(ch);
+    chunk_odd(ch + 1);
+  }
+  if (ch < kch) chunk_even(ch);
+
+  // ---- epilogue: fp32 tile into LDS, then the shared staged store ----
+  float *stg = reinterpret_cast<float *>(smem);
+#pragma unroll
+  for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < MP; ++ni) {
+      const int r = wp * (BP / WP) + ni * 16 + frow;
+      const int col = wc * 64 + mi * 16 + fq * 4;
+      *reinterpret_cast<f32x4 *>(stg + r * SROW + col) = acc[mi][ni];
+    }
+  __syncthreads();
+  store_staged<T, BC, BP, NT, MODE>(a, stg, c0, p0, pblk, tid);
+}
+
 template <typename T, int BC, int BP, int WC>
 int launch_mode(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   a.ncblk = (a.cout + BC - 1) / BC;
@@ -490,8 +865,44 @@ Tile pick_tile(const rr_igemm_desc *d) {
   return {64, 128};
 }
 
+// halo path eligibility (bf16 3x3, whole-row 256-pixel tiles); returns BC or 0
+int halo_bc(const rr_igemm_desc *d) {
+  const char *e = getenv("RR_IGEMM_NOHALO");   // A/B switch (per call)
+  if ((e && atoi(e)) || d->dtype != RR_BF16 || d->mode != RR_CONV3X3 || d->out_nchw) return 0;
+  const int W = d->w;
+  if (!(W == 8 || W == 16 || W == 32 || W == 64)) return 0;
+  const int R = 256 / W;
+  if (d->h % 8) return 0;
+  if (R <= d->h ? (d->h % R) : (R % d->h || d->n % (R / d->h))) return 0;
+  if (d->c_in1 % 64 || d->c_in2 % 64) return 0;
+  if (d->c_out % 128 == 0 && (d->out_split == 0 || d->out_split % 128 == 0)) return 128;
+  if (d->c_out % 64 == 0) return 64;
+  return 0;
+}
+
+template <int BC>
+int launch_halo(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
+  a.ncblk = a.cout / BC;
+  const long long nblk = (long long)(a.P / 256) * a.ncblk;
+  if (nblk > 0x7fffffffLL) return RR_EUNSUPPORTED;
+  const dim3 grid((unsigned)nblk), block(512);
+  switch (d->w) {
+    case 64: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 64, RR_CONV3X3>), grid, block, 0, st, a); break;
+    case 32: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 32, RR_CONV3X3>), grid, block, 0, st, a); break;
+    case 16: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 16, RR_CONV3X3>), grid, block, 0, st, a); break;
+    default: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 8, RR_CONV3X3>), grid, block, 0, st, a); break;
+  }
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
 template <typename T>
 int dispatch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
+  if constexpr (sizeof(T) == 2) {
+    const int hb = halo_bc(d);
+    if (hb == 128) return launch_halo<128>(d, a, st);
+    if (hb == 64) return launch_halo<64>(d, a, st);
+  }
   const Tile t = pick_tile(d);
   if (t.bc == 128) return launch_mode<T, 128, 128, 2>(d, a, st);
   if (t.bp == 256) return launch_mode<T, 64, 256, 1>(d, a, st);
@@ -503,13 +914,13 @@ int dispatch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
 extern "C" int rr_igemm_stat_blocks(const rr_igemm_desc *d) {
   if (!d) return RR_EINVAL;
   const long long P = (long long)d->n * d->h * d->w;
-  const int bp = pick_tile(d).bp;
+  const int bp = halo_bc(d) ? 256 : pick_tile(d).bp;
   return (int)((P + bp - 1) / bp);
 }
 
-extern "C" int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
-                        const void *w, const float *bias, void *y1, void *y2,
-                        const void *mask, float *stats_partial, rr_stream stream) {
+static int fill_args(const rr_igemm_desc *d, const void *x1, const void *x2, const void *w,
+                     const float *bias, void *y1, void *y2, const void *mask,
+                     float *stats_partial, IgemmArgs &a) {
   if (!d || !x1 || !w || !y1) return RR_EINVAL;
   if (d->dtype != RR_F32 && d->dtype != RR_BF16) return RR_EINVAL;
   const int bk = d->dtype == RR_F32 ? 32 : 64;
@@ -524,7 +935,6 @@ extern "C" int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
   if (d->want_stats && !stats_partial) return RR_EINVAL;
   const long long P = (long long)d->n * d->h * d->w;
   if (P > 0x7fffffffLL / 4) return RR_EUNSUPPORTED;
-  IgemmArgs a;
   a.x1 = (const char *)x1; a.x2 = (const char *)x2; a.wt = (const char *)w;
   a.bias = bias; a.y1 = (char *)y1; a.y2 = (char *)y2; a.mask = (const char *)mask;
   a.stats = d->want_stats ? stats_partial : nullptr;
@@ -540,6 +950,50 @@ extern "C" int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
   static const int dbg_env = [] { const char *e = getenv("RR_IGEMM_DBG"); return e ? atoi(e) : 0; }();
   a.dbg = dbg_env;
   a.ncblk = 1;
+  a.bt = nullptr; a.bmean = a.binv = a.baff_s = a.baff_b = a.balpha = nullptr;
+  a.bpart = a.bapart = nullptr;
+  return RR_OK;
+}
+
+extern "C" int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
+                        const void *w, const float *bias, void *y1, void *y2,
+                        const void *mask, float *stats_partial, rr_stream stream) {
+  IgemmArgs a;
+  const int rc = fill_args(d, x1, x2, w, bias, y1, y2, mask, stats_partial, a);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (d->dtype == RR_BF16) return dispatch<bf16_t>(d, a, st);
+  return dispatch<float>(d, a, st);
+}
+
+static int bnbwd_rows(const rr_igemm_desc *d) { return rr_igemm_stat_blocks(d); }
+
+extern "C" size_t rr_igemm_bnbwd_workspace(const rr_igemm_desc *d) {
+  if (!d || d->c_out <= 0) return 0;
+  const int rows = bnbwd_rows(d);
+  if (rows <= 0) return 0;
+  return ((size_t)rows * d->c_out * 3 + (size_t)rows * (d->c_out / 64)) * sizeof(float);
+}
+
+extern "C" int rr_igemm_bnbwd(const rr_igemm_desc *d, const void *dy, const void *w,
+                              const void *t, const float *mean, const float *invstd,
+                              const float *aff_s, const float *aff_b, const float *alpha,
+                              void *gm_out, float *partial, rr_stream stream) {
+  if (!d || !dy || !w || !t || !mean || !invstd || !aff_s || !aff_b || !alpha || !gm_out ||
+      !partial)
+    return RR_EINVAL;
+  if (d->mode != RR_CONV3X3 && d->mode != RR_CONV1X1) return RR_EUNSUPPORTED;
+  if (d->c_in2 || d->out_split || d->has_mask || d->accumulate || d->has_bias || d->want_stats ||
+      d->out_nchw || d->act)
+    return RR_EINVAL;
+  if (d->c_out % 64) return RR_EUNSUPPORTED;      // staged epilogue: whole column tiles
+  IgemmArgs a;
+  const int rc = fill_args(d, dy, nullptr, w, nullptr, gm_out, nullptr, nullptr, nullptr, a);
+  if (rc) return rc;
+  a.bt = (const char *)t;
+  a.bmean = mean; a.binv = invstd; a.baff_s = aff_s; a.baff_b = aff_b; a.balpha = alpha;
+  a.bpart = partial;
+  a.bapart = partial + (size_t)bnbwd_rows(d) * d->c_out * 3;
   hipStream_t st = (hipStream_t)stream;
   if (d->dtype == RR_BF16) return dispatch<bf16_t>(d, a, st);
   return dispatch<float>(d, a, st);

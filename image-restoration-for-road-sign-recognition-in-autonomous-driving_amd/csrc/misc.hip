@@ -364,6 +364,97 @@ __global__ void conv_out_bwd_kernel(int n, int h, int w, int cin, int cout,
   }
 }
 
+// cin == 64 variant: 8 threads per pixel x 8 channels (16-B bf16 / 2 x 16-B
+// f32 vectors), 32 pixels per block pass, 2 passes in flight per iteration.
+// dW partials: shuffle over the 8 pixel lanes of a wave that share a channel
+// group, then the 4 waves through LDS (fixed order).
+template <typename T, int COUT>
+__global__ __launch_bounds__(256) void conv_out_bwd64_kernel(
+    int n, int h, int w, const float *__restrict__ dy, const T *__restrict__ x,
+    const float *__restrict__ wt, T *__restrict__ dx, int mask_relu, float *__restrict__ part,
+    long long px_per_block) {
+  constexpr int CIN = 64;
+  __shared__ float red[4][COUT + 1][CIN];
+  const int cg = threadIdx.x & 7, pl = threadIdx.x >> 3;      // channel group, pixel lane
+  const long long hw = (long long)h * w;
+  const long long P = (long long)n * hw;
+  const long long pb = blockIdx.x * px_per_block;
+  const long long pe = min(P, pb + px_per_block);
+  float wv[COUT][8];
+#pragma unroll
+  for (int co = 0; co < COUT; ++co)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wv[co][j] = wt[co * CIN + cg * 8 + j];
+  float sw[COUT][8], sb[COUT];
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) {
+    sb[co] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sw[co][j] = 0.f;
+  }
+  auto one = [&](long long p) __attribute__((always_inline)) {
+    const long long nn = p / hw, r = p - nn * hw;
+    float d[COUT];
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) d[co] = dy[(nn * COUT + co) * hw + r];
+    const T *xp = x + p * CIN + cg * 8;
+    const f32x4 x0 = load4<T>(xp), x1 = load4<T>(xp + 4);
+    const float xv[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    float g[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int co = 0; co < COUT; ++co) {
+        t += d[co] * wv[co][j];
+        sw[co][j] += d[co] * xv[j];
+      }
+      g[j] = (mask_relu && !(xv[j] > 0.f)) ? 0.f : t;
+    }
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) sb[co] += d[co];
+    if (dx) store8<T>(dx + p * CIN + cg * 8, f32x4{g[0], g[1], g[2], g[3]}, f32x4{g[4], g[5], g[6], g[7]});
+  };
+  long long p = pb + pl;
+  for (; p + 32 < pe; p += 64) {
+    one(p);
+    one(p + 32);
+  }
+  if (p < pe) one(p);
+  // reduce over the 8 pixel lanes of this wave with the same cg (lane bits 3..5)
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = sw[co][j];
+      v += __shfl_xor(v, 8, 64);
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      sw[co][j] = v;
+    }
+    float v = sb[co];
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    sb[co] = v;
+  }
+  const int wv_ = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane < 8) {
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[wv_][co][cg * 8 + j] = sw[co][j];
+      if (cg == 0) red[wv_][COUT][co] = sb[co];
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < COUT * CIN + COUT; i += 256) {
+    const int co = i / CIN, ci = i - co * CIN;
+    part[(long long)blockIdx.x * (COUT + 1) * CIN + i] =
+        red[0][co][ci] + red[1][co][ci] + red[2][co][ci] + red[3][co][ci];
+  }
+}
+
 __global__ void conv_out_bwd_finalize(int cin, int cout, int blocks, const double *__restrict__ part,
                                       float *dw, float *db) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over cout*cin + cout
@@ -896,7 +987,14 @@ extern "C" int rr_conv_out_bwd(int dtype, int n, int h, int w, int cin, int cout
   const long long P = (long long)n * h * w;
   const long long ppb = (P + blocks - 1) / blocks;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == RR_BF16)
+  if (cin == 64 && cout == 3) {
+    if (dtype == RR_BF16)
+      hipLaunchKernelGGL((conv_out_bwd64_kernel<bf16_t, 3>), dim3(blocks), dim3(256), 0, st, n, h, w,
+                         dy, (const bf16_t *)x, wt, (bf16_t *)dx, mask_relu, (float *)ws, ppb);
+    else
+      hipLaunchKernelGGL((conv_out_bwd64_kernel<float, 3>), dim3(blocks), dim3(256), 0, st, n, h, w,
+                         dy, (const float *)x, wt, (float *)dx, mask_relu, (float *)ws, ppb);
+  } else if (dtype == RR_BF16)
     hipLaunchKernelGGL(conv_out_bwd_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, n, h, w, cin,
                        cout, dy, (const bf16_t *)x, wt, (bf16_t *)dx, mask_relu, (float *)ws, ppb);
   else

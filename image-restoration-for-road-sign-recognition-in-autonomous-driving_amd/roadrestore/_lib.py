@@ -45,6 +45,8 @@ S_ = C.c_size_t
 _SIGS = {
     "rr_igemm": (I_, [C.POINTER(IgemmDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_]),
     "rr_igemm_stat_blocks": (I_, [C.POINTER(IgemmDesc)]),
+    "rr_igemm_bnbwd_workspace": (S_, [C.POINTER(IgemmDesc)]),
+    "rr_igemm_bnbwd": (I_, [C.POINTER(IgemmDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_, P_, P_]),
     "rr_wgrad_workspace": (S_, [C.POINTER(WgradDesc)]),
     "rr_wgrad": (I_, [C.POINTER(WgradDesc), P_, P_, P_, P_, P_, S_, P_]),
     "rr_pack_conv": (I_, [I_, I_, I_, I_, P_, P_, P_, P_]),
@@ -60,6 +62,9 @@ _SIGS = {
                               P_, P_]),
     "rr_bn_bwd_finalize": (I_, [C.POINTER(BnBwdDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_, P_,
                                 P_, P_]),
+    "rr_bn_bwd_finalize_rows_workspace": (S_, [I_, I_]),
+    "rr_bn_bwd_finalize_rows": (I_, [C.POINTER(BnBwdDesc), I_, P_, I_, P_, P_, P_, P_, P_, P_, P_,
+                                     P_, S_, P_]),
     "rr_bn_bwd_apply": (I_, [C.POINTER(BnBwdDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_, P_, P_,
                              P_, P_, P_, P_, P_]),
     "rr_channel_sum": (I_, [I_, L_, I_, P_, P_, I_, P_, S_, P_]),

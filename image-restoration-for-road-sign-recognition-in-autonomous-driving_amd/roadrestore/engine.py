@@ -18,6 +18,8 @@ Reference schedules mirrored (file:line in the reference repo):
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import ops
@@ -125,6 +127,10 @@ class GradSink:
         self.view = {}
         return out
 
+
+
+# A/B switch for the fused conv-dgrad + BN/PReLU backward reduce (default on)
+FUSE_BNBWD = os.environ.get("RR_FUSE_BNBWD", "1") not in ("0", "")
 
 def _params(*mods):
     out = []
@@ -319,11 +325,18 @@ def resblock_backward(blk, S, g_out, sink):
                             outs=dict(dgamma0=sink[bn2.weight], dbeta0=sink[bn2.bias]))
         dt2 = r["dt0"]
     ops.wgrad(RR_CONV3X3, dt2, S.a1, None, n, h, w, cout, dw=sink[c2.weight])
-    da1, _, _ = ops.igemm(RR_CONV3X3, dt2, None, n, h, w, S.pk2[1], cout)
-    r1 = ops.bn_backward(da1, S.t1, S.m1, S.i1, bn1.weight, mask_kind=2, aux=S.t1, aff_s=S.s1,
-                         aff_b=S.sh1, alpha=pr.weight,
-                         outs=dict(dgamma0=sink[bn1.weight], dbeta0=sink[bn1.bias],
-                                   dalpha=sink[pr.weight]))
+    outs1 = dict(dgamma0=sink[bn1.weight], dbeta0=sink[bn1.bias], dalpha=sink[pr.weight])
+    if FUSE_BNBWD:
+        # conv2 dgrad whose epilogue applies the PReLU backward and reduces
+        # BN1's backward sums (no separate pass over dL/d(PReLU out))
+        gm1, part, rows, arows = ops.igemm_bnbwd(RR_CONV3X3, dt2, n, h, w, S.pk2[1], cout, S.t1,
+                                                 S.m1, S.i1, S.s1, S.sh1, pr.weight)
+        r1 = ops.bn_backward_rows(gm1, part, rows, arows, S.t1, S.m1, S.i1, bn1.weight,
+                                  outs=outs1)
+    else:
+        da1, _, _ = ops.igemm(RR_CONV3X3, dt2, None, n, h, w, S.pk2[1], cout)
+        r1 = ops.bn_backward(da1, S.t1, S.m1, S.i1, bn1.weight, mask_kind=2, aux=S.t1,
+                             aff_s=S.s1, aff_b=S.sh1, alpha=pr.weight, outs=outs1)
     dt1 = r1["dt0"]
     ops.wgrad(RR_CONV3X3, dt1, x1, x2, n, h, w, cout, dw=sink[c1.weight])
     split = c_in1 if c_in2 else 0

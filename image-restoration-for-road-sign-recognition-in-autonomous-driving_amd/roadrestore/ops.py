@@ -9,6 +9,7 @@ CPU fallback: a missing library or device raises.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -59,6 +60,22 @@ def _kpick_tile(mode, n, h, w, cout, split):
     if cout <= 64 and (P + 255) // 256 >= 512:
         return 64, 256, 1
     return 64, 128, 2
+
+
+def _khalo_bc(mode, dt, n, h, w, c1, c2, cout, split, out_nchw):
+    """Mirror of csrc/igemm.hip halo_bc: BC of the LDS-halo kernel, or 0."""
+    if os.environ.get("RR_IGEMM_NOHALO", "0") not in ("", "0"):
+        return 0
+    if dt != torch.bfloat16 or mode != RR_CONV3X3 or out_nchw or w not in (8, 16, 32, 64):
+        return 0
+    R = 256 // w
+    if h % 8 or (h % R if R <= h else (R % h or n % (R // h))):
+        return 0
+    if c1 % 64 or c2 % 64:
+        return 0
+    if cout % 128 == 0 and (split == 0 or split % 128 == 0):
+        return 128
+    return 64 if cout % 64 == 0 else 0
 
 
 def _ws(nbytes, device):
@@ -136,8 +153,12 @@ def igemm(mode, x1, x2, n, h, w, wpack, cout, bias=None, act=0, out=None, out2=N
         launch()
     else:
         taps = 9 if mode == RR_CONV3X3 else (4 if mode == RR_CONVT_DOWN else 1)
-        bc, bp, wc = _kpick_tile(mode, n, h, w, cout, split)
-        sym = f"igemm_kernel<{'bf16' if dt == torch.bfloat16 else 'f32'},{bc},{bp},{wc},mode{mode}>"
+        hb = _khalo_bc(mode, dt, n, h, w, c1, c2, cout, split, out_nchw)
+        if hb:
+            sym = f"igemm3_halo_kernel<{hb},{w}>"
+        else:
+            bc, bp, wc = _kpick_tile(mode, n, h, w, cout, split)
+            sym = f"igemm_kernel<{'bf16' if dt == torch.bfloat16 else 'f32'},{bc},{bp},{wc},mode{mode}>"
         PROBE(sym, 2.0 * n * h * w * cout * taps * (c1 + c2), launch)
     return out, out2, st
 
@@ -260,6 +281,69 @@ def bn_backward(g, t0, mean0, inv0, gamma0, *, mask_kind=0, aux=None, aff_s=None
                 "rr_bn_bwd_apply")
     return dict(dt0=dt0, dt1=dt1, gm=gm_out, dgamma0=dg0, dbeta0=db0, dgamma1=dg1, dbeta1=db1,
                 dalpha=dal)
+
+
+def igemm_bnbwd(mode, dy, n, h, w, wpack, cout, t, mean, inv, aff_s, aff_b, alpha, out=None):
+    """Conv dgrad fused with the BN -> PReLU backward reduce (rr_igemm_bnbwd).
+    Returns (gm, partial, rows, arows): gm = dL/d(BN out) [n, h, w, cout] and
+    the row partials for ``bn_backward_rows``."""
+    _need_cuda(dy, wpack, t)
+    dt = dy.dtype
+    d = IgemmDesc(rr_dtype(dt), mode, n, h, w, dy.shape[-1], 0, cout, 0, 0, 0, 0, 0, 0, 0)
+    if out is None:
+        out = torch.empty((n, h, w, cout), dtype=dt, device=dy.device)
+    rows = lib().rr_igemm_stat_blocks(C.byref(d))
+    nbytes = lib().rr_igemm_bnbwd_workspace(C.byref(d))
+    part = torch.empty(nbytes // 4, dtype=torch.float32, device=dy.device)
+
+    def launch():
+        lib().check(lib().rr_igemm_bnbwd(C.byref(d), _p(dy), _p(wpack), _p(t), _p(mean), _p(inv),
+                                         _p(aff_s), _p(aff_b), _p(alpha), _p(out), _p(part),
+                                         stream()), "rr_igemm_bnbwd")
+    if PROBE is None:
+        launch()
+    else:
+        taps = 9 if mode == RR_CONV3X3 else 1
+        hb = _khalo_bc(mode, dt, n, h, w, dy.shape[-1], 0, cout, 0, False)
+        if hb:
+            sym = f"igemm3_halo_kernel<{hb},{w}>"
+        else:
+            bc, bp, wc = _kpick_tile(mode, n, h, w, cout, 0)
+            sym = f"igemm_kernel<{'bf16' if dt == torch.bfloat16 else 'f32'},{bc},{bp},{wc},mode{mode}>"
+        PROBE(sym, 2.0 * n * h * w * cout * taps * dy.shape[-1], launch)
+    return out, part, rows, rows * (cout // 64)
+
+
+def bn_backward_rows(gm, part, rows, arows, t0, mean0, inv0, gamma0, outs=None):
+    """BN backward from precomputed row partials (the rr_igemm_bnbwd epilogue):
+    finalize (fp64 fixed order) + apply with gm already PReLU-masked."""
+    Cc = gm.shape[-1]
+    P = gm.numel() // Cc
+    dev = gm.device
+    d = BnBwdDesc(rr_dtype(gm.dtype), P, Cc, 0, 1)
+    o = outs or {}
+    dg0 = o.get("dgamma0")
+    if dg0 is None:
+        dg0 = torch.empty(Cc, dtype=torch.float32, device=dev)
+    db0 = o.get("dbeta0")
+    if db0 is None:
+        db0 = torch.empty_like(dg0)
+    dal = o.get("dalpha")
+    if dal is None:
+        dal = torch.empty(1, dtype=torch.float32, device=dev)
+    coef = torch.empty(Cc * 6, dtype=torch.float32, device=dev)
+    ws = _ws(lib().rr_bn_bwd_finalize_rows_workspace(Cc, rows), dev)
+    apart = part[rows * Cc * 3:]
+    s = stream()
+    lib().check(lib().rr_bn_bwd_finalize_rows(C.byref(d), rows, _p(part), arows, _p(apart),
+                                              _p(gamma0), _p(inv0), _p(dg0), _p(db0), _p(dal),
+                                              _p(coef), _p(ws), ws.numel(), s),
+                "rr_bn_bwd_finalize_rows")
+    dt0 = torch.empty_like(gm)
+    lib().check(lib().rr_bn_bwd_apply(C.byref(d), _p(gm), None, None, None, None, _p(t0), _p(mean0),
+                                      _p(inv0), None, None, None, _p(coef), _p(dt0), None, None, s),
+                "rr_bn_bwd_apply")
+    return dict(dt0=dt0, dgamma0=dg0, dbeta0=db0, dalpha=dal)
 
 
 def channel_sum(x, out=None, accumulate=False):

@@ -84,6 +84,22 @@ int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
 /* number of row blocks the partial stats buffer holds: [blocks][c_out][2] */
 int rr_igemm_stat_blocks(const rr_igemm_desc *d);
 
+/* conv dgrad fused with the backward reduce of the BatchNorm2d -> PReLU pair
+ * that produced its input (ResidualBlock conv_block[1:3], 14:101-103):
+ * the GEMM result is g = dL/d(PReLU out); the epilogue writes
+ *   gm = g * (u > 0 ? 1 : alpha),  u = t * aff_s[c] + aff_b[c] (BN output)
+ * to gm_out and the partials partial[rows][c_out][3] = {sum gm, sum gm*xhat, 0}
+ * (xhat = (t - mean) * invstd) followed by partial_alpha[rows][c_out/64] of
+ * sum(g * u * (u <= 0)), rows = rr_igemm_stat_blocks(d).  Replaces the
+ * separate rr_bn_bwd_reduce pass (mask_kind 2) over dL/d(PReLU out).
+ * d: no bias / split / mask / accumulate / stats / act, c_in2 = 0,
+ * c_out % 64 == 0. */
+size_t rr_igemm_bnbwd_workspace(const rr_igemm_desc *d);
+int rr_igemm_bnbwd(const rr_igemm_desc *d, const void *dy, const void *w, const void *t,
+                   const float *mean, const float *invstd, const float *aff_s,
+                   const float *aff_b, const float *alpha, void *gm_out, float *partial,
+                   rr_stream stream);
+
 /*
  * Weight-gradient GEMM (split over pixels):
  *  RR_CONV3X3 / RR_CONV1X1:  dW[co][ci][ky][kx] = sum_p dy[p,co] x[p+tap,ci]
@@ -177,6 +193,14 @@ int rr_bn_bwd_finalize(const rr_bnbwd_desc *d, const float *partial,
                        const float *gamma1, const float *invstd1,
                        float *dgamma0, float *dbeta0, float *dgamma1, float *dbeta1,
                        float *dalpha, float *coef, rr_stream stream);
+/* finalize from caller-provided row partials [rows][C][3] (e.g. the
+ * rr_igemm_bnbwd epilogue), fp64 fixed-order reduce; nbn = 1.  arows /
+ * apartial: the PReLU alpha partials (0 / NULL when none). */
+size_t rr_bn_bwd_finalize_rows_workspace(int C, int rows);
+int rr_bn_bwd_finalize_rows(const rr_bnbwd_desc *d, int rows, const float *partial, int arows,
+                            const float *apartial, const float *gamma0, const float *invstd0,
+                            float *dgamma0, float *dbeta0, float *dalpha, float *coef,
+                            void *ws, size_t ws_bytes, rr_stream stream);
 /* apply: dt_i = coef_a[c]*(gm - coef_b[c] - xhat_i*coef_c[c]); optional gm out */
 int rr_bn_bwd_apply(const rr_bnbwd_desc *d, const void *g, const void *aux,
                     const float *aff_s, const float *aff_b, const float *alpha,

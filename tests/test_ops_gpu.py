@@ -66,6 +66,62 @@ def test_conv3x3_fwd(dev, dt, n, h, w, cin, cout):
         tol * pre.abs().max().item() * 2
 
 
+# halo-eligible bf16 shapes: (n, h, w, c1, c2, cout, split) -- whole-row
+# 256-pixel tiles (W in {8,16,32,64}), one tile spanning 4 images at 8x8,
+# BC = 128 and 64 column tiles, concat sources and dgrad-style column split
+HALO_SHAPES = [(4, 8, 8, 64, 64, 128, 0), (2, 16, 16, 64, 0, 64, 0), (1, 32, 32, 128, 0, 192, 0),
+               (1, 8, 64, 64, 128, 128, 64), (8, 8, 8, 256, 0, 512, 256), (2, 16, 32, 64, 0, 256, 128)]
+
+
+@pytest.mark.parametrize("halo", [True, False])
+@pytest.mark.parametrize("shape", HALO_SHAPES)
+def test_conv3x3_halo(dev, shape, halo, monkeypatch):
+    """bf16 3x3 conv through the LDS-halo igemm (and the per-tap kernel for
+    A/B): bias + ReLU + BN partial stats, concat input, column split with a
+    relu-backward mask, accumulate.  Inputs bf16-exact, so vs fp32 torch the
+    only error is the bf16 rounding of the output."""
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    monkeypatch.setenv("RR_IGEMM_NOHALO", "0" if halo else "1")
+    n, h, w, c1, c2, cout, split = shape
+    cin = c1 + c2
+    x = rnd(n, cin, h, w, seed=41).bfloat16().float()
+    wt = (rnd(cout, cin, 3, 3, seed=42) * (1.0 / (3 * cin ** 0.5))).bfloat16().float()
+    b = rnd(cout, seed=43)
+    wf, _ = rr.ops.pack_conv(wt.to(dev), torch.bfloat16)
+    bf = torch.bfloat16
+    x1 = nhwc(x[:, :c1], dev, bf)
+    x2 = nhwc(x[:, c1:], dev, bf) if c2 else None
+    pre = F.conv2d(x, wt, None, padding=1)
+
+    def rel(a, r):
+        return ((a - r).norm() / r.norm()).item()
+
+    if not split:
+        y, _, st = rr.ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf, cout, bias=b.to(dev), act=1,
+                                stats=True)
+        assert rel(nchw(y), F.relu(pre + b[None, :, None, None])) < 4e-3
+        s = st.cpu().double().sum(0)
+        assert rel(s[:, 0], pre.double().sum((0, 2, 3))) < 1e-5
+        assert rel(s[:, 1], (pre.double() ** 2).sum((0, 2, 3))) < 1e-5
+    else:
+        # split columns [0, split) -> y1 (masked, accumulated), [split, cout) -> y2
+        mask = rnd(n, split, h, w, seed=44)
+        acc0 = rnd(n, split, h, w, seed=45).bfloat16().float()
+        acc2 = rnd(n, cout - split, h, w, seed=46).bfloat16().float()
+        y1, y2 = nhwc(acc0, dev, bf), nhwc(acc2, dev, bf)
+        # accumulate applies to both column halves (the dgrad of a concat)
+        y1, y2, _ = rr.ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf, cout, out=y1, out2=y2,
+                                 split=split, accumulate=True, mask=None)
+        assert rel(nchw(y1), pre[:, :split] + acc0) < 4e-3
+        assert rel(nchw(y2), pre[:, split:] + acc2) < 4e-3
+        # a plain masked conv over the first split columns
+        wf2, _ = rr.ops.pack_conv(wt[:split].to(dev), bf)
+        ym, _, _ = rr.ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf2, split, mask=nhwc(mask, dev, bf))
+        refm = torch.where(mask.bfloat16().float() > 0, pre[:, :split], torch.zeros(()))
+        assert rel(nchw(ym), refm) < 4e-3
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_conv3x3_concat_dgrad_split(dev, dt):
     """cat((up, skip), 1) read in place (07:112) and the dgrad split."""
@@ -129,6 +185,44 @@ def test_wgrad3_halo(dev, hw, halo, monkeypatch):
     # summation order differs from torch
     rel = ((dw.cpu() - wt.grad).norm() / wt.grad.norm()).item()
     assert rel < 2e-5, rel
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,h,w,C", [(4, 8, 8, 128), (2, 16, 16, 64), (4, 8, 8, 256), (1, 8, 64, 64)])
+def test_igemm_bnbwd_fused(dev, dt, n, h, w, C):
+    """conv dgrad + BN/PReLU backward reduce fused in the epilogue
+    (rr_igemm_bnbwd + rr_bn_bwd_finalize_rows) == the unfused sequence
+    (rr_igemm, then rr_bn_bwd_reduce/finalize/apply with mask_kind 2)."""
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    ops = rr.ops
+    g2 = nhwc(rnd(n, C, h, w, seed=51), dev, dt)
+    wt = (rnd(C, C, 3, 3, seed=52) * (1.0 / (3 * C ** 0.5))).to(dev)
+    _, wd = ops.pack_conv(wt, dt)
+    t1 = nhwc(rnd(n, C, h, w, seed=53) * 2 + 0.3, dev, dt)
+    tf = t1.float().reshape(-1, C)
+    mean = tf.mean(0)
+    inv = 1.0 / torch.sqrt(tf.var(0, unbiased=False) + 1e-5)
+    gamma = (torch.rand(C, generator=torch.Generator().manual_seed(54)) + 0.5).to(dev)
+    beta = (torch.rand(C, generator=torch.Generator().manual_seed(55)) - 0.5).to(dev)
+    s1 = gamma * inv
+    sh1 = beta - mean * s1
+    alpha = torch.tensor([0.23], device=dev)
+    da1, _, _ = ops.igemm(RR_CONV3X3, g2, None, n, h, w, wd, C)
+    ref = ops.bn_backward(da1, t1, mean, inv, gamma, mask_kind=2, aux=t1, aff_s=s1, aff_b=sh1,
+                          alpha=alpha)
+    gm, part, rows, arows = ops.igemm_bnbwd(RR_CONV3X3, g2, n, h, w, wd, C, t1, mean, inv, s1, sh1,
+                                            alpha)
+    got = ops.bn_backward_rows(gm, part, rows, arows, t1, mean, inv, gamma)
+    torch.cuda.synchronize()
+    tol = 1e-5 if dt == torch.float32 else 2e-2   # bf16: the unfused path rounds da1 first
+
+    def rel(a, b):
+        a, b = a.float().cpu(), b.float().cpu()
+        return ((a - b).norm() / b.norm()).item()
+    assert rel(got["dt0"], ref["dt0"]) < tol
+    for k in ("dgamma0", "dbeta0", "dalpha"):
+        assert rel(got[k], ref[k]) < tol, k
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
