@@ -875,7 +875,12 @@ int halo_bc(const rr_igemm_desc *d) {
   if (d->h % 8) return 0;
   if (R <= d->h ? (d->h % R) : (R % d->h || d->n % (R / d->h))) return 0;
   if (d->c_in1 % 64 || d->c_in2 % 64) return 0;
-  if (d->c_out % 128 == 0 && (d->out_split == 0 || d->out_split % 128 == 0)) return 128;
+  // BC = 64 (2 WG/CU) when the K loop is a single 64-channel chunk: the
+  // per-tile prologue / epilogue then dominates and overlap wins
+  const char *e64 = getenv("RR_HALO_BC64_MAXCIN");
+  const int max64 = e64 ? atoi(e64) : 0;
+  const bool wide_ok = d->c_out % 128 == 0 && (d->out_split == 0 || d->out_split % 128 == 0);
+  if (wide_ok && d->c_in1 + d->c_in2 > max64) return 128;
   if (d->c_out % 64 == 0) return 64;
   return 0;
 }

@@ -73,7 +73,8 @@ def _khalo_bc(mode, dt, n, h, w, c1, c2, cout, split, out_nchw):
         return 0
     if c1 % 64 or c2 % 64:
         return 0
-    if cout % 128 == 0 and (split == 0 or split % 128 == 0):
+    max64 = int(os.environ.get("RR_HALO_BC64_MAXCIN", "0") or 0)
+    if cout % 128 == 0 and (split == 0 or split % 128 == 0) and c1 + c2 > max64:
         return 128
     return 64 if cout % 64 == 0 else 0
 
