@@ -607,8 +607,8 @@ template <int W> struct HaloGeom {
 // per CU, one tile's prologue / epilogue overlapping the other's MFMA loop.
 // BC = 128 double-buffers the halo, 1 workgroup per CU.
 template <int BC> struct HaloCfg {
-  static constexpr int HB = BC == 64 ? 1 : 2;
-  static constexpr int OCC = BC == 64 ? 4 : 2;   // min waves per SIMD (launch bound)
+  static constexpr int HB = BC <= 64 ? 1 : 2;
+  static constexpr int OCC = BC <= 64 ? 4 : 2;   // min waves per SIMD (launch bound)
 };
 
 template <int BC, int W, int MODE>
@@ -617,11 +617,14 @@ __global__ __launch_bounds__(512, HaloCfg<BC>::OCC) void igemm3_halo_kernel(Igem
   using G = HaloGeom<W>;
   constexpr int HB = HaloCfg<BC>::HB;
   constexpr int BP = 256, NT = 512;
-  constexpr int WC = BC / 64, WP = 8 / WC;
-  constexpr int MC = 4, MP = BP / WP / 16;
+  // wave grid: WC (channel) x WP (pixel) waves; a wave owns WCH channels
+  // (64, or all 16 for the narrow NCHW image-grad tile)
+  constexpr int WC = BC >= 64 ? BC / 64 : 1, WP = 8 / WC, WCH = BC / WC;
+  constexpr int MC = WCH / 16, MP = BP / WP / 16;
   constexpr int WPLANE = BC * 16;                               // weight planes: BC rows
   constexpr int WBYTES = 8 * WPLANE;
-  constexpr int LW = BC * 8 / NT;                               // weight pieces per thread
+  constexpr int WPIECES = BC * 8;
+  constexpr int LW = (WPIECES + NT - 1) / NT;                   // weight pieces per thread
   constexpr int MAIN = HB * G::HBYTES + 2 * WBYTES;
   constexpr int SROW = BC + 4;
   constexpr int STG = BP * SROW * 4 + 2 * 512 * 4 * 2 + 256;
@@ -665,14 +668,15 @@ __global__ __launch_bounds__(512, HaloCfg<BC>::OCC) void igemm3_halo_kernel(Igem
   for (int i = 0; i < LW; ++i) {
     const int idx = tid + NT * i;
     const int r = 8 * (idx >> 6) + (idx & 7);
-    wrow[i] = a.wt + ((long long)(c0 + r) * a.K) * 2 + pj;
+    // rows past c_out (the narrow tile's padding) load row 0 and are zeroed
+    wrow[i] = a.wt + ((long long)(c0 + r < a.cout ? c0 + r : 0) * a.K) * 2 + pj;
   }
 
   // ---- per-lane fragment bases ----
   const int frow = lane & 15, fq = lane >> 4;
   int abase[MC], bbase[MP];
 #pragma unroll
-  for (int mi = 0; mi < MC; ++mi) abase[mi] = fq * WPLANE + (wc * 64 + mi * 16 + frow) * 16;
+  for (int mi = 0; mi < MC; ++mi) abase[mi] = fq * WPLANE + (wc * WCH + mi * 16 + frow) * 16;
 #pragma unroll
   for (int ni = 0; ni < MP; ++ni) {
     const int q = wp * (BP / WP) + ni * 16 + frow;              // pixel within the tile
@@ -717,7 +721,12 @@ __global__ __launch_bounds__(512, HaloCfg<BC>::OCC) void igemm3_halo_kernel(Igem
     const long long off = ((long long)tap * a.cin + ch * 64) * 2;
 #pragma unroll
     for (int i = 0; i < LW; ++i) {
-      const V v = *reinterpret_cast<const V *>(wrow[i] + off);
+      V v = *reinterpret_cast<const V *>(wrow[i] + off);
+      if constexpr (BC < 64) {
+        const int idx = tid + NT * i;
+        const bool ok = c0 + 8 * (idx >> 6) + (idx & 7) < a.cout;
+        v.x = ok ? v.x : 0u; v.y = ok ? v.y : 0u; v.z = ok ? v.z : 0u; v.w = ok ? v.w : 0u;
+      }
       if constexpr (decltype(setc)::value == 0) wr0[i] = v; else wr1[i] = v;
     }
   };
@@ -728,7 +737,8 @@ __global__ __launch_bounds__(512, HaloCfg<BC>::OCC) void igemm3_halo_kernel(Igem
     for (int i = 0; i < LW; ++i) {
       const int idx = tid + NT * i;
       const int r = 8 * (idx >> 6) + (idx & 7);
-      *reinterpret_cast<V *>(d + ((idx >> 3) & 7) * WPLANE + r * 16) = SET == 0 ? wr0[i] : wr1[i];
+      if (WPIECES % NT == 0 || idx < WPIECES)
+        *reinterpret_cast<V *>(d + ((idx >> 3) & 7) * WPLANE + r * 16) = SET == 0 ? wr0[i] : wr1[i];
     }
   };
 
@@ -828,11 +838,29 @@ __global__ __launch_bounds__(512, HaloCfg<BC>::OCC) void igemm3_halo_kernel(Igem
 #pragma unroll
     for (int ni = 0; ni < MP; ++ni) {
       const int r = wp * (BP / WP) + ni * 16 + frow;
-      const int col = wc * 64 + mi * 16 + fq * 4;
+      const int col = wc * WCH + mi * 16 + fq * 4;
       *reinterpret_cast<f32x4 *>(stg + r * SROW + col) = acc[mi][ni];
     }
   __syncthreads();
-  store_staged<T, BC, BP, NT, MODE>(a, stg, c0, p0, pblk, tid);
+  if constexpr (BC < 64) {
+    // model-boundary image grad: fp32 NCHW, the tile's pixels are whole rows
+    // so each channel plane segment is contiguous
+    float *yo = reinterpret_cast<float *>(a.y1);
+    const int ncol = min(BC, a.cout - c0);
+    for (int i = tid; i < ncol * BP; i += NT) {
+      const int cl = i / BP, r = i - (i / BP) * BP;
+      const int p = p0 + r;
+      if (p >= a.P) continue;
+      const int nn = p / hw, rem = p - nn * hw;
+      float v = stg[r * SROW + cl] + (a.bias ? a.bias[c0 + cl] : 0.f);
+      const long long o = ((long long)nn * a.cout + c0 + cl) * hw + rem;
+      if (a.accumulate) v += yo[o];
+      if (a.act == RR_ACT_RELU) v = fmaxf(v, 0.f);
+      yo[o] = v;
+    }
+  } else {
+    store_staged<T, BC, BP, NT, MODE>(a, stg, c0, p0, pblk, tid);
+  }
 }
 
 template <typename T, int BC, int BP, int WC>
@@ -868,17 +896,20 @@ Tile pick_tile(const rr_igemm_desc *d) {
 // halo path eligibility (bf16 3x3, whole-row 256-pixel tiles); returns BC or 0
 int halo_bc(const rr_igemm_desc *d) {
   const char *e = getenv("RR_IGEMM_NOHALO");   // A/B switch (per call)
-  if ((e && atoi(e)) || d->dtype != RR_BF16 || d->mode != RR_CONV3X3 || d->out_nchw) return 0;
+  if ((e && atoi(e)) || d->dtype != RR_BF16 || d->mode != RR_CONV3X3) return 0;
+  // NCHW fp32 output only through the narrow 16-column tile (image grads)
+  if (d->out_nchw && (d->c_out > 16 || d->want_stats || d->c_in2)) return 0;
   const int W = d->w;
   if (!(W == 8 || W == 16 || W == 32 || W == 64)) return 0;
   const int R = 256 / W;
   if (d->h % 8) return 0;
   if (R <= d->h ? (d->h % R) : (R % d->h || d->n % (R / d->h))) return 0;
   if (d->c_in1 % 64 || d->c_in2 % 64) return 0;
+  if (d->out_nchw) return 16;
   // BC = 64 (2 WG/CU) when the K loop is a single 64-channel chunk: the
   // per-tile prologue / epilogue then dominates and overlap wins
   const char *e64 = getenv("RR_HALO_BC64_MAXCIN");
-  const int max64 = e64 ? atoi(e64) : 0;
+  const int max64 = e64 ? atoi(e64) : 128;   // measured best (tools/ab_igemm.py)
   const bool wide_ok = d->c_out % 128 == 0 && (d->out_split == 0 || d->out_split % 128 == 0);
   if (wide_ok && d->c_in1 + d->c_in2 > max64) return 128;
   if (d->c_out % 64 == 0) return 64;
@@ -887,7 +918,7 @@ int halo_bc(const rr_igemm_desc *d) {
 
 template <int BC>
 int launch_halo(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
-  a.ncblk = a.cout / BC;
+  a.ncblk = (a.cout + BC - 1) / BC;
   const long long nblk = (long long)(a.P / 256) * a.ncblk;
   if (nblk > 0x7fffffffLL) return RR_EUNSUPPORTED;
   const dim3 grid((unsigned)nblk), block(512);
@@ -907,6 +938,7 @@ int dispatch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
     const int hb = halo_bc(d);
     if (hb == 128) return launch_halo<128>(d, a, st);
     if (hb == 64) return launch_halo<64>(d, a, st);
+    if (hb == 16) return launch_halo<16>(d, a, st);
   }
   const Tile t = pick_tile(d);
   if (t.bc == 128) return launch_mode<T, 128, 128, 2>(d, a, st);

@@ -263,6 +263,103 @@ __global__ void im2col3_kernel(int n, int h, int w, int cin, int kpad, const flo
   }
 }
 
+// First 3x3 conv (cin 3 -> cout 64), bf16, fused im2col + MFMA.  K = 27
+// taps + the bias column (k = 27, value 1) padded to 32 = ONE
+// v_mfma_f32_16x16x32_bf16 per 16x16 tile.  The B fragment (lane: pixel
+// l & 15, k = 8 (l >> 4) .. +7) is gathered straight from the NCHW fp32 image
+// (L1/L2-hot: each value is read by 9 taps x neighbouring pixels) and rounded
+// to bf16 exactly as rr_im2col3 does; the A fragments (packed weights
+// [64][32] bf16, rr_pack_conv_in with kpad 32) stay in registers.  A wave
+// owns 64 consecutive pixels x 64 channels; epilogue staged through LDS so
+// every store is a 1 KiB run (8 pixels x 128 B): y_pre = conv + bias,
+// y_act = relu / prelu(alpha) of it (either may be null).
+__global__ __launch_bounds__(256) void conv_in_mfma_kernel(int n, int h, int w,
+                                                           const float *__restrict__ x,
+                                                           const bf16_t *__restrict__ wp, int act,
+                                                           const float *__restrict__ alpha,
+                                                           bf16_t *__restrict__ y_pre,
+                                                           bf16_t *__restrict__ y_act) {
+  constexpr int SR = 68;                       // fp32 staging row (floats), padded
+  __shared__ __attribute__((aligned(16))) float stg[4][64 * SR];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long long hw = (long long)h * w;
+  const long long P = (long long)n * hw;
+  const long long p0 = ((long long)blockIdx.x * 4 + wv) * 64;
+  if (p0 >= P) return;                         // whole wave out of range (no block barrier used)
+  const int fr = lane & 15, q = lane >> 4;
+  // weights: A[mi] = rows co = 16 mi + fr, k = 8q .. 8q+7
+  bf16x8 fa[4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+    fa[mi] = *reinterpret_cast<const bf16x8 *>(wp + (mi * 16 + fr) * 32 + q * 8);
+  // this lane's 8 k's: channel plane offset and tap shift
+  int koff[8], kdy[8], kdx[8], kkind[8];       // kind 0: image tap, 1: bias column, 2: zero
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = q * 8 + j;
+    const int ci = k / 9, t = k - (k / 9) * 9;
+    kdy[j] = t / 3 - 1;
+    kdx[j] = t % 3 - 1;
+    koff[j] = ci;
+    kkind[j] = k < 27 ? 0 : (k == 27 ? 1 : 2);
+  }
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const long long p = p0 + ni * 16 + fr;
+    const bool live = p < P;
+    const long long nn = live ? p / hw : 0;
+    const int rem = live ? (int)(p - nn * hw) : 0;
+    const int yy = rem / w, xx = rem - (rem / w) * w;
+    const float *xb = x + nn * 3 * hw;
+    u16 bits[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = 0.f;
+      if (kkind[j] == 1) {
+        v = 1.f;
+      } else if (kkind[j] == 0) {
+        const int y2 = yy + kdy[j], x2 = xx + kdx[j];
+        if (live && y2 >= 0 && y2 < h && x2 >= 0 && x2 < w) v = xb[koff[j] * hw + y2 * w + x2];
+      }
+      bits[j] = f32_to_bf16(v);                 // RNE, as rr_im2col3's store
+    }
+    bf16x8 fb;
+    __builtin_memcpy(&fb, bits, 16);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+      acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi], fb, f32x4{0.f, 0.f, 0.f, 0.f},
+                                                           0, 0, 0);
+  }
+  // stage: pixel ni*16 + fr, channels 16 mi + 4 q .. +3
+  float *sw = stg[wv];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+      *reinterpret_cast<f32x4 *>(sw + (ni * 16 + fr) * SR + mi * 16 + q * 4) = acc[mi][ni];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS writes landed
+  const float al = act == 2 ? alpha[0] : 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = i * 8 + (lane >> 3), c8 = (lane & 7) * 8;
+    const long long p = p0 + r;
+    if (p >= P) continue;
+    const f32x4 v0 = *reinterpret_cast<const f32x4 *>(sw + r * SR + c8);
+    const f32x4 v1 = *reinterpret_cast<const f32x4 *>(sw + r * SR + c8 + 4);
+    if (y_pre) store8<bf16_t>(y_pre + p * 64 + c8, v0, v1);
+    if (y_act) {
+      f32x4 a0, a1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        a0[k] = v0[k] > 0.f ? v0[k] : (act == 2 ? al * v0[k] : (act == 1 ? 0.f : v0[k]));
+        a1[k] = v1[k] > 0.f ? v1[k] : (act == 2 ? al * v1[k] : (act == 1 ? 0.f : v1[k]));
+      }
+      store8<bf16_t>(y_act + p * 64 + c8, a0, a1);
+    }
+  }
+}
+
 // first-layer weights [co][ci][3][3] (+ bias) -> [co][kpad] GEMM layout
 template <typename T>
 __global__ void pack_in_kernel(int cout, int cin, int kpad, const float *__restrict__ w,
@@ -1182,3 +1279,17 @@ extern "C" int rr_zero(void *p, size_t bytes, rr_stream stream) {
 }
 
 extern "C" const char *rr_version(void) { return "roadrestore-gfx950 0.1"; }
+
+extern "C" int rr_conv_in_mfma(int n, int h, int w, const float *x, const void *wpack32, int act,
+                               const float *alpha, void *y_pre, void *y_act, rr_stream stream) {
+  if (!x || !wpack32 || (!y_pre && !y_act) || n <= 0 || h <= 0 || w <= 0) return RR_EINVAL;
+  if (act < 0 || act > 2 || (act == 2 && !alpha) || (y_act == nullptr && act != 0)) return RR_EINVAL;
+  const long long P = (long long)n * h * w;
+  const long long blocks = (P + 255) / 256;
+  if (blocks > 0x7fffffffLL) return RR_EUNSUPPORTED;
+  hipLaunchKernelGGL(conv_in_mfma_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     n, h, w, x, (const bf16_t *)wpack32, act, alpha, (bf16_t *)y_pre,
+                     (bf16_t *)y_act);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}

@@ -71,6 +71,7 @@ _SIGS = {
     "rr_channel_sum_workspace": (S_, [L_, I_]),
     "rr_maxpool2_fwd": (I_, [I_, I_, I_, I_, I_, P_, P_, P_, P_]),
     "rr_maxpool2_bwd": (I_, [I_, I_, I_, I_, I_, P_, P_, P_, I_, P_, P_]),
+    "rr_conv_in_mfma": (I_, [I_, I_, I_, P_, P_, I_, P_, P_, P_, P_]),
     "rr_im2col3": (I_, [I_, I_, I_, I_, I_, I_, P_, P_, P_]),
     "rr_pack_conv_in": (I_, [I_, I_, I_, I_, P_, P_, P_, P_]),
     "rr_unpack_conv_in_grad": (I_, [I_, I_, I_, P_, P_, P_, P_]),

@@ -159,9 +159,8 @@ def _convT_up(wc, dt, conv, x, n, h, w, need_bwd):
 def simple_unet_forward(m, x, wc, dt, need_bwd):
     n, _, H, W = x.shape
     S = Bag(n=n, H=H, W=W, x=x)
-    e1a, col = ops.first_conv_fwd(x, m.enc1[0].weight, m.enc1[0].bias, dt,
-                                  wc.conv_in(m.enc1[0].weight, m.enc1[0].bias, dt), act=RELU)
-    S.col = col
+    e1a, _ = ops.first_conv_fwd(x, m.enc1[0].weight, m.enc1[0].bias, dt,
+                                wc.conv_in(m.enc1[0].weight, m.enc1[0].bias, dt), act=RELU)
     e1, pk12, _ = _conv3(wc, dt, m.enc1[2], e1a, None, n, H, W, RELU, need_bwd)
     p1, i1 = ops.maxpool2_fwd(e1)
     H2, W2 = H // 2, W // 2
@@ -239,7 +238,9 @@ def simple_unet_backward(m, S, g_out, sink):
     sink.ready(_params(m.enc2))
     ops.maxpool2_bwd(g_p1, S.i1, H, W, out=g_e1, accumulate=True, mask=S.e1)
     g_e1a, _ = _conv3_bwd(m.enc1[2], S.pk12, g_e1, S.e1a, None, n, H, W, sink, mask=S.e1a)
-    ops.first_conv_wgrad(S.col, g_e1a, sink[m.enc1[0].weight], sink[m.enc1[0].bias])
+    # im2col of the input only here (the fused forward never materialises it)
+    ops.first_conv_wgrad(ops.im2col3(S.x, g_e1a.dtype), g_e1a, sink[m.enc1[0].weight],
+                         sink[m.enc1[0].bias])
     sink.ready(_params(m.enc1))
 
 
@@ -364,12 +365,12 @@ def resunet_forward(m, x, wc, dt, training, need_bwd):
             "alignment branch, 14:169-182, is not implemented on this path)")
     S = Bag(n=n, H=H, W=W, x=x)
     pr = m.enc1[1]
-    e1pre, col = ops.first_conv_fwd(x, m.enc1[0].weight, m.enc1[0].bias, dt,
-                                    wc.conv_in(m.enc1[0].weight, m.enc1[0].bias, dt))
-    one, zero = _unit_affine(m.enc1[0].weight.shape[0], x.device)
-    e1 = ops.affine_act(e1pre, one, zero, alpha=pr.weight)
+    # conv + PReLU in one pass (the pre-activation kept for the PReLU backward)
+    e1, e1pre = ops.first_conv_fwd(x, m.enc1[0].weight, m.enc1[0].bias, dt,
+                                   wc.conv_in(m.enc1[0].weight, m.enc1[0].bias, dt), act=2,
+                                   alpha=pr.weight, want_pre=need_bwd)
     if need_bwd:
-        S.e1pre, S.col = e1pre, col
+        S.e1pre = e1pre
     r1, S.res1 = resblock_forward(m.res1, e1, None, n, H, W, wc, dt, training, need_bwd)
     p1, i1 = ops.maxpool2_fwd(r1)
     r2, S.res2 = resblock_forward(m.res2, p1, None, n, H // 2, W // 2, wc, dt, training, need_bwd)
@@ -440,7 +441,8 @@ def resunet_backward(m, S, g_out, sink):
     g_e1, _ = resblock_backward(m.res1, S.res1, g_r1, sink)
     pr = m.enc1[1]
     g_e1pre, _ = ops.prelu_bwd(g_e1, S.e1pre, pr.weight, dalpha=sink[pr.weight])
-    ops.first_conv_wgrad(S.col, g_e1pre, sink[m.enc1[0].weight], sink[m.enc1[0].bias])
+    ops.first_conv_wgrad(ops.im2col3(S.x, g_e1pre.dtype), g_e1pre, sink[m.enc1[0].weight],
+                         sink[m.enc1[0].bias])
     sink.ready(_params(m.enc1))
 
 

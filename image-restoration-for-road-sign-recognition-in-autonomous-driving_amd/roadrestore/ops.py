@@ -66,14 +66,18 @@ def _khalo_bc(mode, dt, n, h, w, c1, c2, cout, split, out_nchw):
     """Mirror of csrc/igemm.hip halo_bc: BC of the LDS-halo kernel, or 0."""
     if os.environ.get("RR_IGEMM_NOHALO", "0") not in ("", "0"):
         return 0
-    if dt != torch.bfloat16 or mode != RR_CONV3X3 or out_nchw or w not in (8, 16, 32, 64):
+    if dt != torch.bfloat16 or mode != RR_CONV3X3 or w not in (8, 16, 32, 64):
+        return 0
+    if out_nchw and (cout > 16 or c2):
         return 0
     R = 256 // w
     if h % 8 or (h % R if R <= h else (R % h or n % (R // h))):
         return 0
     if c1 % 64 or c2 % 64:
         return 0
-    max64 = int(os.environ.get("RR_HALO_BC64_MAXCIN", "0") or 0)
+    if out_nchw:
+        return 16
+    max64 = int(os.environ.get("RR_HALO_BC64_MAXCIN", "128") or 0)
     if cout % 128 == 0 and (split == 0 or split % 128 == 0) and c1 + c2 > max64:
         return 128
     return 64 if cout % 64 == 0 else 0
@@ -390,7 +394,9 @@ def im2col3(x_nchw, dtype, kpad=KPAD_IN):
     return col
 
 
-def pack_conv_in(wt, b, dtype, kpad=KPAD_IN):
+def pack_conv_in(wt, b, dtype, kpad=None):
+    if kpad is None:
+        kpad = conv_in_kpad(dtype, wt.shape[1], wt.shape[0])
     cout, cin = wt.shape[0], wt.shape[1]
     out = torch.empty(cout * kpad, dtype=dtype, device=wt.device)
     lib().check(lib().rr_pack_conv_in(rr_dtype(dtype), cout, cin, kpad, _p(wt.contiguous()), _p(b),
@@ -398,13 +404,44 @@ def pack_conv_in(wt, b, dtype, kpad=KPAD_IN):
     return out
 
 
-def first_conv_fwd(x_nchw, wt, b, dtype, wpack, act=0):
-    """First 3x3 conv (cin = 3) as im2col + K=64 implicit GEMM (bias in the
-    GEMM).  Returns (y NHWC, col) -- col is kept for the weight gradient."""
+KPAD_MFMA = 32    # K of the fused bf16 first conv (rr_conv_in_mfma): 27 taps + bias + pad
+
+
+def conv_in_kpad(dtype, cin=3, cout=64):
+    """K padding of the packed first-layer weights for ``first_conv_fwd``."""
+    return KPAD_MFMA if (dtype == torch.bfloat16 and cin == 3 and cout == 64) else KPAD_IN
+
+
+def first_conv_fwd(x_nchw, wt, b, dtype, wpack, act=0, alpha=None, want_pre=False):
+    """First 3x3 conv (cin = 3), bias folded into the GEMM (07:78, 14:124,
+    VGG16 features[0]).  act: 0 none, 1 ReLU, 2 PReLU(alpha).
+    Returns (y, pre): y the activated NHWC output, pre the pre-activation
+    (only when want_pre, else None).
+
+    bf16 (3 -> 64): one fused launch (rr_conv_in_mfma: im2col in registers,
+    K = 32 MFMA), pack with kpad 32.  fp32 (parity path): im2col + K = 64
+    implicit GEMM (+ the activation pass)."""
     n, cin, h, w = x_nchw.shape
+    cout = wt.shape[0]
+    x_nchw = x_nchw.contiguous()
+    if conv_in_kpad(dtype, cin, cout) == KPAD_MFMA:
+        y = torch.empty((n, h, w, cout), dtype=dtype, device=x_nchw.device)
+        pre = torch.empty_like(y) if (want_pre and act) else None
+        lib().check(lib().rr_conv_in_mfma(n, h, w, _p(x_nchw), _p(wpack), act, _p(alpha),
+                                          _p(pre), _p(y), stream()), "rr_conv_in_mfma")
+        return y, (pre if act else (y if want_pre else None))
     col = im2col3(x_nchw, dtype)
-    y, _, _ = igemm(RR_CONV1X1, col, None, n, h, w, wpack, wt.shape[0], act=act)
-    return y, col
+    if act == 2:
+        pre, _, _ = igemm(RR_CONV1X1, col, None, n, h, w, wpack, cout)
+        one = torch.ones(cout, dtype=torch.float32, device=x_nchw.device)
+        y = affine_act(pre, one, torch.zeros_like(one), alpha=alpha)
+        return y, (pre if want_pre else None)
+    if act == 1 and want_pre:
+        pre, _, _ = igemm(RR_CONV1X1, col, None, n, h, w, wpack, cout)
+        y = torch.clamp_min(pre, 0)
+        return y, pre
+    y, _, _ = igemm(RR_CONV1X1, col, None, n, h, w, wpack, cout, act=act)
+    return y, (y if (want_pre and not act) else None)
 
 
 def first_conv_wgrad(col, dy, dw, db):

@@ -236,6 +236,14 @@ int rr_conv_in_fwd(int dtype, int n, int h, int w, int cin, int cout,
  * rr_wgrad(RR_CONV1X1) on the same im2col matrix. */
 int rr_im2col3(int dtype, int n, int h, int w, int cin, int kpad, const float *x,
                void *col, rr_stream stream);
+/* fused bf16 first conv (cin 3 -> cout 64; 07:78 enc1.0, 14:122 enc1,
+ * VGG16 features[0] 14:189): im2col gathered in registers from the NCHW fp32
+ * image, K = 27 taps + bias column padded to 32, one MFMA per 16x16 tile.
+ * wpack32 = rr_pack_conv_in(RR_BF16, 64, 3, kpad = 32).  y_pre = conv + bias,
+ * y_act = act(y_pre) with act 0 none / 1 relu / 2 prelu(alpha); NHWC bf16
+ * [n][h][w][64], either may be NULL (y_act NULL requires act 0). */
+int rr_conv_in_mfma(int n, int h, int w, const float *x, const void *wpack32, int act,
+                    const float *alpha, void *y_pre, void *y_act, rr_stream stream);
 int rr_pack_conv_in(int dtype, int cout, int cin, int kpad, const float *wt,
                     const float *b, void *out, rr_stream stream);
 /* [cout][kpad] fp32 wgrad of that GEMM -> torch-layout dW [cout][cin][3][3], db */

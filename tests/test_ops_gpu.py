@@ -225,6 +225,58 @@ def test_igemm_bnbwd_fused(dev, dt, n, h, w, C):
         assert rel(got[k], ref[k]) < tol, k
 
 
+@pytest.mark.parametrize("acc", [False, True])
+@pytest.mark.parametrize("n,h,w", [(4, 8, 8), (2, 64, 64), (1, 16, 32), (1, 5, 7)])
+def test_image_grad(dev, n, h, w, acc):
+    """Image grad of the perceptual slice's conv1_1 (64 -> 3, 14:189): bf16
+    dgrad into fp32 NCHW -- the narrow 16-column halo tile where eligible,
+    the per-tap igemm otherwise -- with accumulate."""
+    import roadrestore as rr
+    ops = rr.ops
+    g = rnd(n, 64, h, w, seed=71).bfloat16().float()
+    wt = (rnd(64, 3, 3, 3, seed=72) * 0.1).bfloat16().float()
+    x = torch.zeros(n, 3, h, w, requires_grad=True)
+    F.conv2d(x, wt, None, padding=1).backward(g)
+    base = rnd(n, 3, h, w, seed=73)
+    _, wd = ops.pack_conv(wt.to(dev), torch.bfloat16)
+    out = base.clone().to(dev) if acc else None
+    y = ops.conv_in_dgrad(nhwc(g, dev, torch.bfloat16), wt.to(dev), 3, out=out, accumulate=acc,
+                          wpack_dgrad=wd)
+    ref = x.grad + (base if acc else 0)
+    assert ((y.cpu() - ref).norm() / ref.norm()).item() < 1e-5
+
+
+@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("n,h,w", [(2, 16, 16), (1, 5, 7), (3, 64, 64)])
+def test_first_conv_fused(dev, act, n, h, w):
+    """bf16 fused first conv (rr_conv_in_mfma) vs the im2col + K=64 igemm
+    path and vs fp32 torch on bf16-rounded inputs (07:78, 14:122, VGG f[0])."""
+    import roadrestore as rr
+    ops = rr.ops
+    x = torch.rand(n, 3, h, w, generator=torch.Generator().manual_seed(61))
+    wt = rnd(64, 3, 3, 3, seed=62) * 0.2
+    b = rnd(64, seed=63) * 0.1
+    alpha = torch.tensor([0.2])
+    xb, wb = x.bfloat16().float(), wt.bfloat16().float()
+    pre_ref = F.conv2d(xb, wb, b.bfloat16().float(), padding=1)
+    ref = {0: pre_ref, 1: F.relu(pre_ref), 2: F.prelu(pre_ref, alpha)}[act]
+    wp = ops.pack_conv_in(wt.to(dev), b.to(dev), torch.bfloat16)
+    assert wp.numel() == 64 * ops.KPAD_MFMA
+    y, pre = ops.first_conv_fwd(x.to(dev), wt.to(dev), b.to(dev), torch.bfloat16, wp, act=act,
+                                alpha=alpha.to(dev), want_pre=True)
+
+    def rel(a, r):
+        return ((nchw(a) - r).norm() / r.norm()).item()
+    assert rel(y, ref) < 4e-3
+    assert rel(pre, pre_ref) < 4e-3
+    # same math as the im2col + igemm (K = 64) path
+    col = ops.im2col3(x.to(dev), torch.bfloat16)
+    wp64 = ops.pack_conv_in(wt.to(dev), b.to(dev), torch.bfloat16, kpad=ops.KPAD_IN)
+    from roadrestore._lib import RR_CONV1X1
+    y64, _, _ = ops.igemm(RR_CONV1X1, col, None, n, h, w, wp64, 64)
+    assert ((pre.float() - y64.float()).norm() / y64.float().norm()).item() < 1e-3
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_convT(dev, dt):
     import roadrestore as rr
