@@ -22,12 +22,10 @@ struct bf16_t {
 __device__ __forceinline__ float bf16_to_f32(u16 b) {
   return __uint_as_float(((uint32_t)b) << 16);
 }
-// round-to-nearest-even (NaN-preserving enough for activations)
+// round-to-nearest-even: the language conversion, which gfx950 lowers to
+// v_cvt_pk_bf16_f32 (RNE, NaN stays NaN) -- no per-element branch
 __device__ __forceinline__ u16 f32_to_bf16(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u) return (u16)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (u16)(u >> 16);
+  return __builtin_bit_cast(u16, static_cast<__bf16>(f));
 }
 
 // Element traits: storage <-> fp32

@@ -292,40 +292,46 @@ __global__ __launch_bounds__(256) void conv_in_mfma_kernel(int n, int h, int w,
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
     fa[mi] = *reinterpret_cast<const bf16x8 *>(wp + (mi * 16 + fr) * 32 + q * 8);
-  // this lane's 8 k's: channel plane offset and tap shift
-  int koff[8], kdy[8], kdx[8], kkind[8];       // kind 0: image tap, 1: bias column, 2: zero
+  // this lane's 8 k's: (plane, dy, dx) of the tap; k == 27 is the bias column
+  const int hwi = h * w;
+  int kofs[8], kdy[8], kdx[8];
+  bool ktap[8], kone[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int k = q * 8 + j;
     const int ci = k / 9, t = k - (k / 9) * 9;
     kdy[j] = t / 3 - 1;
     kdx[j] = t % 3 - 1;
-    koff[j] = ci;
-    kkind[j] = k < 27 ? 0 : (k == 27 ? 1 : 2);
+    kofs[j] = ci * hwi + kdy[j] * w + kdx[j];
+    ktap[j] = k < 27;
+    kone[j] = k == 27;
   }
+  const int Pi = (int)P;
+  // raw buffer over the whole image batch (host: 12 P < 2^32 bytes)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(x), 0, (int)(3 * P * 4), 0x00020000);
+  const int pw0 = (int)p0;
   f32x4 acc[4][4];
 #pragma unroll
   for (int ni = 0; ni < 4; ++ni) {
-    const long long p = p0 + ni * 16 + fr;
-    const bool live = p < P;
-    const long long nn = live ? p / hw : 0;
-    const int rem = live ? (int)(p - nn * hw) : 0;
+    // branch-free gather: every lane loads (a clamped, in-bounds address when
+    // the tap is padding) and selects; 32-bit index math (host: 3P < 2^31)
+    const int p = pw0 + ni * 16 + fr;
+    const bool live = p < Pi;
+    const int pc = live ? p : 0;
+    const int nn = pc / hwi, rem = pc - (pc / hwi) * hwi;
     const int yy = rem / w, xx = rem - (rem / w) * w;
-    const float *xb = x + nn * 3 * hw;
-    u16 bits[8];
+    const int base = nn * 3 * hwi + rem;
+    bf16x8 fb;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float v = 0.f;
-      if (kkind[j] == 1) {
-        v = 1.f;
-      } else if (kkind[j] == 0) {
-        const int y2 = yy + kdy[j], x2 = xx + kdx[j];
-        if (live && y2 >= 0 && y2 < h && x2 >= 0 && x2 < w) v = xb[koff[j] * hw + y2 * w + x2];
-      }
-      bits[j] = f32_to_bf16(v);                 // RNE, as rr_im2col3's store
+      const int y2 = yy + kdy[j], x2 = xx + kdx[j];
+      const bool ok = ktap[j] && live && (unsigned)y2 < (unsigned)h && (unsigned)x2 < (unsigned)w;
+      // padding taps: offset past num_records -> the range check returns 0
+      const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+          xr, ok ? (base + kofs[j]) * 4 : 0xffffffff, 0, 0));
+      fb[j] = (__bf16)(v + (kone[j] ? 1.f : 0.f));    // v_cvt_pk_bf16_f32: RNE
     }
-    bf16x8 fb;
-    __builtin_memcpy(&fb, bits, 16);
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
       acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi], fb, f32x4{0.f, 0.f, 0.f, 0.f},
@@ -339,23 +345,26 @@ __global__ __launch_bounds__(256) void conv_in_mfma_kernel(int n, int h, int w,
     for (int ni = 0; ni < 4; ++ni)
       *reinterpret_cast<f32x4 *>(sw + (ni * 16 + fr) * SR + mi * 16 + q * 4) = acc[mi][ni];
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS writes landed
-  const float al = act == 2 ? alpha[0] : 0.f;
+  // negative-side slope: 1 (none), 0 (ReLU), alpha (PReLU)
+  const float slope = act == 2 ? alpha[0] : (act == 1 ? 0.f : 1.f);
+  const int rows = (int)min(64LL, P - p0);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int r = i * 8 + (lane >> 3), c8 = (lane & 7) * 8;
-    const long long p = p0 + r;
-    if (p >= P) continue;
-    const f32x4 v0 = *reinterpret_cast<const f32x4 *>(sw + r * SR + c8);
-    const f32x4 v1 = *reinterpret_cast<const f32x4 *>(sw + r * SR + c8 + 4);
-    if (y_pre) store8<bf16_t>(y_pre + p * 64 + c8, v0, v1);
-    if (y_act) {
-      f32x4 a0, a1;
+    if (r < rows) {
+      const long long p = p0 + r;
+      const f32x4 v0 = *reinterpret_cast<const f32x4 *>(sw + r * SR + c8);
+      const f32x4 v1 = *reinterpret_cast<const f32x4 *>(sw + r * SR + c8 + 4);
+      if (y_pre) store8<bf16_t>(y_pre + p * 64 + c8, v0, v1);
+      if (y_act) {
+        f32x4 a0, a1;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        a0[k] = v0[k] > 0.f ? v0[k] : (act == 2 ? al * v0[k] : (act == 1 ? 0.f : v0[k]));
-        a1[k] = v1[k] > 0.f ? v1[k] : (act == 2 ? al * v1[k] : (act == 1 ? 0.f : v1[k]));
+        for (int k = 0; k < 4; ++k) {
+          a0[k] = v0[k] > 0.f ? v0[k] : slope * v0[k];
+          a1[k] = v1[k] > 0.f ? v1[k] : slope * v1[k];
+        }
+        store8<bf16_t>(y_act + p * 64 + c8, a0, a1);
       }
-      store8<bf16_t>(y_act + p * 64 + c8, a0, a1);
     }
   }
 }
@@ -1285,8 +1294,8 @@ extern "C" int rr_conv_in_mfma(int n, int h, int w, const float *x, const void *
   if (!x || !wpack32 || (!y_pre && !y_act) || n <= 0 || h <= 0 || w <= 0) return RR_EINVAL;
   if (act < 0 || act > 2 || (act == 2 && !alpha) || (y_act == nullptr && act != 0)) return RR_EINVAL;
   const long long P = (long long)n * h * w;
+  if (12 * P >= 0x7fffffffLL) return RR_EUNSUPPORTED;         // 32-bit buffer byte offsets
   const long long blocks = (P + 255) / 256;
-  if (blocks > 0x7fffffffLL) return RR_EUNSUPPORTED;
   hipLaunchKernelGGL(conv_in_mfma_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                      n, h, w, x, (const bf16_t *)wpack32, act, alpha, (bf16_t *)y_pre,
                      (bf16_t *)y_act);
