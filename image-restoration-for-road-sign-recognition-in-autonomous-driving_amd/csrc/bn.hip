@@ -136,6 +136,139 @@ __device__ __forceinline__ f32x4 bwd_gm(const BnBwd &a, long long e, int c, f32x
   return g;
 }
 
+// ---- 8-channel forms (C % 8 == 0, C / 8 divides 256): a thread's channel
+// group is fixed for the whole grid-stride walk, so the per-channel
+// coefficients live in registers and every access is a 16-B vector.
+template <typename T, int MASK>
+__device__ __forceinline__ void bwd_gm8(const BnBwd &a, long long e, const float *s8,
+                                        const float *b8, float al, float *g, float &ag) {
+  f32x4 g0, g1;
+  load8<T>((const T *)a.g + e, g0, g1);
+  g[0] = g0[0]; g[1] = g0[1]; g[2] = g0[2]; g[3] = g0[3];
+  g[4] = g1[0]; g[5] = g1[1]; g[6] = g1[2]; g[7] = g1[3];
+  if constexpr (MASK == 1) {
+    f32x4 m0, m1;
+    load8<T>((const T *)a.aux + e, m0, m1);
+    const float m[8] = {m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] = m[k] > 0.f ? g[k] : 0.f;
+  } else if constexpr (MASK == 2) {
+    f32x4 t0, t1;
+    load8<T>((const T *)a.aux + e, t0, t1);
+    const float t[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float u = t[k] * s8[k] + b8[k];
+      ag += u > 0.f ? 0.f : g[k] * u;
+      g[k] = u > 0.f ? g[k] : al * g[k];
+    }
+  }
+}
+
+template <typename T, int MASK, int NBN>
+__global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwd a, float *__restrict__ part,
+                                                             float *__restrict__ apart,
+                                                             long long rows_per_block) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];   // [R][C][3] + [256]
+  const int TPR = a.C / 8;
+  const int R = 256 / TPR;
+  const int tr = threadIdx.x / TPR, tc = threadIdx.x % TPR;
+  const int c = tc * 8;
+  float m0[8], i0[8], m1[8], i1[8], s8[8], b8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    m0[k] = a.mean0[c + k]; i0[k] = a.inv0[c + k];
+    m1[k] = NBN == 2 ? a.mean1[c + k] : 0.f; i1[k] = NBN == 2 ? a.inv1[c + k] : 0.f;
+    s8[k] = MASK == 2 ? a.aff_s[c + k] : 0.f; b8[k] = MASK == 2 ? a.aff_b[c + k] : 0.f;
+  }
+  const float al = MASK == 2 ? a.alpha[0] : 0.f;
+  float s[3][8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s[0][k] = 0.f; s[1][k] = 0.f; s[2][k] = 0.f; }
+  float asum = 0.f;
+  const long long r0 = blockIdx.x * rows_per_block;
+  const long long r1 = min(a.P, r0 + rows_per_block);
+  for (long long r = r0 + tr; r < r1; r += R) {
+    const long long e = r * a.C + c;
+    float gm[8];
+    bwd_gm8<T, MASK>(a, e, s8, b8, al, gm, asum);
+    f32x4 u0, u1;
+    load8<T>((const T *)a.t0 + e, u0, u1);
+    const float t0[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s[0][k] += gm[k];
+      s[1][k] += gm[k] * ((t0[k] - m0[k]) * i0[k]);
+    }
+    if constexpr (NBN == 2) {
+      load8<T>((const T *)a.t1 + e, u0, u1);
+      const float t1[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[2][k] += gm[k] * ((t1[k] - m1[k]) * i1[k]);
+    }
+  }
+  float *red = sm;                       // [R][C][3]
+  float *ared = sm + (size_t)R * a.C * 3;
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) red[((size_t)tr * a.C + c + k) * 3 + j] = s[j][k];
+  ared[threadIdx.x] = asum;
+  __syncthreads();
+  for (int i = threadIdx.x; i < a.C * 3; i += blockDim.x) {
+    float v = 0.f;
+    for (int rr = 0; rr < R; ++rr) v += red[(size_t)rr * a.C * 3 + i];
+    part[(long long)blockIdx.x * a.C * 3 + i] = v;
+  }
+  if (apart && threadIdx.x == 0) {
+    float v = 0.f;
+    for (int i = 0; i < (int)blockDim.x; ++i) v += ared[i];
+    apart[blockIdx.x] = v;
+  }
+}
+
+template <typename T, int MASK, int NBN, bool GMO>
+__global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(BnBwd a, const float *__restrict__ coef,
+                                                            T *dt0, T *dt1, T *gmo) {
+  const int G = a.C / 8;
+  const int c = (threadIdx.x % G) * 8;   // fixed: G divides the grid stride
+  float cf[2][3][8], mu[2][8], iv[2][8], s8[8], b8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      cf[0][j][k] = coef[(c + k) * 6 + j];
+      cf[1][j][k] = NBN == 2 ? coef[(c + k) * 6 + 3 + j] : 0.f;
+    }
+    mu[0][k] = a.mean0[c + k]; iv[0][k] = a.inv0[c + k];
+    mu[1][k] = NBN == 2 ? a.mean1[c + k] : 0.f; iv[1][k] = NBN == 2 ? a.inv1[c + k] : 0.f;
+    s8[k] = MASK == 2 ? a.aff_s[c + k] : 0.f; b8[k] = MASK == 2 ? a.aff_b[c + k] : 0.f;
+  }
+  const float al = MASK == 2 ? a.alpha[0] : 0.f;
+  const long long rows = a.P;
+  const long long stride = ((long long)gridDim.x * blockDim.x) / G;
+  for (long long r = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / G; r < rows; r += stride) {
+    const long long e = r * a.C + c;
+    float gm[8], ag = 0.f;
+    bwd_gm8<T, MASK>(a, e, s8, b8, al, gm, ag);
+    if constexpr (GMO)
+      store8<T>(gmo + e, f32x4{gm[0], gm[1], gm[2], gm[3]}, f32x4{gm[4], gm[5], gm[6], gm[7]});
+#pragma unroll
+    for (int b = 0; b < NBN; ++b) {
+      f32x4 u0, u1;
+      load8<T>((const T *)(b == 0 ? a.t0 : a.t1) + e, u0, u1);
+      const float t[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float xh = (t[k] - mu[b][k]) * iv[b][k];
+        o[k] = cf[b][0][k] * (gm[k] - cf[b][1][k] - xh * cf[b][2][k]);
+      }
+      store8<T>((b == 0 ? dt0 : dt1) + e, f32x4{o[0], o[1], o[2], o[3]}, f32x4{o[4], o[5], o[6], o[7]});
+    }
+  }
+}
+
 // rows of [P][C] handled by one workgroup: TPR = C/4 threads per row
 template <typename T>
 __global__ void bn_bwd_reduce_kernel(BnBwd a, float *__restrict__ part, float *__restrict__ apart,
@@ -428,6 +561,22 @@ extern "C" int rr_bn_bwd_reduce(const rr_bnbwd_desc *d, const void *g, const voi
   const size_t shm = ((size_t)R * d->C * 3 + 256) * sizeof(float);
   float *apart = partial + (size_t)blocks * d->C * 3;
   hipStream_t st = (hipStream_t)stream;
+  if (d->C % 8 == 0 && 256 % (d->C / 8) == 0) {
+    const size_t shm8 = ((size_t)(256 / (d->C / 8)) * d->C * 3 + 256) * sizeof(float);
+    float *ap = d->mask_kind == 2 ? apart : nullptr;
+#define RR_RED8(TT, M, N) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<TT, M, N>), dim3(blocks), dim3(256), shm8, st, a, partial, ap, rpb)
+#define RR_RED8_T(TT)                                             \
+    switch (d->mask_kind * 2 + (d->nbn - 1)) {                    \
+      case 0: RR_RED8(TT, 0, 1); break; case 1: RR_RED8(TT, 0, 2); break; \
+      case 2: RR_RED8(TT, 1, 1); break; case 3: RR_RED8(TT, 1, 2); break; \
+      case 4: RR_RED8(TT, 2, 1); break; default: RR_RED8(TT, 2, 2); break; \
+    }
+    if (d->dtype == RR_BF16) { RR_RED8_T(bf16_t) } else { RR_RED8_T(float) }
+#undef RR_RED8_T
+#undef RR_RED8
+    RR_CHECK_LAUNCH();
+    return RR_OK;
+  }
   if (d->dtype == RR_BF16)
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st, a, partial,
                        d->mask_kind == 2 ? apart : nullptr, rpb);
@@ -466,8 +615,24 @@ extern "C" int rr_bn_bwd_apply(const rr_bnbwd_desc *d, const void *g, const void
   if (rc) return rc;
   if (!g || !t0 || !coef || !dt0 || (d->nbn == 2 && (!t1 || !dt1))) return RR_EINVAL;
   const BnBwd a = make_bnbwd(d, g, aux, aff_s, aff_b, alpha, t0, mean0, invstd0, t1, mean1, invstd1);
-  const int grid = rr_grid_cap((d->P * d->C / 4 + 255) / 256, 4096);
   hipStream_t st = (hipStream_t)stream;
+  if (d->C % 8 == 0 && 256 % (d->C / 8) == 0) {
+    const int grid8 = rr_grid_cap((d->P * d->C / 8 + 255) / 256, 4096);
+#define RR_APP8(TT, M, N, GM) hipLaunchKernelGGL((bn_bwd_apply8_kernel<TT, M, N, GM>), dim3(grid8), dim3(256), 0, st, a, coef, (TT *)dt0, (TT *)dt1, (TT *)gm_out)
+#define RR_APP8_M(TT, M)                                                        \
+    if (d->nbn == 1) { if (gm_out) RR_APP8(TT, M, 1, true); else RR_APP8(TT, M, 1, false); } \
+    else { if (gm_out) RR_APP8(TT, M, 2, true); else RR_APP8(TT, M, 2, false); }
+#define RR_APP8_T(TT)                                                           \
+    if (d->mask_kind == 0) { RR_APP8_M(TT, 0) } else if (d->mask_kind == 1) { RR_APP8_M(TT, 1) } \
+    else { RR_APP8_M(TT, 2) }
+    if (d->dtype == RR_BF16) { RR_APP8_T(bf16_t) } else { RR_APP8_T(float) }
+#undef RR_APP8_T
+#undef RR_APP8_M
+#undef RR_APP8
+    RR_CHECK_LAUNCH();
+    return RR_OK;
+  }
+  const int grid = rr_grid_cap((d->P * d->C / 4 + 255) / 256, 4096);
   if (d->dtype == RR_BF16)
     hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, dim3(grid), dim3(256), 0, st, a, coef,
                        (bf16_t *)dt0, (bf16_t *)dt1, (bf16_t *)gm_out);

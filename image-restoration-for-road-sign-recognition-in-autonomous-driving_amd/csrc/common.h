@@ -71,6 +71,20 @@ template <> __device__ __forceinline__ void store4<bf16_t>(bf16_t *p, f32x4 v) {
 }
 
 // 8 consecutive elements (one 16-B bf16 store / two 16-B fp32 stores)
+// 8 consecutive elements -> two f32x4 (one 16-B load for bf16)
+template <typename T> __device__ __forceinline__ void load8(const T *p, f32x4 &a, f32x4 &b);
+template <> __device__ __forceinline__ void load8<float>(const float *p, f32x4 &a, f32x4 &b) {
+  a = *reinterpret_cast<const f32x4 *>(p);
+  b = *reinterpret_cast<const f32x4 *>(p + 4);
+}
+template <> __device__ __forceinline__ void load8<bf16_t>(const bf16_t *p, f32x4 &a, f32x4 &b) {
+  const uint4 r = *reinterpret_cast<const uint4 *>(p);
+  a[0] = __uint_as_float(r.x << 16); a[1] = __uint_as_float(r.x & 0xffff0000u);
+  a[2] = __uint_as_float(r.y << 16); a[3] = __uint_as_float(r.y & 0xffff0000u);
+  b[0] = __uint_as_float(r.z << 16); b[1] = __uint_as_float(r.z & 0xffff0000u);
+  b[2] = __uint_as_float(r.w << 16); b[3] = __uint_as_float(r.w & 0xffff0000u);
+}
+
 template <typename T> __device__ __forceinline__ void store8(T *p, f32x4 a, f32x4 b);
 template <> __device__ __forceinline__ void store8<float>(float *p, f32x4 a, f32x4 b) {
   *reinterpret_cast<f32x4 *>(p) = a;

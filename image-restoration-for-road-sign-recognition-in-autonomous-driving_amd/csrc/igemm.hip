@@ -191,12 +191,21 @@ __device__ __forceinline__ void store_staged(const IgemmArgs &a, float *stg, int
     constexpr int TPC = NT / BC;            // threads per channel column
     float *red = stg + BP * SROW;            // [TPC][BC][2]
     const int c = tid % BC, sl = tid / BC;
-    float x = 0.f, y = 0.f;
-    for (int r = sl; r < nvalid; r += TPC) {
-      const float v = stg[r * SROW + c];
-      x += v;
-      y += v * v;
+    // four independent chains (LDS latency, not bandwidth, bounds this loop);
+    // fixed combine order -> deterministic
+    float x0 = 0.f, y0 = 0.f, x1 = 0.f, y1 = 0.f, x2 = 0.f, y2 = 0.f, x3 = 0.f, y3 = 0.f;
+    int r = sl;
+    for (; r + 3 * TPC < nvalid; r += 4 * TPC) {
+      const float v0 = stg[r * SROW + c], v1 = stg[(r + TPC) * SROW + c];
+      const float v2 = stg[(r + 2 * TPC) * SROW + c], v3 = stg[(r + 3 * TPC) * SROW + c];
+      x0 += v0; y0 += v0 * v0; x1 += v1; y1 += v1 * v1;
+      x2 += v2; y2 += v2 * v2; x3 += v3; y3 += v3 * v3;
     }
+    for (; r < nvalid; r += TPC) {
+      const float v = stg[r * SROW + c];
+      x0 += v; y0 += v * v;
+    }
+    const float x = (x0 + x1) + (x2 + x3), y = (y0 + y1) + (y2 + y3);
     red[(sl * BC + c) * 2 + 0] = x;
     red[(sl * BC + c) * 2 + 1] = y;
     __syncthreads();
@@ -824,12 +833,26 @@ __global__ __launch_bounds__(512, HaloCfg<BC>::OCC) void igemm3_halo_kernel(Igem
     stage(ch, std::integral_constant<int, 7>{}, I0{});
     stage(ch, std::integral_constant<int, 8>{}, I1{});
   };
-  int ch = 0;
-  for (; ch + 2 <= kch; ch += 2) {
-    chunk_even(ch);
-    chunk_odd(ch + 1);
+  // diagnostics (RR_IGEMM_DBG, timing only -- results are wrong): bit1 runs
+  // the K loop twice, bit0 skips the epilogue
+  const int reps = (a.dbg & 2) ? 2 : 1;
+  for (int rep = 0; rep < reps; ++rep) {
+    int ch = 0;
+    for (; ch + 2 <= kch; ch += 2) {
+      chunk_even(ch);
+      chunk_odd(ch + 1);
+    }
+    if (ch < kch) chunk_even(ch);
   }
-  if (ch < kch) chunk_even(ch);
+  if (a.dbg & 1) {
+    float t = 0.f;
+#pragma unroll
+    for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < MP; ++ni) t += acc[mi][ni][0];
+    if (t == 1234.5f) a.y1[tid] = 1;   // keep the accumulators live
+    return;
+  }
 
   // ---- epilogue: fp32 tile into LDS, then the shared staged store ----
   float *stg = reinterpret_cast<float *>(smem);
@@ -984,8 +1007,8 @@ static int fill_args(const rr_igemm_desc *d, const void *x1, const void *x2, con
   a.P = (int)P;
   a.cout_t = d->mode == RR_CONVT_UP ? d->c_out / 4 : d->c_out;
   a.out_nchw = d->out_nchw;
-  static const int dbg_env = [] { const char *e = getenv("RR_IGEMM_DBG"); return e ? atoi(e) : 0; }();
-  a.dbg = dbg_env;
+  const char *dbg_env = getenv("RR_IGEMM_DBG");
+  a.dbg = dbg_env ? atoi(dbg_env) : 0;
   a.ncblk = 1;
   a.bt = nullptr; a.bmean = a.binv = a.baff_s = a.baff_b = a.balpha = nullptr;
   a.bpart = a.bapart = nullptr;
