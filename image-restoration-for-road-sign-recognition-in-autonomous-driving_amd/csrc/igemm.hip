@@ -602,33 +602,34 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs a) {
 // Pipeline: one barrier per (chunk, tap) stage; weights prefetched 2 stages
 // ahead in registers, the next chunk's halo loaded at tap 0 and written at
 // tap 8.
-template <int W> struct HaloGeom {
-  static constexpr int R = 256 / W;
+template <int W, int BP> struct HaloGeom {
+  static constexpr int R = BP / W;
   // worst case over H >= 8 with H | R or R | H: R/Hs images of (Hs+2) rows
   static constexpr int HMAX = (R <= 8 ? (R + 2) : (R / 8) * 10) * (W + 2);
   static constexpr int PLANE = ((HMAX * 16 + 255) / 256) * 256;
   static constexpr int HBYTES = 8 * PLANE;
-  static constexpr int LH = (HMAX * 8 + 511) / 512;           // pieces per thread
+  static constexpr int LH = (HMAX * 8 + 2 * BP - 1) / (2 * BP);   // pieces per thread (NT = 2 BP)
 };
 
 // BC = 64 keeps ONE halo buffer (the next chunk's halo is written after an
 // extra barrier at tap 8), so LDS <= 78 KB and VGPRs <= 128: 2 workgroups
 // per CU, one tile's prologue / epilogue overlapping the other's MFMA loop.
 // BC = 128 double-buffers the halo, 1 workgroup per CU.
-template <int BC> struct HaloCfg {
+// BP = 128 (256 threads, ~51 KB LDS at BC = 64): 3 workgroups per CU.
+template <int BC, int BP> struct HaloCfg {
   static constexpr int HB = BC <= 64 ? 1 : 2;
-  static constexpr int OCC = BC <= 64 ? 4 : 2;   // min waves per SIMD (launch bound)
+  static constexpr int OCC = BP == 128 ? (BC <= 64 ? 3 : 2) : (BC <= 64 ? 4 : 2);   // min waves / SIMD
 };
 
-template <int BC, int W, int MODE>
-__global__ __launch_bounds__(512, HaloCfg<BC>::OCC) void igemm3_halo_kernel(IgemmArgs a) {
+template <int BC, int W, int MODE, int BP>
+__global__ __launch_bounds__(2 * BP, (HaloCfg<BC, BP>::OCC)) void igemm3_halo_kernel(IgemmArgs a) {
   using T = bf16_t;
-  using G = HaloGeom<W>;
-  constexpr int HB = HaloCfg<BC>::HB;
-  constexpr int BP = 256, NT = 512;
+  using G = HaloGeom<W, BP>;
+  constexpr int HB = HaloCfg<BC, BP>::HB;
+  constexpr int NT = 2 * BP, NWAVE = NT / 64;
   // wave grid: WC (channel) x WP (pixel) waves; a wave owns WCH channels
   // (64, or all 16 for the narrow NCHW image-grad tile)
-  constexpr int WC = BC >= 64 ? BC / 64 : 1, WP = 8 / WC, WCH = BC / WC;
+  constexpr int WC = BC >= 64 ? BC / 64 : 1, WP = NWAVE / WC, WCH = BC / WC;
   constexpr int MC = WCH / 16, MP = BP / WP / 16;
   constexpr int WPLANE = BC * 16;                               // weight planes: BC rows
   constexpr int WBYTES = 8 * WPLANE;
@@ -636,7 +637,7 @@ __global__ __launch_bounds__(512, HaloCfg<BC>::OCC) void igemm3_halo_kernel(Igem
   constexpr int LW = (WPIECES + NT - 1) / NT;                   // weight pieces per thread
   constexpr int MAIN = HB * G::HBYTES + 2 * WBYTES;
   constexpr int SROW = BC + 4;
-  constexpr int STG = BP * SROW * 4 + 2 * 512 * 4 * 2 + 256;
+  constexpr int STG = BP * SROW * 4 + 2 * NT * 4 * 2 + 256;
   constexpr int SMEM = MAIN > STG ? MAIN : STG;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   char *const hbuf = smem;                                      // [HB][HBYTES]
@@ -916,6 +917,16 @@ Tile pick_tile(const rr_igemm_desc *d) {
   return {64, 128};
 }
 
+// halo tile height: 256 pixels, or 128 (RR_HALO_BP=128) -- per call
+int halo_bp(const rr_igemm_desc *d) {
+  const char *e = getenv("RR_HALO_BP");
+  const int bp = e ? atoi(e) : 256;
+  if (bp != 128) return 256;
+  const int R = 128 / d->w;
+  if (R <= d->h ? (d->h % R) : (R % d->h || d->n % (R / d->h))) return 256;
+  return 128;
+}
+
 // halo path eligibility (bf16 3x3, whole-row 256-pixel tiles); returns BC or 0
 int halo_bc(const rr_igemm_desc *d) {
   const char *e = getenv("RR_IGEMM_NOHALO");   // A/B switch (per call)
@@ -939,17 +950,17 @@ int halo_bc(const rr_igemm_desc *d) {
   return 0;
 }
 
-template <int BC>
+template <int BC, int BP>
 int launch_halo(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   a.ncblk = (a.cout + BC - 1) / BC;
-  const long long nblk = (long long)(a.P / 256) * a.ncblk;
+  const long long nblk = (long long)(a.P / BP) * a.ncblk;
   if (nblk > 0x7fffffffLL) return RR_EUNSUPPORTED;
-  const dim3 grid((unsigned)nblk), block(512);
+  const dim3 grid((unsigned)nblk), block(2 * BP);
   switch (d->w) {
-    case 64: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 64, RR_CONV3X3>), grid, block, 0, st, a); break;
-    case 32: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 32, RR_CONV3X3>), grid, block, 0, st, a); break;
-    case 16: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 16, RR_CONV3X3>), grid, block, 0, st, a); break;
-    default: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 8, RR_CONV3X3>), grid, block, 0, st, a); break;
+    case 64: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 64, RR_CONV3X3, BP>), grid, block, 0, st, a); break;
+    case 32: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 32, RR_CONV3X3, BP>), grid, block, 0, st, a); break;
+    case 16: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 16, RR_CONV3X3, BP>), grid, block, 0, st, a); break;
+    default: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 8, RR_CONV3X3, BP>), grid, block, 0, st, a); break;
   }
   RR_CHECK_LAUNCH();
   return RR_OK;
@@ -959,9 +970,15 @@ template <typename T>
 int dispatch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
     const int hb = halo_bc(d);
-    if (hb == 128) return launch_halo<128>(d, a, st);
-    if (hb == 64) return launch_halo<64>(d, a, st);
-    if (hb == 16) return launch_halo<16>(d, a, st);
+    const int bp = (hb && hb <= 64) ? halo_bp(d) : 256;
+    if (bp == 128) {
+      if (hb == 64) return launch_halo<64, 128>(d, a, st);
+      if (hb == 16) return launch_halo<16, 128>(d, a, st);
+    } else {
+      if (hb == 128) return launch_halo<128, 256>(d, a, st);
+      if (hb == 64) return launch_halo<64, 256>(d, a, st);
+      if (hb == 16) return launch_halo<16, 256>(d, a, st);
+    }
   }
   const Tile t = pick_tile(d);
   if (t.bc == 128) return launch_mode<T, 128, 128, 2>(d, a, st);
@@ -974,7 +991,8 @@ int dispatch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
 extern "C" int rr_igemm_stat_blocks(const rr_igemm_desc *d) {
   if (!d) return RR_EINVAL;
   const long long P = (long long)d->n * d->h * d->w;
-  const int bp = halo_bc(d) ? 256 : pick_tile(d).bp;
+  const int hb = halo_bc(d);
+  const int bp = hb ? (hb <= 64 ? halo_bp(d) : 256) : pick_tile(d).bp;
   return (int)((P + bp - 1) / bp);
 }
 
