@@ -53,6 +53,10 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="capture the step in a HIP graph and replay it (1/0; default: on at N=1)")
+    ap.add_argument("--probe-steps", type=int, default=3,
+                    help="eager steps timed per kernel for the roofline in graph mode")
     return ap.parse_args()
 
 
@@ -147,7 +151,8 @@ def main():
     flatten_parameters(model)
     dp = DataParallel(model) if world > 1 else None
     gscale = dp.grad_scale if dp else 1.0
-    opt = rr.AdamW(model.parameters(), lr=2e-4, weight_decay=1e-4)
+    use_graph = a.graph == 1 or (a.graph == -1 and world == 1)
+    opt = rr.AdamW(model.parameters(), lr=2e-4, weight_decay=1e-4, capturable=use_graph)
 
     # synthetic GTSRB-shaped batch: clean ~ U{0..255}/255, bad = fog + noise
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
@@ -167,19 +172,51 @@ def main():
 
     for _ in range(a.warmup):
         step()
-    probe = None if a.no_probe else KernelProbe()
+    graph = None
+    if use_graph:
+        # one whole training step (fwd, L1 + perceptual, bwd, AdamW with the
+        # device-side step count, weight re-packs) as a HIP graph; the
+        # allocator is warmed on the capture side stream first (torch recipe)
+        # (the warmup on the side stream keeps older AccumulateGrad nodes on
+        # the default stream; the mismatch is intentional and harmless here)
+        setw = getattr(torch.autograd.graph, "set_warn_on_accumulate_grad_stream_mismatch", None)
+        if setw is not None:
+            setw(False)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                step()
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            loss_g = step()
+        torch.cuda.synchronize()
+    probe = None if (a.no_probe or graph is not None) else KernelProbe()
     ops.PROBE = probe
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        loss = step()
+        if graph is not None:
+            graph.replay()
+        else:
+            loss = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
     ops.PROBE = None
+    if graph is not None:
+        loss = loss_g
+        if not a.no_probe:
+            # kernel durations for the roofline: the same kernels, timed eagerly
+            probe = KernelProbe()
+            ops.PROBE = probe
+            for _ in range(a.probe_steps):
+                step()
+            ops.PROBE = None
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -201,8 +238,11 @@ def main():
                 "flop_per_launch": fl / cnt}
         tot_fl = sum(v[1] for v in agg.values())
         tot_ms = sum(v[2] for v in agg.values())
-        kernels = {"conv_gemm_ms_per_step": round(tot_ms / a.steps, 3),
-                   "conv_gemm_tflops": round(tot_fl / (tot_ms * 1e-3) / 1e12, 2)}
+        nprobe = a.probe_steps if graph is not None else a.steps
+        kernels = {"conv_gemm_ms_per_step": round(tot_ms / nprobe, 3),
+                   "conv_gemm_tflops": round(tot_fl / (tot_ms * 1e-3) / 1e12, 2),
+                   "probe": "eager steps after the graph timing" if graph is not None
+                            else "the timed steps"}
 
     imgs = world * B * a.steps
     value = imgs / el
@@ -217,6 +257,7 @@ def main():
                                "perceptual + bwd + AdamW), 14_train_unified_advanced.py",
                    "model": "ResUNet", "global_batch": world * B, "per_gpu_batch": B,
                    "image": [H, H, 3], "parallelism": f"dp{world}",
+                   "hip_graph": graph is not None,
                    "flop_per_image": FLOP_STEP_WITH_PERC if w_perc else FLOP_RESUNET_FWDBWD},
         "achieved_model_tflops": round(value * (FLOP_STEP_WITH_PERC if w_perc else
                                                 FLOP_RESUNET_FWDBWD) / 1e12, 2),

@@ -788,6 +788,39 @@ __global__ void adamw_kernel(long long count, float *__restrict__ p, const float
   }
 }
 
+// capturable form (HIP graphs): the step count lives on the device, bumped
+// by its own launch, and the bias corrections are computed per block in
+// double from the same float betas the host path uses
+__global__ void adamw_step_inc_kernel(int64_t *step) { *step += 1; }
+
+__global__ void adamw_dev_kernel(long long count, float *__restrict__ p, const float *__restrict__ g,
+                                 float *__restrict__ m, float *__restrict__ v, float lr, float b1,
+                                 float b2, float eps, float wd, int decoupled,
+                                 const int64_t *__restrict__ step_dev) {
+  __shared__ float bc[2];
+  if (threadIdx.x == 0) {
+    const double st = (double)*step_dev;
+    bc[0] = (float)(1.0 - pow((double)b1, st));
+    bc[1] = (float)sqrt(1.0 - pow((double)b2, st));
+  }
+  __syncthreads();
+  const float bc1 = bc[0], sbc2 = bc[1];
+  const float step = lr / bc1;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < count;
+       i += (long long)gridDim.x * blockDim.x) {
+    float pv = p[i];
+    float gv = g[i];
+    if (decoupled) pv *= (1.f - lr * wd);
+    else if (wd != 0.f) gv += wd * pv;
+    float mv = m[i];
+    mv = mv + (1.f - b1) * (gv - mv);
+    float vv = v[i] * b2 + (1.f - b2) * gv * gv;
+    const float denom = sqrtf(vv) / sbc2 + eps;
+    pv = pv - step * (mv / denom);
+    p[i] = pv; m[i] = mv; v[i] = vv;
+  }
+}
+
 __global__ void to_u8_kernel(int n, int c, int h, int w, const float *__restrict__ x,
                              uint8_t *__restrict__ out, int bgr) {
   const long long total = (long long)n * h * w * c;
@@ -1235,6 +1268,20 @@ extern "C" int rr_adamw(long long count, float *param, const float *grad, float 
   dim3 g(rr_grid_cap((count + 255) / 256, 8192)), b(256);
   hipLaunchKernelGGL(adamw_kernel, g, b, 0, (hipStream_t)stream, count, param, grad, m, v, lr,
                      beta1, beta2, eps, weight_decay, decoupled, (float)bc1, (float)sqrt(bc2));
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_adamw_dev(long long count, float *param, const float *grad, float *m, float *v,
+                            float lr, float beta1, float beta2, float eps, float weight_decay,
+                            int decoupled, int64_t *step_dev, rr_stream stream) {
+  if (count <= 0 || !param || !grad || !m || !v || !step_dev) return RR_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(adamw_step_inc_kernel, dim3(1), dim3(1), 0, st, step_dev);
+  RR_CHECK_LAUNCH();
+  dim3 g(rr_grid_cap((count + 255) / 256, 8192)), b(256);
+  hipLaunchKernelGGL(adamw_dev_kernel, g, b, 0, st, count, param, grad, m, v, lr, beta1, beta2, eps,
+                     weight_decay, decoupled, step_dev);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

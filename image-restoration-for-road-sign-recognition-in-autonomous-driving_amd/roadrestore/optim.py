@@ -68,10 +68,14 @@ def _span(tensors):
 class _FusedAdamBase(torch.optim.Optimizer):
     decoupled = True
 
-    def __init__(self, params, lr, betas, eps, weight_decay):
+    def __init__(self, params, lr, betas, eps, weight_decay, capturable=False):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
         self._gstate = {}
+        # capturable: the step count lives on the device (rr_adamw_dev) so a
+        # HIP-graph replay of optimizer.step() advances the bias correction;
+        # the learning rate is then fixed at capture time
+        self.capturable = capturable
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -108,12 +112,25 @@ class _FusedAdamBase(torch.optim.Optimizer):
                         st["exp_avg_sq"] = gstate["v"][off:off + p.numel()].view(p.shape)
                         off += p.numel()
                 total = gstate["m"].numel()
-                lib().check(lib().rr_adamw(total, pspan[0][0], gspan[0][0], gstate["m"].data_ptr(),
-                                           gstate["v"].data_ptr(), float(group["lr"]), float(b1),
-                                           float(b2), float(group["eps"]),
-                                           float(group["weight_decay"]), int(self.decoupled), step,
-                                           ops.stream()), "rr_adamw")
+                if self.capturable:
+                    if "step_dev" not in gstate:
+                        gstate["step_dev"] = torch.full((1,), step - 1, dtype=torch.int64,
+                                                        device=ps[0].device)
+                    lib().check(lib().rr_adamw_dev(
+                        total, pspan[0][0], gspan[0][0], gstate["m"].data_ptr(),
+                        gstate["v"].data_ptr(), float(group["lr"]), float(b1), float(b2),
+                        float(group["eps"]), float(group["weight_decay"]), int(self.decoupled),
+                        gstate["step_dev"].data_ptr(), ops.stream()), "rr_adamw_dev")
+                else:
+                    lib().check(lib().rr_adamw(total, pspan[0][0], gspan[0][0],
+                                               gstate["m"].data_ptr(), gstate["v"].data_ptr(),
+                                               float(group["lr"]), float(b1), float(b2),
+                                               float(group["eps"]), float(group["weight_decay"]),
+                                               int(self.decoupled), step, ops.stream()), "rr_adamw")
             else:
+                if self.capturable:
+                    raise RuntimeError("capturable Adam/AdamW needs flattened parameters "
+                                       "(roadrestore.optim.flatten_parameters)")
                 for p in ps:
                     st = self.state.setdefault(p, {})
                     if "exp_avg" not in st:
@@ -136,8 +153,9 @@ class AdamW(_FusedAdamBase):
 
     decoupled = True
 
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
-        super().__init__(params, lr, betas, eps, weight_decay)
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2,
+                 capturable=False):
+        super().__init__(params, lr, betas, eps, weight_decay, capturable)
 
 
 class Adam(_FusedAdamBase):
@@ -145,5 +163,6 @@ class Adam(_FusedAdamBase):
 
     decoupled = False
 
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
-        super().__init__(params, lr, betas, eps, weight_decay)
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                 capturable=False):
+        super().__init__(params, lr, betas, eps, weight_decay, capturable)

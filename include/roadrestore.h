@@ -302,6 +302,11 @@ int rr_loss_bwd(int kind, int dtype, long long count, const void *a,
 int rr_adamw(long long count, float *param, const float *grad, float *m,
              float *v, float lr, float beta1, float beta2, float eps,
              float weight_decay, int decoupled, int step, rr_stream stream);
+/* capturable AdamW/Adam (HIP graphs): *step_dev is incremented on the stream
+ * first, then the update reads it; bias corrections as above, on device. */
+int rr_adamw_dev(long long count, float *param, const float *grad, float *m, float *v,
+                 float lr, float beta1, float beta2, float eps, float weight_decay,
+                 int decoupled, int64_t *step_dev, rr_stream stream);
 
 /* inference post-processing (17:84-92): clamp(0,1)*255 -> uint8 HWC */
 int rr_to_uint8_hwc(int n, int c, int h, int w, const float *x, uint8_t *out,

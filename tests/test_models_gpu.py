@@ -293,3 +293,55 @@ def test_multi_step_training_matches_oracle(dev):
         out = m(bad.to(dev)).cpu()
         ref = R.simple_unet_forward(p, bad)
     assert (out - ref).abs().mean().item() <= 1e-3
+
+
+def test_hip_graph_training_step_matches_eager(dev):
+    """A whole ResUNet unified training step (fwd, L1 + perceptual, bwd,
+    capturable AdamW, weight re-packs) captured in a HIP graph and replayed
+    must do exactly what the eager steps do (same kernels, device-side step
+    count for the bias correction)."""
+    import roadrestore as rr
+    from roadrestore.optim import flatten_parameters
+    torch.manual_seed(3)
+    B, H = 4, 32
+    g = torch.Generator(device=dev).manual_seed(5)
+    clean = torch.rand((B, 3, H, H), generator=g, device=dev)
+    bad = (clean * 0.5 + 0.4).clamp(0, 1)
+
+    def make(capturable):
+        torch.manual_seed(7)
+        m = rr.ResUNet().to(dev)
+        m.compute_dtype = torch.bfloat16
+        m.train()
+        perc = rr.VGGPerceptualLoss().to(dev)
+        perc.compute_dtype = torch.bfloat16
+        flatten_parameters(m)
+        opt = rr.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-4, capturable=capturable)
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            loss = rr.unified_loss(m(bad), clean, perc, 0.1)
+            loss.backward()
+            opt.step()
+            return loss
+        return m, step
+
+    ma, step_a = make(False)
+    for _ in range(4):
+        la = step_a()
+    mb, step_b = make(True)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step_b()                                   # 1 eager step
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        lb = step_b()                              # recorded, not executed
+    for _ in range(3):
+        graph.replay()                             # steps 2..4
+    torch.cuda.synchronize()
+    assert abs(la.item() - lb.item()) <= 1e-6 * abs(la.item()), (la.item(), lb.item())
+    for (na, pa), (nb, pb) in zip(ma.named_parameters(), mb.named_parameters()):
+        d = (pa - pb).abs().max().item()
+        assert d <= 1e-6 * max(1.0, pa.abs().max().item()), (na, d)
