@@ -86,6 +86,28 @@ class KernelProbe:
         return agg
 
 
+PMC_TRAFFIC = os.path.join(REPO, "profiles", "r1_pmc_traffic.json")
+
+
+def _norm_sym(sym):
+    return (sym.replace(" ", "").replace("::", "").replace("bf16_t", "bf16").replace("mode", "")
+            .rstrip(">"))
+
+
+def pmc_traffic(sym):
+    """HBM bytes per launch of ``sym`` from the committed rocprofv3 PMC
+    summary (FETCH_SIZE x2 + WRITE_SIZE, separate passes; tools/pmc_traffic.py)."""
+    try:
+        tab = json.load(open(PMC_TRAFFIC))
+    except (OSError, ValueError):
+        return None
+    key = _norm_sym(sym)
+    for k, v in tab.items():
+        if _norm_sym(k).startswith(key):
+            return v["hbm_bytes_per_launch"]
+    return None
+
+
 def cpu_baseline(seconds, size):
     """The CPU restatement of the same unified step (oracle, fp32), timed on
     the host: a bounded sample of the workload (batch 8)."""
@@ -232,8 +254,12 @@ def main():
         sym, (cnt, fl, ms) = max(agg.items(), key=lambda kv: kv[1][2])
         ach = fl / (ms * 1e-3) / 1e12
         pk = PEAK["bf16" if dt == torch.bfloat16 else "f32"]
+        traffic = pmc_traffic(sym)
         roof = {"bound": "mfma", "kernel": sym, "achieved": round(ach, 2), "peak": pk,
-                "unit": "TFLOP/s", "frac": round(ach / pk, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(ach / pk, 4), "traffic": traffic,
+                "traffic_note": "HBM bytes per launch, rocprofv3 FETCH_SIZE x2 (gfx950) + "
+                                "WRITE_SIZE in separate --pmc passes of this bench "
+                                "(profiles/r1_pmc_traffic.json)" if traffic else None,
                 "launches": cnt, "avg_launch_ms": round(ms / cnt, 4),
                 "flop_per_launch": fl / cnt}
         tot_fl = sum(v[1] for v in agg.values())
