@@ -66,18 +66,18 @@ class KernelProbe:
     def __init__(self):
         self.rec = []
 
-    def __call__(self, sym, flops, launch):
+    def __call__(self, sym, flops, launch, tag=None):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
         launch()
         e.record()
-        self.rec.append((sym, flops, s, e))
+        self.rec.append((sym, flops, s, e, tag))
 
     def summary(self):
         torch.cuda.synchronize()
         agg = {}
-        for sym, fl, s, e in self.rec:
+        for sym, fl, s, e, _ in self.rec:
             ms = s.elapsed_time(e)
             a = agg.setdefault(sym, [0, 0.0, 0.0])
             a[0] += 1

@@ -1,0 +1,27 @@
+// stream3.h -- internal interface of the row-streaming 3x3 conv (stream3.hip),
+// called from rr_igemm / rr_igemm_bnbwd (igemm.hip).  Not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/roadrestore.h"
+
+struct S3Args {
+  const char *x;             // NHWC bf16 input [n][h][w][64]
+  const char *wt;            // packed bf16 weights [64][9][64] (fwd or dgrad pack)
+  const float *bias;         // [64] or null
+  char *y;                   // NHWC bf16 output [n][h][w][64]
+  const char *mask;          // relu-backward mask (NHWC bf16) or null
+  float *stats;              // [nwg][64][2] pre-bias partial sums or null
+  int n, h;                  // w is the template width
+  int act, accumulate;
+  // BN -> PReLU backward epilogue (rr_igemm_bnbwd), bt != null selects it
+  const char *bt;
+  const float *bmean, *binv, *baff_s, *baff_b, *balpha;
+  float *bpart, *bapart;     // [nwg][64][3], [nwg]
+};
+
+// 0 when the descriptor is not handled by the streaming kernel, else the
+// number of workgroups (= rows of the stats / bnbwd partial slabs)
+int stream3_blocks(const rr_igemm_desc *d);
+// launch; returns an RR_* status
+int stream3_launch(const rr_igemm_desc *d, const S3Args &a, hipStream_t st);

@@ -48,7 +48,7 @@ def _need_cuda(*ts):
             raise RuntimeError("roadrestore ops need device tensors (no CPU fallback)")
 
 
-# Optional launch probe (bench.py): probe(kernel_symbol, algorithmic_flops, launch_fn)
+# Optional launch probe (bench.py): probe(kernel_symbol, algorithmic_flops, launch_fn, shape_tag)
 PROBE = None
 
 
@@ -81,6 +81,18 @@ def _khalo_bc(mode, dt, n, h, w, c1, c2, cout, split, out_nchw):
     if cout % 128 == 0 and (split == 0 or split % 128 == 0) and c1 + c2 > max64:
         return 128
     return 64 if cout % 64 == 0 else 0
+
+
+def _kstream3(mode, dt, n, h, w, c1, c2, cout, split, out_nchw):
+    """Mirror of csrc/stream3.hip stream3_blocks: the row-streaming kernel?"""
+    if os.environ.get("RR_STREAM3", "1") in ("0",):
+        return False
+    if dt != torch.bfloat16 or mode != RR_CONV3X3 or w not in (32, 64):
+        return False
+    if c1 != 64 or c2 or cout != 64 or split or out_nchw:
+        return False
+    rps = 128 // w
+    return h % rps == 0 and n * h // rps >= 256
 
 
 def _ws(nbytes, device):
@@ -159,12 +171,15 @@ def igemm(mode, x1, x2, n, h, w, wpack, cout, bias=None, act=0, out=None, out2=N
     else:
         taps = 9 if mode == RR_CONV3X3 else (4 if mode == RR_CONVT_DOWN else 1)
         hb = _khalo_bc(mode, dt, n, h, w, c1, c2, cout, split, out_nchw)
-        if hb:
+        if _kstream3(mode, dt, n, h, w, c1, c2, cout, split, out_nchw):
+            sym = f"stream3_kernel<{w}>"
+        elif hb:
             sym = f"igemm3_halo_kernel<{hb},{w}>"
         else:
             bc, bp, wc = _kpick_tile(mode, n, h, w, cout, split)
             sym = f"igemm_kernel<{'bf16' if dt == torch.bfloat16 else 'f32'},{bc},{bp},{wc},mode{mode}>"
-        PROBE(sym, 2.0 * n * h * w * cout * taps * (c1 + c2), launch)
+        PROBE(sym, 2.0 * n * h * w * cout * taps * (c1 + c2), launch,
+              f"fwd m{mode} {n}x{h}x{w} c{c1}+{c2}->{cout}")
     return out, out2, st
 
 
@@ -192,7 +207,8 @@ def wgrad(mode, dy, x1, x2, n, h, w, cout, dw=None, accumulate=False, dw_shape=N
         ba = 128 if CA % 128 == 0 else 64
         bb = 128 if (CB % 128 == 0 and (cout if convT else c1) % 128 == 0 and c2 % 128 == 0) else 64
         sym = f"wgrad_kernel<{'bf16' if dy.dtype == torch.bfloat16 else 'f32'},{ba},{bb},mode{mode}>"
-        PROBE(sym, 2.0 * CA * CB * taps * n * h * w, launch)
+        PROBE(sym, 2.0 * CA * CB * taps * n * h * w, launch,
+              f"wgrad m{mode} {n}x{h}x{w} c{c1}+{c2}->{cout}")
     return dw
 
 
@@ -310,12 +326,15 @@ def igemm_bnbwd(mode, dy, n, h, w, wpack, cout, t, mean, inv, aff_s, aff_b, alph
     else:
         taps = 9 if mode == RR_CONV3X3 else 1
         hb = _khalo_bc(mode, dt, n, h, w, dy.shape[-1], 0, cout, 0, False)
-        if hb:
+        if _kstream3(mode, dt, n, h, w, dy.shape[-1], 0, cout, 0, False):
+            sym = f"stream3_kernel<{w}>"
+        elif hb:
             sym = f"igemm3_halo_kernel<{hb},{w}>"
         else:
             bc, bp, wc = _kpick_tile(mode, n, h, w, cout, 0)
             sym = f"igemm_kernel<{'bf16' if dt == torch.bfloat16 else 'f32'},{bc},{bp},{wc},mode{mode}>"
-        PROBE(sym, 2.0 * n * h * w * cout * taps * dy.shape[-1], launch)
+        PROBE(sym, 2.0 * n * h * w * cout * taps * dy.shape[-1], launch,
+              f"bnbwd m{mode} {n}x{h}x{w} c{dy.shape[-1]}->{cout}")
     return out, part, rows, rows * (cout // 64)
 
 

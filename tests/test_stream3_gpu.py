@@ -1,0 +1,151 @@
+"""Row-streaming 3x3 conv (csrc/stream3.hip): the 64 -> 64 channel bf16 conv
+at W = 64 / 32 (ResUNet res1 / dec1 / dec2, VGG16 conv1_2) vs fp32 torch and
+vs the tiled halo kernel (RR_STREAM3=0).  Shapes put workgroup row ranges
+across image boundaries (uneven splits, short images) so the ring's
+pre-load steps and zero-padding rows are exercised.  Inputs are bf16-exact,
+so against fp32 torch the only error is the bf16 rounding of the output."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+BF = torch.bfloat16
+
+
+def rnd(*shape, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g)
+
+
+def nhwc(x, dev):
+    return x.permute(0, 2, 3, 1).contiguous().to(dev, BF)
+
+
+def nchw(y):
+    return y.float().permute(0, 3, 1, 2).contiguous().cpu()
+
+
+def rel(a, r):
+    a, r = a.float().cpu(), r.float().cpu()
+    return ((a - r).norm() / r.norm().clamp_min(1e-30)).item()
+
+
+# (n, h, w): nsteps = n*h/(128/w) >= 256 workgroups
+SHAPES = [(8, 64, 64), (9, 64, 64), (33, 16, 64), (32, 32, 32), (41, 32, 32), (130, 8, 32)]
+
+
+def _blocks(n, h, w):
+    import ctypes as C
+    import roadrestore as rr
+    from roadrestore._lib import IgemmDesc, RR_BF16, RR_CONV3X3
+    d = IgemmDesc(RR_BF16, RR_CONV3X3, n, h, w, 64, 0, 64, 0, 0, 0, 1, 0, 1, 0)
+    return rr.lib().rr_igemm_stat_blocks(C.byref(d))
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_stream3_selected(dev, shape, monkeypatch):
+    """the streaming kernel owns these shapes (256 partial rows), and the
+    RR_STREAM3=0 switch hands them back to the tiled kernel"""
+    n, h, w = shape
+    assert _blocks(n, h, w) == 256
+    monkeypatch.setenv("RR_STREAM3", "0")
+    assert _blocks(n, h, w) == (n * h * w) // 256
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_stream3_fwd_stats(dev, shape, monkeypatch):
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    n, h, w = shape
+    x = rnd(n, 64, h, w, seed=1).bfloat16().float()
+    wt = (rnd(64, 64, 3, 3, seed=2) / 24.0).bfloat16().float()
+    b = rnd(64, seed=3)
+    pre = F.conv2d(x, wt, None, padding=1)
+    wf, _ = rr.ops.pack_conv(wt.to(dev), BF)
+    outs = {}
+    for tag in ("1", "0"):
+        monkeypatch.setenv("RR_STREAM3", tag)
+        y, _, st = rr.ops.igemm(RR_CONV3X3, nhwc(x, dev), None, n, h, w, wf, 64, bias=b.to(dev),
+                                stats=True)
+        yr, _, _ = rr.ops.igemm(RR_CONV3X3, nhwc(x, dev), None, n, h, w, wf, 64, bias=b.to(dev),
+                                act=1)
+        torch.cuda.synchronize()
+        outs[tag] = (nchw(y), st.double().sum(0).cpu(), nchw(yr))
+    y, s, yr = outs["1"]
+    assert rel(y, pre + b[None, :, None, None]) < 4e-3
+    assert rel(yr, F.relu(pre + b[None, :, None, None])) < 4e-3
+    assert rel(s[:, 0], pre.double().sum((0, 2, 3))) < 1e-5
+    assert rel(s[:, 1], (pre.double() ** 2).sum((0, 2, 3))) < 1e-5
+    # vs the tiled kernel: same bf16 rounding of the same fp32 sums
+    assert rel(y, outs["0"][0]) < 1e-3
+    assert rel(s, outs["0"][1]) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(9, 64, 64), (41, 32, 32)])
+@pytest.mark.parametrize("acc,msk,act", [(True, False, 0), (False, True, 0), (True, True, 0),
+                                         (True, False, 1)])
+def test_stream3_load_epilogue(dev, shape, acc, msk, act, monkeypatch):
+    """dgrad epilogues: accumulate into y (identity-shortcut grad), relu
+    backward mask (VGG conv1_2 dgrad), both."""
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    monkeypatch.setenv("RR_STREAM3", "1")
+    n, h, w = shape
+    x = rnd(n, 64, h, w, seed=11).bfloat16().float()
+    wt = (rnd(64, 64, 3, 3, seed=12) / 24.0).bfloat16().float()
+    y0 = rnd(n, 64, h, w, seed=13).bfloat16().float()
+    m = rnd(n, 64, h, w, seed=14).bfloat16().float()
+    pre = F.conv2d(x, wt, None, padding=1)
+    ref = pre + (y0 if acc else 0)
+    if act:
+        ref = F.relu(ref)
+    if msk:
+        ref = torch.where(m > 0, ref, torch.zeros(()))
+    wf, _ = rr.ops.pack_conv(wt.to(dev), BF)
+    out = nhwc(y0, dev) if acc else None
+    y, _, _ = rr.ops.igemm(RR_CONV3X3, nhwc(x, dev), None, n, h, w, wf, 64, out=out,
+                           accumulate=acc, act=act, mask=nhwc(m, dev) if msk else None)
+    assert rel(nchw(y), ref) < 4e-3
+
+
+@pytest.mark.parametrize("shape", [(8, 64, 64), (9, 64, 64), (41, 32, 32)])
+def test_stream3_bnbwd(dev, shape, monkeypatch):
+    """conv dgrad + BN/PReLU backward reduce fused in the streaming epilogue
+    == the tiled kernel's fused path == the unfused sequence."""
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    ops = rr.ops
+    n, h, w = shape
+    C = 64
+    g2 = nhwc(rnd(n, C, h, w, seed=51), dev)
+    wt = (rnd(C, C, 3, 3, seed=52) * (1.0 / (3 * C ** 0.5))).to(dev)
+    _, wd = ops.pack_conv(wt, BF)
+    t1 = nhwc(rnd(n, C, h, w, seed=53) * 2 + 0.3, dev)
+    tf = t1.float().reshape(-1, C)
+    mean = tf.mean(0)
+    inv = 1.0 / torch.sqrt(tf.var(0, unbiased=False) + 1e-5)
+    gamma = (torch.rand(C, generator=torch.Generator().manual_seed(54)) + 0.5).to(dev)
+    beta = (torch.rand(C, generator=torch.Generator().manual_seed(55)) - 0.5).to(dev)
+    s1 = gamma * inv
+    sh1 = beta - mean * s1
+    alpha = torch.tensor([0.23], device=dev)
+    monkeypatch.setenv("RR_STREAM3", "0")
+    da1, _, _ = ops.igemm(RR_CONV3X3, g2, None, n, h, w, wd, C)
+    ref = ops.bn_backward(da1, t1, mean, inv, gamma, mask_kind=2, aux=t1, aff_s=s1, aff_b=sh1,
+                          alpha=alpha)
+    res = {}
+    for tag in ("0", "1"):
+        monkeypatch.setenv("RR_STREAM3", tag)
+        gm, part, rows, arows = ops.igemm_bnbwd(RR_CONV3X3, g2, n, h, w, wd, C, t1, mean, inv, s1,
+                                                sh1, alpha)
+        if tag == "1":
+            assert rows == 256 and arows == 256
+        res[tag] = ops.bn_backward_rows(gm, part, rows, arows, t1, mean, inv, gamma)
+    torch.cuda.synchronize()
+    got, tiled = res["1"], res["0"]
+    assert rel(got["dt0"], ref["dt0"]) < 2e-2
+    for k in ("dgamma0", "dbeta0", "dalpha"):
+        assert rel(got[k], ref[k]) < 2e-2, k
+        assert rel(got[k], tiled[k]) < 1e-4, k
+    assert rel(got["dt0"], tiled["dt0"]) < 2e-3
