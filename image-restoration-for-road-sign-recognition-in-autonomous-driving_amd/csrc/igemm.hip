@@ -991,7 +991,7 @@ int dispatch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
 
 extern "C" int rr_igemm_stat_blocks(const rr_igemm_desc *d) {
   if (!d) return RR_EINVAL;
-  if (const int sb = stream3_blocks(d)) return sb;
+  if (const int sb = stream3_blocks(d, 0)) return sb;
   const long long P = (long long)d->n * d->h * d->w;
   const int hb = halo_bc(d);
   const int bp = hb ? (hb <= 64 ? halo_bp(d) : 256) : pick_tile(d).bp;
@@ -1042,13 +1042,13 @@ extern "C" int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
   const int rc = fill_args(d, x1, x2, w, bias, y1, y2, mask, stats_partial, a);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
-  if (stream3_blocks(d)) {
+  if (stream3_blocks(d, 0)) {
     S3Args s{};
     s.x = a.x1; s.wt = a.wt; s.bias = a.bias; s.y = a.y1;
     s.mask = d->has_mask ? a.mask : nullptr;
     s.stats = a.stats;
     s.n = d->n; s.h = d->h; s.act = d->act; s.accumulate = d->accumulate;
-    return stream3_launch(d, s, st);
+    return stream3_launch(d, s, 0, st);
   }
   if (d->dtype == RR_BF16) return dispatch<bf16_t>(d, a, st);
   return dispatch<float>(d, a, st);
@@ -1083,13 +1083,13 @@ extern "C" int rr_igemm_bnbwd(const rr_igemm_desc *d, const void *dy, const void
   a.bpart = partial;
   a.bapart = partial + (size_t)bnbwd_rows(d) * d->c_out * 3;
   hipStream_t st = (hipStream_t)stream;
-  if (stream3_blocks(d)) {
+  if (stream3_blocks(d, 1)) {
     S3Args s{};
     s.x = a.x1; s.wt = a.wt; s.y = a.y1;
     s.n = d->n; s.h = d->h;
     s.bt = a.bt; s.bmean = mean; s.binv = invstd; s.baff_s = aff_s; s.baff_b = aff_b;
     s.balpha = alpha; s.bpart = a.bpart; s.bapart = a.bapart;
-    return stream3_launch(d, s, st);
+    return stream3_launch(d, s, 1, st);
   }
   if (d->dtype == RR_BF16) return dispatch<bf16_t>(d, a, st);
   return dispatch<float>(d, a, st);

@@ -21,7 +21,10 @@ struct S3Args {
 };
 
 // 0 when the descriptor is not handled by the streaming kernel, else the
-// number of workgroups (= rows of the stats / bnbwd partial slabs)
-int stream3_blocks(const rr_igemm_desc *d);
+// number of workgroups (= rows of the stats / bnbwd partial slabs); bnbwd:
+// the rr_igemm_bnbwd epilogue.  Eligibility does not depend on the epilogue
+// beyond the supported flag sets, so the partial-row count a caller sizes
+// from the plain descriptor matches the launch.
+int stream3_blocks(const rr_igemm_desc *d, int bnbwd);
 // launch; returns an RR_* status
-int stream3_launch(const rr_igemm_desc *d, const S3Args &a, hipStream_t st);
+int stream3_launch(const rr_igemm_desc *d, const S3Args &a, int bnbwd, hipStream_t st);

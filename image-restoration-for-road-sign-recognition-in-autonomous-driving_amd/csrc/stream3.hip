@@ -11,23 +11,33 @@
 // weights from L2 for every tile and only overlaps a tile's loads with the
 // other workgroup's MFMAs.  Here:
 //   * one persistent 512-thread workgroup per CU walks a contiguous range of
-//     output rows (whole images at batch 512) in 128-pixel steps
-//     (RPS = 128 / W rows);
+//     output rows (whole images at batch 512) in steps of SPX = 64 MP
+//     pixels (RPS = SPX / W image rows);
 //   * every input row is read ONCE: rows land by LDS-DMA
 //     (global_load_lds_dwordx4) in a ring of RING padded rows, D steps ahead
 //     of the MFMAs; a step's three input-row windows for the taps are slots
 //     of that ring (the zero padding rows / columns come from a zero page);
 //   * the weights (64 x 576 bf16 = 72 KB) live in registers for the whole
 //     kernel: wave (wc, wp) owns output channels [32 wc, 32 wc + 32) -- its
-//     A fragments, 144 VGPRs -- and 32 pixels of each step;
-//   * the epilogue stores from the accumulators (4 NHWC channels per lane)
-//     and keeps BN statistics / BN-backward sums in registers across all the
-//     workgroup's steps (one reduction at the end, per-workgroup partials).
+//     A fragments, 144 VGPRs -- and 16 MP pixels of each step;
+//   * the epilogue (compile-time flags F) stores from the accumulators (4
+//     NHWC channels per lane) and keeps BN statistics / BN-backward sums in
+//     registers across all the workgroup's steps (one reduction at the end,
+//     per-workgroup partials).
+// The per-step scalar work (ring slots, DMA addresses, cursor, waits) is
+// fixed, so epilogues without global loads use 256-pixel steps (MP = 4),
+// twice the MFMA work per unit of overhead; those with loads (accumulate,
+// relu mask, BN backward) keep 128-pixel steps for their operand registers.
 //
-// Ring row image ("k-planes", as the halo kernel): plane j = 16-B channel
-// chunk j of the W + 2 padded pixels, plane size PL = 0 mod 256 B, so a
-// ds_read_b128 16-lane group (8 pixels of chunk q, 8 of chunk q + 1 --
-// the MFMA B fragment map) hits 16 distinct bank slots for any pixel base.
+// Ring row image: the W + 2 zero-padded pixels of an input row, 128 B each
+// (64 channels), pixel-major, with the 16-B channel chunks of pixel p
+// XOR-permuted: slot s of pixel p holds chunk s ^ swz(p mod 16).  A DMA
+// piece is then 8 whole pixels = 1 KB of contiguous NHWC input (8 cache
+// lines per instruction instead of 64 for a channel-planar image), and the
+// MFMA B reads stay conflict-free: a ds_read_b128 16-lane group reads 16
+// consecutive pixels, 8 at chunk c and 8 at chunk c + 1 (c even); swz (see
+// s3_swz) makes those 16 bank slots distinct for pixel offsets 0, 1, 2 mod
+// 16 -- the three tap columns of a 16-pixel block, the only offsets read.
 //
 // vmcnt accounting: LDS-DMA, the epilogue's global loads and its stores share
 // the in-order vector-memory counter.  Iteration u issues, in this order:
@@ -36,7 +46,10 @@
 //   (D - 1) DMAW + S [v-D computed] + (E + S) * #computed in (v-D, v)
 // of its ops are outstanding (exactly the ops younger than DMA(v)), then a
 // raw s_barrier publishes every wave's rows.  A plain __syncthreads would
-// drain all DMA in flight (vmcnt(0)).
+// drain all DMA in flight (vmcnt(0)).  The epilogue loads and the B-fragment
+// reads are inline asm with their own counted waits: with an LDS-DMA in
+// flight hipcc waits vmcnt(0) / lgkmcnt(0) for the results of ordinary
+// loads, which would drain the prefetch every step.
 #include "common.h"
 #include "stream3.h"
 
@@ -47,22 +60,36 @@ namespace {
 
 constexpr int S3_WG = 256;   // workgroups: one per CU on MI355X (fixed: deterministic partial rows)
 
-template <int W> struct S3Geo {
-  static constexpr int RPS = 128 / W;                          // image rows per step
-  static constexpr int PL = W == 64 ? 1536 : 768;              // plane bytes >= (W + 2) * 16
-  static constexpr int ROWB = 8 * PL;                          // one padded row, 64 channels
-  static constexpr int SCRATCH = 4096;                         // bnbwd coefficients
-  static constexpr int RING = (((160 * 1024 - SCRATCH) / ROWB) / RPS) * RPS;
+enum : int { F_BIAS = 1, F_STATS = 2, F_RELU = 4, F_ACC = 8, F_MASK = 16, F_BNBWD = 32 };
+
+// chunk swizzle: the 16 pixels of a B read at pixel offset P in {0, 1, 2}
+// mod 16 need distinct (p & 1, chunk ^ swz(p)) pairs with chunks c (outer 8
+// lanes) and c + 1 (inner 8); for each pixel parity the 8 values e_k =
+// swz(2k + parity) must satisfy {e0,e1,e2^1,e3^1,e4^1,e5^1,e6,e7} and
+// {e0,e1,e2,e3^1,e4^1,e5^1,e6^1,e7} both = {0..7}, i.e. e2 == e6 and the
+// other six fill the rest: e = 2 3 0 5 4 7 0 7 (checked for every lane group)
+__host__ __device__ constexpr int s3_swz(int p) { return (0x70745032u >> (4 * ((p >> 1) & 7))) & 0xf; }
+
+template <int W, int MP> struct S3Geo {
+  static constexpr int SPX = 64 * MP;                          // pixels per step
+  static constexpr int RPS = SPX / W;                          // image rows per step
+  // padded pixels per ring row: >= W + 2, and a step's rows split into whole
+  // 1-KB DMA pieces over the 8 waves
+  static constexpr int RPX = W == 32 ? 48 : (MP == 4 ? 80 : 96);
+  static constexpr int ROWB = RPX * 128;                       // one padded row, 64 channels
+  static constexpr int SCRATCH = 2048;                         // bnbwd coefficients
+  static constexpr int RING = (160 * 1024 - SCRATCH) / ROWB;   // ring rows
   static constexpr int D = (RING - 2) / RPS - 1;               // steps of prefetch in flight
-  static constexpr int DMAW = RPS * ROWB / 1024 / 8;           // DMA instructions / wave / step
+  static constexpr int DMAW = RPS * ROWB / 8192;               // DMA instructions / wave / step
   static constexpr int LDS = RING * ROWB + SCRATCH;
   static_assert((RPS * ROWB) % 8192 == 0, "a step's rows must split evenly over 8 waves");
-  static_assert(PL % 256 == 0 && PL >= (W + 2) * 16, "plane size");
+  static_assert(ROWB % 1024 == 0, "DMA pieces never straddle ring rows");
+  static_assert(RPX >= W + 2 && ROWB % 256 == 0, "row size");
   static_assert(D >= 2 && (D + 1) * RPS + 2 <= RING, "ring");
+  static_assert(LDS <= 160 * 1024, "LDS");
 };
 
 enum { S3_PRE = 0, S3_COMP = 1 };
-enum { EPI_PLAIN = 0, EPI_LOAD = 1, EPI_BNBWD = 2 };
 
 #define S3_W1(n) \
   case n: asm volatile("s_waitcnt vmcnt(" #n ")\n\ts_barrier" ::: "memory"); break;
@@ -77,8 +104,13 @@ __device__ __forceinline__ void wait_vm_barrier(int n) {
     default: asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory"); break;
   }
 }
+template <int N> __device__ __forceinline__ void wait_vm_barrier_c() {
+  static_assert(N >= 0 && N <= 63, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
 
 typedef unsigned long long u64;
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 // 8-byte global load the compiler's waitcnt pass does not see (the caller
 // waits with an explicit vmcnt that names the result registers)
@@ -87,9 +119,15 @@ __device__ __forceinline__ u64 load_b64_async(const char *p) {
   asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
   return r;
 }
-// LDS read of 8 bytes outside the compiler's view: its waitcnt pass puts a
-// vmcnt(0) (drain all LDS-DMA) before a visible ds_read it cannot separate
-// from the DMA destination
+// LDS reads outside the compiler's view: its waitcnt pass puts a vmcnt(0)
+// (drain all LDS-DMA) before a visible ds_read it cannot separate from the
+// DMA destination
+__device__ __forceinline__ f32x4 lds_read_4(const float *p) {
+  f32x4 r;
+  const uint32_t a = (uint32_t)(uintptr_t)p;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(a) : "memory");
+  return r;
+}
 __device__ __forceinline__ void lds_read_2x4(const float *p, f32x4 &lo, f32x4 &hi) {
   const uint32_t a = (uint32_t)(uintptr_t)p;
   asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
@@ -100,21 +138,34 @@ __device__ __forceinline__ f32x4 unpack4(u64 v) {
   return f32x4{__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
                __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
 }
+__device__ __forceinline__ uint2 pack4(f32x4 g) {
+  uint2 o;
+  o.x = (uint32_t)f32_to_bf16(g[0]) | ((uint32_t)f32_to_bf16(g[1]) << 16);
+  o.y = (uint32_t)f32_to_bf16(g[2]) | ((uint32_t)f32_to_bf16(g[3]) << 16);
+  return o;
+}
 
 struct Cur {
-  int kind, n, y0, c;   // virtual step: pre-load or compute of output rows [y0, y0 + RPS) of image n
+  int kind, n, y0, c;   // virtual step: pre-load, or compute of output rows [y0, y0 + RPS) of image n
 };
 
-template <int W, int EPI>
+template <int W, int MP, int F>
 __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
-  using G = S3Geo<W>;
-  constexpr int RPS = G::RPS, PL = G::PL, ROWB = G::ROWB, RING = G::RING, D = G::D;
+  using G = S3Geo<W, MP>;
+  constexpr int RPS = G::RPS, ROWB = G::ROWB, RING = G::RING, D = G::D;
   constexpr int DMAW = G::DMAW;
-  constexpr int MC = 2, MP = 2;                 // 32 channels x 32 pixels per wave
+  constexpr int MC = 2;                         // 32 output channels per wave
+  constexpr bool BNBWD = (F & F_BNBWD) != 0;
+  constexpr bool ACC = (F & F_ACC) != 0, MASK = (F & F_MASK) != 0;
+  constexpr bool STATS = (F & F_STATS) != 0;
+  constexpr int NE = BNBWD ? 1 : (ACC ? 1 : 0) + (MASK ? 1 : 0);   // epilogue loads per block
+  constexpr int E = MC * MP * NE, S = MP;          // S: 16-B stores per step
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
   float *coef = reinterpret_cast<float *>(smem + RING * ROWB);   // [64][2]
 
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  // wave-uniform indices in SGPRs (the address math of a step is scalar)
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wc = wv & 1, wp = wv >> 1;
   const int frow = lane & 15, fq = lane >> 4;
   const int H = a.h;
@@ -134,14 +185,8 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
         wr[mi][tap][kb] =
             *reinterpret_cast<const bf16x8 *>(a.wt + ((co * 9 + tap) * 64 + kb * 32 + fq * 8) * 2);
   }
-  f32x4 bia[MC];
-#pragma unroll
-  for (int mi = 0; mi < MC; ++mi) {
-    const int c = wc * 32 + mi * 16 + fq * 4;
-    bia[mi] = a.bias ? *reinterpret_cast<const f32x4 *>(a.bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
   float al = 0.f;
-  if constexpr (EPI == EPI_BNBWD) {
+  if constexpr (BNBWD) {
     if (tid < 64) {
       // u = t * s + b (BN out = PReLU in)
       coef[tid * 2 + 0] = a.baff_s[tid];
@@ -150,34 +195,41 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     al = a.balpha[0];
     __syncthreads();
   }
+  if constexpr ((F & F_BIAS) != 0) {
+    // the bias is read from LDS per step (8 fewer VGPRs held over the loop)
+    if (tid < 64) coef[tid] = a.bias[tid];
+    __syncthreads();
+  }
 
-  // ---- LDS-DMA lanes: row-in-step and byte offset inside a pixel row --------
-  const long long zoff = (long long)((uintptr_t)rr_zero_page - (uintptr_t)a.x);   // zero rows
-  int drow[DMAW], dofs[DMAW];
+  // ---- LDS-DMA pieces: a 1-KB piece lies in one ring row, so its row and
+  // chunk are wave-uniform; the lane's plane / pixel is fixed ----
+  const long long zoff = (long long)((uintptr_t)rr_zero_page - (uintptr_t)a.x);   // zero source
+  int drow[DMAW], dchk[DMAW], dofs[DMAW];
 #pragma unroll
   for (int i = 0; i < DMAW; ++i) {
-    const int off = (wv * DMAW + i) * 1024 + lane * 16;
-    const int r = off / ROWB, o = off - r * ROWB;
-    const int pl = o / PL, x = (o - pl * PL) / 16 - 1;
-    drow[i] = r;
-    dofs[i] = (x >= 0 && x < W) ? (x * 64 + pl * 8) * 2 : -1;
+    const int piece = (wv * DMAW + i) * 1024;
+    drow[i] = piece / ROWB;
+    dchk[i] = piece - drow[i] * ROWB;
+    const int o = dchk[i] + lane * 16;
+    const int px = o / 128, x = px - 1, chunk = ((o / 16) & 7) ^ s3_swz(px & 15);
+    dofs[i] = (x >= 0 && x < W) ? x * 128 + chunk * 16 : -1;
   }
-  auto issue = [&](int v, const Cur &cu, bool live) __attribute__((always_inline)) {
-    char *reg = smem + ((v * RPS) % RING) * ROWB;
+  // DMA of virtual step `cu` into the ring rows starting at slot `slot`
+  auto issue = [&](int slot, const Cur &cu, bool live) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < DMAW; ++i) {
-      // keeps the compiler from hoisting DMAW 64-bit row bases out of the
-      // loop (VGPR pressure: the weights hold 144)
-      asm volatile("" : "+v"(dofs[i]));
       const int r = drow[i];
-      int y = cu.kind == S3_PRE ? cu.y0 - RPS + 1 + r : cu.y0 + 1 + r;
-      const bool ok = live && dofs[i] >= 0 && y >= 0 && y < H && (cu.kind != S3_PRE || r >= RPS - 2);
-      // one base pointer + a selected offset: a pointer select (or one
-      // across address spaces) becomes a divergent branch, i.e. two
-      // exec-masked DMA instructions, which breaks the vmcnt accounting
-      const long long off = ok ? ((long long)(cu.n * H + y) * W) * 128 + dofs[i] : zoff;
+      const int y = cu.kind == S3_PRE ? cu.y0 - RPS + 1 + r : cu.y0 + 1 + r;
+      const bool rok = live & (y >= 0) & (y < H) & ((cu.kind != S3_PRE) | (r >= RPS - 2));   // uniform
+      const long long rbase = ((long long)(cu.n * H + y) * W) * 128;
+      // one base pointer + selected offsets (no pointer select / branch: two
+      // exec-masked DMA instructions would break the vmcnt accounting)
+      long long off = dofs[i] >= 0 ? rbase + dofs[i] : zoff;
+      off = rok ? off : zoff;
+      int s = slot + r;
+      s = s >= RING ? s - RING : s;
       __builtin_amdgcn_global_load_lds((const void *)(a.x + off),
-                                       LDS_PTR(reg + (wv * DMAW + i) * 1024), 16, 0, 0);
+                                       LDS_PTR(smem + s * ROWB + dchk[i]), 16, 0, 0);
     }
   };
   auto advance = [&](Cur &cu) __attribute__((always_inline)) {
@@ -190,163 +242,233 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     }
   };
 
-  // ---- per-wave pixel blocks of a step ----
-  int bq[MP], bx[MP], lpart[MP];
+  // ---- per-wave pixel blocks of a step and lane parts ----
+  // the wave's 16 MP pixels start at row q0, column x0 (uniform); block ni
+  // sits NRW(ni) rows and XO(ni) columns further (compile time: x0 + 16 MP
+  // never crosses more than the rows the geometry implies)
+  constexpr int NR = (16 * MP + W - 1) / W;     // distinct image rows of a wave's pixels
+  const int q0 = (wp * 16 * MP) / W, x0 = (wp * 16 * MP) % W;
+  static_assert(W >= 16 * MP || (16 * MP) % W == 0, "block rows");
+  // lane part of a B read for tap column dx and k-half kb: pixel frow + dx of
+  // the block, chunk kb * 4 + fq through the swizzle
+  uint32_t boff[3][2];
 #pragma unroll
-  for (int ni = 0; ni < MP; ++ni) {
-    const int p = wp * 32 + ni * 16;
-    bq[ni] = p / W;
-    bx[ni] = p % W;
-    lpart[ni] = fq * PL + (bx[ni] + frow) * 16;
-  }
+  for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+      boff[dx][kb] = (frow + dx) * 128 + (((kb * 4 + fq) ^ s3_swz((frow + dx) & 15)) * 16);
+  const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+  const uint32_t le = (frow * 64 + wc * 32 + fq * 4) * 2;                // lane part of an output (acc layout)
+  // widened stores (permlane16 swaps, see epilogue): lane part of a 16-B store
+  const uint32_t le2 = frow * 128 + (wc * 32 + (fq & 1) * 16 + (fq & 2) * 4) * 2;
 
-  // running epilogue sums: stats (sum, sum sq) or bnbwd (sum gm, sum gm xhat)
+  // running epilogue sums: stats (sum, sum sq) or bnbwd (sum gm, sum gm t)
   f32x4 r0[MC], r1[MC];
   float ra = 0.f;
 #pragma unroll
   for (int mi = 0; mi < MC; ++mi) { r0[mi] = f32x4{0.f, 0.f, 0.f, 0.f}; r1[mi] = r0[mi]; }
 
-  const int E = EPI == EPI_PLAIN ? 0
-                                 : (EPI == EPI_BNBWD ? MC * MP
-                                                     : MC * MP * ((a.accumulate ? 1 : 0) + (a.mask ? 1 : 0)));
-  constexpr int S = MC * MP;
+  u64 ev0[MC][MP], ev1[MC][MP];
+  f32x4 acc[MC][MP];
+  auto load_e = [&](long long pix0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < MP; ++ni) {
+        const long long ub = (pix0 + q0 * W + x0 + ni * 16) * 128 + mi * 32;   // uniform
+        if constexpr (BNBWD) ev0[mi][ni] = load_b64_async(a.bt + ub + le);
+        if constexpr (!BNBWD && ACC) ev0[mi][ni] = load_b64_async(a.y + ub + le);
+        if constexpr (!BNBWD && MASK) ev1[mi][ni] = load_b64_async(a.mask + ub + le);
+      }
+  };
+  auto wait_e = [&]() __attribute__((always_inline)) {
+    // the epilogue loads are older than the DMAW DMAs issued after them
+    if constexpr (NE > 0) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMAW) : "memory");
+#pragma unroll
+      for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < MP; ++ni) {
+          if constexpr (BNBWD || ACC) asm volatile("" : "+v"(ev0[mi][ni]));
+          if constexpr (MASK && !BNBWD) asm volatile("" : "+v"(ev1[mi][ni]));
+        }
+    }
+  };
+  auto mfma_step = [&](int s0) __attribute__((always_inline)) {
+    // ring slot of input row y0 - 1 + r is s0 + r (mod RING); s0 + r < 2 RING
+    uint32_t rba[3][NR];                        // per tap row dy and image row: ring row base (uniform)
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {
+        int r = s0 + q0 + k + dy;
+        r = r >= RING ? r - RING : r;
+        rba[dy][k] = sbase + r * ROWB + x0 * 128;
+      }
+    // 18 (tap, k-half) groups; the B fragments of group q + 1 are read before
+    // group q's MFMAs (counted lgkmcnt(MP): the prefetched group stays in flight)
+    i32x4 fb[2][MP];
+#pragma unroll
+    for (int ni = 0; ni < MP; ++ni)
+      asm volatile("ds_read_b128 %0, %1 offset:%2"
+                   : "=v"(fb[0][ni]) : "v"(rba[0][(ni * 16) / W] + boff[0][0]),
+                     "i"(((ni * 16) % W) * 128));
+#pragma unroll
+    for (int q = 0; q < 18; ++q) {
+      if (q + 1 < 18) {
+        const int t1 = (q + 1) >> 1, kb1 = (q + 1) & 1;
+#pragma unroll
+        for (int ni = 0; ni < MP; ++ni)
+          asm volatile("ds_read_b128 %0, %1 offset:%2"
+                       : "=v"(fb[(q + 1) & 1][ni])
+                       : "v"(rba[t1 / 3][(ni * 16) / W] + boff[t1 % 3][kb1]),
+                         "i"(((ni * 16) % W) * 128));
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(MP) : "memory");
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+#pragma unroll
+      for (int ni = 0; ni < MP; ++ni) asm volatile("" : "+v"(fb[q & 1][ni]));
+#pragma unroll
+      for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < MP; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              wr[mi][q >> 1][q & 1], __builtin_bit_cast(bf16x8, fb[q & 1][ni]),
+              q == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[mi][ni], 0, 0, 0);
+    }
+  };
+  // epilogue: lane = pixel (frow) x 4 channels of each 16 x 16 block
+  auto epilogue = [&](long long pix0) __attribute__((always_inline)) {
+    uint2 pk[MC][MP];
+#pragma unroll
+    for (int mi = 0; mi < MC; ++mi) {
+      const int c = wc * 32 + mi * 16 + fq * 4;
+      f32x4 k01, k23;                           // (s, b) of channels c .. c + 3
+      if constexpr (BNBWD) lds_read_2x4(coef + c * 2, k01, k23);
+      f32x4 bia;
+      if constexpr ((F & F_BIAS) != 0) bia = lds_read_4(coef + c);
+#pragma unroll
+      for (int ni = 0; ni < MP; ++ni) {
+        const long long ub = (pix0 + q0 * W + x0 + ni * 16) * 128 + mi * 32;     // uniform
+        f32x4 g = acc[mi][ni];
+        if constexpr (BNBWD) {
+          const f32x4 t = unpack4(ev0[mi][ni]);
+          f32x4 gm;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            // sum gm * xhat = inv (sum gm t) - inv mean (sum gm): the affine
+            // part is applied once per channel at the end
+            const float ks = j < 2 ? k01[2 * j] : k23[2 * j - 4];
+            const float kb = j < 2 ? k01[2 * j + 1] : k23[2 * j - 3];
+            const float u = t[j] * ks + kb;
+            ra += u > 0.f ? 0.f : g[j] * u;
+            gm[j] = u > 0.f ? g[j] : al * g[j];
+            r0[mi][j] += gm[j];
+            r1[mi][j] += gm[j] * t[j];
+          }
+          g = gm;
+        } else {
+          if constexpr (STATS) {
+            r0[mi] += g;
+            r1[mi] += g * g;
+          }
+          if constexpr ((F & F_BIAS) != 0) g += bia;
+          if constexpr (ACC) g += unpack4(ev0[mi][ni]);
+          if constexpr ((F & F_RELU) != 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) g[j] = fmaxf(g[j], 0.f);
+          }
+          if constexpr (MASK) {
+            const f32x4 mk = unpack4(ev1[mi][ni]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) g[j] = mk[j] > 0.f ? g[j] : 0.f;
+          }
+        }
+        pk[mi][ni] = pack4(g);
+      }
+    }
+    // widened stores: per pixel-block pair (A, B) two permlane16 swap levels
+    // turn the accumulator layout (lane: 4 channels of one pixel) into 16 B
+    // per lane, 4 lanes = the wave's 32 channels (64 B) of one pixel:
+    //  1. per mi, swap(A, B) on each dword: rows 0/2 hold 8 channels of A's
+    //     pixel, rows 1/3 8 channels of B's (odd rows of vdst <-> even rows
+    //     of src);
+    //  2. swap(mi 0, mi 1) on each of the 4 dwords: register 0 holds pixel A,
+    //     register 1 pixel B, channel start (fq & 1) * 16 + (fq & 2) * 4.
+    // 16 swaps + MP/2 * 2 16-B stores instead of 2 MP 8-B stores.
+#pragma unroll
+    for (int j = 0; j < MP / 2; ++j) {
+      uint32_t v[MC][4];
+#pragma unroll
+      for (int mi = 0; mi < MC; ++mi) {
+        const auto rx = __builtin_amdgcn_permlane16_swap(pk[mi][2 * j].x, pk[mi][2 * j + 1].x, false, false);
+        const auto ry = __builtin_amdgcn_permlane16_swap(pk[mi][2 * j].y, pk[mi][2 * j + 1].y, false, false);
+        v[mi][0] = rx[0]; v[mi][1] = ry[0]; v[mi][2] = rx[1]; v[mi][3] = ry[1];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v[0][k], v[1][k], false, false);
+        v[0][k] = r[0];
+        v[1][k] = r[1];
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ni = 2 * j + h;
+        const long long ub = (pix0 + q0 * W + x0 + ni * 16) * 128;             // uniform
+        *reinterpret_cast<uint4 *>(a.y + ub + le2) = make_uint4(v[h][0], v[h][1], v[h][2], v[h][3]);
+      }
+    }
+  };
 
   // weights / bias / coefficients resident before any DMA is in flight: the
   // compiler's own wait for them would otherwise drain the prologue DMAs
   __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0) (gfx9 encoding)
-  Cur ld, cp;
+  Cur ld;
   ld.c = cbeg;
   ld.n = cbeg / spi;
   ld.y0 = (cbeg - ld.n * spi) * RPS;
   ld.kind = S3_PRE;
-  cp = ld;
+  Cur cp = ld;
+  int lslot = 0;                                // ring slot of the loader's step
 #pragma unroll
   for (int k = 0; k < D; ++k) {
-    issue(k, ld, ld.c < cend);
+    issue(lslot, ld, ld.c < cend);
     advance(ld);
+    lslot += RPS;
+    lslot = lslot >= RING ? lslot - RING : lslot;
   }
+  int cslot = RING - 2;                         // ring slot of the compute step's row y0 - 1
   unsigned hist = 0;                            // bit j: iteration v-1-j computed
+  constexpr int YSS = (D - 1) * DMAW + S + (E + S) * (D - 1);     // steady state
+  constexpr unsigned FULL = (1u << D) - 1;
 #pragma unroll 1
-  for (int v = 0; cp.c < cend; ++v) {
-    const int younger = (D - 1) * DMAW + (((hist >> (D - 1)) & 1) ? S : 0) +
-                        (E + S) * __builtin_popcount(hist & ((1u << (D - 1)) - 1));
-    wait_vm_barrier(younger);
+  while (cp.c < cend) {
+    if ((hist & FULL) == FULL) {
+      wait_vm_barrier_c<YSS < 63 ? YSS : 63>();
+    } else {
+      wait_vm_barrier((D - 1) * DMAW + (((hist >> (D - 1)) & 1) ? S : 0) +
+                      (E + S) * __builtin_popcount(hist & ((1u << (D - 1)) - 1)));
+    }
     const bool comp = cp.kind == S3_COMP;
     const long long pix0 = (long long)(cp.n * H + cp.y0) * W;
-    // epilogue loads BEFORE this iteration's DMA: the compiler's wait for
-    // them then leaves the new DMA in flight (see the vmcnt accounting above)
-    // (inline asm: with an LDS-DMA in flight hipcc waits vmcnt(0) for any
-    // ordinary load's result, which would drain the prefetch every step)
-    u64 ev0[MC][MP], ev1[MC][MP];
-    if constexpr (EPI != EPI_PLAIN) {
-      if (comp) {
-#pragma unroll
-        for (int mi = 0; mi < MC; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < MP; ++ni) {
-            const long long e = (pix0 + bq[ni] * W + bx[ni] + frow) * 64 + wc * 32 + mi * 16 + fq * 4;
-            if constexpr (EPI == EPI_BNBWD) {
-              ev0[mi][ni] = load_b64_async(a.bt + e * 2);
-            } else {
-              if (a.accumulate) ev0[mi][ni] = load_b64_async(a.y + e * 2);
-              if (a.mask) ev1[mi][ni] = load_b64_async(a.mask + e * 2);
-            }
-          }
-      }
-      __builtin_amdgcn_sched_barrier(0);
+    // epilogue loads BEFORE this iteration's DMA (see the vmcnt accounting)
+    if constexpr (NE > 0) {
+      if (comp) load_e(pix0);
     }
-    issue(v + D, ld, ld.c < cend);
+    __builtin_amdgcn_sched_barrier(0);
+    issue(lslot, ld, ld.c < cend);
     advance(ld);
+    lslot += RPS;
+    lslot = lslot >= RING ? lslot - RING : lslot;
+    __builtin_amdgcn_sched_barrier(0);
     if (comp) {
-      f32x4 acc[MC][MP];
-#pragma unroll
-      for (int mi = 0; mi < MC; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < MP; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int s0 = v * RPS - 2;               // ring slot of input row y0 - 1
-#pragma unroll
-      for (int dy = 0; dy < 3; ++dy) {
-        const char *rb[MP];
-#pragma unroll
-        for (int ni = 0; ni < MP; ++ni) rb[ni] = smem + ((s0 + bq[ni] + dy) % RING) * ROWB + lpart[ni];
-#pragma unroll
-        for (int dx = 0; dx < 3; ++dx)
-#pragma unroll
-          for (int kb = 0; kb < 2; ++kb) {
-            bf16x8 fb[MP];
-#pragma unroll
-            for (int ni = 0; ni < MP; ++ni)
-              fb[ni] = *reinterpret_cast<const bf16x8 *>(rb[ni] + kb * 4 * PL + dx * 16);
-#pragma unroll
-            for (int mi = 0; mi < MC; ++mi)
-#pragma unroll
-              for (int ni = 0; ni < MP; ++ni)
-                acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[mi][dy * 3 + dx][kb], fb[ni],
-                                                                     acc[mi][ni], 0, 0, 0);
-          }
-      }
-      // ---- epilogue: lane = pixel (frow) x 4 channels ----
-      if constexpr (EPI != EPI_PLAIN) {
-        // the epilogue loads are older than this step's DMAW DMAs
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(%8)"
-                     : "+v"(ev0[0][0]), "+v"(ev0[0][1]), "+v"(ev0[1][0]), "+v"(ev0[1][1]),
-                       "+v"(ev1[0][0]), "+v"(ev1[0][1]), "+v"(ev1[1][0]), "+v"(ev1[1][1])
-                     : "n"(DMAW));
-      }
-#pragma unroll
-      for (int mi = 0; mi < MC; ++mi) {
-        const int c = wc * 32 + mi * 16 + fq * 4;
-        f32x4 k01, k23;                         // (s, b) of channels c .. c + 3
-        if constexpr (EPI == EPI_BNBWD) lds_read_2x4(coef + c * 2, k01, k23);
-#pragma unroll
-        for (int ni = 0; ni < MP; ++ni) {
-          const long long e = (pix0 + bq[ni] * W + bx[ni] + frow) * 64 + c;
-          f32x4 g = acc[mi][ni];
-          if constexpr (EPI == EPI_BNBWD) {
-            const f32x4 t = unpack4(ev0[mi][ni]);
-            f32x4 gm;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              // sum gm * xhat = inv (sum gm t) - inv mean (sum gm): the
-              // affine part is applied once per channel at the end
-              const float ks = j < 2 ? k01[2 * j] : k23[2 * j - 4];
-              const float kb = j < 2 ? k01[2 * j + 1] : k23[2 * j - 3];
-              const float u = t[j] * ks + kb;
-              ra += u > 0.f ? 0.f : g[j] * u;
-              gm[j] = u > 0.f ? g[j] : al * g[j];
-              r0[mi][j] += gm[j];
-              r1[mi][j] += gm[j] * t[j];
-            }
-            g = gm;
-          } else {
-            if (a.stats) {
-              r0[mi] += g;
-              r1[mi] += g * g;
-            }
-            g += bia[mi];
-            if constexpr (EPI == EPI_LOAD) {
-              if (a.accumulate) g += unpack4(ev0[mi][ni]);
-            }
-            if (a.act == RR_ACT_RELU) {
-#pragma unroll
-              for (int j = 0; j < 4; ++j) g[j] = fmaxf(g[j], 0.f);
-            }
-            if constexpr (EPI == EPI_LOAD) {
-              if (a.mask) {
-                const f32x4 mk = unpack4(ev1[mi][ni]);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) g[j] = mk[j] > 0.f ? g[j] : 0.f;
-              }
-            }
-          }
-          uint2 o;
-          o.x = (uint32_t)f32_to_bf16(g[0]) | ((uint32_t)f32_to_bf16(g[1]) << 16);
-          o.y = (uint32_t)f32_to_bf16(g[2]) | ((uint32_t)f32_to_bf16(g[3]) << 16);
-          *reinterpret_cast<uint2 *>(a.y + e * 2) = o;
-        }
-      }
+      mfma_step(cslot);
+      wait_e();
+      epilogue(pix0);
     }
+    cslot += RPS;
+    cslot = cslot >= RING ? cslot - RING : cslot;
     hist = (hist << 1) | (comp ? 1u : 0u);
     advance(cp);
   }
@@ -355,69 +477,95 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
   __syncthreads();
 
   // ---- per-workgroup partials: lanes of one channel (frow) -> waves (wp) ----
-  const bool want = EPI == EPI_BNBWD || a.stats;
-  if (!want) return;
-#pragma unroll
-  for (int mi = 0; mi < MC; ++mi)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        r0[mi][j] += __shfl_xor(r0[mi][j], o, 64);
-        r1[mi][j] += __shfl_xor(r1[mi][j], o, 64);
-      }
-  float *red = reinterpret_cast<float *>(smem);   // [4 wp][64][2] + [8 waves]
-  if (frow == 0) {
+  if constexpr (STATS || BNBWD) {
 #pragma unroll
     for (int mi = 0; mi < MC; ++mi)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = wc * 32 + mi * 16 + fq * 4 + j;
-        red[(wp * 64 + c) * 2 + 0] = r0[mi][j];
-        red[(wp * 64 + c) * 2 + 1] = r1[mi][j];
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          r0[mi][j] += __shfl_xor(r0[mi][j], o, 64);
+          r1[mi][j] += __shfl_xor(r1[mi][j], o, 64);
+        }
+    float *red = reinterpret_cast<float *>(smem);   // [4 wp][64][2] + [8 waves]
+    if (frow == 0) {
+#pragma unroll
+      for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = wc * 32 + mi * 16 + fq * 4 + j;
+          red[(wp * 64 + c) * 2 + 0] = r0[mi][j];
+          red[(wp * 64 + c) * 2 + 1] = r1[mi][j];
+        }
+    }
+    if constexpr (BNBWD) {
+      ra = wave_sum(ra);
+      if (lane == 0) red[4 * 64 * 2 + wv] = ra;
+    }
+    __syncthreads();
+    if (tid < 64) {
+      float x = 0.f, y = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        x += red[(q * 64 + tid) * 2 + 0];
+        y += red[(q * 64 + tid) * 2 + 1];
       }
-  }
-  if constexpr (EPI == EPI_BNBWD) {
-    ra = wave_sum(ra);
-    if (lane == 0) red[4 * 64 * 2 + wv] = ra;
-  }
-  __syncthreads();
-  if (tid < 64) {
-    float x = 0.f, y = 0.f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      x += red[(q * 64 + tid) * 2 + 0];
-      y += red[(q * 64 + tid) * 2 + 1];
+      if constexpr (BNBWD) {
+        float *pp = a.bpart + ((long long)blockIdx.x * 64 + tid) * 3;
+        pp[0] = x;
+        pp[1] = a.binv[tid] * (y - a.bmean[tid] * x);
+        pp[2] = 0.f;
+      } else {
+        a.stats[((long long)blockIdx.x * 64 + tid) * 2 + 0] = x;
+        a.stats[((long long)blockIdx.x * 64 + tid) * 2 + 1] = y;
+      }
     }
-    if constexpr (EPI == EPI_BNBWD) {
-      float *pp = a.bpart + ((long long)blockIdx.x * 64 + tid) * 3;
-      pp[0] = x;
-      pp[1] = a.binv[tid] * (y - a.bmean[tid] * x);
-      pp[2] = 0.f;
-    } else {
-      a.stats[((long long)blockIdx.x * 64 + tid) * 2 + 0] = x;
-      a.stats[((long long)blockIdx.x * 64 + tid) * 2 + 1] = y;
-    }
-  }
-  if constexpr (EPI == EPI_BNBWD) {
-    if (tid == 0) {
-      float s = 0.f;
+    if constexpr (BNBWD) {
+      if (tid == 0) {
+        float s = 0.f;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) s += red[4 * 64 * 2 + q];
-      a.bapart[blockIdx.x] = s;
+        for (int q = 0; q < 8; ++q) s += red[4 * 64 * 2 + q];
+        a.bapart[blockIdx.x] = s;
+      }
     }
   }
 }
 
+// epilogue flag set of a call, or -1 when the streaming kernel has no
+// instance for it (the tiled kernel takes the call)
+int s3_flags(const rr_igemm_desc *d, bool bnbwd) {
+  if (bnbwd) return F_BNBWD;
+  const int f = (d->has_bias ? F_BIAS : 0) | (d->want_stats ? F_STATS : 0) |
+                (d->act == RR_ACT_RELU ? F_RELU : 0) | (d->accumulate ? F_ACC : 0) |
+                (d->has_mask ? F_MASK : 0);
+  switch (f) {
+    case 0: case F_BIAS: case F_STATS: case F_BIAS | F_STATS: case F_RELU: case F_BIAS | F_RELU:
+    case F_ACC: case F_MASK: case F_ACC | F_MASK:
+      return f;
+    default:
+      return -1;
+  }
+}
+
+template <int W, int MP, int F>
+void launch1(const S3Args &a, int P, hipStream_t st) {
+  hipLaunchKernelGGL((stream3_kernel<W, MP, F>), dim3(S3_WG), dim3(512), 0, st, a, P / (64 * MP));
+}
+
 template <int W>
-int launch_w(const S3Args &a, int nsteps, hipStream_t st) {
-  const dim3 grid(S3_WG), block(512);
-  if (a.bt) {
-    hipLaunchKernelGGL((stream3_kernel<W, EPI_BNBWD>), grid, block, 0, st, a, nsteps);
-  } else if (a.accumulate || a.mask) {
-    hipLaunchKernelGGL((stream3_kernel<W, EPI_LOAD>), grid, block, 0, st, a, nsteps);
-  } else {
-    hipLaunchKernelGGL((stream3_kernel<W, EPI_PLAIN>), grid, block, 0, st, a, nsteps);
+int launch_w(const S3Args &a, int f, int P, hipStream_t st) {
+  switch (f) {
+    case 0: launch1<W, 4, 0>(a, P, st); break;
+    case F_BIAS: launch1<W, 4, F_BIAS>(a, P, st); break;
+    case F_STATS: launch1<W, 4, F_STATS>(a, P, st); break;
+    case F_BIAS | F_STATS: launch1<W, 4, F_BIAS | F_STATS>(a, P, st); break;
+    case F_RELU: launch1<W, 4, F_RELU>(a, P, st); break;
+    case F_BIAS | F_RELU: launch1<W, 4, F_BIAS | F_RELU>(a, P, st); break;
+    case F_ACC: launch1<W, 2, F_ACC>(a, P, st); break;
+    case F_MASK: launch1<W, 2, F_MASK>(a, P, st); break;
+    case F_ACC | F_MASK: launch1<W, 2, F_ACC | F_MASK>(a, P, st); break;
+    case F_BNBWD: launch1<W, 2, F_BNBWD>(a, P, st); break;
+    default: return RR_EUNSUPPORTED;
   }
   RR_CHECK_LAUNCH();
   return RR_OK;
@@ -425,23 +573,25 @@ int launch_w(const S3Args &a, int nsteps, hipStream_t st) {
 
 }  // namespace
 
-int stream3_blocks(const rr_igemm_desc *d) {
+int stream3_blocks(const rr_igemm_desc *d, int bnbwd) {
   const char *e = getenv("RR_STREAM3");
   if (e && !atoi(e)) return 0;
   if (d->dtype != RR_BF16 || d->mode != RR_CONV3X3) return 0;
   if (d->c_in1 != 64 || d->c_in2 != 0 || d->c_out != 64 || d->out_split || d->out_nchw) return 0;
   if (d->w != 64 && d->w != 32) return 0;
-  const int rps = 128 / d->w;
-  if (d->h % rps) return 0;
-  const long long nsteps = (long long)d->n * d->h / rps;
-  if (nsteps < S3_WG) return 0;                 // every workgroup gets >= 1 step
-  if ((long long)d->n * d->h * d->w * 64 > INT_MAX) return 0;
+  if (s3_flags(d, bnbwd != 0) < 0) return 0;
+  // eligibility independent of the step size: whole 256-pixel steps (the
+  // larger one) and at least one per workgroup
+  if (d->h % (256 / d->w)) return 0;
+  const long long P = (long long)d->n * d->h * d->w;
+  if (P < 256LL * S3_WG || P * 64 > INT_MAX) return 0;
   return S3_WG;
 }
 
-int stream3_launch(const rr_igemm_desc *d, const S3Args &a, hipStream_t st) {
-  if (!stream3_blocks(d)) return RR_EUNSUPPORTED;
-  const int nsteps = (int)((long long)d->n * d->h / (128 / d->w));
-  if (d->w == 64) return launch_w<64>(a, nsteps, st);
-  return launch_w<32>(a, nsteps, st);
+int stream3_launch(const rr_igemm_desc *d, const S3Args &a, int bnbwd, hipStream_t st) {
+  if (!stream3_blocks(d, bnbwd)) return RR_EUNSUPPORTED;
+  const int f = s3_flags(d, bnbwd != 0);
+  const int P = d->n * d->h * d->w;
+  if (d->w == 64) return launch_w<64>(a, f, P, st);
+  return launch_w<32>(a, f, P, st);
 }

@@ -84,15 +84,14 @@ def _khalo_bc(mode, dt, n, h, w, c1, c2, cout, split, out_nchw):
 
 
 def _kstream3(mode, dt, n, h, w, c1, c2, cout, split, out_nchw):
-    """Mirror of csrc/stream3.hip stream3_blocks: the row-streaming kernel?"""
+    """Mirror of csrc/stream3.hip stream3_blocks (probe naming only)."""
     if os.environ.get("RR_STREAM3", "1") in ("0",):
         return False
     if dt != torch.bfloat16 or mode != RR_CONV3X3 or w not in (32, 64):
         return False
     if c1 != 64 or c2 or cout != 64 or split or out_nchw:
         return False
-    rps = 128 // w
-    return h % rps == 0 and n * h // rps >= 256
+    return h % (256 // w) == 0 and n * h * w >= 65536
 
 
 def _ws(nbytes, device):

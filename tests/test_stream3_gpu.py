@@ -31,8 +31,9 @@ def rel(a, r):
     return ((a - r).norm() / r.norm().clamp_min(1e-30)).item()
 
 
-# (n, h, w): nsteps = n*h/(128/w) >= 256 workgroups
-SHAPES = [(8, 64, 64), (9, 64, 64), (33, 16, 64), (32, 32, 32), (41, 32, 32), (130, 8, 32)]
+# (n, h, w): >= one 256-pixel step per workgroup (P >= 65536, h % (256 / w) == 0);
+# uneven splits and short images put workgroup ranges across image boundaries
+SHAPES = [(16, 64, 64), (17, 64, 64), (65, 16, 64), (64, 32, 32), (81, 32, 32), (257, 8, 32)]
 
 
 def _blocks(n, h, w):
@@ -49,6 +50,8 @@ def test_stream3_selected(dev, shape, monkeypatch):
     RR_STREAM3=0 switch hands them back to the tiled kernel"""
     n, h, w = shape
     assert _blocks(n, h, w) == 256
+    # too small for one step per workgroup / not whole steps: tiled kernel
+    assert _blocks(n // 2 if n * h * w // 2 < 65536 else 1, h, w) != 256
     monkeypatch.setenv("RR_STREAM3", "0")
     assert _blocks(n, h, w) == (n * h * w) // 256
 
@@ -82,12 +85,12 @@ def test_stream3_fwd_stats(dev, shape, monkeypatch):
     assert rel(s, outs["0"][1]) < 1e-5
 
 
-@pytest.mark.parametrize("shape", [(9, 64, 64), (41, 32, 32)])
+@pytest.mark.parametrize("shape", [(17, 64, 64), (81, 32, 32)])
 @pytest.mark.parametrize("acc,msk,act", [(True, False, 0), (False, True, 0), (True, True, 0),
-                                         (True, False, 1)])
+                                         (False, False, 1), (False, False, 0)])
 def test_stream3_load_epilogue(dev, shape, acc, msk, act, monkeypatch):
     """dgrad epilogues: accumulate into y (identity-shortcut grad), relu
-    backward mask (VGG conv1_2 dgrad), both."""
+    backward mask (VGG conv1_2 dgrad), both; plain and ReLU without bias."""
     import roadrestore as rr
     from roadrestore._lib import RR_CONV3X3
     monkeypatch.setenv("RR_STREAM3", "1")
@@ -109,7 +112,7 @@ def test_stream3_load_epilogue(dev, shape, acc, msk, act, monkeypatch):
     assert rel(nchw(y), ref) < 4e-3
 
 
-@pytest.mark.parametrize("shape", [(8, 64, 64), (9, 64, 64), (41, 32, 32)])
+@pytest.mark.parametrize("shape", [(16, 64, 64), (17, 64, 64), (81, 32, 32)])
 def test_stream3_bnbwd(dev, shape, monkeypatch):
     """conv dgrad + BN/PReLU backward reduce fused in the streaming epilogue
     == the tiled kernel's fused path == the unfused sequence."""
