@@ -128,10 +128,13 @@ __device__ __forceinline__ f32x4 lds_read_4(const float *p) {
   asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(a) : "memory");
   return r;
 }
+// (early-clobber outputs: the first read's destination must not be the
+// second read's address register -- the LDS queue can hold the second read
+// past the first one's data return)
 __device__ __forceinline__ void lds_read_2x4(const float *p, f32x4 &lo, f32x4 &hi) {
   const uint32_t a = (uint32_t)(uintptr_t)p;
   asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
-               : "=v"(lo), "=v"(hi) : "v"(a) : "memory");
+               : "=&v"(lo), "=&v"(hi) : "v"(a) : "memory");
 }
 __device__ __forceinline__ f32x4 unpack4(u64 v) {
   const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
@@ -149,7 +152,7 @@ struct Cur {
   int kind, n, y0, c;   // virtual step: pre-load, or compute of output rows [y0, y0 + RPS) of image n
 };
 
-template <int W, int MP, int F>
+template <int W, int MP, int F, int STAG>
 __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
   using G = S3Geo<W, MP>;
   constexpr int RPS = G::RPS, ROWB = G::ROWB, RING = G::RING, D = G::D;
@@ -350,7 +353,6 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
       if constexpr ((F & F_BIAS) != 0) bia = lds_read_4(coef + c);
 #pragma unroll
       for (int ni = 0; ni < MP; ++ni) {
-        const long long ub = (pix0 + q0 * W + x0 + ni * 16) * 128 + mi * 32;     // uniform
         f32x4 g = acc[mi][ni];
         if constexpr (BNBWD) {
           const f32x4 t = unpack4(ev0[mi][ni]);
@@ -439,19 +441,40 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     lslot = lslot >= RING ? lslot - RING : lslot;
   }
   int cslot = RING - 2;                         // ring slot of the compute step's row y0 - 1
+  // Stagger: waves w and w + 4 share a SIMD.  The "late" half runs the
+  // epilogue of step v - 1 right after the barrier of step v and then the
+  // MFMAs of step v, while the early half runs MFMAs then epilogue of step v:
+  // on every SIMD one wave's epilogue / DMA issue / loop control overlaps
+  // the other's MFMAs, with one barrier per step and no extra registers
+  // (acc of v - 1 is consumed before the MFMAs of v overwrite it).
+  const bool late = STAG && wv >= 4;
+  // vmcnt accounting, ops younger than DMA(v) (issued in iteration v - D):
+  //   early, iteration u: E(u) DMA(u+D) S(u)
+  //     -> (D-1) M + S c(v-D) + (E+S) sum_{v-D<u<v} c(u)
+  //   late, iteration u: S(u-1) E(u) DMA(u+D)
+  //     -> (D-1) M + S sum_{v-D<=u<=v-2} c(u) + E sum_{v-D<u<v} c(u)
   unsigned hist = 0;                            // bit j: iteration v-1-j computed
-  constexpr int YSS = (D - 1) * DMAW + S + (E + S) * (D - 1);     // steady state
   constexpr unsigned FULL = (1u << D) - 1;
+  constexpr int YE = (D - 1) * DMAW + S + (E + S) * (D - 1);      // steady state, early
+  constexpr int YL = (D - 1) * DMAW + S * (D - 1) + E * (D - 1);  // steady state, late
+  long long ppix = 0;                           // late half: the step whose epilogue is pending
+  bool pcomp = false;
 #pragma unroll 1
   while (cp.c < cend) {
     if ((hist & FULL) == FULL) {
-      wait_vm_barrier_c<YSS < 63 ? YSS : 63>();
+      if (late) wait_vm_barrier_c<YL < 63 ? YL : 63>();
+      else wait_vm_barrier_c<YE < 63 ? YE : 63>();
     } else {
-      wait_vm_barrier((D - 1) * DMAW + (((hist >> (D - 1)) & 1) ? S : 0) +
-                      (E + S) * __builtin_popcount(hist & ((1u << (D - 1)) - 1)));
+      const unsigned inner = hist & ((1u << (D - 1)) - 1);          // c(v-1) .. c(v-D+1)
+      const int y = late ? (D - 1) * DMAW + S * __builtin_popcount((hist >> 1) & ((1u << (D - 1)) - 1)) +
+                               E * __builtin_popcount(inner)
+                         : (D - 1) * DMAW + (((hist >> (D - 1)) & 1) ? S : 0) +
+                               (E + S) * __builtin_popcount(inner);
+      wait_vm_barrier(y);
     }
     const bool comp = cp.kind == S3_COMP;
     const long long pix0 = (long long)(cp.n * H + cp.y0) * W;
+    if (late && pcomp) epilogue(ppix);          // its loads were waited for last iteration
     // epilogue loads BEFORE this iteration's DMA (see the vmcnt accounting)
     if constexpr (NE > 0) {
       if (comp) load_e(pix0);
@@ -464,14 +487,21 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     __builtin_amdgcn_sched_barrier(0);
     if (comp) {
       mfma_step(cslot);
+      // wait for the epilogue loads in the iteration that issued them: the
+      // compiler does not know the asm loads are asynchronous, so their
+      // registers must not be live across the loop back-edge (it may copy
+      // them there before the data has landed)
       wait_e();
-      epilogue(pix0);
+      if (!late) epilogue(pix0);
     }
+    ppix = pix0;
+    pcomp = comp;
     cslot += RPS;
     cslot = cslot >= RING ? cslot - RING : cslot;
     hist = (hist << 1) | (comp ? 1u : 0u);
     advance(cp);
   }
+  if (late && pcomp) epilogue(ppix);            // the late half's last epilogue
   // drain the ring's trailing (dummy) DMA before the LDS is reused / released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -549,7 +579,11 @@ int s3_flags(const rr_igemm_desc *d, bool bnbwd) {
 
 template <int W, int MP, int F>
 void launch1(const S3Args &a, int P, hipStream_t st) {
-  hipLaunchKernelGGL((stream3_kernel<W, MP, F>), dim3(S3_WG), dim3(512), 0, st, a, P / (64 * MP));
+  // the late-epilogue stagger measured faster only for 256-pixel steps
+  // without the BN-statistics registers (it keeps acc live across the loop
+  // back-edge: the stats variants spill with it)
+  constexpr int STAG = (MP == 4 && !(F & F_STATS)) ? 1 : 0;
+  hipLaunchKernelGGL((stream3_kernel<W, MP, F, STAG>), dim3(S3_WG), dim3(512), 0, st, a, P / (64 * MP));
 }
 
 template <int W>

@@ -15,6 +15,7 @@ dev = torch.device("cuda:0")
 B = int(os.environ.get("B", 512))
 reps = int(os.environ.get("REPS", 20))
 variants = os.environ.get("VARIANTS", "1,0").split(",")
+varenv = os.environ.get("VARENV", "RR_STREAM3")     # the env switch the variants set
 only = os.environ.get("CASE")          # e.g. "64:fwd+stats"
 rounds = int(os.environ.get("ROUNDS", 2))
 
@@ -51,6 +52,7 @@ for H in ((64, 32) if not only else (int(only.split(":")[0]),)):
     fl = 2.0 * P * 64 * 576
     cases = {
         "fwd+stats": (lambda: ops.igemm(RR_CONV3X3, x, None, B, H, H, wf, 64, bias=b, stats=True), 2),
+        "fwd+relu": (lambda: ops.igemm(RR_CONV3X3, x, None, B, H, H, wf, 64, bias=b, act=1), 2),
         "dgrad+acc": (lambda: ops.igemm(RR_CONV3X3, x, None, B, H, H, wd, 64, out=y0, accumulate=True), 3),
         "bnbwd": (lambda: ops.igemm_bnbwd(RR_CONV3X3, x, B, H, H, wd, 64, t1, mean, inv, s1, sh1, al), 3),
     }
@@ -59,12 +61,12 @@ for H in ((64, 32) if not only else (int(only.split(":")[0]),)):
             if only and name != only.split(":")[1]:
                 continue
             for v in variants:
-                os.environ["RR_STREAM3"] = v
+                os.environ[varenv] = v
                 ms = timeit(fn)
                 res.setdefault((H, name, v), []).append(ms)
 for (H, name, v), ms in res.items():
     m = min(ms)
     P = B * H * H
-    passes = 2 if name == "fwd+stats" else 3
-    print(f"W={H:2d} {name:10s} stream3={v}: {m * 1e3:7.1f} us  {2.0 * P * 64 * 576 / m / 1e9:7.1f} TF/s "
+    passes = 2 if name.startswith("fwd") else 3
+    print(f"W={H:2d} {name:10s} {varenv}={v}: {m * 1e3:7.1f} us  {2.0 * P * 64 * 576 / m / 1e9:7.1f} TF/s "
           f" {passes * P * 128 / m / 1e6:7.1f} GB/s")
