@@ -1,0 +1,25 @@
+// swgrad.h -- internal interface of the row-streaming 3x3 weight gradient
+// (swgrad.hip), called from rr_wgrad (wgrad.hip).  Not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/roadrestore.h"
+
+struct SWArgs {
+  const char *dy;            // NHWC bf16 [n][h][w][64]
+  const char *x1, *x2;       // NHWC bf16 [n][h][w][c1], [n][h][w][c2] (concat input)
+  int c1, c2;
+  float *partial;            // [nwg_ps][64][9][c1 + c2] partial dW slabs
+  int n, h;                  // w is the template width
+  int nwg_ps;                // workgroups per 64-channel input slice
+  int nsteps;                // 128-pixel steps (n h w / 128)
+  unsigned long long *ts;    // debug phase timestamps [nwg][4] or null
+};
+
+// nonzero when the descriptor is handled by the streaming kernel
+int swgrad_ok(const rr_wgrad_desc *d);
+// number of [64][9][c_in1 + c_in2] fp32 partial slabs the kernel writes
+int swgrad_nsplit(const rr_wgrad_desc *d);
+// launches the streaming kernel into ws (the caller reduces the slabs)
+int swgrad_launch(const rr_wgrad_desc *d, const void *dy, const void *x1, const void *x2, void *ws,
+                  hipStream_t st);

@@ -22,6 +22,7 @@
 //   bf16: two ds_read_b64_tr_b16 per fragment (4 pixels each), 16x16x32 MFMA
 //   f32 : ds_read_b32 per fragment, 16x16x4 f32 MFMA (exact fp32)
 #include "common.h"
+#include "swgrad.h"
 
 #include <cstdlib>
 
@@ -604,6 +605,8 @@ static HaloPlan halo_plan(const rr_wgrad_desc *d) {
 
 extern "C" size_t rr_wgrad_workspace(const rr_wgrad_desc *d) {
   if (!d) return 0;
+  if (swgrad_ok(d))
+    return (size_t)swgrad_nsplit(d) * d->c_out * 9 * (d->c_in1 + d->c_in2) * sizeof(float);
   if (halo_ok(d)) {
     const HaloPlan hp = halo_plan(d);
     return (size_t)hp.nsplit * d->c_out * 9 * (d->c_in1 + d->c_in2) * sizeof(float);
@@ -641,6 +644,14 @@ extern "C" int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
   a.fd_w = make_fastdiv((uint32_t)d->w);
   a.fd_hw = make_fastdiv((uint32_t)(d->h * d->w));
   hipStream_t st = (hipStream_t)stream;
+  if (swgrad_ok(d)) {
+    const int rc = swgrad_launch(d, dy, x1, x2, ws, st);
+    if (rc) return rc;
+    launch_reduce((const float *)ws, dw, d->c_out, d->c_in1 + d->c_in2, 9, swgrad_nsplit(d),
+                  d->accumulate, st);
+    RR_CHECK_LAUNCH();
+    return RR_OK;
+  }
   if (halo_ok(d)) {
     const HaloPlan hp = halo_plan(d);
     Halo3Args ha;

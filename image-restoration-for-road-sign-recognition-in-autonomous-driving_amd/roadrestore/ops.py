@@ -94,6 +94,17 @@ def _kstream3(mode, dt, n, h, w, c1, c2, cout, split, out_nchw):
     return h % (256 // w) == 0 and n * h * w >= 65536
 
 
+def _kswgrad(mode, dt, n, h, w, c1, c2, cout):
+    """Mirror of csrc/swgrad.hip swgrad_ok (probe naming only)."""
+    if os.environ.get("RR_SWGRAD", "1") in ("0",):
+        return False
+    if dt != torch.bfloat16 or mode != RR_CONV3X3 or cout != 64 or w not in (32, 64):
+        return False
+    if c1 <= 0 or c1 % 64 or c2 % 64 or c1 + c2 > 192 or h % (128 // w):
+        return False
+    return n * h * w >= 128 * 256
+
+
 def _ws(nbytes, device):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
@@ -206,6 +217,8 @@ def wgrad(mode, dy, x1, x2, n, h, w, cout, dw=None, accumulate=False, dw_shape=N
         ba = 128 if CA % 128 == 0 else 64
         bb = 128 if (CB % 128 == 0 and (cout if convT else c1) % 128 == 0 and c2 % 128 == 0) else 64
         sym = f"wgrad_kernel<{'bf16' if dy.dtype == torch.bfloat16 else 'f32'},{ba},{bb},mode{mode}>"
+        if _kswgrad(mode, dy.dtype, n, h, w, c1, c2, cout):
+            sym = f"swgrad_kernel<{w}>"
         PROBE(sym, 2.0 * CA * CB * taps * n * h * w, launch,
               f"wgrad m{mode} {n}x{h}x{w} c{c1}+{c2}->{cout}")
     return dw

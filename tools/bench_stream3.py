@@ -48,12 +48,14 @@ for H in ((64, 32) if not only else (int(only.split(":")[0]),)):
     s1 = torch.ones(64, device=dev)
     sh1 = torch.zeros(64, device=dev)
     al = torch.tensor([0.25], device=dev)
+    dwb = torch.empty(64, 64, 3, 3, device=dev)
     P = B * H * H
     fl = 2.0 * P * 64 * 576
     cases = {
         "fwd+stats": (lambda: ops.igemm(RR_CONV3X3, x, None, B, H, H, wf, 64, bias=b, stats=True), 2),
         "fwd+relu": (lambda: ops.igemm(RR_CONV3X3, x, None, B, H, H, wf, 64, bias=b, act=1), 2),
         "dgrad+acc": (lambda: ops.igemm(RR_CONV3X3, x, None, B, H, H, wd, 64, out=y0, accumulate=True), 3),
+        "wgrad": (lambda: ops.wgrad(RR_CONV3X3, y0, x, None, B, H, H, 64, dw=dwb), 2),
         "bnbwd": (lambda: ops.igemm_bnbwd(RR_CONV3X3, x, B, H, H, wd, 64, t1, mean, inv, s1, sh1, al), 3),
     }
     for _ in range(rounds):                  # interleaved rounds (rule 24)
@@ -67,6 +69,6 @@ for H in ((64, 32) if not only else (int(only.split(":")[0]),)):
 for (H, name, v), ms in res.items():
     m = min(ms)
     P = B * H * H
-    passes = 2 if name.startswith("fwd") else 3
+    passes = 2 if name.startswith("fwd") or name == "wgrad" else 3
     print(f"W={H:2d} {name:10s} {varenv}={v}: {m * 1e3:7.1f} us  {2.0 * P * 64 * 576 / m / 1e9:7.1f} TF/s "
           f" {passes * P * 128 / m / 1e6:7.1f} GB/s")
