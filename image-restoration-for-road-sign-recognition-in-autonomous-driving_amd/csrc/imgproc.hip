@@ -1,0 +1,527 @@
+// imgproc.hip -- the image I/O either side of the networks (SURVEY §8f rows 2
+// and 4), on device:
+//
+//   * rr_resize_bilinear_u8: torchvision Resize((oh, ow)) on a PIL image, i.e.
+//     PIL Image.resize(BILINEAR) (17:66, 18:28-32), bit-exact: PIL's separable
+//     two-pass resample with antialiasing support (filter support scaled by
+//     the downscale factor), coefficients normalised in double and rounded to
+//     22-bit fixed point, an 8-bit clip after each pass.  Optionally fused with
+//     ToTensor (x / 255 in fp32) and Normalize ((x - mean) / std in fp32, 18:31)
+//     into an NCHW fp32 batch.
+//   * rr_ssim_u8: skimage structural_similarity(a, b, data_range=255,
+//     channel_axis=2) (08:125): 7x7 uniform window, sample covariance
+//     (49/48), K1 = .01, K2 = .03, mean of S over the interior (3-pixel border
+//     cropped), mean over channels, fp64.
+//
+// Both are HBM-bound byte work: no MFMA, one thread per output pixel (resize)
+// or per output column (SSIM), coalesced along the innermost NHWC axis.
+#include "common.h"
+
+#include <cmath>
+
+namespace {
+
+// ---------------------------------------------------------------- resize ----
+constexpr int RS_PREC = 22;        // PIL PRECISION_BITS = 32 - 8 - 2
+constexpr int RS_MAXK = 255;       // taps per output (downscale up to 127x)
+
+struct RsAxis {
+  int in_size, out_size, ksize;
+  int *bounds;                     // [out][2]: first tap, tap count
+  int *kk;                         // [out][ksize] fixed-point coefficients
+};
+
+// PIL precompute_coeffs + normalize_coeffs_8bpc (Resample.c), evaluated in
+// the same double operations in the same order; contraction into FMA would
+// change the rounding, so it is off for this function.
+__device__ void rs_coeffs_one(const RsAxis &ax, int xx) {
+#pragma clang fp contract(off)
+  const double scale = (double)ax.in_size / ax.out_size;
+  const double filterscale = scale < 1.0 ? 1.0 : scale;
+  const double support = 1.0 * filterscale;                  // bilinear support 1.0
+  const double center = 0.0 + (xx + 0.5) * scale;
+  const double ss = 1.0 / filterscale;
+  int xmin = (int)(center - support + 0.5);
+  if (xmin < 0) xmin = 0;
+  int xmax = (int)(center + support + 0.5);
+  if (xmax > ax.in_size) xmax = ax.in_size;
+  xmax -= xmin;
+  // the filter value of tap x (evaluated twice: sum first, then normalise --
+  // the same doubles both times, and no private array in scratch)
+  auto tap = [&](int x) {
+    double t = ((double)(x + xmin) - center + 0.5) * ss;
+    t = t < 0.0 ? -t : t;
+    return t < 1.0 ? 1.0 - t : 0.0;
+  };
+  double ww = 0.0;
+  for (int x = 0; x < xmax; ++x) ww += tap(x);
+  int *o = ax.kk + (long long)xx * ax.ksize;
+  for (int x = 0; x < ax.ksize; ++x) {
+    double v = 0.0;
+    if (x < xmax) v = ww != 0.0 ? tap(x) / ww : tap(x);
+    o[x] = v < 0 ? (int)(-0.5 + v * (double)(1 << RS_PREC)) : (int)(0.5 + v * (double)(1 << RS_PREC));
+  }
+  ax.bounds[2 * xx] = xmin;
+  ax.bounds[2 * xx + 1] = xmax;
+}
+
+__global__ void rs_coeffs_kernel(RsAxis h, RsAxis v) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < h.out_size) rs_coeffs_one(h, i);
+  else if (i < h.out_size + v.out_size) rs_coeffs_one(v, i - h.out_size);
+}
+
+__device__ __forceinline__ int rs_clip8(int s) {          // PIL clip8: lookups[s >> 22]
+  const int v = s >> RS_PREC;
+  return v < 0 ? 0 : (v > 255 ? 255 : v);
+}
+
+// horizontal pass over source rows [y_first, y_first + rows): [n][h][w][C] ->
+// tmp [n][rows][ow][C]
+template <int C>
+__global__ void rs_horiz_kernel(int n, int h, int w, int ow, int y_first, int rows, int ksize,
+                                const int *__restrict__ bounds, const int *__restrict__ kk,
+                                const uint8_t *__restrict__ in, uint8_t *__restrict__ tmp) {
+  const long long total = (long long)n * rows * ow;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int ox = (int)(i % ow);
+    const long long r = i / ow;                    // n * rows + row
+    const int img = (int)(r / rows), y = (int)(r % rows) + y_first;
+    const int xmin = bounds[2 * ox], xcnt = bounds[2 * ox + 1];
+    const int *k = kk + (long long)ox * ksize;
+    const uint8_t *src = in + (((long long)img * h + y) * w + xmin) * C;
+    int s[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) s[c] = 1 << (RS_PREC - 1);
+    for (int x = 0; x < xcnt; ++x) {
+      const int kx = k[x];
+#pragma unroll
+      for (int c = 0; c < C; ++c) s[c] += (int)src[x * C + c] * kx;
+    }
+    uint8_t *dst = tmp + i * C;
+#pragma unroll
+    for (int c = 0; c < C; ++c) dst[c] = (uint8_t)rs_clip8(s[c]);
+  }
+}
+
+struct RsNorm { float mean[4], std[4]; };
+
+// vertical pass: tmp [n][rows][ow][C] -> u8 [n][oh][ow][C] (MODE 0) or fp32
+// NCHW ToTensor (+ Normalize) (MODE 1)
+template <int C, int MODE>
+__global__ void rs_vert_kernel(int n, int rows, int oh, int ow, int ksize, int y_first,
+                               const int *__restrict__ bounds, const int *__restrict__ kk,
+                               const uint8_t *__restrict__ tmp, void *__restrict__ out, RsNorm nm,
+                               int normalize) {
+  const long long total = (long long)n * oh * ow;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int ox = (int)(i % ow);
+    const long long r = i / ow;
+    const int img = (int)(r / oh), oy = (int)(r % oh);
+    const int ymin = bounds[2 * oy] - y_first, ycnt = bounds[2 * oy + 1];
+    const int *k = kk + (long long)oy * ksize;
+    const uint8_t *src = tmp + (((long long)img * rows + ymin) * ow + ox) * C;
+    int s[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) s[c] = 1 << (RS_PREC - 1);
+    for (int y = 0; y < ycnt; ++y) {
+      const int ky = k[y];
+#pragma unroll
+      for (int c = 0; c < C; ++c) s[c] += (int)src[(long long)y * ow * C + c] * ky;
+    }
+    if constexpr (MODE == 0) {
+      uint8_t *dst = (uint8_t *)out + i * C;
+#pragma unroll
+      for (int c = 0; c < C; ++c) dst[c] = (uint8_t)rs_clip8(s[c]);
+    } else {
+      float *dst = (float *)out;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        float v = (float)rs_clip8(s[c]) / 255.0f;                 // ToTensor: .div(255)
+        if (normalize) v = (v - nm.mean[c]) / nm.std[c];          // Normalize: sub_, div_
+        dst[(((long long)img * C + c) * oh + oy) * ow + ox] = v;
+      }
+    }
+  }
+}
+
+struct RsPlan {
+  int kh, kv, y_first, rows;
+  size_t off_bh, off_kh, off_bv, off_kv, off_tmp, total;
+};
+
+// host mirror of the bound computation for the rows the vertical pass reads
+// (PIL ybox_first / ybox_last); same double expressions as rs_coeffs_one
+static void rs_vbox(int in_size, int out_size, int *first, int *last) {
+  const double scale = (double)in_size / out_size;
+  const double support = scale < 1.0 ? 1.0 : scale;
+  auto lo = [&](int yy) {
+    const double c = 0.0 + (yy + 0.5) * scale;
+    int a = (int)(c - support + 0.5);
+    return a < 0 ? 0 : a;
+  };
+  auto hi = [&](int yy) {
+    const double c = 0.0 + (yy + 0.5) * scale;
+    int b = (int)(c + support + 0.5);
+    return b > in_size ? in_size : b;
+  };
+  *first = lo(0);
+  *last = hi(out_size - 1);   // bounds[last] start + count = clamped xmax
+}
+
+static int rs_ksize(int in_size, int out_size) {
+  const double scale = (double)in_size / out_size;
+  const double support = scale < 1.0 ? 1.0 : scale;
+  return (int)std::ceil(support) * 2 + 1;
+}
+
+static bool rs_plan(int n, int h, int w, int c, int oh, int ow, RsPlan *p) {
+  if (n <= 0 || h <= 0 || w <= 0 || oh <= 0 || ow <= 0 || c < 1 || c > 4) return false;
+  p->kh = rs_ksize(w, ow);
+  p->kv = rs_ksize(h, oh);
+  if (p->kh > RS_MAXK || p->kv > RS_MAXK) return false;
+  int f, l;
+  rs_vbox(h, oh, &f, &l);
+  p->y_first = f;
+  p->rows = l - f;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t o = 0;
+  p->off_bh = o; o = al(o + (size_t)ow * 2 * 4);
+  p->off_kh = o; o = al(o + (size_t)ow * p->kh * 4);
+  p->off_bv = o; o = al(o + (size_t)oh * 2 * 4);
+  p->off_kv = o; o = al(o + (size_t)oh * p->kv * 4);
+  p->off_tmp = o; o = al(o + (size_t)n * p->rows * ow * c);
+  p->total = o;
+  return true;
+}
+
+// ------------------------------------------------------------------ SSIM ----
+constexpr int SS_T = 256;
+
+// one workgroup per (image, channel): thread = output column, sliding 7-row
+// window of exact integer 7x7 sums (x, y, x^2, y^2, xy); S in fp64; fixed-order
+// reduction -> per-(image, channel) mean of S over the cropped interior
+__global__ __launch_bounds__(SS_T) void ssim_kernel(int h, int w, int C, const uint8_t *__restrict__ a,
+                                                    const uint8_t *__restrict__ b,
+                                                    double *__restrict__ chan_mean) {
+  const int img = blockIdx.x / C, ch = blockIdx.x % C;
+  const uint8_t *pa = a + (long long)img * h * w * C + ch;
+  const uint8_t *pb = b + (long long)img * h * w * C + ch;
+  const double C1 = (0.01 * 255.0) * (0.01 * 255.0), C2 = (0.03 * 255.0) * (0.03 * 255.0);
+  const double cov_norm = 49.0 / 48.0;
+  double acc = 0.0;
+  for (int cx = 3 + threadIdx.x; cx < w - 3; cx += SS_T) {
+    auto hsum = [&](int y, int &sx, int &sy, int &sxx, int &syy, int &sxy) {
+      sx = sy = sxx = syy = sxy = 0;
+      const long long base = ((long long)y * w + cx - 3) * C;
+#pragma unroll
+      for (int d = 0; d < 7; ++d) {
+        const int x = pa[base + d * C], y2 = pb[base + d * C];
+        sx += x; sy += y2; sxx += x * x; syy += y2 * y2; sxy += x * y2;
+      }
+    };
+    int vx = 0, vy = 0, vxx = 0, vyy = 0, vxy = 0;
+    for (int y = 0; y < h; ++y) {
+      int sx, sy, sxx, syy, sxy;
+      hsum(y, sx, sy, sxx, syy, sxy);
+      vx += sx; vy += sy; vxx += sxx; vyy += syy; vxy += sxy;
+      if (y >= 7) {
+        hsum(y - 7, sx, sy, sxx, syy, sxy);
+        vx -= sx; vy -= sy; vxx -= sxx; vyy -= syy; vxy -= sxy;
+      }
+      if (y >= 6) {
+        const double ux = vx / 49.0, uy = vy / 49.0;
+        const double uxx = vxx / 49.0, uyy = vyy / 49.0, uxy = vxy / 49.0;
+        const double sxv = cov_norm * (uxx - ux * ux);
+        const double syv = cov_norm * (uyy - uy * uy);
+        const double sxyv = cov_norm * (uxy - ux * uy);
+        const double A1 = 2 * ux * uy + C1, A2 = 2 * sxyv + C2;
+        const double B1 = ux * ux + uy * uy + C1, B2 = sxv + syv + C2;
+        acc += (A1 * A2) / (B1 * B2);
+      }
+    }
+  }
+  __shared__ double red[SS_T];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = SS_T / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) chan_mean[blockIdx.x] = red[0] / ((double)(h - 6) * (w - 6));
+}
+
+__global__ void ssim_chan_mean_kernel(int n, int C, const double *__restrict__ chan_mean,
+                                      double *__restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double s = 0.0;
+  for (int c = 0; c < C; ++c) s += chan_mean[(long long)i * C + c];
+  out[i] = s / C;
+}
+
+}  // namespace
+
+extern "C" size_t rr_resize_workspace(int n, int h, int w, int c, int oh, int ow) {
+  RsPlan p;
+  return rs_plan(n, h, w, c, oh, ow, &p) ? p.total : 0;
+}
+
+extern "C" int rr_resize_bilinear_u8(int n, int h, int w, int c, int oh, int ow, const uint8_t *in,
+                                     int out_kind, const float *mean, const float *std, void *out,
+                                     void *ws, size_t ws_bytes, rr_stream stream) {
+  RsPlan p;
+  if (!in || !out || !ws || (out_kind != 0 && out_kind != 1)) return RR_EINVAL;
+  if (!rs_plan(n, h, w, c, oh, ow, &p)) return RR_EUNSUPPORTED;
+  if (ws_bytes < p.total) return RR_EWORKSPACE;
+  if ((mean == nullptr) != (std == nullptr) || (mean && out_kind != 1)) return RR_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  char *base = (char *)ws;
+  RsAxis ah{w, ow, p.kh, (int *)(base + p.off_bh), (int *)(base + p.off_kh)};
+  RsAxis av{h, oh, p.kv, (int *)(base + p.off_bv), (int *)(base + p.off_kv)};
+  hipLaunchKernelGGL(rs_coeffs_kernel, dim3((ow + oh + 63) / 64), dim3(64), 0, st, ah, av);
+  RR_CHECK_LAUNCH();
+  uint8_t *tmp = (uint8_t *)(base + p.off_tmp);
+  const long long th = (long long)n * p.rows * ow, tv = (long long)n * oh * ow;
+  const dim3 gh(rr_grid_cap((th + 255) / 256, 8192)), gv(rr_grid_cap((tv + 255) / 256, 8192)), b(256);
+  RsNorm nm{};
+  for (int i = 0; i < c; ++i) {
+    nm.mean[i] = mean ? mean[i] : 0.f;
+    nm.std[i] = std ? std[i] : 1.f;
+  }
+  const int norm = mean != nullptr;
+#define RS_LAUNCH(CC)                                                                              \
+  hipLaunchKernelGGL(rs_horiz_kernel<CC>, gh, b, 0, st, n, h, w, ow, p.y_first, p.rows, p.kh,    \
+                     ah.bounds, ah.kk, in, tmp);                                                   \
+  if (out_kind == 0)                                                                               \
+    hipLaunchKernelGGL((rs_vert_kernel<CC, 0>), gv, b, 0, st, n, p.rows, oh, ow, p.kv, p.y_first, \
+                       av.bounds, av.kk, tmp, out, nm, norm);                                      \
+  else                                                                                             \
+    hipLaunchKernelGGL((rs_vert_kernel<CC, 1>), gv, b, 0, st, n, p.rows, oh, ow, p.kv, p.y_first, \
+                       av.bounds, av.kk, tmp, out, nm, norm);
+  switch (c) {
+    case 1: RS_LAUNCH(1) break;
+    case 2: RS_LAUNCH(2) break;
+    case 3: RS_LAUNCH(3) break;
+    default: RS_LAUNCH(4) break;
+  }
+#undef RS_LAUNCH
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" size_t rr_ssim_workspace(int n, int c) {
+  return n > 0 && c > 0 ? (size_t)n * c * sizeof(double) : 0;
+}
+
+extern "C" int rr_ssim_u8(int n, int h, int w, int c, const uint8_t *a, const uint8_t *b, double *out,
+                          void *ws, size_t ws_bytes, rr_stream stream) {
+  if (!a || !b || !out || !ws || n <= 0 || c <= 0) return RR_EINVAL;
+  if (h < 7 || w < 7) return RR_EINVAL;                     // skimage: win_size > image side
+  if (ws_bytes < rr_ssim_workspace(n, c)) return RR_EWORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  double *cm = (double *)ws;
+  hipLaunchKernelGGL(ssim_kernel, dim3(n * c), dim3(SS_T), 0, st, h, w, c, a, b, cm);
+  RR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(ssim_chan_mean_kernel, dim3((n + 255) / 256), dim3(256), 0, st, n, c, cm, out);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+// ------------------------------------------------------------ distortion ----
+// The dynamic distortion generator 14:31-64 (fog -> noise -> motion blur, each
+// drawn per image) and the fixed compound variant 16:14-37 (blur -> fog ->
+// noise), per image on device, with the reference's numpy dtype semantics:
+//   img / 255 in fp32; fog out * f32(t) + f32(A (1 - t)) in fp32; noise added
+//   in fp64 (np.random.normal is float64, so the image becomes float64);
+//   clip(x * 255, 0, 255).astype(uint8) truncates; cv2.filter2D on uint8 with
+//   the fp32-converted kernel: fp32 sum over the taps in row-major order,
+//   BORDER_REFLECT_101, anchor (k / 2, k / 2), round half to even, saturate.
+// Noise: the caller's fp64 field (parity runs) or Philox4x32-10 normals
+// (Box-Muller in fp64) keyed by (seed, element index).
+
+struct DistCfg {
+  int n, h, w, c, mode;                 // mode 0: 14:31-64 order, 1: 16:14-37 order
+  const uint8_t *in;
+  uint8_t *out, *tmp;
+  const rr_distort_param *prm;
+  const float *taps;                    // [n][RR_DISTORT_KMAX^2], row-major
+  const double *noise;                  // [n][h][w][c] or null -> Philox
+  unsigned long long seed;
+};
+
+__device__ __forceinline__ void philox_round(uint32_t &c0, uint32_t &c1, uint32_t &c2, uint32_t &c3,
+                                             uint32_t k0, uint32_t k1) {
+  const unsigned long long p0 = (unsigned long long)0xD2511F53u * c0;
+  const unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c2;
+  const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0;
+  const uint32_t h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+  const uint32_t n0 = h1 ^ c1 ^ k0, n2 = h0 ^ c3 ^ k1;
+  c0 = n0; c1 = l1; c2 = n2; c3 = l0;
+}
+
+// standard normal for element e (Philox4x32-10, 2 x 53-bit uniforms, Box-Muller)
+__device__ double philox_normal(unsigned long long seed, unsigned long long e) {
+  uint32_t c0 = (uint32_t)e, c1 = (uint32_t)(e >> 32), c2 = 0x9E3779B9u, c3 = 0;
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    philox_round(c0, c1, c2, c3, k0, k1);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  const double u1 = ((((unsigned long long)c0 << 21) ^ c1) & ((1ull << 53) - 1)) * 0x1p-53 + 0x1p-54;
+  const double u2 = ((((unsigned long long)c2 << 21) ^ c3) & ((1ull << 53) - 1)) * 0x1p-53;
+  return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+}
+
+__device__ __forceinline__ uint8_t trunc_u8(double v) {    // np.clip(v, 0, 255).astype(uint8)
+  v = v < 0.0 ? 0.0 : (v > 255.0 ? 255.0 : v);
+  return (uint8_t)(int)v;
+}
+__device__ __forceinline__ uint8_t trunc_u8f(float v) {
+  v = v < 0.f ? 0.f : (v > 255.f ? 255.f : v);
+  return (uint8_t)(int)v;
+}
+
+// fog then noise on x = img / 255 (fp32); returns clip(x * 255).astype(u8)
+// in the dtype the reference holds at that point
+__device__ __forceinline__ uint8_t fog_noise(const DistCfg &a, const rr_distort_param &p, float x,
+                                             long long e) {
+#pragma clang fp contract(off)
+  if (p.flags & RR_DISTORT_FOG) x = x * p.fog_mul + p.fog_add;
+  if (p.flags & RR_DISTORT_NOISE) {
+    const double nz = a.noise ? a.noise[e] : p.sigma * philox_normal(a.seed, (unsigned long long)e);
+    return trunc_u8(((double)x + nz) * 255.0);
+  }
+  return trunc_u8f(x * 255.f);
+}
+
+__device__ __forceinline__ int reflect101(int p, int len) {
+  if (len == 1) return 0;
+  while ((unsigned)p >= (unsigned)len) p = p < 0 ? -p : 2 * len - 2 - p;
+  return p;
+}
+
+// stage 1 (per element): mode 0: fog/noise -> u8 (the blur input, or the
+// output if no blur); mode 1: (img / 255 * 255).astype(u8), the blur input
+__global__ void distort_pre_kernel(DistCfg a) {
+#pragma clang fp contract(off)
+  const long long per = (long long)a.h * a.w * a.c, total = per * a.n;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int img = (int)(e / per);
+    const rr_distort_param p = a.prm[img];
+    const float x = (float)a.in[e] / 255.0f;
+    const bool blur = p.flags & RR_DISTORT_BLUR;
+    uint8_t v;
+    if (a.mode == 0) v = fog_noise(a, p, x, e);
+    else v = trunc_u8f(x * 255.f);
+    if (blur) a.tmp[e] = v;
+    else if (a.mode == 0) a.out[e] = v;
+    else a.out[e] = fog_noise(a, p, (float)v / 255.0f, e);
+  }
+}
+
+// stage 2 (blurred images only): filter2D of tmp, then mode 0: the u8 result
+// ((t / 255) * 255 truncated), mode 1: fog + noise on it
+__global__ void distort_blur_kernel(DistCfg a) {
+#pragma clang fp contract(off)
+  const long long hw = (long long)a.h * a.w, total = hw * a.n;
+  for (long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x; q < total;
+       q += (long long)gridDim.x * blockDim.x) {
+    const int img = (int)(q / hw);
+    const rr_distort_param p = a.prm[img];
+    if (!(p.flags & RR_DISTORT_BLUR)) continue;
+    const int rem = (int)(q - (long long)img * hw), y = rem / a.w, x = rem % a.w;
+    const int k = p.ksize, anc = k / 2;
+    const float *kt = a.taps + (long long)img * RR_DISTORT_KMAX * RR_DISTORT_KMAX;
+    const uint8_t *src = a.tmp + (long long)img * hw * a.c;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < k; ++i) {
+      const int yy = reflect101(y + i - anc, a.h);
+      for (int j = 0; j < k; ++j) {
+        const float kv = kt[i * RR_DISTORT_KMAX + j];
+        if (kv == 0.f) continue;                             // cv2 drops zero taps
+        const int xx = reflect101(x + j - anc, a.w);
+        const uint8_t *px = src + ((long long)yy * a.w + xx) * a.c;
+        for (int c = 0; c < a.c; ++c) s[c] = s[c] + kv * (float)px[c];
+      }
+    }
+    for (int c = 0; c < a.c; ++c) {
+      float r = rintf(s[c]);                                 // saturate_cast<uchar>: cvRound
+      r = r < 0.f ? 0.f : (r > 255.f ? 255.f : r);
+      const long long e = q * a.c + c;
+      const float t = (float)(int)r / 255.0f;
+      a.out[e] = a.mode == 0 ? trunc_u8f(t * 255.f) : fog_noise(a, p, t, e);
+    }
+  }
+}
+
+extern "C" size_t rr_distort_workspace(int n, int h, int w, int c) {
+  return n > 0 && h > 0 && w > 0 && c > 0 ? (size_t)n * h * w * c : 0;
+}
+
+extern "C" int rr_distort_u8(int n, int h, int w, int c, int mode, const uint8_t *in, uint8_t *out,
+                             const rr_distort_param *params, const float *taps, const double *noise,
+                             unsigned long long seed, void *ws, size_t ws_bytes, rr_stream stream) {
+  if (!in || !out || !params || !taps || !ws || n <= 0 || h <= 0 || w <= 0) return RR_EINVAL;
+  if (c < 1 || c > 4 || (mode != 0 && mode != 1)) return RR_EINVAL;
+  if (ws_bytes < rr_distort_workspace(n, h, w, c)) return RR_EWORKSPACE;
+  DistCfg a{n, h, w, c, mode, in, out, (uint8_t *)ws, params, taps, noise, seed};
+  hipStream_t st = (hipStream_t)stream;
+  const long long te = (long long)n * h * w * c, tp = (long long)n * h * w;
+  hipLaunchKernelGGL(distort_pre_kernel, dim3(rr_grid_cap((te + 255) / 256, 8192)), dim3(256), 0, st, a);
+  RR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(distort_blur_kernel, dim3(rr_grid_cap((tp + 255) / 256, 8192)), dim3(256), 0, st, a);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+// cv2.getRotationMatrix2D((k / 2, k / 2), angle, 1) + cv2.warpAffine of
+// np.diag(np.ones(k)) (INTER_LINEAR, BORDER_CONSTANT 0, dsize (k, k)) / k,
+// converted to fp32 as filter2D does (14:55-59, 16:20-21).  Host code: the
+// reference builds this kernel on the host per image too; it is <= 225 taps.
+// warpAffine: inverted matrix, 10-bit fixed-point source coordinates rounded
+// half-even, 1/32-pixel interpolation table of fp32 bilinear weights.
+extern "C" int rr_motion_blur_kernel(int k, int angle, float *taps) {
+  if (!taps || k < 1 || k > RR_DISTORT_KMAX) return RR_EINVAL;
+  const double cx = (float)(k / 2.0), cy = cx;
+  const double ang = angle * 3.14159265358979323846 / 180.0;
+  const double alpha = std::cos(ang) * 1.0, beta = std::sin(ang) * 1.0;
+  double M[6] = {alpha, beta, (1 - alpha) * cx - beta * cy, -beta, alpha, beta * cx + (1 - alpha) * cy};
+  double D = M[0] * M[4] - M[1] * M[3];
+  D = D != 0 ? 1. / D : 0;
+  const double A11 = M[4] * D, A22 = M[0] * D;
+  M[0] = A11; M[1] *= -D; M[3] *= -D; M[4] = A22;
+  const double b1 = -M[0] * M[2] - M[1] * M[5], b2 = -M[3] * M[2] - M[4] * M[5];
+  M[2] = b1; M[5] = b2;
+  auto rnd = [](double v) { return (int)std::nearbyint(v); };   // cvRound: half to even
+  float tab1[32][2];
+  for (int i = 0; i < 32; ++i) {
+    const float x = i * (1.f / 32);
+    tab1[i][0] = 1.f - x;
+    tab1[i][1] = x;
+  }
+  for (int y = 0; y < k; ++y)
+    for (int x = 0; x < k; ++x) {
+      const int X0 = rnd((M[1] * y + M[2]) * 1024) + 16, Y0 = rnd((M[4] * y + M[5]) * 1024) + 16;
+      const int X = (X0 + rnd(M[0] * x * 1024)) >> 5, Y = (Y0 + rnd(M[3] * x * 1024)) >> 5;
+      const int sx = X >> 5, sy = Y >> 5, fx = X & 31, fy = Y & 31;
+      const float w[4] = {tab1[fy][0] * tab1[fx][0], tab1[fy][0] * tab1[fx][1],
+                          tab1[fy][1] * tab1[fx][0], tab1[fy][1] * tab1[fx][1]};
+      auto src = [&](int xx, int yy) -> double {               // np.diag(np.ones(k)), 0 outside
+        return xx >= 0 && yy >= 0 && xx < k && yy < k && xx == yy ? 1.0 : 0.0;
+      };
+      double v = 0.0;
+      if (!(sx >= k || sx + 1 < 0 || sy >= k || sy + 1 < 0))
+        v = src(sx, sy) * w[0] + src(sx + 1, sy) * w[1] + src(sx, sy + 1) * w[2] + src(sx + 1, sy + 1) * w[3];
+      taps[y * RR_DISTORT_KMAX + x] = (float)(v / k);
+    }
+  for (int y = 0; y < RR_DISTORT_KMAX; ++y)
+    for (int x = 0; x < RR_DISTORT_KMAX; ++x)
+      if (y >= k || x >= k) taps[y * RR_DISTORT_KMAX + x] = 0.f;
+  return RR_OK;
+}

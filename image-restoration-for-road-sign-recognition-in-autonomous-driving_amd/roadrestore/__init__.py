@@ -7,7 +7,7 @@ Compute runs in hand-written HIP kernels behind a C ABI (include/roadrestore.h,
 libroadrestore.so in this directory); PyTorch supplies device memory, streams
 and torch.distributed (RCCL) only.
 """
-from . import ops  # noqa: F401
+from . import imgproc, ops  # noqa: F401
 from ._lib import EXPORTED, LIB_PATH, lib  # noqa: F401
 from .nn import (AdaptiveAvgPool2d, BatchNorm2d, Conv2d, ConvTranspose2d, Dropout,  # noqa: F401
                  L1Loss, Linear, MaxPool2d, MSELoss, PReLU, ReLU, ResidualBlock, ResUNet,

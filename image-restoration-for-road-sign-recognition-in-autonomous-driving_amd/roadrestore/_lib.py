@@ -35,6 +35,14 @@ class BnBwdDesc(C.Structure):
                 ("mask_kind", C.c_int32), ("nbn", C.c_int32)]
 
 
+class DistortParam(C.Structure):
+    _fields_ = [("sigma", C.c_double), ("fog_mul", C.c_float), ("fog_add", C.c_float),
+                ("flags", C.c_int32), ("ksize", C.c_int32)]
+
+
+RR_DISTORT_FOG, RR_DISTORT_NOISE, RR_DISTORT_BLUR = 1, 2, 4
+RR_DISTORT_KMAX = 15
+
 P_ = C.c_void_p
 I_ = C.c_int
 L_ = C.c_longlong
@@ -94,6 +102,13 @@ _SIGS = {
     "rr_psnr_u8": (I_, [I_, L_, P_, P_, P_, P_]),
     "rr_argmax_rows": (I_, [I_, I_, P_, P_, P_]),
     "rr_adaptive_avgpool_flatten": (I_, [I_, I_, I_, I_, I_, I_, I_, P_, P_, P_]),
+    "rr_resize_workspace": (S_, [I_, I_, I_, I_, I_, I_]),
+    "rr_resize_bilinear_u8": (I_, [I_, I_, I_, I_, I_, I_, P_, I_, P_, P_, P_, P_, S_, P_]),
+    "rr_ssim_workspace": (S_, [I_, I_]),
+    "rr_ssim_u8": (I_, [I_, I_, I_, I_, P_, P_, P_, P_, S_, P_]),
+    "rr_distort_workspace": (S_, [I_, I_, I_, I_]),
+    "rr_distort_u8": (I_, [I_, I_, I_, I_, I_, P_, P_, P_, P_, P_, C.c_ulonglong, P_, S_, P_]),
+    "rr_motion_blur_kernel": (I_, [I_, I_, P_]),
     "rr_zero": (I_, [P_, S_, P_]),
     "rr_version": (C.c_char_p, []),
 }

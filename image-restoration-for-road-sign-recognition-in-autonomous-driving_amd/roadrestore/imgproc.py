@@ -1,0 +1,161 @@
+"""Device-batched image I/O around the networks.
+
+The reference runs these per image on the host (cv2 / PIL / skimage in
+DataLoader workers and in the inference loop).  Here they take a whole
+[n, h, w, c] uint8 batch resident on the GPU and run as HIP kernels
+(csrc/imgproc.hip) behind the C ABI:
+
+* ``Resize`` / ``ToTensor`` / ``Normalize`` / ``Compose`` -- torchvision's
+  transform names and argument meaning (17:66, 18:28-32); ``Resize`` is
+  PIL's bilinear resample bit for bit, and ``Compose([Resize, ToTensor,
+  Normalize])`` runs as one fused pass.
+* ``apply_random_distortions`` -- 14:31-64, the per-image random draws made
+  with Python's ``random`` in the reference's order, the noise field drawn on
+  device (Philox4x32-10) instead of ``np.random.normal``.
+* ``apply_compound_distortion`` -- 16:14-37 (blur 10 @ 45 deg, fog 0.5, noise
+  var 0.02).
+* ``psnr`` / ``ssim`` -- 08:123-125 (skimage semantics, data_range 255).
+"""
+from __future__ import annotations
+
+import random as _random
+
+import torch
+
+from . import ops
+from ._lib import (RR_DISTORT_BLUR, RR_DISTORT_FOG, RR_DISTORT_KMAX, RR_DISTORT_NOISE,
+                   DistortParam)
+
+__all__ = ["Resize", "ToTensor", "Normalize", "Compose", "apply_random_distortions",
+           "apply_compound_distortion", "distortion_params", "psnr", "ssim",
+           "IMAGENET_MEAN", "IMAGENET_STD"]
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)      # 18:31
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+# 14:23-25
+PROB_NOISE = 0.5
+PROB_BLUR = 0.5
+PROB_FOG = 0.5
+
+
+def _check_u8(x):
+    if not isinstance(x, torch.Tensor) or x.dtype != torch.uint8 or x.dim() != 4:
+        raise TypeError("expected a [n, h, w, c] uint8 device batch")
+
+
+class Resize:
+    """torchvision ``Resize((h, w))`` on PIL images (bilinear): u8 -> u8."""
+
+    def __init__(self, size):
+        if isinstance(size, int):
+            raise NotImplementedError("Resize(int) (aspect-preserving) is not used by the reference")
+        self.size = (int(size[0]), int(size[1]))
+
+    def __call__(self, x):
+        _check_u8(x)
+        return ops.resize_bilinear_u8(x, self.size[0], self.size[1], out="u8")
+
+
+class ToTensor:
+    """u8 [n, h, w, c] -> fp32 [n, c, h, w] / 255."""
+
+    def __call__(self, x):
+        _check_u8(x)
+        n, h, w, c = x.shape
+        return ops.resize_bilinear_u8(x, h, w, out="f32")
+
+
+class Normalize:
+    """``(x - mean) / std`` per channel in fp32 (torchvision's
+    ``sub_().div_()``).  It runs fused into the resample pass of
+    ``Compose([Resize, ToTensor, Normalize])`` -- the only way the reference
+    uses it (18:28-32); on its own it raises rather than fall back to ATen."""
+
+    def __init__(self, mean, std):
+        self.mean, self.std = tuple(mean), tuple(std)
+
+    def __call__(self, x):
+        raise NotImplementedError("Normalize runs fused: Compose([Resize(...), ToTensor(), "
+                                  "Normalize(...)])")
+
+
+class Compose:
+    """Sequential transforms; ``[Resize, ToTensor]`` and ``[Resize, ToTensor,
+    Normalize]`` prefixes fuse into one resample pass writing fp32 NCHW."""
+
+    def __init__(self, transforms):
+        self.transforms = list(transforms)
+
+    def __call__(self, x):
+        t = self.transforms
+        i = 0
+        if len(t) >= 2 and isinstance(t[0], Resize) and isinstance(t[1], ToTensor):
+            mean = std = None
+            i = 2
+            if len(t) >= 3 and isinstance(t[2], Normalize):
+                mean, std = t[2].mean, t[2].std
+                i = 3
+            _check_u8(x)
+            x = ops.resize_bilinear_u8(x, t[0].size[0], t[0].size[1], out="f32", mean=mean, std=std)
+        for tr in t[i:]:
+            x = tr(x)
+        return x
+
+
+def distortion_params(n, rng=None):
+    """Per-image draws of apply_random_distortions (14:36-58) in the
+    reference's order with Python's ``random``: -> (params, taps [n, K, K])."""
+    rng = rng or _random
+    params, taps = [], torch.zeros(n, RR_DISTORT_KMAX, RR_DISTORT_KMAX)
+    for i in range(n):
+        p = DistortParam(0.0, 1.0, 0.0, 0, 0)
+        if rng.random() < PROB_FOG:
+            intensity = rng.uniform(0.3, 0.7)
+            A = 0.9
+            t = 1.0 - intensity * rng.uniform(0.8, 1.2)
+            p.flags |= RR_DISTORT_FOG
+            p.fog_mul, p.fog_add = t, A * (1 - t)          # stored as fp32, as numpy casts them
+        if rng.random() < PROB_NOISE:
+            var = rng.uniform(0.01, 0.03)
+            p.flags |= RR_DISTORT_NOISE
+            p.sigma = var ** 0.5
+        if rng.random() < PROB_BLUR:
+            degree = rng.randint(5, 15)
+            angle = rng.randint(0, 360)
+            if degree > 1:
+                p.flags |= RR_DISTORT_BLUR
+                p.ksize = degree
+                taps[i] = ops.motion_blur_kernel(degree, angle)
+        params.append(p)
+    return params, taps
+
+
+def apply_random_distortions(x, rng=None, seed=None, noise=None):
+    """14:31-64 on a [n, h, w, c] uint8 device batch."""
+    _check_u8(x)
+    params, taps = distortion_params(x.shape[0], rng)
+    if seed is None:
+        seed = (rng or _random).getrandbits(64)
+    return ops.distort_u8(x, params, taps, mode=0, noise=noise, seed=seed)
+
+
+def apply_compound_distortion(x, seed=0, noise=None):
+    """16:14-37 on a [n, h, w, c] uint8 device batch: blur (10, 45 deg) ->
+    fog (intensity 0.5, A 0.9) -> noise (var 0.02)."""
+    _check_u8(x)
+    n = x.shape[0]
+    t, A = 1.0 - 0.5, 0.9
+    p = DistortParam(0.02 ** 0.5, t, A * (1 - t), RR_DISTORT_FOG | RR_DISTORT_NOISE | RR_DISTORT_BLUR, 10)
+    taps = ops.motion_blur_kernel(10, 45).unsqueeze(0).expand(n, -1, -1).contiguous()
+    return ops.distort_u8(x, [p] * n, taps, mode=1, noise=noise, seed=seed)
+
+
+def psnr(a, b):
+    """per-image PSNR (08:123, data_range 255) of [n, h, w, c] uint8 batches"""
+    return ops.psnr_u8(a, b)
+
+
+def ssim(a, b):
+    """per-image SSIM (08:125, data_range 255, channel_axis=2)"""
+    return ops.ssim_u8(a, b)

@@ -14,7 +14,7 @@ import os
 import torch
 
 from ._lib import (RR_BF16, RR_F32, RR_CONV1X1, RR_CONV3X3, RR_CONVT_DOWN, RR_CONVT_UP,
-                   BnBwdDesc, IgemmDesc, WgradDesc, lib)
+                   RR_DISTORT_KMAX, BnBwdDesc, DistortParam, IgemmDesc, WgradDesc, lib)
 
 __all__ = [
     "rr_dtype", "stream", "pack_conv", "pack_convT", "bias_tile4", "igemm", "wgrad",
@@ -22,7 +22,8 @@ __all__ = [
     "maxpool2_fwd", "maxpool2_bwd", "conv_in_fwd", "conv_in_wgrad", "conv_in_dgrad",
     "prelu_bwd", "conv_out_fwd", "conv_out_bwd", "nchw_to_nhwc", "nhwc_to_nchw",
     "loss_fwd", "loss_bwd", "adamw_", "to_uint8_hwc", "psnr_u8", "argmax_rows",
-    "adaptive_avgpool_flatten", "zero_",
+    "adaptive_avgpool_flatten", "zero_", "resize_bilinear_u8", "ssim_u8", "distort_u8",
+    "motion_blur_kernel",
 ]
 
 
@@ -647,6 +648,94 @@ def adaptive_avgpool_flatten(x, oh=7, ow=7):
     y = torch.empty((n, Cc * oh * ow), dtype=x.dtype, device=x.device)
     lib().check(lib().rr_adaptive_avgpool_flatten(rr_dtype(x.dtype), n, h, w, Cc, oh, ow, _p(x),
                                                   _p(y), stream()), "rr_adaptive_avgpool_flatten")
+    return y
+
+
+def _ws(nbytes, device):
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+def resize_bilinear_u8(x, oh, ow, out="u8", mean=None, std=None):
+    """PIL-exact bilinear resize of a [n, h, w, c] uint8 batch (torchvision
+    Resize((oh, ow)) on PIL images, 17:66 / 18:28-32).  out="u8": [n, oh, ow,
+    c] uint8; out="f32": [n, c, oh, ow] fp32 ToTensor (+ Normalize(mean, std))."""
+    _need_cuda(x)
+    if x.dtype != torch.uint8 or x.dim() != 4:
+        raise TypeError("resize_bilinear_u8 expects a [n, h, w, c] uint8 tensor")
+    n, h, w, c = x.shape
+    x = x.contiguous()
+    if out == "u8":
+        y = torch.empty((n, oh, ow, c), dtype=torch.uint8, device=x.device)
+        kind = 0
+    elif out == "f32":
+        y = torch.empty((n, c, oh, ow), dtype=torch.float32, device=x.device)
+        kind = 1
+    else:
+        raise ValueError(out)
+    L = lib()
+    wsb = L.rr_resize_workspace(n, h, w, c, oh, ow)
+    if wsb == 0:
+        raise RuntimeError(f"rr_resize_bilinear_u8: unsupported shape {tuple(x.shape)} -> {(oh, ow)}")
+    ws = _ws(wsb, x.device)
+    mp = sp = None
+    if mean is not None:
+        mp = (C.c_float * c)(*[float(v) for v in mean])
+        sp = (C.c_float * c)(*[float(v) for v in std])
+    L.check(L.rr_resize_bilinear_u8(n, h, w, c, oh, ow, _p(x), kind,
+                                    C.cast(mp, C.c_void_p) if mp is not None else None,
+                                    C.cast(sp, C.c_void_p) if sp is not None else None,
+                                    _p(y), _p(ws), wsb, stream()), "rr_resize_bilinear_u8")
+    return y
+
+
+def ssim_u8(a, b):
+    """per-image skimage SSIM (data_range 255, channel_axis=2) of two
+    [n, h, w, c] uint8 batches (08:125) -> fp64 [n]"""
+    _need_cuda(a, b)
+    if a.shape != b.shape or a.dtype != torch.uint8 or a.dim() != 4:
+        raise TypeError("ssim_u8 expects two equal [n, h, w, c] uint8 tensors")
+    n, h, w, c = a.shape
+    out = torch.empty(n, dtype=torch.float64, device=a.device)
+    L = lib()
+    wsb = L.rr_ssim_workspace(n, c)
+    ws = _ws(wsb, a.device)
+    L.check(L.rr_ssim_u8(n, h, w, c, _p(a.contiguous()), _p(b.contiguous()), _p(out), _p(ws), wsb,
+                         stream()), "rr_ssim_u8")
+    return out
+
+
+def motion_blur_kernel(degree, angle):
+    """host: the [KMAX, KMAX] fp32 taps of the 14:55-59 motion-blur kernel"""
+    buf = (C.c_float * (RR_DISTORT_KMAX * RR_DISTORT_KMAX))()
+    lib().check(lib().rr_motion_blur_kernel(int(degree), int(angle), C.cast(buf, C.c_void_p)),
+                "rr_motion_blur_kernel")
+    return torch.frombuffer(bytearray(buf), dtype=torch.float32).view(RR_DISTORT_KMAX, RR_DISTORT_KMAX)
+
+
+def distort_u8(x, params, taps, mode=0, noise=None, seed=0):
+    """distortion generator on a [n, h, w, c] uint8 batch: ``params`` is a
+    list of n DistortParam, ``taps`` [n, KMAX, KMAX] fp32 (host or device),
+    ``noise`` an optional fp64 [n, h, w, c] field (else Philox(seed))."""
+    _need_cuda(x)
+    n, h, w, c = x.shape
+    x = x.contiguous()
+    if len(params) != n:
+        raise ValueError("one DistortParam per image")
+    arr = (DistortParam * n)(*params)
+    prm = torch.frombuffer(bytearray(arr), dtype=torch.uint8).to(x.device)
+    taps = taps.to(x.device, torch.float32).contiguous()
+    if tuple(taps.shape) != (n, RR_DISTORT_KMAX, RR_DISTORT_KMAX):
+        raise ValueError("taps must be [n, KMAX, KMAX]")
+    if noise is not None:
+        noise = noise.to(x.device, torch.float64).contiguous()
+        if tuple(noise.shape) != (n, h, w, c):
+            raise ValueError("noise must match the image batch")
+    y = torch.empty_like(x)
+    L = lib()
+    wsb = L.rr_distort_workspace(n, h, w, c)
+    ws = _ws(wsb, x.device)
+    L.check(L.rr_distort_u8(n, h, w, c, int(mode), _p(x), _p(y), _p(prm), _p(taps), _p(noise),
+                            int(seed) & (2 ** 64 - 1), _p(ws), wsb, stream()), "rr_distort_u8")
     return y
 
 

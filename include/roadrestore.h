@@ -322,6 +322,54 @@ int rr_argmax_rows(int n, int k, const float *logits, int64_t *out,
 int rr_adaptive_avgpool_flatten(int dtype, int n, int h, int w, int C, int oh,
                                 int ow, const void *x, void *y, rr_stream stream);
 
+/* ---- image I/O either side of the networks ---- */
+
+/* torchvision Resize((oh, ow)) of a PIL image == PIL Image.resize(BILINEAR)
+ * (17_run_unified_inference.py:66, 18_test_unified_benchmark.py:28-32),
+ * bit-exact, batched: in [n][h][w][c] uint8 (c <= 4).  out_kind 0: uint8
+ * [n][oh][ow][c]; 1: fp32 [n][c][oh][ow] = ToTensor (x / 255) and, when
+ * mean/std (host arrays of c floats) are given, Normalize (18:31). */
+size_t rr_resize_workspace(int n, int h, int w, int c, int oh, int ow);
+int rr_resize_bilinear_u8(int n, int h, int w, int c, int oh, int ow,
+                          const uint8_t *in, int out_kind, const float *mean,
+                          const float *std, void *out, void *workspace,
+                          size_t workspace_bytes, rr_stream stream);
+
+/* skimage structural_similarity(a, b, data_range=255, channel_axis=2)
+ * (08_run_inference.py:125) per image of [n][h][w][c] uint8, fp64 out[n] */
+size_t rr_ssim_workspace(int n, int c);
+int rr_ssim_u8(int n, int h, int w, int c, const uint8_t *a, const uint8_t *b,
+               double *out, void *workspace, size_t workspace_bytes,
+               rr_stream stream);
+
+/* distortion generator: apply_random_distortions 14:31-64 (mode 0: fog ->
+ * noise -> motion blur) and apply_compound_distortion 16:14-37 (mode 1:
+ * blur -> fog -> noise), per image parameters (drawn by the caller as the
+ * reference draws them).  fog: x * fog_mul + fog_add in fp32 (fog_mul =
+ * f32(t), fog_add = f32(A (1 - t))); noise: + N(0, sigma) in fp64, from
+ * `noise` ([n][h][w][c] fp64) when given, else Philox4x32-10(seed); blur:
+ * cv2.filter2D with the ksize x ksize taps of `taps` ([n][KMAX][KMAX]
+ * fp32, rr_motion_blur_kernel), BORDER_REFLECT_101. */
+#define RR_DISTORT_KMAX 15
+enum { RR_DISTORT_FOG = 1, RR_DISTORT_NOISE = 2, RR_DISTORT_BLUR = 4 };
+typedef struct rr_distort_param {
+  double sigma;       /* noise standard deviation (var ** 0.5)            */
+  float fog_mul;      /* f32(t)                                           */
+  float fog_add;      /* f32(A * (1 - t))                                 */
+  int32_t flags;      /* RR_DISTORT_* bits                                */
+  int32_t ksize;      /* motion-blur degree (kernel side), <= KMAX        */
+} rr_distort_param;
+size_t rr_distort_workspace(int n, int h, int w, int c);
+int rr_distort_u8(int n, int h, int w, int c, int mode, const uint8_t *in,
+                  uint8_t *out, const rr_distort_param *params,
+                  const float *taps, const double *noise,
+                  unsigned long long seed, void *workspace,
+                  size_t workspace_bytes, rr_stream stream);
+/* host: the motion-blur kernel of 14:55-59 / 16:20-21 (cv2
+ * getRotationMatrix2D + warpAffine of np.diag(np.ones(k)), / k, as fp32)
+ * into taps[KMAX][KMAX] (row-major, zero outside k x k) */
+int rr_motion_blur_kernel(int k, int angle, float *taps);
+
 /* async memset of a device buffer (zero_grad of the flat buffers) */
 int rr_zero(void *p, size_t bytes, rr_stream stream);
 
