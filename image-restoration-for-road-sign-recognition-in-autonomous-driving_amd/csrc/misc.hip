@@ -36,6 +36,40 @@ __global__ void pack_conv_kernel(int co_n, int ci_n, int k, const float *__restr
   }
 }
 
+// all conv packs of a network in one launch: job j owns elements
+// [begin_j, begin_{j+1}) of the concatenated fp32 weights; a thread finds its
+// job by binary search over the begins (staged in LDS)
+constexpr int PACKB_MAX = 256;
+template <typename T>
+__global__ void pack_conv_batch_kernel(int count, const rr_pack_job *__restrict__ jobs, long long total) {
+  __shared__ long long beg[PACKB_MAX + 1];
+  for (int j = threadIdx.x; j < count; j += blockDim.x) beg[j] = jobs[j].begin;
+  if (threadIdx.x == 0) beg[count] = total;
+  __syncthreads();
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int lo = 0, hi = count - 1;                         // last j with beg[j] <= i
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (beg[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    const rr_pack_job jb = jobs[lo];
+    const long long e = i - beg[lo];
+    const int kk = jb.k * jb.k;
+    const int t = (int)(e % kk);
+    const long long r = e / kk;
+    const int ci = (int)(r % jb.c_in);
+    const int co = (int)(r / jb.c_in);
+    const float v = jb.w[e];
+    if (jb.w_fwd) Elt<T>::store((T *)jb.w_fwd, ((long long)co * kk + t) * jb.c_in + ci, v);
+    if (jb.w_dgrad) {
+      const int ky = t / jb.k, kx = t % jb.k;
+      const int tf = (jb.k - 1 - ky) * jb.k + (jb.k - 1 - kx);
+      Elt<T>::store((T *)jb.w_dgrad, ((long long)ci * kk + tf) * jb.c_out + co, v);
+    }
+  }
+}
+
 template <typename T>
 __global__ void pack_convT_kernel(int ci_n, int co_n, const float *__restrict__ w,
                                   T *__restrict__ wu, T *__restrict__ wdn) {
@@ -927,6 +961,19 @@ extern "C" int rr_pack_conv(int dtype, int c_out, int c_in, int k, const float *
   else
     hipLaunchKernelGGL(pack_conv_kernel<float>, g, b, 0, st, c_out, c_in, k, w, (float *)w_fwd,
                        (float *)w_dgrad);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_pack_conv_batch(int dtype, int count, const rr_pack_job *jobs, long long total,
+                                  rr_stream stream) {
+  if (!jobs || count <= 0 || count > PACKB_MAX || total <= 0) return RR_EINVAL;
+  dim3 g(rr_grid_cap((total + 255) / 256, 1024)), b(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(pack_conv_batch_kernel<bf16_t>, g, b, 0, st, count, jobs, total);
+  else
+    hipLaunchKernelGGL(pack_conv_batch_kernel<float>, g, b, 0, st, count, jobs, total);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

@@ -40,6 +40,12 @@ class DistortParam(C.Structure):
                 ("flags", C.c_int32), ("ksize", C.c_int32)]
 
 
+class PackJob(C.Structure):
+    _fields_ = [("w", C.c_void_p), ("w_fwd", C.c_void_p), ("w_dgrad", C.c_void_p),
+                ("c_out", C.c_int32), ("c_in", C.c_int32), ("k", C.c_int32), ("pad_", C.c_int32),
+                ("begin", C.c_int64)]
+
+
 RR_DISTORT_FOG, RR_DISTORT_NOISE, RR_DISTORT_BLUR = 1, 2, 4
 RR_DISTORT_KMAX = 15
 
@@ -58,6 +64,7 @@ _SIGS = {
     "rr_wgrad_workspace": (S_, [C.POINTER(WgradDesc)]),
     "rr_wgrad": (I_, [C.POINTER(WgradDesc), P_, P_, P_, P_, P_, S_, P_]),
     "rr_pack_conv": (I_, [I_, I_, I_, I_, P_, P_, P_, P_]),
+    "rr_pack_conv_batch": (I_, [I_, I_, P_, L_, P_]),
     "rr_pack_convT": (I_, [I_, I_, I_, P_, P_, P_, P_]),
     "rr_bias_tile4": (I_, [I_, P_, P_, P_]),
     "rr_bn_finalize": (I_, [I_, I_, L_, P_, P_, P_, P_, P_, P_, F_, F_, P_, P_, P_, P_, P_, P_,

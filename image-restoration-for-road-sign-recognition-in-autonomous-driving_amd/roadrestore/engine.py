@@ -41,17 +41,29 @@ class Bag(dict):
 class WeightCache:
     """Packed (compute layout / dtype) copies of fp32 weights, re-packed when
     the parameter's version counter moves (every optimizer step) and always
-    while a HIP graph is being captured (so replays re-pack)."""
+    while a HIP graph is being captured (so replays re-pack).
+
+    Conv packs are batched: the convs a forward requests are recorded (the
+    plan), and ``begin()`` at the start of every later forward re-packs all
+    of them in ONE launch (ops.PackBatch) when any is stale or a graph is
+    being captured; the per-layer ``conv()`` calls then hit those packs."""
 
     def __init__(self):
         self._c = {}
+        self._plan = {}          # id(w) -> [w, dtype, dgrad], first-request order
+        self._batch = None
+        self._fresh = {}         # key -> (ver, packed), set by begin()
+
+    @staticmethod
+    def _ver(w, also=None):
+        from .optim import GENERATION
+        return (w.data_ptr(), w._version, GENERATION[0],
+                None if also is None else (also.data_ptr(), also._version))
 
     def _get(self, w, dtype, kind, fn, also=None):
-        from .optim import GENERATION
         cap = torch.cuda.is_current_stream_capturing()
         key = (id(w), dtype, kind)
-        ver = (w.data_ptr(), w._version, GENERATION[0],
-               None if also is None else (also.data_ptr(), also._version))
+        ver = self._ver(w, also)
         e = None if cap else self._c.get(key)
         if e is not None and e[0] == ver:
             return e[1]
@@ -60,8 +72,48 @@ class WeightCache:
             self._c[key] = (ver, v)
         return v
 
+    def begin(self):
+        """Start of a forward: one batched re-pack of every planned conv."""
+        self._fresh = {}
+        if not self._plan:
+            return
+        cap = torch.cuda.is_current_stream_capturing()
+        ent = list(self._plan.values())
+        keys = [(id(w), dt, "conv+d" if dg else "conv") for w, dt, dg in ent]
+        vers = [self._ver(w) for w, _, _ in ent]
+        ok = self._batch is not None and self._batch.valid() and \
+            self._batch.entries == [tuple(e) for e in ent]
+        if not ok and not cap and all(w.is_contiguous() for w, _, _ in ent) and \
+                len({dt for _, dt, _ in ent}) == 1:
+            # built eagerly (its job table is a host -> device copy, which a
+            # capture does not allow), also when nothing is stale yet
+            self._batch = ops.PackBatch([tuple(e) for e in ent])
+            ok = True
+        if not cap and all(self._c.get(k, (None,))[0] == v for k, v in zip(keys, vers)):
+            return
+        if not ok:
+            return                                   # per-layer packs instead
+        outs = self._batch.run()
+        for k, v, o in zip(keys, vers, outs):
+            self._fresh[k] = (v, o)
+            if not cap:
+                self._c[k] = (v, o)
+
     def conv(self, w, dtype, dgrad):
         kind = "conv+d" if dgrad else "conv"
+        ver = self._ver(w)
+        for k in ((id(w), dtype, kind),) + (() if dgrad else ((id(w), dtype, "conv+d"),)):
+            f = self._fresh.get(k)
+            if f is not None and f[0] == ver:
+                return f[1]
+        p = self._plan.get(id(w))
+        if p is None:
+            self._plan[id(w)] = [w, dtype, dgrad]
+        elif p[1] != dtype:
+            self._plan = {id(w): [w, dtype, dgrad]}   # compute dtype changed: new plan
+            self._batch = None
+        elif dgrad and not p[2]:
+            p[2] = True
         return self._get(w, dtype, kind, lambda: ops.pack_conv(w, dtype, True, dgrad))
 
     def convT(self, w, dtype, down):
@@ -157,6 +209,7 @@ def _convT_up(wc, dt, conv, x, n, h, w, need_bwd):
 
 
 def simple_unet_forward(m, x, wc, dt, need_bwd):
+    wc.begin()
     n, _, H, W = x.shape
     S = Bag(n=n, H=H, W=W, x=x)
     e1a, _ = ops.first_conv_fwd(x, m.enc1[0].weight, m.enc1[0].bias, dt,
@@ -358,6 +411,7 @@ def resunet_block_names():
 
 
 def resunet_forward(m, x, wc, dt, training, need_bwd):
+    wc.begin()
     n, _, H, W = x.shape
     if H % 8 or W % 8:
         raise NotImplementedError(
@@ -472,6 +526,7 @@ def vgg_layers(features, upto=None):
 
 def vgg_features_forward(features, x, wc, dt, upto=None, need_bwd=False):
     """x: NCHW fp32 image.  Returns NHWC features and the saved state."""
+    wc.begin()
     n, _, H, W = x.shape
     layers = vgg_layers(features, upto)
     S = Bag(n=n, H=H, W=W, acts=[], layers=layers)

@@ -14,7 +14,7 @@ import os
 import torch
 
 from ._lib import (RR_BF16, RR_F32, RR_CONV1X1, RR_CONV3X3, RR_CONVT_DOWN, RR_CONVT_UP,
-                   RR_DISTORT_KMAX, BnBwdDesc, DistortParam, IgemmDesc, WgradDesc, lib)
+                   RR_DISTORT_KMAX, BnBwdDesc, DistortParam, IgemmDesc, PackJob, WgradDesc, lib)
 
 __all__ = [
     "rr_dtype", "stream", "pack_conv", "pack_convT", "bias_tile4", "igemm", "wgrad",
@@ -122,6 +122,43 @@ def pack_conv(w: torch.Tensor, dtype: torch.dtype, fwd=True, dgrad=True):
     lib().check(lib().rr_pack_conv(rr_dtype(dtype), co, ci, k, _p(w.contiguous()), _p(wf),
                                    _p(wd), stream()), "rr_pack_conv")
     return wf, wd
+
+
+class PackBatch:
+    """All conv packs of a network as ONE launch (rr_pack_conv_batch): the
+    packed outputs are allocated once and re-packed in place each call, from
+    a job table kept in device memory.  ``entries``: [(w, dtype, dgrad)]."""
+
+    def __init__(self, entries):
+        dt = {e[1] for e in entries}
+        if len(dt) != 1:
+            raise ValueError("one compute dtype per pack batch")
+        self.dtype = dt.pop()
+        self.entries = list(entries)
+        self.out = []
+        jobs = (PackJob * len(entries))()
+        begin = 0
+        for j, (w, _, dgrad) in enumerate(entries):
+            _need_cuda(w)
+            if not w.is_contiguous():
+                raise ValueError("pack batch needs contiguous weights")
+            co, ci, k, _ = w.shape
+            wf = torch.empty(co * k * k * ci, dtype=self.dtype, device=w.device)
+            wd = torch.empty(co * k * k * ci, dtype=self.dtype, device=w.device) if dgrad else None
+            self.out.append((wf, wd))
+            jobs[j] = PackJob(_p(w), _p(wf), _p(wd), co, ci, k, 0, begin)
+            begin += w.numel()
+        self.total = begin
+        self.sig = tuple(w.data_ptr() for w, _, _ in entries)
+        self.table = torch.frombuffer(bytearray(jobs), dtype=torch.uint8).to(entries[0][0].device)
+
+    def valid(self):
+        return self.sig == tuple(w.data_ptr() for w, _, _ in self.entries)
+
+    def run(self):
+        lib().check(lib().rr_pack_conv_batch(rr_dtype(self.dtype), len(self.entries), _p(self.table),
+                                             self.total, stream()), "rr_pack_conv_batch")
+        return self.out
 
 
 def pack_convT(w: torch.Tensor, dtype: torch.dtype, up=True, down=True):
@@ -649,10 +686,6 @@ def adaptive_avgpool_flatten(x, oh=7, ow=7):
     lib().check(lib().rr_adaptive_avgpool_flatten(rr_dtype(x.dtype), n, h, w, Cc, oh, ow, _p(x),
                                                   _p(y), stream()), "rr_adaptive_avgpool_flatten")
     return y
-
-
-def _ws(nbytes, device):
-    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
 
 
 def resize_bilinear_u8(x, oh, ow, out="u8", mean=None, std=None):

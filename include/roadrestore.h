@@ -126,6 +126,19 @@ int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
 int rr_pack_conv(int dtype, int c_out, int c_in, int k, const float *w,
                  void *w_fwd, void *w_dgrad, rr_stream stream);
 /* convT [ci][co][2][2] -> up [tap*co][ci] and down [ci][tap][co] */
+/* every conv pack of a network in one launch (the per-step re-pack after the
+ * optimizer step): jobs[count] in DEVICE memory, job j covering elements
+ * [begin, next begin) of a virtual concatenation of the fp32 weights; total =
+ * sum of c_out * c_in * k * k.  Same layouts as rr_pack_conv. */
+typedef struct rr_pack_job {
+  const float *w;      /* [c_out][c_in][k][k] fp32                         */
+  void *w_fwd;         /* [c_out][k*k][c_in] or NULL                       */
+  void *w_dgrad;       /* [c_in][flipped k*k][c_out] or NULL               */
+  int32_t c_out, c_in, k, pad_;
+  int64_t begin;       /* first element of this job                        */
+} rr_pack_job;
+int rr_pack_conv_batch(int dtype, int count, const rr_pack_job *jobs,
+                       long long total, rr_stream stream);
 int rr_pack_convT(int dtype, int c_in, int c_out, const float *w,
                   void *w_up, void *w_down, rr_stream stream);
 /* replicate bias over the 4 taps of a convT: b4[tap*co] = b[co] */

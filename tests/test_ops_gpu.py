@@ -440,3 +440,25 @@ def test_losses_adamw_postproc(dev):
     lg = rnd(9, 43, seed=32)
     lg[3, 5] = lg[3, 7] = lg[3].max() + 1       # tie: first index wins (18:47)
     assert torch.equal(rr.ops.argmax_rows(lg.to(dev)).cpu(), R.top1(lg))
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_pack_conv_batch_equals_single_packs(dev, dt):
+    """rr_pack_conv_batch (one launch for a network's convs) == rr_pack_conv
+    per weight, bitwise, including 1x1 and fwd-only entries"""
+    from roadrestore import ops
+    shapes = [(64, 3, 3, True), (64, 64, 3, True), (128, 64, 1, True), (3, 64, 1, False),
+              (512, 256, 3, True), (7, 5, 3, False)]
+    ws = [rnd(co, ci, k, k, seed=i).to(dev) for i, (co, ci, k, _) in enumerate(shapes)]
+    pb = ops.PackBatch([(w, dt, dg) for w, (_, _, _, dg) in zip(ws, shapes)])
+    outs = pb.run()
+    for w, (co, ci, k, dg), (bf, bd) in zip(ws, shapes, outs):
+        sf, sd = ops.pack_conv(w, dt, True, dg)
+        assert torch.equal(bf, sf)
+        assert (bd is None) == (not dg)
+        if dg:
+            assert torch.equal(bd, sd)
+    # in place: a weight update is picked up by the next run
+    ws[1].mul_(2)
+    outs = pb.run()
+    assert torch.equal(outs[1][0], ops.pack_conv(ws[1], dt, True, True)[0])
