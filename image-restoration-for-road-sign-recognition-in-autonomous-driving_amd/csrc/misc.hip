@@ -205,6 +205,144 @@ __global__ void conv_in_wgrad_kernel(int n, int h, int w, int cin, int cout,
   }
 }
 
+// First-conv weight + bias grad fused with the backward of its activation
+// (14:122-123: Conv2d(3, 64) -> PReLU; 07:78: -> ReLU), straight from the
+// NCHW fp32 image: no im2col matrix and no materialised pre-activation grad.
+//   gp[p][co] = t > 0 ? g : alpha g  (ReLU: 0),   dalpha = sum_{t<=0} g t
+//   dW[co][n] = sum_p gp[p][co] patch[p][n],  n = ci*9 + ky*3 + kx (< 27),
+//   column 27 of patch = 1  ->  db[co] = sum_p gp[p][co]
+// bf16 MFMA 16x16x32 over 64-pixel steps: A = gp^T from an LDS transpose
+// (channel rows of 64 pixels), B = the 32 patch rows of the same pixels,
+// staged per step in LDS from the image (zero padded).  Per block:
+// a fixed pixel range -> one [64][32] partial slab (+ a dalpha row), reduced
+// by rr_colreduce + conv_in_wgrad_act_finalize in fixed order.
+constexpr int CIA_NPX = 64;
+constexpr int CIA_ROW = CIA_NPX + 8;                  // bf16 per LDS row (144 B)
+__global__ __launch_bounds__(256) void conv_in_wgrad_act_kernel(
+    int n, int h, int w, const float *__restrict__ x, const bf16_t *__restrict__ g,
+    const bf16_t *__restrict__ t, int act, const float *__restrict__ alpha,
+    float *__restrict__ part, long long ppb) {
+  // gT: gp^T, 64 channel rows of the step's 64 pixels; pT: the 32 patch rows
+  // (27 image taps, a ones row, 4 zero rows) of the same pixels, bf16
+  __shared__ __attribute__((aligned(16))) u16 gT[64 * CIA_ROW];
+  __shared__ __attribute__((aligned(16))) u16 pT[32 * CIA_ROW];
+  __shared__ float red[256];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const long long P = (long long)n * h * w, hw = (long long)h * w;
+  const long long p0 = blockIdx.x * ppb, p1 = min(P, p0 + ppb);
+  const float al = act == 2 ? alpha[0] : 0.f;
+  float sa = 0.f;
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  const int lc = tid & 7, lpp = tid >> 3;             // gp load: 8-channel chunk, pixel pair
+  const int bn = lane & 15, bk = lane >> 4;           // fragment col / k-block
+  const int sj = tid & 63, sg = tid >> 6;             // patch staging: pixel, row group
+  // registers of one step's operands, loaded a step ahead of their use
+  uint4 rg[2], rt[2];
+  float rp[8];
+  auto load_step = [&](long long q0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const long long p = q0 + 2 * lpp + j;
+      const bool ok = p < p1;
+      const long long e = (ok ? p : p0) * 64 + lc * 8;
+      rg[j] = *reinterpret_cast<const uint4 *>(g + e);
+      rt[j] = *reinterpret_cast<const uint4 *>(t + e);
+      if (!ok) rg[j] = uint4{0u, 0u, 0u, 0u};
+    }
+    const long long p = q0 + sj;
+    const bool live = p < p1;
+    int img = 0, y = 0, xx0 = 0;
+    if (live) {
+      img = (int)(p / hw);
+      const int rem = (int)(p - img * hw);
+      y = rem / w;
+      xx0 = rem - y * w;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = sg + 4 * u;
+      float val = 0.f;
+      if (r < 27) {
+        const int ci = r / 9, ky = (r % 9) / 3, kx = r % 3;
+        const int yy = y + ky - 1, xx = xx0 + kx - 1;
+        const bool ok = live && yy >= 0 && yy < h && xx >= 0 && xx < w;
+        const float vv = x[ok ? (((long long)img * 3 + ci) * h + yy) * w + xx : 0];
+        val = ok ? vv : 0.f;
+      } else if (r == 27) {
+        val = live ? 1.f : 0.f;
+      }
+      rp[u] = val;
+    }
+  };
+  auto bf = [](uint32_t word, int hi) { return __uint_as_float(hi ? (word & 0xffff0000u) : (word << 16)); };
+  if (p0 < p1) load_step(p0);
+  for (long long q0 = p0; q0 < p1; q0 += CIA_NPX) {
+    // ---- gp for pixels q0 + 2 lpp, +1, channels 8 lc .. +7 -> gT[co][px] ----
+    u16 v[2][8];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t gw[4] = {rg[j].x, rg[j].y, rg[j].z, rg[j].w};
+      const uint32_t tw[4] = {rt[j].x, rt[j].y, rt[j].z, rt[j].w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float gg = bf(gw[k >> 1], k & 1), tt = bf(tw[k >> 1], k & 1);
+        const float gp = tt > 0.f ? gg : al * gg;
+        sa += tt > 0.f ? 0.f : gg * tt;
+        v[j][k] = f32_to_bf16(gp);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      *reinterpret_cast<uint32_t *>(&gT[(lc * 8 + k) * CIA_ROW + 2 * lpp]) =
+          (uint32_t)v[0][k] | ((uint32_t)v[1][k] << 16);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) pT[(sg + 4 * u) * CIA_ROW + sj] = f32_to_bf16(rp[u]);
+    __syncthreads();
+    if (q0 + CIA_NPX < p1) load_step(q0 + CIA_NPX);     // next step's operands in flight
+    // ---- MFMA: wave wv owns channels 16 wv .. +15, both 32-pixel k-steps ----
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int px = ks * 32 + bk * 8;
+      const bf16x8 fa = *reinterpret_cast<const bf16x8 *>(&gT[(wv * 16 + bn) * CIA_ROW + px]);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const bf16x8 fb = *reinterpret_cast<const bf16x8 *>(&pT[(nb * 16 + bn) * CIA_ROW + px]);
+        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[nb], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  // ---- partial slab [64][32] + dalpha row [32] ----
+  float *pw = part + (long long)blockIdx.x * (64 * 32 + 32);
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pw[(wv * 16 + 4 * bk + i) * 32 + nb * 16 + bn] = acc[nb][i];
+  red[tid] = sa;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] += red[tid + o];
+    __syncthreads();
+  }
+  if (tid < 32) pw[64 * 32 + tid] = tid == 0 ? red[0] : 0.f;
+}
+
+__global__ void conv_in_wgrad_act_finalize(int chunks, const double *__restrict__ part, float *dw,
+                                           float *db, float *dalpha) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over 64 * 32 + 1
+  const int cols = 64 * 32 + 32;
+  if (i > 64 * 32) return;
+  double s = 0;
+  for (int b = 0; b < chunks; ++b) s += part[(long long)b * cols + i];
+  if (i == 64 * 32) {
+    if (dalpha) dalpha[0] = (float)s;
+    return;
+  }
+  const int co = i / 32, j = i % 32;
+  if (j < 27) dw[co * 27 + j] = (float)s;
+  else if (j == 27 && db) db[co] = (float)s;
+}
+
 __global__ void conv_in_wgrad_finalize(int cout, int kk, int blocks, const double *__restrict__ part,
                                        float *dw, float *db) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over cout*32
@@ -1093,6 +1231,42 @@ extern "C" int rr_conv_in_wgrad(int dtype, int n, int h, int w, int cin, int cou
   if (chunks < 0) return RR_ELAUNCH;
   hipLaunchKernelGGL(conv_in_wgrad_finalize, dim3((cout * 32 + 255) / 256), dim3(256), 0, st, cout,
                      cin * 9, chunks, (const double *)red, dw, db);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+static int conv_in_act_blocks(long long P) {
+  long long b = (P + 511) / 512;
+  if (b > 2048) b = 2048;
+  return (int)(b < 1 ? 1 : b);
+}
+
+extern "C" size_t rr_conv_in_wgrad_act_workspace(int n, int h, int w) {
+  const int blocks = conv_in_act_blocks((long long)n * h * w);
+  return (size_t)blocks * (64 * 32 + 32) * sizeof(float) + rr_colreduce_bytes(blocks, 64 * 32 + 32);
+}
+
+extern "C" int rr_conv_in_wgrad_act(int n, int h, int w, const float *x, const void *dy,
+                                    const void *t_pre, int act, const float *alpha, float *dw,
+                                    float *db, float *dalpha, void *ws, size_t ws_bytes,
+                                    rr_stream stream) {
+  if (!x || !dy || !t_pre || !dw || n <= 0 || h <= 0 || w <= 0) return RR_EINVAL;
+  if (act < 1 || act > 2 || (act == 2 && !alpha)) return RR_EINVAL;
+  const long long P = (long long)n * h * w;
+  const int blocks = conv_in_act_blocks(P);
+  const size_t pbytes = (size_t)blocks * (64 * 32 + 32) * sizeof(float);
+  if (!ws || ws_bytes < pbytes + rr_colreduce_bytes(blocks, 64 * 32 + 32)) return RR_EWORKSPACE;
+  long long ppb = (P + blocks - 1) / blocks;
+  ppb = (ppb + CIA_NPX - 1) / CIA_NPX * CIA_NPX;            // whole 64-pixel steps (8-aligned)
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(conv_in_wgrad_act_kernel, dim3(blocks), dim3(256), 0, st, n, h, w, x,
+                     (const bf16_t *)dy, (const bf16_t *)t_pre, act, alpha, (float *)ws, ppb);
+  RR_CHECK_LAUNCH();
+  double *red = (double *)((char *)ws + pbytes);
+  const int chunks = rr_colreduce((const float *)ws, blocks, 64 * 32 + 32, red, st);
+  if (chunks < 0) return RR_ELAUNCH;
+  hipLaunchKernelGGL(conv_in_wgrad_act_finalize, dim3((64 * 32 + 1 + 255) / 256), dim3(256), 0, st,
+                     chunks, (const double *)red, dw, db, act == 2 ? dalpha : nullptr);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

@@ -93,6 +93,8 @@ _SIGS = {
     "rr_conv_in_fwd": (I_, [I_, I_, I_, I_, I_, I_, P_, P_, P_, I_, P_, P_, P_]),
     "rr_conv_in_wgrad": (I_, [I_, I_, I_, I_, I_, I_, P_, P_, P_, P_, P_, S_, P_]),
     "rr_conv_in_wgrad_workspace": (S_, [I_, I_, I_, I_, I_]),
+    "rr_conv_in_wgrad_act_workspace": (S_, [I_, I_, I_]),
+    "rr_conv_in_wgrad_act": (I_, [I_, I_, I_, P_, P_, P_, I_, P_, P_, P_, P_, P_, S_, P_]),
     "rr_conv_in_dgrad": (I_, [I_, I_, I_, I_, I_, I_, P_, P_, P_, I_, P_]),
     "rr_prelu_bwd": (I_, [I_, L_, P_, P_, P_, P_, P_, I_, P_, P_]),
     "rr_conv_out_fwd": (I_, [I_, I_, I_, I_, I_, I_, P_, P_, P_, P_, P_]),

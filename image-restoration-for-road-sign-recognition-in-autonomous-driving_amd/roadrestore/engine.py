@@ -471,6 +471,11 @@ def resunet_zero_grad_params(m):
     return z
 
 
+# A/B switch for the fused first-conv backward (RR_FUSED_FIRST_WGRAD=0: the
+# prelu_bwd + im2col + wgrad sequence)
+_FUSED_FIRST_WGRAD = os.environ.get("RR_FUSED_FIRST_WGRAD", "1") != "0"
+
+
 def resunet_backward(m, S, g_out, sink):
     n, H, W = S.n, S.H, S.W
     g_d1, _, _ = ops.conv_out_bwd(g_out, S.d1, m.final.weight, mask_relu=False,
@@ -494,9 +499,14 @@ def resunet_backward(m, S, g_out, sink):
     ops.maxpool2_bwd(g_p1, S.i1, H, W, out=g_r1, accumulate=True)
     g_e1, _ = resblock_backward(m.res1, S.res1, g_r1, sink)
     pr = m.enc1[1]
-    g_e1pre, _ = ops.prelu_bwd(g_e1, S.e1pre, pr.weight, dalpha=sink[pr.weight])
-    ops.first_conv_wgrad(ops.im2col3(S.x, g_e1pre.dtype), g_e1pre, sink[m.enc1[0].weight],
-                         sink[m.enc1[0].bias])
+    if g_e1.dtype == torch.bfloat16 and W % 8 == 0 and _FUSED_FIRST_WGRAD:
+        # PReLU backward + first-conv wgrad in one pass over the image
+        ops.first_conv_wgrad_act(S.x, g_e1, S.e1pre, 2, pr.weight, sink[m.enc1[0].weight],
+                                 sink[m.enc1[0].bias], dalpha=sink[pr.weight])
+    else:
+        g_e1pre, _ = ops.prelu_bwd(g_e1, S.e1pre, pr.weight, dalpha=sink[pr.weight])
+        ops.first_conv_wgrad(ops.im2col3(S.x, g_e1pre.dtype), g_e1pre, sink[m.enc1[0].weight],
+                             sink[m.enc1[0].bias])
     sink.ready(_params(m.enc1))
 
 

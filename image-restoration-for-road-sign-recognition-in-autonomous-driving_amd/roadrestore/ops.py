@@ -23,7 +23,7 @@ __all__ = [
     "prelu_bwd", "conv_out_fwd", "conv_out_bwd", "nchw_to_nhwc", "nhwc_to_nchw",
     "loss_fwd", "loss_bwd", "adamw_", "to_uint8_hwc", "psnr_u8", "argmax_rows",
     "adaptive_avgpool_flatten", "zero_", "resize_bilinear_u8", "ssim_u8", "distort_u8",
-    "motion_blur_kernel",
+    "motion_blur_kernel", "first_conv_wgrad_act",
 ]
 
 
@@ -521,6 +521,22 @@ def first_conv_wgrad(col, dy, dw, db):
     g = wgrad(RR_CONV1X1, dy, col, None, n, h, w, cout, dw_shape=(cout, kpad, 1, 1))
     lib().check(lib().rr_unpack_conv_in_grad(cout, cin, kpad, _p(g), _p(dw), _p(db), stream()),
                 "rr_unpack_conv_in_grad")
+    return dw, db
+
+
+def first_conv_wgrad_act(x_nchw, dy, t_pre, act, alpha, dw, db, dalpha=None):
+    """First-conv weight/bias grad fused with its ReLU (act 1) / PReLU (act
+    2) backward, from the NCHW fp32 image (rr_conv_in_wgrad_act)."""
+    _need_cuda(x_nchw, dy, t_pre)
+    n, cin, h, w = x_nchw.shape
+    if cin != 3 or dy.shape[-1] != 64 or dy.dtype != torch.bfloat16 or t_pre.dtype != torch.bfloat16:
+        raise ValueError("rr_conv_in_wgrad_act: 3 -> 64 channels, bf16 grads")
+    L = lib()
+    wsb = L.rr_conv_in_wgrad_act_workspace(n, h, w)
+    ws = _ws(wsb, dy.device)
+    L.check(L.rr_conv_in_wgrad_act(n, h, w, _p(x_nchw.contiguous()), _p(dy), _p(t_pre), int(act),
+                                   _p(alpha), _p(dw), _p(db), _p(dalpha), _p(ws), wsb, stream()),
+            "rr_conv_in_wgrad_act")
     return dw, db
 
 

@@ -268,6 +268,16 @@ int rr_conv_in_wgrad(int dtype, int n, int h, int w, int cin, int cout,
                      void *ws, size_t ws_bytes, rr_stream stream);
 size_t rr_conv_in_wgrad_workspace(int n, int h, int w, int cin, int cout);
 /* input grad of that conv (VGG perceptual slice dgrad reaching the image) */
+/* first-conv (3 -> 64) weight + bias grad fused with the backward of its
+ * activation (act 1 ReLU 07:78, 2 PReLU 14:122-123), from the NCHW fp32
+ * image, the bf16 NHWC grad of the activation output dy and the bf16
+ * pre-activation t: dw [64][27], db [64], dalpha [1] (PReLU) written;
+ * bf16 MFMA, deterministic */
+size_t rr_conv_in_wgrad_act_workspace(int n, int h, int w);
+int rr_conv_in_wgrad_act(int n, int h, int w, const float *x, const void *dy,
+                         const void *t_pre, int act, const float *alpha,
+                         float *dw, float *db, float *dalpha, void *workspace,
+                         size_t workspace_bytes, rr_stream stream);
 int rr_conv_in_dgrad(int dtype, int n, int h, int w, int cin, int cout,
                      const void *dy, const float *wt, float *dx, int accumulate,
                      rr_stream stream);

@@ -462,3 +462,37 @@ def test_pack_conv_batch_equals_single_packs(dev, dt):
     ws[1].mul_(2)
     outs = pb.run()
     assert torch.equal(outs[1][0], ops.pack_conv(ws[1], dt, True, True)[0])
+
+
+@pytest.mark.parametrize("act", [1, 2])
+@pytest.mark.parametrize("n,h,w", [(3, 16, 24), (2, 64, 64), (1, 8, 8)])
+def test_first_conv_wgrad_act_fused(dev, act, n, h, w):
+    """rr_conv_in_wgrad_act (ReLU/PReLU backward + first-conv wgrad from the
+    image) against an fp64 CPU sum over the same bf16-rounded operands"""
+    from roadrestore import ops
+    x = torch.rand(n, 3, h, w, generator=torch.Generator().manual_seed(1))
+    g = rnd(n, h, w, 64, seed=2).bfloat16()
+    t = rnd(n, h, w, 64, seed=3).bfloat16()
+    alpha = torch.tensor([0.25])
+    dw = torch.full((64, 3, 3, 3), float("nan"), device=dev)
+    db = torch.full((64,), float("nan"), device=dev)
+    da = torch.full((1,), float("nan"), device=dev)
+    ops.first_conv_wgrad_act(x.to(dev), g.to(dev), t.to(dev), act, alpha.to(dev), dw, db,
+                             dalpha=da if act == 2 else None)
+    gf, tf = g.float(), t.float()
+    a = 0.25 if act == 2 else 0.0
+    gp = torch.where(tf > 0, gf, a * gf).bfloat16().double()          # [n, h, w, 64]
+    xb = x.bfloat16().double()
+    xp = F.pad(xb, (1, 1, 1, 1))
+    ref = torch.zeros(64, 3, 3, 3, dtype=torch.float64)
+    for ky in range(3):
+        for kx in range(3):
+            patch = xp[:, :, ky:ky + h, kx:kx + w]                    # [n, 3, h, w]
+            ref[:, :, ky, kx] = torch.einsum("nhwo,nchw->oc", gp, patch)
+    refb = gp.sum((0, 1, 2))
+    s = ref.abs().max().item()
+    assert (dw.cpu().double() - ref).abs().max().item() <= 2e-4 * s
+    assert (db.cpu().double() - refb).abs().max().item() <= 2e-4 * max(1.0, refb.abs().max().item())
+    if act == 2:
+        refa = (gf.double() * tf.double() * (tf <= 0)).sum().item()
+        assert abs(da.item() - refa) <= 1e-4 * max(1.0, abs(refa))
