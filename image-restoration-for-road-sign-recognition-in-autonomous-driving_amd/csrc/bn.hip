@@ -103,6 +103,72 @@ __global__ void affine_act_kernel(long long P, int C, const T *__restrict__ x,
   }
 }
 
+// residual tail + MaxPool2d(2, 2) in one pass (14:114-115 then 14:125-131):
+// y = relu(x * scale + shift + res * rs + rb) for the 4 pixels of a pooling
+// window (8 channels per thread), and the window max / first-max index of
+// the STORED (dtype-rounded) values -- exactly what maxpool2_fwd would read
+template <typename T>
+__global__ void affine_act_pool_kernel(int n, int h, int w, int C, const T *__restrict__ x,
+                                       const float *__restrict__ scale, const float *__restrict__ shift,
+                                       const T *__restrict__ res, const float *__restrict__ rs,
+                                       const float *__restrict__ rb, int relu, T *__restrict__ y,
+                                       T *__restrict__ yp, uint8_t *__restrict__ idx) {
+  const int ho = h / 2, wo = w / 2, G = C / 8;
+  const long long total = (long long)n * ho * wo * G;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int gq = (int)(i % G);
+    const long long op = i / G;
+    const int ox = (int)(op % wo);
+    const long long tq = op / wo;
+    const int oy = (int)(tq % ho);
+    const int nn = (int)(tq / ho);
+    const int c = gq * 8;
+    const f32x4 s0 = *reinterpret_cast<const f32x4 *>(scale + c), s1 = *reinterpret_cast<const f32x4 *>(scale + c + 4);
+    const f32x4 b0 = *reinterpret_cast<const f32x4 *>(shift + c), b1 = *reinterpret_cast<const f32x4 *>(shift + c + 4);
+    f32x4 r0s = {1.f, 1.f, 1.f, 1.f}, r1s = r0s, r0b = {0.f, 0.f, 0.f, 0.f}, r1b = r0b;
+    if (rs) {
+      r0s = *reinterpret_cast<const f32x4 *>(rs + c); r1s = *reinterpret_cast<const f32x4 *>(rs + c + 4);
+      r0b = *reinterpret_cast<const f32x4 *>(rb + c); r1b = *reinterpret_cast<const f32x4 *>(rb + c + 4);
+    }
+    float m[8];
+    uint8_t id[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const long long e = (((long long)nn * h + 2 * oy + (k >> 1)) * w + 2 * ox + (k & 1)) * C + c;
+      f32x4 v0, v1, q0, q1;
+      load8<T>(x + e, v0, v1);
+      v0 = v0 * s0 + b0;
+      v1 = v1 * s1 + b1;
+      if (res) {
+        load8<T>(res + e, q0, q1);
+        if (rs) { q0 = q0 * r0s + r0b; q1 = q1 * r1s + r1b; }
+        v0 += q0;
+        v1 += q1;
+      }
+      if (relu) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v0[j] = fmaxf(v0[j], 0.f); v1[j] = fmaxf(v1[j], 0.f); }
+      }
+      store8<T>(y + e, v0, v1);
+      // compare the stored values: round to T and back
+      T rt[8];
+      const float vv[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        Elt<T>::store(rt, j, vv[j]);
+        const float sv = Elt<T>::load(rt, j);
+        if (k == 0) { m[j] = sv; id[j] = 0; }
+        else if (sv > m[j] || (sv != sv && m[j] == m[j])) { m[j] = sv; id[j] = (uint8_t)k; }
+      }
+    }
+    store8<T>(yp + op * C + c, f32x4{m[0], m[1], m[2], m[3]}, f32x4{m[4], m[5], m[6], m[7]});
+    *reinterpret_cast<uint2 *>(idx + op * C + c) =
+        uint2{(uint32_t)id[0] | ((uint32_t)id[1] << 8) | ((uint32_t)id[2] << 16) | ((uint32_t)id[3] << 24),
+              (uint32_t)id[4] | ((uint32_t)id[5] << 8) | ((uint32_t)id[6] << 16) | ((uint32_t)id[7] << 24)};
+  }
+}
+
 // ---------------------------------------------------------------------------
 // BN backward
 struct BnBwd {
@@ -515,6 +581,29 @@ extern "C" int rr_affine_act(int dtype, long long P, int C, const void *x, const
     hipLaunchKernelGGL(affine_act_kernel<float>, dim3(grid), dim3(256), 0, st, P, C,
                        (const float *)x, scale, shift, alpha, (const float *)res, res_scale,
                        res_shift, relu, (float *)y);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_affine_act_pool(int dtype, int n, int h, int w, int C, const void *x,
+                                  const float *scale, const float *shift, const void *res,
+                                  const float *res_scale, const float *res_shift, int relu, void *y,
+                                  void *y_pool, uint8_t *idx, rr_stream stream) {
+  if (n <= 0 || h <= 0 || w <= 0 || h % 2 || w % 2 || C <= 0 || C % 8 || !x || !scale || !shift ||
+      !y || !y_pool || !idx)
+    return RR_EINVAL;
+  if ((res_scale == nullptr) != (res_shift == nullptr) || (res_scale && !res)) return RR_EINVAL;
+  const long long total = (long long)n * (h / 2) * (w / 2) * (C / 8);
+  const int grid = rr_grid_cap((total + 255) / 256, 8192);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(affine_act_pool_kernel<bf16_t>, dim3(grid), dim3(256), 0, st, n, h, w, C,
+                       (const bf16_t *)x, scale, shift, (const bf16_t *)res, res_scale, res_shift, relu,
+                       (bf16_t *)y, (bf16_t *)y_pool, idx);
+  else
+    hipLaunchKernelGGL(affine_act_pool_kernel<float>, dim3(grid), dim3(256), 0, st, n, h, w, C,
+                       (const float *)x, scale, shift, (const float *)res, res_scale, res_shift, relu,
+                       (float *)y, (float *)y_pool, idx);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

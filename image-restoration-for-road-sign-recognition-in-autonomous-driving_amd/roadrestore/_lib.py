@@ -72,6 +72,7 @@ _SIGS = {
     "rr_bn_finalize_workspace": (S_, [I_, I_]),
     "rr_bn_eval_affine": (I_, [I_, P_, P_, P_, P_, F_, P_, P_, P_]),
     "rr_affine_act": (I_, [I_, L_, I_, P_, P_, P_, P_, P_, P_, P_, I_, P_, P_]),
+    "rr_affine_act_pool": (I_, [I_, I_, I_, I_, I_, P_, P_, P_, P_, P_, P_, I_, P_, P_, P_, P_]),
     "rr_bn_bwd_blocks": (I_, [C.POINTER(BnBwdDesc)]),
     "rr_bn_bwd_reduce": (I_, [C.POINTER(BnBwdDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_, P_, P_,
                               P_, P_]),

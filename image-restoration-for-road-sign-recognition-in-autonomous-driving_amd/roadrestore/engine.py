@@ -314,7 +314,9 @@ def block_has_shortcut(blk):
     return len(blk.shortcut) > 0
 
 
-def resblock_forward(blk, x1, x2, n, h, w, wc, dt, training, need_bwd):
+def resblock_forward(blk, x1, x2, n, h, w, wc, dt, training, need_bwd, pool=False):
+    """-> (out, S), or (out, S, (pooled, idx)) with ``pool`` (the 2x2 max-pool
+    that follows the encoder blocks, fused into the residual tail)."""
     cb = blk.conv_block
     c1, bn1, pr, c2, bn2 = cb[0], cb[1], cb[2], cb[3], cb[4]
     cout = c1.weight.shape[0]
@@ -333,17 +335,25 @@ def resblock_forward(blk, x1, x2, n, h, w, wc, dt, training, need_bwd):
         s, _, sts = ops.igemm(RR_CONV1X1, x1, x2, n, h, w, pks[0], cout, bias=sc0.bias,
                               stats=training)
         ss, shs, ms, is_ = _bn_affine(sc1, sts, sc0.bias, P, training)
-        out = ops.affine_act(t2, s2, sh2, res=s, res_scale=ss, res_shift=shs, relu=True)
+        res, rsc, rsh = s, ss, shs
         if need_bwd:
             S.update(s=s, ms=ms, is_=is_, pks=pks)
     else:
         if x2 is not None:
             raise RuntimeError("identity shortcut with a concatenated input")
-        out = ops.affine_act(t2, s2, sh2, res=x1, relu=True)
+        res, rsc, rsh = x1, None, None
+    pooled = None
+    if pool and _FUSED_POOL and h % 2 == 0 and w % 2 == 0 and cout % 8 == 0:
+        out, yp, idx = ops.affine_act_pool(t2, s2, sh2, res=res, res_scale=rsc, res_shift=rsh, relu=True)
+        pooled = (yp, idx)
+    else:
+        out = ops.affine_act(t2, s2, sh2, res=res, res_scale=rsc, res_shift=rsh, relu=True)
+        if pool:
+            pooled = ops.maxpool2_fwd(out)
     if need_bwd:
         S.update(t1=t1, a1=a1, t2=t2, out=out, s1=s1, sh1=sh1, m1=m1, i1=i1, m2=m2, i2=i2,
                  pk1=pk1, pk2=pk2)
-    return out, S
+    return (out, S, pooled) if pool else (out, S)
 
 
 def resblock_zero_grad_params(blk):
@@ -425,12 +435,12 @@ def resunet_forward(m, x, wc, dt, training, need_bwd):
                                    alpha=pr.weight, want_pre=need_bwd)
     if need_bwd:
         S.e1pre = e1pre
-    r1, S.res1 = resblock_forward(m.res1, e1, None, n, H, W, wc, dt, training, need_bwd)
-    p1, i1 = ops.maxpool2_fwd(r1)
-    r2, S.res2 = resblock_forward(m.res2, p1, None, n, H // 2, W // 2, wc, dt, training, need_bwd)
-    p2, i2 = ops.maxpool2_fwd(r2)
-    r3, S.res3 = resblock_forward(m.res3, p2, None, n, H // 4, W // 4, wc, dt, training, need_bwd)
-    p3, i3 = ops.maxpool2_fwd(r3)
+    r1, S.res1, (p1, i1) = resblock_forward(m.res1, e1, None, n, H, W, wc, dt, training, need_bwd,
+                                            pool=True)
+    r2, S.res2, (p2, i2) = resblock_forward(m.res2, p1, None, n, H // 2, W // 2, wc, dt, training,
+                                            need_bwd, pool=True)
+    r3, S.res3, (p3, i3) = resblock_forward(m.res3, p2, None, n, H // 4, W // 4, wc, dt, training,
+                                            need_bwd, pool=True)
     b = p3
     for i in range(3):
         b, S[f"bottleneck.{i}"] = resblock_forward(m.bottleneck[i], b, None, n, H // 8, W // 8, wc,
@@ -474,6 +484,8 @@ def resunet_zero_grad_params(m):
 # A/B switch for the fused first-conv backward (RR_FUSED_FIRST_WGRAD=0: the
 # prelu_bwd + im2col + wgrad sequence)
 _FUSED_FIRST_WGRAD = os.environ.get("RR_FUSED_FIRST_WGRAD", "1") != "0"
+# A/B switch for the residual tail + max-pool fusion (RR_FUSED_POOL=0: separate pool)
+_FUSED_POOL = os.environ.get("RR_FUSED_POOL", "1") != "0"
 
 
 def resunet_backward(m, S, g_out, sink):

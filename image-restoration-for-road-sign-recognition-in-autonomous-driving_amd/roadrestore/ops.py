@@ -23,7 +23,7 @@ __all__ = [
     "prelu_bwd", "conv_out_fwd", "conv_out_bwd", "nchw_to_nhwc", "nhwc_to_nchw",
     "loss_fwd", "loss_bwd", "adamw_", "to_uint8_hwc", "psnr_u8", "argmax_rows",
     "adaptive_avgpool_flatten", "zero_", "resize_bilinear_u8", "ssim_u8", "distort_u8",
-    "motion_blur_kernel", "first_conv_wgrad_act",
+    "motion_blur_kernel", "first_conv_wgrad_act", "affine_act_pool",
 ]
 
 
@@ -303,6 +303,19 @@ def affine_act(x, scale, shift, alpha=None, res=None, res_scale=None, res_shift=
                                     _p(alpha), _p(res), _p(res_scale), _p(res_shift), int(relu),
                                     _p(out), stream()), "rr_affine_act")
     return out
+
+
+def affine_act_pool(x, scale, shift, res=None, res_scale=None, res_shift=None, relu=True):
+    """Residual tail fused with MaxPool2d(2, 2): -> (y, y_pool, idx)."""
+    _need_cuda(x)
+    n, h, w, Cc = x.shape
+    y = torch.empty_like(x)
+    yp = torch.empty((n, h // 2, w // 2, Cc), dtype=x.dtype, device=x.device)
+    idx = torch.empty((n, h // 2, w // 2, Cc), dtype=torch.uint8, device=x.device)
+    lib().check(lib().rr_affine_act_pool(rr_dtype(x.dtype), n, h, w, Cc, _p(x), _p(scale), _p(shift),
+                                         _p(res), _p(res_scale), _p(res_shift), int(relu), _p(y),
+                                         _p(yp), _p(idx), stream()), "rr_affine_act_pool")
+    return y, yp, idx
 
 
 def bn_backward(g, t0, mean0, inv0, gamma0, *, mask_kind=0, aux=None, aff_s=None, aff_b=None,

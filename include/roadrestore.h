@@ -194,6 +194,14 @@ typedef struct {
   int32_t mask_kind;
   int32_t nbn;          /* 1 or 2 */
 } rr_bnbwd_desc;
+/* residual tail (as rr_affine_act, without PReLU) over an [n][h][w][C] NHWC
+ * activation fused with MaxPool2d(2, 2) (14:125-131): y, the pooled y_pool
+ * [n][h/2][w/2][C] and the first-max window index idx (as rr_maxpool2_fwd,
+ * on the stored values) */
+int rr_affine_act_pool(int dtype, int n, int h, int w, int C, const void *x,
+                       const float *scale, const float *shift, const void *res,
+                       const float *res_scale, const float *res_shift, int relu,
+                       void *y, void *y_pool, uint8_t *idx, rr_stream stream);
 int rr_bn_bwd_blocks(const rr_bnbwd_desc *d);
 int rr_bn_bwd_reduce(const rr_bnbwd_desc *d, const void *g, const void *aux,
                      const float *aff_s, const float *aff_b, const float *alpha,

@@ -496,3 +496,21 @@ def test_first_conv_wgrad_act_fused(dev, act, n, h, w):
     if act == 2:
         refa = (gf.double() * tf.double() * (tf <= 0)).sum().item()
         assert abs(da.item() - refa) <= 1e-4 * max(1.0, abs(refa))
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shortcut", [False, True])
+def test_affine_act_pool_equals_separate(dev, dt, shortcut):
+    """rr_affine_act_pool == rr_affine_act then rr_maxpool2_fwd, bitwise
+    (the pooling compares the stored, dtype-rounded values); ties included"""
+    from roadrestore import ops
+    n, h, w, C = 3, 8, 12, 64
+    x = rnd(n, h, w, C, seed=1).to(dev, dt)
+    x[:, 0::2, 0::2, :8] = x[:, 1::2, 1::2, :8]          # forced window ties
+    res = rnd(n, h, w, C, seed=2).to(dev, dt)
+    sc, sh = (rnd(C, seed=3) * 0.5 + 1).to(dev), rnd(C, seed=4).to(dev)
+    rs, rb = ((rnd(C, seed=5) * 0.5 + 1).to(dev), rnd(C, seed=6).to(dev)) if shortcut else (None, None)
+    y0 = ops.affine_act(x, sc, sh, res=res, res_scale=rs, res_shift=rb, relu=True)
+    p0, i0 = ops.maxpool2_fwd(y0)
+    y1, p1, i1 = ops.affine_act_pool(x, sc, sh, res=res, res_scale=rs, res_shift=rb, relu=True)
+    assert torch.equal(y0, y1) and torch.equal(p0, p1) and torch.equal(i0, i1)
