@@ -153,10 +153,19 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    # rehearsal switches for the N > 1 path on a 1-GPU box (never set by the
+    # driver): RR_BENCH_ONE_DEVICE=1 puts every rank on cuda:0,
+    # RR_DIST_BACKEND=gloo replaces RCCL (which refuses two ranks on one GPU)
+    if os.environ.get("RR_BENCH_ONE_DEVICE") == "1":
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("RR_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import roadrestore as rr
     from roadrestore import ops
@@ -214,8 +223,10 @@ def main():
         with torch.cuda.graph(graph):
             loss_g = step()
         torch.cuda.synchronize()
-    probe = None if (a.no_probe or graph is not None) else KernelProbe()
-    ops.PROBE = probe
+    # the kernel probe (HIP events around every GEMM launch) never runs inside
+    # the timed region: it times separate eager steps afterwards
+    probe = None
+    ops.PROBE = None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -229,16 +240,16 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    ops.PROBE = None
     if graph is not None:
         loss = loss_g
-        if not a.no_probe:
-            # kernel durations for the roofline: the same kernels, timed eagerly
-            probe = KernelProbe()
-            ops.PROBE = probe
-            for _ in range(a.probe_steps):
-                step()
-            ops.PROBE = None
+    if not a.no_probe:
+        # kernel durations for the roofline: the same kernels, timed eagerly
+        # (every rank runs these steps: the backward's all-reduces pair up)
+        probe = KernelProbe()
+        ops.PROBE = probe
+        for _ in range(a.probe_steps):
+            step()
+        ops.PROBE = None
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -264,11 +275,9 @@ def main():
                 "flop_per_launch": fl / cnt}
         tot_fl = sum(v[1] for v in agg.values())
         tot_ms = sum(v[2] for v in agg.values())
-        nprobe = a.probe_steps if graph is not None else a.steps
-        kernels = {"conv_gemm_ms_per_step": round(tot_ms / nprobe, 3),
+        kernels = {"conv_gemm_ms_per_step": round(tot_ms / a.probe_steps, 3),
                    "conv_gemm_tflops": round(tot_fl / (tot_ms * 1e-3) / 1e12, 2),
-                   "probe": "eager steps after the graph timing" if graph is not None
-                            else "the timed steps"}
+                   "probe": f"{a.probe_steps} eager steps after the timed region"}
 
     imgs = world * B * a.steps
     value = imgs / el
