@@ -174,6 +174,9 @@ __global__ void affine_act_pool_kernel(int n, int h, int w, int C, const T *__re
 struct BnBwd {
   long long P;
   int C, mask_kind, nbn;
+  int h, w;                         // mask_kind 3: pixel grid of the rows
+  const void *pdy;                  // mask_kind 3: pooled grad [n][h/2][w/2][C]
+  const uint8_t *pidx;              // mask_kind 3: window index of the max
   const void *g, *aux;
   const float *aff_s, *aff_b, *alpha;
   const void *t0, *t1;
@@ -212,7 +215,26 @@ __device__ __forceinline__ void bwd_gm8(const BnBwd &a, long long e, const float
   load8<T>((const T *)a.g + e, g0, g1);
   g[0] = g0[0]; g[1] = g0[1]; g[2] = g0[2]; g[3] = g0[3];
   g[4] = g1[0]; g[5] = g1[1]; g[6] = g1[2]; g[7] = g1[3];
-  if constexpr (MASK == 1) {
+  if constexpr (MASK == 3) {
+    // + the MaxPool2d(2, 2) backward: the pooled grad goes to the window's
+    // first max (rr_maxpool2_bwd's routing), added before the ReLU mask
+    const int C = a.C;
+    const int r = (int)(e / C), c = (int)(e - (long long)r * C);
+    const int hw = a.h * a.w;
+    const int nn = r / hw, rem = r - nn * hw, y = rem / a.w, x = rem - y * a.w;
+    const long long op = ((long long)nn * (a.h >> 1) + (y >> 1)) * (a.w >> 1) + (x >> 1);
+    const int k = ((y & 1) << 1) | (x & 1);
+    const uint2 id = *reinterpret_cast<const uint2 *>(a.pidx + op * C + c);
+    f32x4 p0, p1;
+    load8<T>((const T *)a.pdy + op * C + c, p0, p1);
+    const float pv[8] = {p0[0], p0[1], p0[2], p0[3], p1[0], p1[1], p1[2], p1[3]};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ij = (int)(((j < 4 ? id.x : id.y) >> (8 * (j & 3))) & 0xff);
+      g[j] += ij == k ? pv[j] : 0.f;
+    }
+  }
+  if constexpr (MASK == 1 || MASK == 3) {
     f32x4 m0, m1;
     load8<T>((const T *)a.aux + e, m0, m1);
     const float m[8] = {m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
@@ -616,7 +638,12 @@ extern "C" int rr_bn_bwd_blocks(const rr_bnbwd_desc *d) {
 static int bnbwd_check(const rr_bnbwd_desc *d) {
   if (!d || d->P <= 0 || d->C <= 0 || d->C % 4 || d->C / 4 > 256) return RR_EINVAL;
   if (d->nbn != 1 && d->nbn != 2) return RR_EINVAL;
-  if (d->mask_kind < 0 || d->mask_kind > 2) return RR_EINVAL;
+  if (d->mask_kind < 0 || d->mask_kind > 3) return RR_EINVAL;
+  if (d->mask_kind == 3) {
+    if (!d->pool_dy || !d->pool_idx || d->h <= 0 || d->w <= 0 || d->h % 2 || d->w % 2 ||
+        d->P % ((long long)d->h * d->w) || d->C % 8 || 256 % (d->C / 8) || d->P > 0x7fffffffLL)
+      return RR_EUNSUPPORTED;               // 8-channel kernels only
+  }
   return RR_OK;
 }
 
@@ -626,6 +653,7 @@ static BnBwd make_bnbwd(const rr_bnbwd_desc *d, const void *g, const void *aux,
                         const float *mean1, const float *inv1) {
   BnBwd a;
   a.P = d->P; a.C = d->C; a.mask_kind = d->mask_kind; a.nbn = d->nbn;
+  a.h = d->h; a.w = d->w; a.pdy = d->pool_dy; a.pidx = d->pool_idx;
   a.g = g; a.aux = aux; a.aff_s = aff_s; a.aff_b = aff_b; a.alpha = alpha;
   a.t0 = t0; a.t1 = t1; a.mean0 = mean0; a.inv0 = inv0; a.mean1 = mean1; a.inv1 = inv1;
   return a;
@@ -658,7 +686,8 @@ extern "C" int rr_bn_bwd_reduce(const rr_bnbwd_desc *d, const void *g, const voi
     switch (d->mask_kind * 2 + (d->nbn - 1)) {                    \
       case 0: RR_RED8(TT, 0, 1); break; case 1: RR_RED8(TT, 0, 2); break; \
       case 2: RR_RED8(TT, 1, 1); break; case 3: RR_RED8(TT, 1, 2); break; \
-      case 4: RR_RED8(TT, 2, 1); break; default: RR_RED8(TT, 2, 2); break; \
+      case 4: RR_RED8(TT, 2, 1); break; case 5: RR_RED8(TT, 2, 2); break; \
+      case 6: RR_RED8(TT, 3, 1); break; default: RR_RED8(TT, 3, 2); break; \
     }
     if (d->dtype == RR_BF16) { RR_RED8_T(bf16_t) } else { RR_RED8_T(float) }
 #undef RR_RED8_T
@@ -713,7 +742,7 @@ extern "C" int rr_bn_bwd_apply(const rr_bnbwd_desc *d, const void *g, const void
     else { if (gm_out) RR_APP8(TT, M, 2, true); else RR_APP8(TT, M, 2, false); }
 #define RR_APP8_T(TT)                                                           \
     if (d->mask_kind == 0) { RR_APP8_M(TT, 0) } else if (d->mask_kind == 1) { RR_APP8_M(TT, 1) } \
-    else { RR_APP8_M(TT, 2) }
+    else if (d->mask_kind == 2) { RR_APP8_M(TT, 2) } else { RR_APP8_M(TT, 3) }
     if (d->dtype == RR_BF16) { RR_APP8_T(bf16_t) } else { RR_APP8_T(float) }
 #undef RR_APP8_T
 #undef RR_APP8_M

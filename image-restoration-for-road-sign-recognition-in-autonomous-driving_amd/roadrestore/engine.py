@@ -364,7 +364,9 @@ def resblock_zero_grad_params(blk):
     return z
 
 
-def resblock_backward(blk, S, g_out, sink):
+def resblock_backward(blk, S, g_out, sink, pool=None):
+    """``pool=(dy_pool, idx)``: the output also fed a 2x2 max-pool whose
+    backward is fused into the tail BN backward (no separate pass)."""
     cb = blk.conv_block
     c1, bn1, pr, c2, bn2 = cb[0], cb[1], cb[2], cb[3], cb[4]
     n, h, w = S.n, S.h, S.w
@@ -377,14 +379,14 @@ def resblock_backward(blk, S, g_out, sink):
     gx1 = gx2 = None
     if has_sc:
         sc0, sc1 = blk.shortcut[0], blk.shortcut[1]
-        r = ops.bn_backward(g_out, S.t2, S.m2, S.i2, bn2.weight, mask_kind=1, aux=S.out,
+        r = ops.bn_backward(g_out, S.t2, S.m2, S.i2, bn2.weight, mask_kind=1, aux=S.out, pool=pool,
                             t1=S.s, mean1=S.ms, inv1=S.is_, gamma1=sc1.weight,
                             outs=dict(dgamma0=sink[bn2.weight], dbeta0=sink[bn2.bias],
                                       dgamma1=sink[sc1.weight], dbeta1=sink[sc1.bias]))
         dt2, ds = r["dt0"], r["dt1"]
     else:
         gx1 = torch.empty_like(x1)
-        r = ops.bn_backward(g_out, S.t2, S.m2, S.i2, bn2.weight, mask_kind=1, aux=S.out,
+        r = ops.bn_backward(g_out, S.t2, S.m2, S.i2, bn2.weight, mask_kind=1, aux=S.out, pool=pool,
                             want_gm=True, gm_out=gx1,
                             outs=dict(dgamma0=sink[bn2.weight], dbeta0=sink[bn2.bias]))
         dt2 = r["dt0"]
@@ -486,6 +488,8 @@ def resunet_zero_grad_params(m):
 _FUSED_FIRST_WGRAD = os.environ.get("RR_FUSED_FIRST_WGRAD", "1") != "0"
 # A/B switch for the residual tail + max-pool fusion (RR_FUSED_POOL=0: separate pool)
 _FUSED_POOL = os.environ.get("RR_FUSED_POOL", "1") != "0"
+# A/B switch for the encoder max-pool backward fused into the tail BN backward
+_FUSED_POOL_BWD = os.environ.get("RR_FUSED_POOL_BWD", "1") != "0"
 
 
 def resunet_backward(m, S, g_out, sink):
@@ -504,12 +508,19 @@ def resunet_backward(m, S, g_out, sink):
     sink.ready(_params(m.up3))
     for i in (2, 1, 0):
         g_b, _ = resblock_backward(m.bottleneck[i], S[f"bottleneck.{i}"], g_b, sink)
-    ops.maxpool2_bwd(g_b, S.i3, H // 4, W // 4, out=g_r3, accumulate=True)
-    g_p2, _ = resblock_backward(m.res3, S.res3, g_r3, sink)
-    ops.maxpool2_bwd(g_p2, S.i2, H // 2, W // 2, out=g_r2, accumulate=True)
-    g_p1, _ = resblock_backward(m.res2, S.res2, g_r2, sink)
-    ops.maxpool2_bwd(g_p1, S.i1, H, W, out=g_r1, accumulate=True)
-    g_e1, _ = resblock_backward(m.res1, S.res1, g_r1, sink)
+    if _FUSED_POOL_BWD and g_b.dtype == torch.bfloat16:
+        # each encoder block's output fed the skip concat and the pool: the
+        # pool backward runs inside that block's tail BN backward
+        g_p2, _ = resblock_backward(m.res3, S.res3, g_r3, sink, pool=(g_b, S.i3))
+        g_p1, _ = resblock_backward(m.res2, S.res2, g_r2, sink, pool=(g_p2, S.i2))
+        g_e1, _ = resblock_backward(m.res1, S.res1, g_r1, sink, pool=(g_p1, S.i1))
+    else:
+        ops.maxpool2_bwd(g_b, S.i3, H // 4, W // 4, out=g_r3, accumulate=True)
+        g_p2, _ = resblock_backward(m.res3, S.res3, g_r3, sink)
+        ops.maxpool2_bwd(g_p2, S.i2, H // 2, W // 2, out=g_r2, accumulate=True)
+        g_p1, _ = resblock_backward(m.res2, S.res2, g_r2, sink)
+        ops.maxpool2_bwd(g_p1, S.i1, H, W, out=g_r1, accumulate=True)
+        g_e1, _ = resblock_backward(m.res1, S.res1, g_r1, sink)
     pr = m.enc1[1]
     if g_e1.dtype == torch.bfloat16 and W % 8 == 0 and _FUSED_FIRST_WGRAD:
         # PReLU backward + first-conv wgrad in one pass over the image

@@ -320,15 +320,23 @@ def affine_act_pool(x, scale, shift, res=None, res_scale=None, res_shift=None, r
 
 def bn_backward(g, t0, mean0, inv0, gamma0, *, mask_kind=0, aux=None, aff_s=None, aff_b=None,
                 alpha=None, t1=None, mean1=None, inv1=None, gamma1=None, want_gm=False,
-                gm_out=None, outs=None):
+                gm_out=None, outs=None, pool=None):
     """Full BN backward (reduce + finalize + apply) for one or two BNs that
     share the upstream gradient.  Returns dict with dt0, dt1, gm, dgamma0,
-    dbeta0, dgamma1, dbeta1, dalpha."""
+    dbeta0, dgamma1, dbeta1, dalpha.  ``pool=(dy_pool, idx)`` with
+    mask_kind 1: the 2x2 max-pool backward is added to g before the ReLU mask
+    (mask kind 3, g: [n, h, w, C])."""
     Cc = g.shape[-1]
     P = g.numel() // Cc
     nbn = 2 if t1 is not None else 1
     dev = g.device
-    d = BnBwdDesc(rr_dtype(g.dtype), P, Cc, mask_kind, nbn)
+    d = BnBwdDesc(rr_dtype(g.dtype), P, Cc, mask_kind, nbn, 0, 0, None, None)
+    if pool is not None:
+        if mask_kind != 1 or g.dim() != 4:
+            raise ValueError("pool backward fusion needs the ReLU mask and an [n, h, w, C] grad")
+        pdy, pidx = pool
+        d.mask_kind, d.h, d.w = 3, g.shape[1], g.shape[2]
+        d.pool_dy, d.pool_idx = _p(pdy.contiguous()), _p(pidx)
     blocks = lib().rr_bn_bwd_blocks(C.byref(d))
     part = torch.empty(blocks * Cc * 3 + blocks, dtype=torch.float32, device=dev)
     s = stream()

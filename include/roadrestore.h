@@ -191,8 +191,14 @@ typedef struct {
   int32_t dtype;
   int64_t P;
   int32_t C;
-  int32_t mask_kind;
+  int32_t mask_kind;    /* 0 none, 1 ReLU (aux = ReLU output), 2 PReLU (aux = t),
+                           3 ReLU + MaxPool2d(2,2) backward: g + unpool(pool_dy, pool_idx)
+                           before the mask (the encoder block output feeds both the
+                           skip concat and the pool, 14:125-131) */
   int32_t nbn;          /* 1 or 2 */
+  int32_t h, w;         /* mask_kind 3: the [P] rows are [n][h][w] pixels (h, w even) */
+  const void *pool_dy;  /* mask_kind 3: [n][h/2][w/2][C] grad of the pooled output */
+  const uint8_t *pool_idx; /* mask_kind 3: rr_maxpool2_fwd / rr_affine_act_pool index */
 } rr_bnbwd_desc;
 /* residual tail (as rr_affine_act, without PReLU) over an [n][h][w][C] NHWC
  * activation fused with MaxPool2d(2, 2) (14:125-131): y, the pooled y_pool

@@ -33,7 +33,9 @@ def test_descriptor_layouts():
     from roadrestore._lib import BnBwdDesc, IgemmDesc, WgradDesc
     assert ctypes.sizeof(IgemmDesc) == 15 * 4
     assert ctypes.sizeof(WgradDesc) == 9 * 4
-    assert ctypes.sizeof(BnBwdDesc) == 32     # int32, pad, int64, 3 x int32, pad (C layout)
+    # int32, pad, int64, 5 x int32, pad, 2 pointers (C layout of rr_bnbwd_desc)
+    assert ctypes.sizeof(BnBwdDesc) == 56
+    assert (BnBwdDesc.h.offset, BnBwdDesc.pool_dy.offset, BnBwdDesc.pool_idx.offset) == (28, 40, 48)
 
 
 def test_status_codes_raise():

@@ -514,3 +514,33 @@ def test_affine_act_pool_equals_separate(dev, dt, shortcut):
     p0, i0 = ops.maxpool2_fwd(y0)
     y1, p1, i1 = ops.affine_act_pool(x, sc, sh, res=res, res_scale=rs, res_shift=rb, relu=True)
     assert torch.equal(y0, y1) and torch.equal(p0, p1) and torch.equal(i0, i1)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("nbn", [1, 2])
+def test_bn_backward_pool_fused(dev, dt, nbn):
+    """mask kind 3 (the encoder max-pool backward inside the tail BN
+    backward) == rr_maxpool2_bwd(accumulate) then mask kind 1; fp32 to
+    rounding, bf16 within bf16 storage of the summed gradient"""
+    from roadrestore import ops
+    n, h, w, C = 2, 8, 12, 64
+    g = rnd(n, h, w, C, seed=1).to(dev, dt)
+    out = rnd(n, h, w, C, seed=2).to(dev, dt)
+    t0 = rnd(n, h, w, C, seed=3).to(dev, dt)
+    t1 = rnd(n, h, w, C, seed=4).to(dev, dt) if nbn == 2 else None
+    _, idx = ops.maxpool2_fwd(out)
+    pdy = rnd(n, h // 2, w // 2, C, seed=5).to(dev, dt)
+    m0, i0 = rnd(C, seed=6).to(dev), (rnd(C, seed=7).abs() + 0.5).to(dev)
+    m1, i1 = (rnd(C, seed=8).to(dev), (rnd(C, seed=9).abs() + 0.5).to(dev)) if nbn == 2 else (None, None)
+    gam0 = rnd(C, seed=10).to(dev)
+    gam1 = rnd(C, seed=11).to(dev) if nbn == 2 else None
+    kw = dict(mask_kind=1, aux=out, t1=t1, mean1=m1, inv1=i1, gamma1=gam1, want_gm=True)
+    fused = ops.bn_backward(g, t0, m0, i0, gam0, pool=(pdy, idx), **kw)
+    g2 = g.clone()
+    ops.maxpool2_bwd(pdy, idx, h, w, out=g2, accumulate=True)
+    sep = ops.bn_backward(g2, t0, m0, i0, gam0, **kw)
+    tol = 1e-5 if dt == torch.float32 else 2e-2
+    for k in ("dt0", "gm", "dgamma0", "dbeta0") + (("dt1", "dgamma1", "dbeta1") if nbn == 2 else ()):
+        a, b = fused[k].float(), sep[k].float()
+        rel = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+        assert rel <= tol, (k, rel)
