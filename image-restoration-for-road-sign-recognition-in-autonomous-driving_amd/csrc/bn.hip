@@ -103,6 +103,54 @@ __global__ void affine_act_kernel(long long P, int C, const T *__restrict__ x,
   }
 }
 
+// 8-channel form of affine_act_kernel (C % 8 == 0, C / 8 divides 256): the
+// thread's channel group is fixed over the grid-stride walk, so scale / shift
+// live in registers and every access is a 16-B vector
+template <typename T>
+__global__ void affine_act8_kernel(long long P, int C, const T *__restrict__ x,
+                                   const float *__restrict__ scale, const float *__restrict__ shift,
+                                   const float *alpha, const T *__restrict__ res,
+                                   const float *__restrict__ rs, const float *__restrict__ rb,
+                                   int relu, T *__restrict__ y) {
+  const int G = C / 8;
+  const int c = (threadIdx.x % G) * 8;
+  const f32x4 s0 = *reinterpret_cast<const f32x4 *>(scale + c), s1 = *reinterpret_cast<const f32x4 *>(scale + c + 4);
+  const f32x4 b0 = *reinterpret_cast<const f32x4 *>(shift + c), b1 = *reinterpret_cast<const f32x4 *>(shift + c + 4);
+  f32x4 r0s = {1.f, 1.f, 1.f, 1.f}, r1s = r0s, r0b = {0.f, 0.f, 0.f, 0.f}, r1b = r0b;
+  if (rs) {
+    r0s = *reinterpret_cast<const f32x4 *>(rs + c); r1s = *reinterpret_cast<const f32x4 *>(rs + c + 4);
+    r0b = *reinterpret_cast<const f32x4 *>(rb + c); r1b = *reinterpret_cast<const f32x4 *>(rb + c + 4);
+  }
+  const float al = alpha ? alpha[0] : 0.f;
+  const long long stride = ((long long)gridDim.x * blockDim.x) / G;
+  for (long long r = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / G; r < P; r += stride) {
+    const long long e = r * C + c;
+    f32x4 v0, v1;
+    load8<T>(x + e, v0, v1);
+    v0 = v0 * s0 + b0;
+    v1 = v1 * s1 + b1;
+    if (alpha) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v0[k] = v0[k] > 0.f ? v0[k] : al * v0[k];
+        v1[k] = v1[k] > 0.f ? v1[k] : al * v1[k];
+      }
+    }
+    if (res) {
+      f32x4 q0, q1;
+      load8<T>(res + e, q0, q1);
+      if (rs) { q0 = q0 * r0s + r0b; q1 = q1 * r1s + r1b; }
+      v0 += q0;
+      v1 += q1;
+    }
+    if (relu) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { v0[k] = fmaxf(v0[k], 0.f); v1[k] = fmaxf(v1[k], 0.f); }
+    }
+    store8<T>(y + e, v0, v1);
+  }
+}
+
 // residual tail + MaxPool2d(2, 2) in one pass (14:114-115 then 14:125-131):
 // y = relu(x * scale + shift + res * rs + rb) for the 4 pixels of a pooling
 // window (8 channels per thread), and the window max / first-max index of
@@ -593,8 +641,21 @@ extern "C" int rr_affine_act(int dtype, long long P, int C, const void *x, const
                              rr_stream stream) {
   if (P <= 0 || C <= 0 || C % 4 || !x || !scale || !shift || !y) return RR_EINVAL;
   if ((res_scale == nullptr) != (res_shift == nullptr)) return RR_EINVAL;
-  const int grid = rr_grid_cap((P * C / 4 + 255) / 256, 4096);
   hipStream_t st = (hipStream_t)stream;
+  if (C % 8 == 0 && 256 % (C / 8) == 0) {
+    const int grid8 = rr_grid_cap((P * C / 8 + 255) / 256, 4096);
+    if (dtype == RR_BF16)
+      hipLaunchKernelGGL(affine_act8_kernel<bf16_t>, dim3(grid8), dim3(256), 0, st, P, C,
+                         (const bf16_t *)x, scale, shift, alpha, (const bf16_t *)res, res_scale,
+                         res_shift, relu, (bf16_t *)y);
+    else
+      hipLaunchKernelGGL(affine_act8_kernel<float>, dim3(grid8), dim3(256), 0, st, P, C,
+                         (const float *)x, scale, shift, alpha, (const float *)res, res_scale,
+                         res_shift, relu, (float *)y);
+    RR_CHECK_LAUNCH();
+    return RR_OK;
+  }
+  const int grid = rr_grid_cap((P * C / 4 + 255) / 256, 4096);
   if (dtype == RR_BF16)
     hipLaunchKernelGGL(affine_act_kernel<bf16_t>, dim3(grid), dim3(256), 0, st, P, C,
                        (const bf16_t *)x, scale, shift, alpha, (const bf16_t *)res, res_scale,

@@ -779,6 +779,79 @@ __global__ void maxpool_fwd_kernel(int n, int h, int w, int C, const T *__restri
   }
 }
 
+// 8-channel forms (C % 8 == 0, < 2^31 elements): 16-B accesses, 32-bit
+// index math; same routing (first max in window order) and NaN rule
+template <typename T>
+__global__ void maxpool_fwd8_kernel(int n, int h, int w, int C, const T *__restrict__ x,
+                                    T *__restrict__ y, uint8_t *__restrict__ idx) {
+  const int ho = h / 2, wo = w / 2, G = C / 8;
+  const int total = n * ho * wo * G;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int g = i % G, op = i / G;
+    const int ox = op % wo, t = op / wo, oy = t % ho, nn = t / ho;
+    const long long base = (((long long)nn * h + 2 * oy) * w + 2 * ox) * C + g * 8;
+    f32x4 a0, a1;
+    load8<T>(x + base, a0, a1);
+    float m[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    uint8_t id[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      f32x4 v0, v1;
+      load8<T>(x + base + ((long long)(k >> 1) * w + (k & 1)) * C, v0, v1);
+      const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        if (v[c] > m[c] || (v[c] != v[c] && m[c] == m[c])) { m[c] = v[c]; id[c] = (uint8_t)k; }
+    }
+    store8<T>(y + (long long)op * C + g * 8, f32x4{m[0], m[1], m[2], m[3]}, f32x4{m[4], m[5], m[6], m[7]});
+    *reinterpret_cast<uint2 *>(idx + (long long)op * C + g * 8) =
+        uint2{(uint32_t)id[0] | ((uint32_t)id[1] << 8) | ((uint32_t)id[2] << 16) | ((uint32_t)id[3] << 24),
+              (uint32_t)id[4] | ((uint32_t)id[5] << 8) | ((uint32_t)id[6] << 16) | ((uint32_t)id[7] << 24)};
+  }
+}
+
+template <typename T>
+__global__ void maxpool_bwd8_kernel(int n, int h, int w, int C, const T *__restrict__ dy,
+                                    const uint8_t *__restrict__ idx, T *__restrict__ dx,
+                                    int accumulate, const T *__restrict__ mask) {
+  const int ho = h / 2, wo = w / 2, G = C / 8;
+  const int total = n * h * w * G;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int g = i % G, p = i / G;
+    const int xx = p % w, t = p / w, yy = t % h, nn = t / h;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int oy = yy >> 1, ox = xx >> 1;
+    if (oy < ho && ox < wo) {
+      const long long o = ((long long)(nn * ho + oy) * wo + ox) * C + g * 8;
+      const uint2 id = *reinterpret_cast<const uint2 *>(idx + o);
+      const int k = (yy & 1) * 2 + (xx & 1);
+      f32x4 d0, d1;
+      load8<T>(dy + o, d0, d1);
+      const float d[8] = {d0[0], d0[1], d0[2], d0[3], d1[0], d1[1], d1[2], d1[3]};
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = (int)(((j < 4 ? id.x : id.y) >> (8 * (j & 3))) & 0xff) == k ? d[j] : 0.f;
+    }
+    const long long e = (long long)p * C + g * 8;
+    if (accumulate) {
+      f32x4 a0, a1;
+      load8<T>(dx + e, a0, a1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[j] += a0[j]; v[j + 4] += a1[j]; }
+    }
+    if (mask) {
+      f32x4 m0, m1;
+      load8<T>(mask + e, m0, m1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = m0[j] > 0.f ? v[j] : 0.f;
+        v[j + 4] = m1[j] > 0.f ? v[j + 4] : 0.f;
+      }
+    }
+    store8<T>(dx + e, f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]});
+  }
+}
+
 template <typename T>
 __global__ void maxpool_bwd_kernel(int n, int h, int w, int C, const T *__restrict__ dy,
                                    const uint8_t *__restrict__ idx, T *__restrict__ dx,
@@ -1373,9 +1446,21 @@ extern "C" int rr_conv_out_bwd(int dtype, int n, int h, int w, int cin, int cout
 extern "C" int rr_maxpool2_fwd(int dtype, int n, int h, int w, int C, const void *x, void *y,
                                uint8_t *idx, rr_stream stream) {
   if (!x || !y || !idx || C % 4 || h < 2 || w < 2) return RR_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  if (C % 8 == 0 && (long long)n * h * w * C < 0x7fffffffLL) {
+    const long long t8 = (long long)n * (h / 2) * (w / 2) * (C / 8);
+    dim3 g8(rr_grid_cap((t8 + 255) / 256, 8192)), b8(256);
+    if (dtype == RR_BF16)
+      hipLaunchKernelGGL(maxpool_fwd8_kernel<bf16_t>, g8, b8, 0, st, n, h, w, C, (const bf16_t *)x,
+                         (bf16_t *)y, idx);
+    else
+      hipLaunchKernelGGL(maxpool_fwd8_kernel<float>, g8, b8, 0, st, n, h, w, C, (const float *)x,
+                         (float *)y, idx);
+    RR_CHECK_LAUNCH();
+    return RR_OK;
+  }
   const long long total = (long long)n * (h / 2) * (w / 2) * (C / 4);
   dim3 g(rr_grid_cap((total + 255) / 256, 8192)), b(256);
-  hipStream_t st = (hipStream_t)stream;
   if (dtype == RR_BF16)
     hipLaunchKernelGGL(maxpool_fwd_kernel<bf16_t>, g, b, 0, st, n, h, w, C, (const bf16_t *)x,
                        (bf16_t *)y, idx);
@@ -1390,9 +1475,21 @@ extern "C" int rr_maxpool2_bwd(int dtype, int n, int h, int w, int C, const void
                                const uint8_t *idx, void *dx, int accumulate, const void *mask,
                                rr_stream stream) {
   if (!dy || !idx || !dx || C % 4) return RR_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  if (C % 8 == 0 && (long long)n * h * w * C < 0x7fffffffLL) {
+    const long long t8 = (long long)n * h * w * (C / 8);
+    dim3 g8(rr_grid_cap((t8 + 255) / 256, 8192)), b8(256);
+    if (dtype == RR_BF16)
+      hipLaunchKernelGGL(maxpool_bwd8_kernel<bf16_t>, g8, b8, 0, st, n, h, w, C, (const bf16_t *)dy,
+                         idx, (bf16_t *)dx, accumulate, (const bf16_t *)mask);
+    else
+      hipLaunchKernelGGL(maxpool_bwd8_kernel<float>, g8, b8, 0, st, n, h, w, C, (const float *)dy,
+                         idx, (float *)dx, accumulate, (const float *)mask);
+    RR_CHECK_LAUNCH();
+    return RR_OK;
+  }
   const long long total = (long long)n * h * w * (C / 4);
   dim3 g(rr_grid_cap((total + 255) / 256, 8192)), b(256);
-  hipStream_t st = (hipStream_t)stream;
   if (dtype == RR_BF16)
     hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, g, b, 0, st, n, h, w, C, (const bf16_t *)dy, idx,
                        (bf16_t *)dx, accumulate, (const bf16_t *)mask);

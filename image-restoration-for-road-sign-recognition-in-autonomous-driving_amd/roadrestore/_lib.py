@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libroadrestore.so")
+# RR_LIB_PATH: load another build of the same ABI (A/B of two builds on one box)
+LIB_PATH = os.environ.get("RR_LIB_PATH") or os.path.join(_HERE, "libroadrestore.so")
 
 RR_F32, RR_BF16 = 0, 1
 RR_CONV3X3, RR_CONV1X1, RR_CONVT_UP, RR_CONVT_DOWN = 0, 1, 2, 3

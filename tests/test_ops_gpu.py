@@ -347,9 +347,11 @@ def test_bn_train_fwd_bwd(dev, dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_maxpool(dev, dt):
+@pytest.mark.parametrize("C,h,w", [(64, 8, 10), (12, 9, 11), (128, 7, 6)])
+def test_maxpool(dev, dt, C, h, w):
+    """8-channel (C % 8 == 0) and 4-channel kernels, floor mode on odd sizes"""
     import roadrestore as rr
-    n, C, h, w = 2, 64, 8, 10
+    n = 2
     x = F.relu(rnd(n, C, h, w, seed=20))          # many exact-zero ties after ReLU
     x[0, 0, 0, :4] = 1.0                            # explicit ties inside a window
     if dt == torch.bfloat16:
