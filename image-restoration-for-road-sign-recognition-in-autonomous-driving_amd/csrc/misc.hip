@@ -983,6 +983,80 @@ __global__ void loss_partial_kernel(int kind, long long count, const T *__restri
   if (threadIdx.x == 0) part[blockIdx.x] = (float)red[0];
 }
 
+// 8-element forms (count % 8 == 0): 16-B loads, the 8 terms summed in fp32
+// in a fixed order, then into the fp64 per-thread sum
+template <typename T>
+__global__ void loss_partial8_kernel(int kind, long long count, const T *__restrict__ a,
+                                     const T *__restrict__ b, float *__restrict__ part) {
+  __shared__ double red[256];
+  double s = 0;
+  const long long n8 = count / 8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8;
+       i += (long long)gridDim.x * blockDim.x) {
+    f32x4 a0, a1, b0, b1;
+    load8<T>(a + i * 8, a0, a1);
+    load8<T>(b + i * 8, b0, b1);
+    const f32x4 d0 = a0 - b0, d1 = a1 - b1;
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t += kind == 0 ? fabsf(d0[k]) : d0[k] * d0[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t += kind == 0 ? fabsf(d1[k]) : d1[k] * d1[k];
+    s += t;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = (float)red[0];
+}
+
+template <typename T>
+__global__ void loss_bwd8_kernel(int kind, long long count, const T *__restrict__ a,
+                                 const T *__restrict__ b, const float *gs, float scale,
+                                 T *__restrict__ ga, T *__restrict__ gb, int accumulate,
+                                 int mask_a_pos) {
+  const float g = (gs ? gs[0] : 1.f) * scale;
+  const long long n8 = count / 8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8;
+       i += (long long)gridDim.x * blockDim.x) {
+    f32x4 a0, a1, b0, b1;
+    load8<T>(a + i * 8, a0, a1);
+    load8<T>(b + i * 8, b0, b1);
+    const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    const float bv[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float d = av[k] - bv[k];
+      v[k] = kind == 0 ? (d > 0.f ? g : (d < 0.f ? -g : 0.f)) : 2.f * g * d;
+      if (mask_a_pos && !(av[k] > 0.f)) v[k] = 0.f;
+    }
+    if (ga) {
+      f32x4 o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
+      if (accumulate) {
+        f32x4 c0, c1;
+        load8<T>(ga + i * 8, c0, c1);
+        o0 = c0 + o0;
+        o1 = c1 + o1;
+      }
+      store8<T>(ga + i * 8, o0, o1);
+    }
+    if (gb) {
+      f32x4 o0 = {-v[0], -v[1], -v[2], -v[3]}, o1 = {-v[4], -v[5], -v[6], -v[7]};
+      if (accumulate) {
+        f32x4 c0, c1;
+        load8<T>(gb + i * 8, c0, c1);
+        o0 = c0 + o0;
+        o1 = c1 + o1;
+      }
+      store8<T>(gb + i * 8, o0, o1);
+    }
+  }
+}
+
 __global__ void loss_finalize(int blocks, const float *__restrict__ part, float *out, double scale,
                               int accumulate) {
   __shared__ double red[256];
@@ -1545,12 +1619,22 @@ extern "C" int rr_loss_fwd(int kind, int dtype, long long count, const void *a, 
   const int blocks = loss_blocks(count);
   if (!ws || ws_bytes < (size_t)blocks * sizeof(float)) return RR_EWORKSPACE;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == RR_BF16)
-    hipLaunchKernelGGL(loss_partial_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, kind, count,
-                       (const bf16_t *)a, (const bf16_t *)b, (float *)ws);
-  else
-    hipLaunchKernelGGL(loss_partial_kernel<float>, dim3(blocks), dim3(256), 0, st, kind, count,
-                       (const float *)a, (const float *)b, (float *)ws);
+  const bool v8 = count % 8 == 0 && ((uintptr_t)a | (uintptr_t)b) % 16 == 0;
+  if (dtype == RR_BF16) {
+    if (v8)
+      hipLaunchKernelGGL(loss_partial8_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, kind, count,
+                         (const bf16_t *)a, (const bf16_t *)b, (float *)ws);
+    else
+      hipLaunchKernelGGL(loss_partial_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, kind, count,
+                         (const bf16_t *)a, (const bf16_t *)b, (float *)ws);
+  } else {
+    if (v8)
+      hipLaunchKernelGGL(loss_partial8_kernel<float>, dim3(blocks), dim3(256), 0, st, kind, count,
+                         (const float *)a, (const float *)b, (float *)ws);
+    else
+      hipLaunchKernelGGL(loss_partial_kernel<float>, dim3(blocks), dim3(256), 0, st, kind, count,
+                         (const float *)a, (const float *)b, (float *)ws);
+  }
   RR_CHECK_LAUNCH();
   hipLaunchKernelGGL(loss_finalize, dim3(1), dim3(256), 0, st, blocks, (const float *)ws,
                      out_scalar, (double)scale / (double)count, accumulate);
@@ -1565,6 +1649,19 @@ extern "C" int rr_loss_bwd(int kind, int dtype, long long count, const void *a, 
   dim3 g(rr_grid_cap((count + 255) / 256, 8192)), bl(256);
   const float sc = scale / (float)count;
   hipStream_t st = (hipStream_t)stream;
+  if (count % 8 == 0 && ((uintptr_t)a | (uintptr_t)b | (uintptr_t)ga | (uintptr_t)gb) % 16 == 0) {
+    dim3 g8(rr_grid_cap((count / 8 + 255) / 256, 8192));
+    if (dtype == RR_BF16)
+      hipLaunchKernelGGL(loss_bwd8_kernel<bf16_t>, g8, bl, 0, st, kind, count, (const bf16_t *)a,
+                         (const bf16_t *)b, gscale_dev, sc, (bf16_t *)ga, (bf16_t *)gb, accumulate,
+                         mask_a_pos);
+    else
+      hipLaunchKernelGGL(loss_bwd8_kernel<float>, g8, bl, 0, st, kind, count, (const float *)a,
+                         (const float *)b, gscale_dev, sc, (float *)ga, (float *)gb, accumulate,
+                         mask_a_pos);
+    RR_CHECK_LAUNCH();
+    return RR_OK;
+  }
   if (dtype == RR_BF16)
     hipLaunchKernelGGL(loss_bwd_kernel<bf16_t>, g, bl, 0, st, kind, count, (const bf16_t *)a,
                        (const bf16_t *)b, gscale_dev, sc, (bf16_t *)ga, (bf16_t *)gb, accumulate,

@@ -546,3 +546,27 @@ def test_bn_backward_pool_fused(dev, dt, nbn):
         a, b = fused[k].float(), sep[k].float()
         rel = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
         assert rel <= tol, (k, rel)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("count", [4096, 4093])
+@pytest.mark.parametrize("kind", [0, 1])
+def test_loss_vector_and_scalar_paths(dev, dt, count, kind):
+    """rr_loss_fwd / rr_loss_bwd: the 8-element vector kernels (count % 8 ==
+    0) and the scalar ones agree with the torch formula (L1: mean |a-b|, MSE:
+    mean (a-b)^2; grads incl. accumulate and the mask on a > 0)"""
+    from roadrestore import ops
+    a = rnd(count, seed=40).to(dev, dt)
+    b = rnd(count, seed=41).to(dev, dt)
+    af, bf = a.double().cpu(), b.double().cpu()
+    ref = (af - bf).abs().mean() if kind == 0 else ((af - bf) ** 2).mean()
+    got = ops.loss_fwd(kind, a, b).item()
+    assert abs(got - ref.item()) <= 1e-5 * max(1.0, abs(ref.item()))
+    d = af - bf
+    gref = (torch.sign(d) if kind == 0 else 2 * d) / count
+    gref = torch.where(af > 0, gref, torch.zeros_like(gref))
+    base = rnd(count, seed=42).to(dev, dt)
+    ga = ops.loss_bwd(kind, a, b, ga=base.clone(), accumulate=True, mask_a_pos=True)
+    tol = 1e-6 if dt == torch.float32 else 1e-2
+    err = (ga.double().cpu() - (base.double().cpu() + gref)).abs().max().item()
+    assert err <= tol * max(1.0, base.abs().max().item()), err
