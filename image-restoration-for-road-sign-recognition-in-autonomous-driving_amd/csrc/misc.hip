@@ -1743,6 +1743,20 @@ extern "C" int rr_adaptive_avgpool_flatten(int dtype, int n, int h, int w, int C
   return RR_OK;
 }
 
+// running loss on device (14:246 `running_loss += loss.item()` without the
+// per-step host sync): acc[0] += x[0] in fp64, count[0] += 1
+__global__ void scalar_accumulate_kernel(const float *__restrict__ x, double *acc, int64_t *count) {
+  acc[0] += (double)x[0];
+  count[0] += 1;
+}
+
+extern "C" int rr_scalar_accumulate(const float *x, double *acc, int64_t *count, rr_stream stream) {
+  if (!x || !acc || !count) return RR_EINVAL;
+  hipLaunchKernelGGL(scalar_accumulate_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, x, acc, count);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
 extern "C" int rr_zero(void *p, size_t bytes, rr_stream stream) {
   if (!p) return RR_EINVAL;
   if (hipMemsetAsync(p, 0, bytes, (hipStream_t)stream) != hipSuccess) return RR_ELAUNCH;

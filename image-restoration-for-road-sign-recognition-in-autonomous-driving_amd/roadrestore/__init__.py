@@ -12,6 +12,6 @@ from ._lib import EXPORTED, LIB_PATH, lib  # noqa: F401
 from .nn import (AdaptiveAvgPool2d, BatchNorm2d, Conv2d, ConvTranspose2d, Dropout,  # noqa: F401
                  L1Loss, Linear, MaxPool2d, MSELoss, PReLU, ReLU, ResidualBlock, ResUNet,
                  SimpleUNet, VGG, VGGPerceptualLoss, default_compute_dtype, unified_loss, vgg16)
-from .optim import Adam, AdamW, CosineAnnealingLR  # noqa: F401
+from .optim import Adam, AdamW, CosineAnnealingLR, RunningLoss  # noqa: F401
 
 __version__ = "0.1.0"

@@ -121,6 +121,7 @@ _SIGS = {
     "rr_distort_workspace": (S_, [I_, I_, I_, I_]),
     "rr_distort_u8": (I_, [I_, I_, I_, I_, I_, P_, P_, P_, P_, P_, C.c_ulonglong, P_, S_, P_]),
     "rr_motion_blur_kernel": (I_, [I_, I_, P_]),
+    "rr_scalar_accumulate": (I_, [P_, P_, P_, P_]),
     "rr_zero": (I_, [P_, S_, P_]),
     "rr_version": (C.c_char_p, []),
 }

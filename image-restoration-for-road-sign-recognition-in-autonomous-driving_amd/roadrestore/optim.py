@@ -166,3 +166,40 @@ class Adam(_FusedAdamBase):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
                  capturable=False):
         super().__init__(params, lr, betas, eps, weight_decay, capturable)
+
+
+class RunningLoss:
+    """Device-side running loss: ``add(loss)`` is one asynchronous launch
+    (rr_scalar_accumulate), replacing the reference's per-step
+    ``running_loss += loss.item()`` (14:246), which synchronises the host with
+    the GPU every step.  ``mean()`` / ``total()`` synchronise once (per epoch);
+    ``reset()`` starts a new epoch.  Capturable in a HIP graph."""
+
+    def __init__(self, device=None):
+        from . import ops
+        self._ops = ops
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.acc = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.count = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def add(self, loss):
+        from ._lib import lib
+        if loss.dtype != torch.float32 or loss.numel() != 1 or not loss.is_cuda:
+            raise TypeError("RunningLoss.add expects a 1-element fp32 device tensor")
+        lib().check(lib().rr_scalar_accumulate(loss.data_ptr(), self.acc.data_ptr(),
+                                               self.count.data_ptr(), self._ops.stream()),
+                    "rr_scalar_accumulate")
+
+    def total(self):
+        return self.acc.item()
+
+    def steps(self):
+        return int(self.count.item())
+
+    def mean(self):
+        n = self.steps()
+        return self.acc.item() / n if n else float("nan")
+
+    def reset(self):
+        self._ops.zero_(self.acc)
+        self._ops.zero_(self.count)

@@ -407,6 +407,11 @@ int rr_distort_u8(int n, int h, int w, int c, int mode, const uint8_t *in,
  * into taps[KMAX][KMAX] (row-major, zero outside k x k) */
 int rr_motion_blur_kernel(int k, int angle, float *taps);
 
+/* running loss on device: acc[0] += x[0] (fp64), count[0] += 1 -- the
+ * reference's per-step `running_loss += loss.item()` (14:246) without a host
+ * sync; read acc / count once per epoch */
+int rr_scalar_accumulate(const float *x, double *acc, int64_t *count, rr_stream stream);
+
 /* async memset of a device buffer (zero_grad of the flat buffers) */
 int rr_zero(void *p, size_t bytes, rr_stream stream);
 

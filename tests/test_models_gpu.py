@@ -345,3 +345,30 @@ def test_hip_graph_training_step_matches_eager(dev):
     for (na, pa), (nb, pb) in zip(ma.named_parameters(), mb.named_parameters()):
         d = (pa - pb).abs().max().item()
         assert d <= 1e-6 * max(1.0, pa.abs().max().item()), (na, d)
+
+
+def test_running_loss_on_device(dev):
+    """RunningLoss (14:246 `run_loss += loss.item()` without the per-step
+    sync): fp64 device sum, count, mean; reset; also inside a HIP graph"""
+    import roadrestore as rr
+    rl = rr.RunningLoss(dev)
+    vals = [0.5, 0.25, 1e-3, 3.0]
+    for v in vals:
+        rl.add(torch.tensor([v], device=dev))
+    assert rl.steps() == 4
+    assert abs(rl.total() - sum(float(torch.tensor(v)) for v in vals)) < 1e-12
+    assert abs(rl.mean() - sum(float(torch.tensor(v)) for v in vals) / 4) < 1e-12
+    rl.reset()
+    assert rl.steps() == 0 and rl.total() == 0.0
+    x = torch.tensor([2.0], device=dev)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g):
+            rl.add(x)
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert rl.steps() == 3 and rl.total() == 6.0
