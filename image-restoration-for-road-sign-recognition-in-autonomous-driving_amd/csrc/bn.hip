@@ -464,26 +464,33 @@ __global__ void bn_bwd_reduce_kernel(BnBwd a, float *__restrict__ part, float *_
 }
 
 // coef[C][2][3] = {gamma*invstd, mean(gm), mean(gm*xhat)} per BN
+// one workgroup per channel: 256 row lanes sum the partial rows in a fixed
+// order, then a fixed LDS tree (the old 16-channel blocks left most of the
+// chip idle on <= 1024 rows: 18.6 us at C = 64)
 template <typename PT>
-__global__ void bn_bwd_finalize_kernel(int C, int blocks, double count, int nbn,
-                                       const PT *__restrict__ part, int ablocks, const float *apart,
-                                       const float *g0, const float *inv0, const float *g1,
-                                       const float *inv1, float *dg0, float *db0, float *dg1,
-                                       float *db1, float *dalpha, float *coef) {
-  __shared__ double red[3][16][17];
-  const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
+    int C, int blocks, double count, int nbn, const PT *__restrict__ part, int ablocks,
+    const float *apart, const float *g0, const float *inv0, const float *g1, const float *inv1,
+    float *dg0, float *db0, float *dg1, float *db1, float *dalpha, float *coef) {
+  __shared__ double red[3][256];
+  const int c = blockIdx.x, t = threadIdx.x;
   double s0 = 0, s1 = 0, s2 = 0;
-  if (c < C) {
-    for (int b = sl; b < blocks; b += 16) {
-      const PT *p = part + ((long long)b * C + c) * 3;
-      s0 += p[0]; s1 += p[1]; s2 += p[2];
-    }
+  for (int b = t; b < blocks; b += 256) {
+    const PT *p = part + ((long long)b * C + c) * 3;
+    s0 += p[0]; s1 += p[1]; s2 += p[2];
   }
-  red[0][sl][cl] = s0; red[1][sl][cl] = s1; red[2][sl][cl] = s2;
+  red[0][t] = s0; red[1][t] = s1; red[2][t] = s2;
   __syncthreads();
-  if (sl == 0 && c < C) {
-    for (int k = 1; k < 16; ++k) { s0 += red[0][k][cl]; s1 += red[1][k][cl]; s2 += red[2][k][cl]; }
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+      red[0][t] += red[0][t + o];
+      red[1][t] += red[1][t + o];
+      red[2][t] += red[2][t + o];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    s0 = red[0][0]; s1 = red[1][0]; s2 = red[2][0];
     if (db0) db0[c] = (float)s0;
     if (dg0) dg0[c] = (float)s1;
     coef[c * 6 + 0] = (g0 ? g0[c] : 1.f) * inv0[c];
@@ -499,15 +506,14 @@ __global__ void bn_bwd_finalize_kernel(int C, int blocks, double count, int nbn,
   }
   if (blockIdx.x == 0 && apart && dalpha) {
     __syncthreads();
-    __shared__ double ar[256];
     double v = 0;
-    for (int b = threadIdx.x; b < ablocks; b += blockDim.x) v += apart[b];
-    ar[threadIdx.x] = v;
+    for (int b = t; b < ablocks; b += 256) v += apart[b];
+    red[0][t] = v;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      double t = 0;
-      for (int i = 0; i < (int)blockDim.x; ++i) t += ar[i];
-      dalpha[0] = (float)t;
+    if (t == 0) {
+      double tt = 0;
+      for (int i = 0; i < 256; ++i) tt += red[0][i];
+      dalpha[0] = (float)tt;
     }
   }
 }
@@ -776,7 +782,7 @@ extern "C" int rr_bn_bwd_finalize(const rr_bnbwd_desc *d, const float *partial,
   if (!partial || !invstd0 || !coef || (d->nbn == 2 && !invstd1)) return RR_EINVAL;
   const int blocks = reduce_blocks(d->P);
   const float *apart = d->mask_kind == 2 ? partial + (size_t)blocks * d->C * 3 : nullptr;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3((d->C + 15) / 16), dim3(256), 0,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3(d->C), dim3(256), 0,
                      (hipStream_t)stream, d->C, blocks, (double)d->P, d->nbn, partial, blocks, apart,
                      gamma0, invstd0, gamma1, invstd1, dgamma0, dbeta0, dgamma1, dbeta1, dalpha,
                      coef);
@@ -865,7 +871,7 @@ extern "C" int rr_bn_bwd_finalize_rows(const rr_bnbwd_desc *d, int rows, const f
   hipStream_t st = (hipStream_t)stream;
   const int chunks = rr_colreduce(partial, rows, d->C * 3, (double *)ws, st);
   if (chunks < 0) return RR_ELAUNCH;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel<double>, dim3((d->C + 15) / 16), dim3(256), 0, st,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<double>, dim3(d->C), dim3(256), 0, st,
                      d->C, chunks, (double)d->P, 1, (const double *)ws, arows, apartial, gamma0,
                      invstd0, nullptr, nullptr, dgamma0, dbeta0, nullptr, nullptr, dalpha, coef);
   RR_CHECK_LAUNCH();
