@@ -408,7 +408,15 @@ def resblock_backward(blk, S, g_out, sink, pool=None):
     split = c_in1 if c_in2 else 0
     if has_sc:
         ops.wgrad(RR_CONV1X1, ds, x1, x2, n, h, w, cout, dw=sink[sc0.weight])
-        gx1, gx2, _ = ops.igemm(RR_CONV3X3, dt1, None, n, h, w, S.pk1[1], cin, split=split)
+        if _SPLIT_DGRAD and split == 64 and cin == 128 and cout == 64:
+            # dec1 (64 + 64 -> 64): each half of the concat grad is a 64 -> 64
+            # dgrad over a contiguous slice of the packed weights, the shape
+            # the row-streaming kernel serves
+            half = 64 * 9 * cout
+            gx1, _, _ = ops.igemm(RR_CONV3X3, dt1, None, n, h, w, S.pk1[1][:half], 64)
+            gx2, _, _ = ops.igemm(RR_CONV3X3, dt1, None, n, h, w, S.pk1[1][half:], 64)
+        else:
+            gx1, gx2, _ = ops.igemm(RR_CONV3X3, dt1, None, n, h, w, S.pk1[1], cin, split=split)
         ops.igemm(RR_CONV1X1, ds, None, n, h, w, S.pks[1], cin, out=gx1, out2=gx2, split=split,
                   accumulate=True)
     else:
@@ -490,6 +498,8 @@ _FUSED_FIRST_WGRAD = os.environ.get("RR_FUSED_FIRST_WGRAD", "1") != "0"
 _FUSED_POOL = os.environ.get("RR_FUSED_POOL", "1") != "0"
 # A/B switch for the encoder max-pool backward fused into the tail BN backward
 _FUSED_POOL_BWD = os.environ.get("RR_FUSED_POOL_BWD", "1") != "0"
+# A/B switch: dec1's concat dgrad as two 64 -> 64 row-streaming launches
+_SPLIT_DGRAD = os.environ.get("RR_SPLIT_DGRAD", "1") != "0"
 
 
 def resunet_backward(m, S, g_out, sink):
