@@ -6,12 +6,13 @@
 #include "../../include/roadrestore.h"
 
 struct SWArgs {
-  const char *dy;            // NHWC bf16 [n][h][w][64]
+  const char *dy;            // NHWC bf16 [n][h][w][cout]; a workgroup reads one 64-channel slice
   const char *x1, *x2;       // NHWC bf16 [n][h][w][c1], [n][h][w][c2] (concat input)
   int c1, c2;
-  float *partial;            // [nwg_ps][64][9][c1 + c2] partial dW slabs
+  int cout;                  // dy channels (a multiple of 64)
+  float *partial;            // [nwg_ps][cout][9][c1 + c2] partial dW slabs
   int n, h;                  // w is the template width
-  int nwg_ps;                // workgroups per 64-channel input slice
+  int nwg_ps;                // workgroups per (dy slice, input slice) pair
   int nsteps;                // 128-pixel steps (n h w / 128)
   unsigned long long *ts;    // debug phase timestamps [nwg][4] or null
 };

@@ -108,7 +108,11 @@ __global__ __launch_bounds__(512, 2) void swgrad_kernel(SWArgs a) {
   const int wc = wv & 1, wk = wv >> 1;          // output channels 32 wc.., input channels 16 wk..
   const int H = a.h;
   const int spi = H / RPS;
-  const int slice = blockIdx.x / a.nwg_ps, r = blockIdx.x - slice * a.nwg_ps;
+  // workgroup -> (dy slice ds, input slice, pixel range r)
+  const int nxs = (a.c1 + a.c2) / 64;
+  const int sq = blockIdx.x / a.nwg_ps, r = blockIdx.x - sq * a.nwg_ps;
+  const int ds = sq / nxs, slice = sq - ds * nxs;
+  const int dys = a.cout * 2;                              // bytes per dy pixel
   const int cbeg = (int)((long long)r * a.nsteps / a.nwg_ps);
   const int cend = (int)((long long)(r + 1) * a.nsteps / a.nwg_ps);
   const int ci0 = slice * 64;
@@ -146,7 +150,7 @@ __global__ __launch_bounds__(512, 2) void swgrad_kernel(SWArgs a) {
       const int p = 8 * tt + (lane >> 3), chunk = (lane & 7) ^ sw_swz(p & 15);
       prow[i] = 0;
       pdst[i] = tt * 1024;
-      pofs[i] = (uint32_t)(p * 128 + chunk * 16);
+      pofs[i] = (uint32_t)(p * dys + ds * 128 + chunk * 16);
     }
   }
   const long long xrow_b = (long long)W * xpb;             // bytes per image row of the source
@@ -161,7 +165,7 @@ __global__ __launch_bounds__(512, 2) void swgrad_kernel(SWArgs a) {
       __builtin_amdgcn_global_load_lds((const void *)(base + pofs[i]),
                                        LDS_PTR(smem + seg * RPS * ROWB + pdst[i]), 16, 0, 0);
     } else {
-      const char *base = live ? a.dy + (long long)(cu.n * H + cu.y0) * (W * 128) : a.dy;
+      const char *base = live ? a.dy + (long long)(cu.n * H + cu.y0) * W * dys : a.dy;
       __builtin_amdgcn_global_load_lds((const void *)(base + pofs[i]),
                                        LDS_PTR(smem + DYOFF + seg * DYB + pdst[i]), 16, 0, 0);
     }
@@ -293,7 +297,7 @@ __global__ __launch_bounds__(512, 2) void swgrad_kernel(SWArgs a) {
   // column ci = 16 wk + (lane & 15); LDS [col 32 = 16 wc + 4 g + e][tap][ci 64]
   __syncthreads();
   const int CB = a.c1 + a.c2;
-  float *const pw = a.partial + (long long)r * (64 * 9) * CB + ci0;
+  float *const pw = a.partial + ((long long)r * a.cout + ds * 64) * 9 * CB + ci0;
   float *const st = reinterpret_cast<float *>(smem);
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
@@ -316,12 +320,12 @@ __global__ __launch_bounds__(512, 2) void swgrad_kernel(SWArgs a) {
 
 }  // namespace
 
-static int sw_slices(const rr_wgrad_desc *d) { return (d->c_in1 + d->c_in2) / 64; }
+static int sw_slices(const rr_wgrad_desc *d) { return (d->c_in1 + d->c_in2) / 64 * (d->c_out / 64); }
 
 int swgrad_ok(const rr_wgrad_desc *d) {
   const char *e = getenv("RR_SWGRAD");
   if (e && !atoi(e)) return 0;
-  if (d->dtype != RR_BF16 || d->mode != RR_CONV3X3 || d->c_out != 64) return 0;
+  if (d->dtype != RR_BF16 || d->mode != RR_CONV3X3 || d->c_out % 64 || d->c_out > 128) return 0;
   if (d->w != 64 && d->w != 32) return 0;
   if (d->c_in1 % 64 || d->c_in2 % 64 || d->c_in1 + d->c_in2 > 192 || d->c_in1 <= 0) return 0;
   if (d->h % (128 / d->w)) return 0;
@@ -341,6 +345,7 @@ int swgrad_launch(const rr_wgrad_desc *d, const void *dy, const void *x1, const 
   a.x2 = (const char *)x2;
   a.c1 = d->c_in1;
   a.c2 = d->c_in2;
+  a.cout = d->c_out;
   a.partial = (float *)ws;
   a.n = d->n;
   a.h = d->h;

@@ -99,7 +99,7 @@ def _kswgrad(mode, dt, n, h, w, c1, c2, cout):
     """Mirror of csrc/swgrad.hip swgrad_ok (probe naming only)."""
     if os.environ.get("RR_SWGRAD", "1") in ("0",):
         return False
-    if dt != torch.bfloat16 or mode != RR_CONV3X3 or cout != 64 or w not in (32, 64):
+    if dt != torch.bfloat16 or mode != RR_CONV3X3 or cout % 64 or cout > 128 or w not in (32, 64):
         return False
     if c1 <= 0 or c1 % 64 or c2 % 64 or c1 + c2 > 192 or h % (128 // w):
         return False
