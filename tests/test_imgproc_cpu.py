@@ -98,3 +98,37 @@ def test_imgproc_workspace_queries():
     assert lib.rr_resize_workspace(1, 30, 30, 5, 224, 224) == 0        # c > 4
     assert lib.rr_ssim_workspace(8, 3) == 8 * 3 * 8
     assert lib.rr_distort_workspace(2, 64, 64, 3) == 2 * 64 * 64 * 3
+
+
+def test_distortion_params_follow_reference_draw_order():
+    """imgproc.distortion_params draws exactly what 14:36-58 draws, in the
+    same order, from the same Python `random` stream (host logic, no GPU)"""
+    import random
+    from roadrestore import imgproc
+    from roadrestore._lib import RR_DISTORT_BLUR, RR_DISTORT_FOG, RR_DISTORT_NOISE
+    n = 64
+    params, taps = imgproc.distortion_params(n, random.Random(123))
+    rng = random.Random(123)
+    seen = set()
+    for i in range(n):
+        p = params[i]
+        fog = rng.random() < 0.5
+        if fog:
+            intensity = rng.uniform(0.3, 0.7)
+            t = 1.0 - intensity * rng.uniform(0.8, 1.2)
+            assert p.fog_mul == np.float32(t) and p.fog_add == np.float32(0.9 * (1 - t))
+        noise = rng.random() < 0.5
+        if noise:
+            assert p.sigma == rng.uniform(0.01, 0.03) ** 0.5
+        blur = rng.random() < 0.5
+        if blur:
+            degree, angle = rng.randint(5, 15), rng.randint(0, 360)
+            assert p.ksize == degree
+            assert np.array_equal(taps[i][:degree, :degree].numpy(), I.motion_blur_kernel(degree, angle))
+        else:
+            assert not taps[i].any()
+        assert bool(p.flags & RR_DISTORT_FOG) == fog
+        assert bool(p.flags & RR_DISTORT_NOISE) == noise
+        assert bool(p.flags & RR_DISTORT_BLUR) == blur
+        seen.add((fog, noise, blur))
+    assert len(seen) == 8                                    # every branch combination drawn
