@@ -22,30 +22,43 @@ import torch.distributed as dist
 
 
 class DataParallel:
-    def __init__(self, model, process_group=None, bucket_mb=25.0, broadcast_params=True):
+    def __init__(self, model, process_group=None, bucket_mb=25.0, tail_mb=4.0,
+                 broadcast_params=True):
         self.model = model
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.bucket_bytes = int(bucket_mb * 2 ** 20)
+        self.tail_bytes = int(tail_mb * 2 ** 20)
         layout = model.grad_layout()
         order, zero = model._grad_order()
         zs = {id(z) for z in zero}
         self.zero_ids = zs
-        # bucket plan over the non-zero part of the flat layout (readiness order)
+        # bucket plan over the non-zero part of the flat layout (readiness
+        # order), cut from the END: the last bucket only becomes ready when
+        # the whole backward is done, so its all-reduce is exposed -- it is
+        # kept to <= tail_mb (ResUNet: res3..enc1, 3.5 MB), the others to
+        # ~bucket_mb (they overlap the rest of the backward)
         self.buckets = []          # (start, end, param-id set)
-        off = sum(p.numel() for p in layout if id(p) in zs)
-        cur, cur_start, cur_bytes = set(), off, 0
+        start = sum(p.numel() for p in layout if id(p) in zs)
+        items, off = [], start
         for p in layout:
             if id(p) in zs:
                 continue
-            cur.add(id(p))
-            cur_bytes += p.numel() * 4
+            items.append((off, off + p.numel(), id(p)))
             off += p.numel()
-            if cur_bytes >= self.bucket_bytes:
-                self.buckets.append((cur_start, off, cur))
-                cur, cur_start, cur_bytes = set(), off, 0
+        rev, cur, cur_bytes, limit = [], [], 0, self.tail_bytes
+        for it in reversed(items):
+            nb = (it[1] - it[0]) * 4
+            if cur and cur_bytes + nb > limit:
+                rev.append(cur)
+                cur, cur_bytes, limit = [], 0, self.bucket_bytes
+            cur.append(it)
+            cur_bytes += nb
         if cur:
-            self.buckets.append((cur_start, off, cur))
+            rev.append(cur)
+        for b in reversed(rev):
+            b = b[::-1]
+            self.buckets.append((b[0][0], b[-1][1], {i for _, _, i in b}))
         self._pending = []
         self._done = set()
         self._launched = set()

@@ -81,3 +81,23 @@ def test_data_parallel_gloo_world2():
         assert nb >= 4, nb
         assert 0 < early < nb, (early, nb)       # buckets go out while backward continues
         assert gs == 0.5
+
+
+def test_bucket_plan_contiguous_with_small_tail():
+    """DataParallel buckets tile the non-zero part of the flat gradient in
+    readiness order, contiguously, and the last (exposed) bucket is small"""
+    import roadrestore as rr
+    from roadrestore.parallel import DataParallel
+    m = rr.ResUNet()
+    dp = DataParallel(m, broadcast_params=False, bucket_mb=25.0, tail_mb=4.0)
+    layout = m.grad_layout()
+    _, zero = m._grad_order()
+    zs = {id(z) for z in zero}
+    start = sum(p.numel() for p in layout if id(p) in zs)
+    total = sum(p.numel() for p in layout)
+    assert dp.buckets[0][0] == start and dp.buckets[-1][1] == total
+    for (a0, b0, _), (a1, _, _) in zip(dp.buckets, dp.buckets[1:]):
+        assert b0 == a1
+    ids = set().union(*(b[2] for b in dp.buckets))
+    assert ids == {id(p) for p in layout if id(p) not in zs}
+    assert (dp.buckets[-1][1] - dp.buckets[-1][0]) * 4 <= 4 * 2 ** 20
