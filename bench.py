@@ -290,7 +290,7 @@ def main():
                 "random-init weights",
         "config": {"workload": "cfg3: ResUNet unified train step (fwd + L1 + 0.1*VGG16[:16] "
                                "perceptual + bwd + AdamW), 14_train_unified_advanced.py",
-                   "model": "ResUNet", "global_batch": world * B, "per_gpu_batch": B,
+                   "global_batch": world * B, "per_gpu_batch": B,
                    "image": [H, H, 3], "parallelism": f"dp{world}",
                    "hip_graph": graph is not None,
                    "flop_per_image": FLOP_STEP_WITH_PERC if w_perc else FLOP_RESUNET_FWDBWD},
