@@ -61,6 +61,7 @@ struct IgemmArgs {
   const float *bmean, *binv, *baff_s, *baff_b, *balpha;
   float *bpart, *bapart;                       // [npblk][cout][3], [npblk][cout/64]
   int dbg;            // diagnostics (RR_IGEMM_DBG): bit0 skip epilogue, bit1 K loop x2
+  int xcd;            // XCD-aware tile order (RR_XCD_MAP=0 disables)
 };
 
 template <typename T> struct Frag;
@@ -292,8 +293,14 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs a) {
   const int lane = tid & 63;
   const int wv = tid >> 6;
   const int wc = wv % WC, wp = wv / WC;
-  const int cblk = blockIdx.x % a.ncblk;
-  const int pblk = blockIdx.x / a.ncblk;
+  // XCD-aware tile order, as in igemm3_halo_kernel (a.xcd)
+  int tile = blockIdx.x;
+  if (a.xcd) {
+    const int per = (int)gridDim.x / 8;
+    if ((int)blockIdx.x < per * 8) tile = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
+  }
+  const int cblk = tile % a.ncblk;
+  const int pblk = tile / a.ncblk;
   const int c0 = cblk * BC;
   const int p0 = pblk * BP;
 
@@ -646,7 +653,16 @@ __global__ __launch_bounds__(2 * BP, (HaloCfg<BC, BP>::OCC)) void igemm3_halo_ke
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wc = wv % WC, wp = wv / WC;
-  const int cblk = blockIdx.x % a.ncblk, pblk = blockIdx.x / a.ncblk;
+  // XCD-aware tile order (a.xcd): workgroup b runs on XCD b % 8, so XCD x
+  // takes the contiguous tile range [x T/8, (x+1) T/8) -- the column blocks
+  // of a pixel tile and the neighbouring tiles sharing its halo rows then
+  // meet in one L2.  The remainder (T % 8) keeps the linear order.
+  int tile = blockIdx.x;
+  if (a.xcd) {
+    const int per = (int)gridDim.x / 8;
+    if ((int)blockIdx.x < per * 8) tile = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
+  }
+  const int cblk = tile % a.ncblk, pblk = tile / a.ncblk;
   const int c0 = cblk * BC, p0 = pblk * BP;
 
   // ---- tile geometry (uniform) ----
@@ -1029,6 +1045,8 @@ static int fill_args(const rr_igemm_desc *d, const void *x1, const void *x2, con
   a.out_nchw = d->out_nchw;
   const char *dbg_env = getenv("RR_IGEMM_DBG");
   a.dbg = dbg_env ? atoi(dbg_env) : 0;
+  const char *xcd_env = getenv("RR_XCD_MAP");   // A/B switch (default on)
+  a.xcd = xcd_env ? atoi(xcd_env) : 1;
   a.ncblk = 1;
   a.bt = nullptr; a.bmean = a.binv = a.baff_s = a.baff_b = a.balpha = nullptr;
   a.bpart = a.bapart = nullptr;
