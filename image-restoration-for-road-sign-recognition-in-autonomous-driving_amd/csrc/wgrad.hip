@@ -39,7 +39,17 @@ struct WgradArgs {
   int split_len;           // pixels per split (multiple of BKP)
   int nablk, nbblk;
   FastDiv fd_w, fd_hw;
+  int xcd;                 // XCD-aware workgroup order (RR_XCD_MAP)
 };
+
+// XCD-aware order (workgroup b runs on XCD b % 8): XCD x takes the
+// contiguous index range [x T/8, (x+1) T/8), so the tiles of one split --
+// which read the same dy / x pixels -- share an L2; the T % 8 tail is linear
+__device__ __forceinline__ int xcd_order(int b, int xcd) {
+  if (!xcd) return b;
+  const int per = (int)gridDim.x / 8;
+  return b < per * 8 ? (b & 7) * per + (b >> 3) : b;
+}
 
 constexpr int BKP_PLAN = 64;   // split lengths are multiples of this
 
@@ -87,7 +97,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wa = wv & 1, wb = wv >> 1;
-  int bid = blockIdx.x;
+  int bid = xcd_order(blockIdx.x, a.xcd);
   const int ablk = bid % a.nablk; bid /= a.nablk;
   const int bt = bid % (a.nbblk * a.taps); bid /= (a.nbblk * a.taps);
   const int split = bid;
@@ -271,6 +281,7 @@ struct Halo3Args {
   int stages;              // total 64-pixel stages (P / 64)
   int split_stages;        // stages per split
   int nablk, nbblk;
+  int xcd;                 // XCD-aware workgroup order (RR_XCD_MAP)
 };
 
 template <int W>
@@ -292,7 +303,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wa = wv & 1, wb = wv >> 1;
-  int bid = blockIdx.x;
+  int bid = xcd_order(blockIdx.x, a.xcd);
   const int ablk = bid % a.nablk; bid /= a.nablk;
   const int bblk = bid % a.nbblk; bid /= a.nbblk;
   const int split = bid;
@@ -641,6 +652,8 @@ extern "C" int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
   a.P = (int)P;
   a.split_len = pl.split_len;
   a.nablk = pl.nablk; a.nbblk = pl.nbblk;
+  const char *xcd_env = getenv("RR_XCD_MAP");
+  a.xcd = xcd_env ? atoi(xcd_env) : 1;
   a.fd_w = make_fastdiv((uint32_t)d->w);
   a.fd_hw = make_fastdiv((uint32_t)(d->h * d->w));
   hipStream_t st = (hipStream_t)stream;
@@ -662,6 +675,7 @@ extern "C" int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
     ha.lw = __builtin_ctz((unsigned)d->w);
     ha.stages = hp.stages; ha.split_stages = hp.split_stages;
     ha.nablk = ha.CA / 64; ha.nbblk = ha.CB / 64;
+    ha.xcd = a.xcd;
     const dim3 grid((unsigned)(ha.nablk * ha.nbblk * hp.nsplit)), block(256);
     switch (d->w) {
       case 64: hipLaunchKernelGGL(wgrad3_halo_kernel<64>, grid, block, 0, st, ha); break;
