@@ -1,7 +1,8 @@
 // swgrad.hip -- row-streaming 3x3 bf16 weight gradient for the wide layers
-// whose output gradient has 64 channels (64 x 64 and 32 x 32 maps): res1 and
-// dec1 conv1 / conv2, dec2 conv1 (a 64 + 128 channel concat input) and conv2
-// of ResUNet (14_train_unified_advanced.py:96-115, 151-186).
+// (64 x 64 and 32 x 32 maps) whose output gradient has 64 or 128 channels:
+// res1, res2, dec1 and dec2 conv1 / conv2 of ResUNet (14_train_unified_advanced.py:96-115,
+// 151-186), concat inputs of up to 192 channels.  A 128-channel dy is read as
+// two 64-channel slices: a workgroup owns one (dy slice, input slice) pair.
 //
 //   dW[co][tap][ci] = sum_p dy[p][co] * x[p + tap][ci]
 //
@@ -10,8 +11,8 @@
 // batch brings the step's NEW input rows into a ring of zero-haloed rows
 // (every input row is read once) and the step's 128 x 64 dy tile into a
 // 4-tile ring, D = 2 steps ahead of the MFMAs.  The workgroup owns one
-// 64-channel slice of the input (concat inputs: 2 or 3 slices) and
-// accumulates the whole 64 x 576 dW slice in registers over all its pixels;
+// 64-channel slice of the input (concat inputs: 2 or 3 slices) and of dy, and
+// accumulates the whole 64 x 576 dW block in registers over all its pixels;
 // the per-workgroup partial slabs are summed by rr_wgrad's fixed-order
 // reduce (deterministic, no float atomics).
 //
