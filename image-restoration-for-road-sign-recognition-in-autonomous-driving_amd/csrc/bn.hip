@@ -17,6 +17,52 @@ namespace {
 // finalize of the conv-epilogue statistics -> scale / shift / running stats
 // partial [blocks][C][2] of the pre-bias accumulator.
 // 256 threads = 16 channels x 16 block-slices; double accumulation.
+// BN statistics finalize straight from the raw fp32 per-tile partials
+// [rows][C][2] (no column-reduce launch): one workgroup per channel, 256 row
+// lanes in a fixed order + an LDS tree, then the same per-channel math as
+// bn_finalize_kernel
+__global__ __launch_bounds__(256) void bn_finalize_direct_kernel(
+    int C, int rows, double count, const float *__restrict__ part, const float *bias,
+    const float *gamma, const float *beta, float *rmean, float *rvar, float momentum, float eps,
+    float *scale, float *shift, float *smean, float *sinv, int64_t *nbt) {
+  __shared__ double red[2][256];
+  const int c = blockIdx.x, t = threadIdx.x;
+  if (nbt && c == 0 && t == 0) nbt[0] += 1;
+  double s1 = 0.0, s2 = 0.0;
+  for (int b = t; b < rows; b += 256) {
+    const float *p = part + ((long long)b * C + c) * 2;
+    s1 += p[0];
+    s2 += p[1];
+  }
+  red[0][t] = s1;
+  red[1][t] = s2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) { red[0][t] += red[0][t + o]; red[1][t] += red[1][t + o]; }
+    __syncthreads();
+  }
+  if (t == 0) {
+    s1 = red[0][0];
+    s2 = red[1][0];
+    const double mean_acc = s1 / count;
+    double var = s2 / count - mean_acc * mean_acc;
+    if (var < 0) var = 0;
+    const double mean = mean_acc + (bias ? (double)bias[c] : 0.0);
+    const double inv = 1.0 / sqrt(var + (double)eps);
+    const double g = gamma ? (double)gamma[c] : 1.0;
+    const double bt = beta ? (double)beta[c] : 0.0;
+    scale[c] = (float)(g * inv);
+    shift[c] = (float)(bt - mean * g * inv);
+    if (smean) smean[c] = (float)mean;
+    if (sinv) sinv[c] = (float)inv;
+    if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+    if (rvar) {
+      const double unb = count > 1 ? var * count / (count - 1) : var;
+      rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+    }
+  }
+}
+
 __global__ void bn_finalize_kernel(int C, int blocks, double count, const double *__restrict__ part,
                                    const float *bias, const float *gamma, const float *beta,
                                    float *rmean, float *rvar, float momentum, float eps,
@@ -621,6 +667,13 @@ extern "C" int rr_bn_finalize(int C, int blocks, long long count, const float *p
   if (C <= 0 || blocks <= 0 || count <= 0 || !part || !scale || !shift) return RR_EINVAL;
   if (!ws || ws_bytes < rr_colreduce_bytes(blocks, C * 2)) return RR_EWORKSPACE;
   hipStream_t st = (hipStream_t)stream;
+  if (blocks <= 8192) {
+    hipLaunchKernelGGL(bn_finalize_direct_kernel, dim3(C), dim3(256), 0, st, C, blocks, (double)count,
+                       part, bias, gamma, beta, running_mean, running_var, momentum, eps, scale, shift,
+                       save_mean, save_invstd, num_batches_tracked);
+    RR_CHECK_LAUNCH();
+    return RR_OK;
+  }
   const int chunks = rr_colreduce(part, blocks, C * 2, (double *)ws, st);
   if (chunks < 0) return RR_ELAUNCH;
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st,
