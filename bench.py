@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--graph", type=int, default=-1,
-                    help="capture the step in a HIP graph and replay it (1/0; default: on at N=1)")
+                    help="capture the step in a HIP graph and replay it (1/0; default: on)")
     ap.add_argument("--probe-steps", type=int, default=3,
                     help="eager steps timed per kernel for the roofline in graph mode")
     return ap.parse_args()
@@ -160,7 +160,11 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # RR_BENCH_DP1=1 (with torchrun --nproc-per-node 1): the N > 1 step at
+    # world size 1 -- an RCCL group of one rank and DataParallel with
+    # force_comm, so every bucket all-reduce runs (and is graph-captured)
+    dp1 = os.environ.get("RR_BENCH_DP1") == "1"
+    if world > 1 or dp1:
         backend = os.environ.get("RR_DIST_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -180,9 +184,11 @@ def main():
     perc = rr.VGGPerceptualLoss().to(dev)
     perc.compute_dtype = dt
     flatten_parameters(model)
-    dp = DataParallel(model) if world > 1 else None
+    dp = DataParallel(model, force_comm=dp1) if world > 1 or dp1 else None
     gscale = dp.grad_scale if dp else 1.0
-    use_graph = a.graph == 1 or (a.graph == -1 and world == 1)
+    # the HIP graph needs graph-capturable collectives: RcclComm (any N on
+    # GPUs); the gloo rehearsal backend runs eagerly
+    use_graph = a.graph == 1 or (a.graph == -1 and (dp is None or dp.rccl is not None))
     opt = rr.AdamW(model.parameters(), lr=2e-4, weight_decay=1e-4, capturable=use_graph)
 
     # synthetic GTSRB-shaped batch: clean ~ U{0..255}/255, bad = fog + noise
@@ -220,9 +226,23 @@ def main():
                 step()
         torch.cuda.current_stream().wait_stream(side)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            loss_g = step()
+        # at N > 1 the bucket all-reduces (RCCL, comm side stream forked from
+        # the capture stream) are recorded into the graph with the rest
+        # thread_local: RCCL's watchdog thread keeps polling the events of the
+        # eager warmup collectives while this thread captures
         torch.cuda.synchronize()
+        try:
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+                loss_g = step()
+            torch.cuda.synchronize()
+        except Exception as e:                      # pragma: no cover - safety net
+            # a capture that fails the same way on every rank: time eagerly
+            print(f"bench: HIP-graph capture failed ({type(e).__name__}: {e}); "
+                  "timing eager steps", file=sys.stderr, flush=True)
+            graph = None
+            if dp is not None:
+                dp.finish()
+            torch.cuda.synchronize()
     # the kernel probe (HIP events around every GEMM launch) never runs inside
     # the timed region: it times separate eager steps afterwards
     probe = None
@@ -305,7 +325,9 @@ def main():
         rec["cpu_baseline"] = cpu_baseline(a.cpu_baseline_seconds, H)
     if rank == 0:
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if dp is not None:
+        dp.close()
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

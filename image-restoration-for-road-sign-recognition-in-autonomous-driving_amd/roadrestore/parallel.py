@@ -11,20 +11,97 @@ into one flat fp32 buffer laid out in the order the gradients become final
 ``DataParallel`` cuts that buffer into ~``bucket_mb`` contiguous buckets and
 launches each bucket's all-reduce (in place, no packing copy) on a side
 stream as soon as its last gradient is written, so communication overlaps
-the rest of the backward; the optimizer waits for the comm stream.  The
+the rest of the backward; the optimizer waits for the comm stream.  On GPUs
+the all-reduces are bare ncclAllReduce calls on a communicator of our own
+(``RcclComm``), so the whole step, bucket all-reduces included, is HIP-graph
+capturable: the side stream forks from and joins the capturing stream and
+the collectives are recorded into the graph (bench.py captures it at every N).  The
 1/world_size average is folded into the loss gradient (``grad_scale``), the
 exactly-zero gradients (conv biases before a train-mode BN) are not sent.
 """
 from __future__ import annotations
 
+import ctypes
+import os
+
 import torch
 import torch.distributed as dist
 
 
+class _UniqueId(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_char * 128)]     # NCCL_UNIQUE_ID_BYTES
+
+
+class RcclComm:
+    """A communicator of its own on the RCCL library torch ships (rccl.h:
+    ncclGetUniqueId / ncclCommInitRank / ncclAllReduce), for the gradient
+    all-reduce of the data-parallel step.
+
+    Why not ``dist.all_reduce``: ProcessGroupNCCL's watchdog thread polls the
+    completion event of every work it issues, and polling an event recorded
+    into a HIP graph under capture is an error that kills the process.  A
+    bare ncclAllReduce on the caller's stream has no such host-side state, so
+    the whole step -- bucket all-reduces included -- captures into one HIP
+    graph and replays at N > 1 as it does at N = 1.  The unique id travels
+    over the existing torch process group (rank 0 -> all)."""
+
+    NCCL_FLOAT32, NCCL_SUM = 7, 0
+
+    def __init__(self, process_group=None, device=None):
+        path = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+        if not os.path.exists(path):
+            path = "librccl.so"
+        self.lib = lib = ctypes.CDLL(path)
+        lib.ncclGetErrorString.restype = ctypes.c_char_p
+        lib.ncclCommInitRank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
+                                         _UniqueId, ctypes.c_int]
+        lib.ncclAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                      ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                      ctypes.c_void_p]
+        lib.ncclCommDestroy.argtypes = [ctypes.c_void_p]
+        self.rank = dist.get_rank(process_group)
+        self.world = dist.get_world_size(process_group)
+        uid = _UniqueId()
+        if self.rank == 0:
+            self._check(lib.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
+        # raw 128 bytes (the c_char field itself reads as NUL-terminated bytes)
+        obj = [ctypes.string_at(ctypes.addressof(uid), 128) if self.rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=process_group)
+        if len(obj[0]) != 128:
+            raise RuntimeError("RcclComm: bad unique id from rank 0")
+        ctypes.memmove(ctypes.addressof(uid), obj[0], 128)
+        self.comm = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            self._check(lib.ncclCommInitRank(ctypes.byref(self.comm), self.world, uid, self.rank),
+                        "ncclCommInitRank")
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what}: {self.lib.ncclGetErrorString(rc).decode()} ({rc})")
+
+    def all_reduce_(self, t, stream=None):
+        """In-place sum of a contiguous fp32 device tensor over the ranks,
+        enqueued on ``stream`` (default: the current stream)."""
+        if t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda:
+            raise ValueError("RcclComm.all_reduce_ takes a contiguous fp32 device tensor")
+        st = stream if stream is not None else torch.cuda.current_stream(t.device)
+        self._check(self.lib.ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(),
+                                           self.NCCL_FLOAT32, self.NCCL_SUM, self.comm,
+                                           st.cuda_stream), "ncclAllReduce")
+
+    def close(self):
+        if self.comm:
+            self.lib.ncclCommDestroy(self.comm)
+            self.comm = ctypes.c_void_p()
+
+
 class DataParallel:
     def __init__(self, model, process_group=None, bucket_mb=25.0, tail_mb=4.0,
-                 broadcast_params=True):
+                 broadcast_params=True, force_comm=False, comm=None):
         self.model = model
+        # force_comm: launch the bucket all-reduces even at world size 1 (a
+        # 1-GPU rehearsal of the N > 1 step, e.g. its HIP-graph capture)
+        self.force_comm = force_comm
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.bucket_bytes = int(bucket_mb * 2 ** 20)
@@ -65,6 +142,16 @@ class DataParallel:
         self.comm_stream = None
         if torch.cuda.is_available() and next(model.parameters()).is_cuda:
             self.comm_stream = torch.cuda.Stream()
+        # comm: "rccl" = RcclComm (graph-capturable, the default on GPUs with
+        # an RCCL process group), "torch" = dist.all_reduce (gloo on CPU)
+        if comm is None:
+            comm = os.environ.get("RR_DP_COMM")
+        if comm is None:
+            comm = ("rccl" if self.comm_stream is not None and dist.is_initialized()
+                    and dist.get_backend(process_group) == "nccl" else "torch")
+        self.rccl = None
+        if comm == "rccl" and (self.world > 1 or force_comm):
+            self.rccl = RcclComm(process_group, next(model.parameters()).device)
         model.set_grad_ready_hook(self._on_ready)
         if broadcast_params and self.world > 1:
             with torch.no_grad():
@@ -76,7 +163,7 @@ class DataParallel:
         return 1.0 / self.world
 
     def _on_ready(self, sink, params):
-        if self.world == 1:
+        if self.world == 1 and not self.force_comm:
             return
         for p in params:
             self._done.add(id(p))
@@ -85,13 +172,15 @@ class DataParallel:
                 continue
             self._launched.add(bi)
             view = sink.flat[a:b]
-            if self.comm_stream is not None:
+            if self.rccl is not None:
+                self.comm_stream.wait_stream(torch.cuda.current_stream())
+                self.rccl.all_reduce_(view, self.comm_stream)   # joined in finish()
+            elif self.comm_stream is not None:
                 self.comm_stream.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(self.comm_stream):
-                    work = dist.all_reduce(view, group=self.pg, async_op=True)
+                    self._pending.append(dist.all_reduce(view, group=self.pg, async_op=True))
             else:
-                work = dist.all_reduce(view, group=self.pg, async_op=True)
-            self._pending.append(work)
+                self._pending.append(dist.all_reduce(view, group=self.pg, async_op=True))
         if len(self._launched) == len(self.buckets):
             self.finish()
 
@@ -104,6 +193,11 @@ class DataParallel:
         self._pending = []
         self._done = set()
         self._launched = set()
+
+    def close(self):
+        if self.rccl is not None:
+            self.rccl.close()
+            self.rccl = None
 
     def __call__(self, x):
         return self.model(x)

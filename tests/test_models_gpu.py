@@ -347,6 +347,76 @@ def test_hip_graph_training_step_matches_eager(dev):
         assert d <= 1e-6 * max(1.0, pa.abs().max().item()), (na, d)
 
 
+def test_hip_graph_dp_step_with_rccl_matches_eager(dev):
+    """The N > 1 bench step (DataParallel bucket all-reduces on the comm
+    stream, launched from the backward's ready hooks) captured in a HIP graph:
+    rehearsed on one GPU with a world-size-1 RCCL group and force_comm, so
+    every bucket's ncclAllReduce (RcclComm) is really recorded into the graph.  Replay must
+    equal the eager DP steps (an all-reduce over one rank is the identity)."""
+    import socket
+    import torch.distributed as dist
+    import roadrestore as rr
+    from roadrestore.optim import flatten_parameters
+    from roadrestore.parallel import DataParallel
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    store = dist.TCPStore("127.0.0.1", port, 1, True)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
+    try:
+        B, H = 4, 32
+        g = torch.Generator(device=dev).manual_seed(5)
+        clean = torch.rand((B, 3, H, H), generator=g, device=dev)
+        bad = (clean * 0.5 + 0.4).clamp(0, 1)
+
+        def make(capturable):
+            torch.manual_seed(7)
+            m = rr.ResUNet().to(dev)
+            m.compute_dtype = torch.bfloat16
+            m.train()
+            perc = rr.VGGPerceptualLoss().to(dev)
+            perc.compute_dtype = torch.bfloat16
+            flatten_parameters(m)
+            dp = DataParallel(m, bucket_mb=4.0, force_comm=True)
+            opt = rr.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-4, capturable=capturable)
+
+            def step():
+                opt.zero_grad(set_to_none=True)
+                loss = rr.unified_loss(m(bad), clean, perc, 0.1, grad_scale=dp.grad_scale)
+                loss.backward()
+                opt.step()
+                return loss
+            return m, dp, step
+
+        ma, dpa, step_a = make(False)
+        for _ in range(4):
+            la = step_a()
+        assert len(dpa.buckets) > 2
+        mb, dpb, step_b = make(True)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            step_b()
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+            lb = step_b()
+        assert not dpb._pending and not dpb._launched      # every bucket joined
+        for _ in range(3):
+            graph.replay()
+        torch.cuda.synchronize()
+        assert abs(la.item() - lb.item()) <= 1e-6 * abs(la.item()), (la.item(), lb.item())
+        for (na, pa), (nb, pb) in zip(ma.named_parameters(), mb.named_parameters()):
+            d = (pa - pb).abs().max().item()
+            assert d <= 1e-6 * max(1.0, pa.abs().max().item()), (na, d)
+        for dp in (dpa, dpb):
+            assert dp.rccl is not None                     # the RcclComm path
+            dp.close()
+    finally:
+        dist.destroy_process_group()
+
+
 def test_running_loss_on_device(dev):
     """RunningLoss (14:246 `run_loss += loss.item()` without the per-step
     sync): fp64 device sum, count, mean; reset; also inside a HIP graph"""
