@@ -610,13 +610,13 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs a) {
 // Pipeline: one barrier per (chunk, tap) stage; weights prefetched 2 stages
 // ahead in registers, the next chunk's halo loaded at tap 0 and written at
 // tap 8.
-template <int W, int BP> struct HaloGeom {
+template <int W, int BP, int NT = 2 * BP> struct HaloGeom {
   static constexpr int R = BP / W;
   // worst case over H >= 8 with H | R or R | H: R/Hs images of (Hs+2) rows
   static constexpr int HMAX = (R <= 8 ? (R + 2) : (R / 8) * 10) * (W + 2);
   static constexpr int PLANE = ((HMAX * 16 + 255) / 256) * 256;
   static constexpr int HBYTES = 8 * PLANE;
-  static constexpr int LH = (HMAX * 8 + 2 * BP - 1) / (2 * BP);   // pieces per thread (NT = 2 BP)
+  static constexpr int LH = (HMAX * 8 + NT - 1) / NT;             // pieces per thread
 };
 
 // BC = 64 keeps ONE halo buffer (the next chunk's halo is written after an
@@ -624,17 +624,20 @@ template <int W, int BP> struct HaloGeom {
 // per CU, one tile's prologue / epilogue overlapping the other's MFMA loop.
 // BC = 128 double-buffers the halo, 1 workgroup per CU.
 // BP = 128 (256 threads, ~51 KB LDS at BC = 64): 3 workgroups per CU.
-template <int BC, int BP> struct HaloCfg {
+// NT = BP (4 waves at BP = 256, RR_HALO_NT=256): each wave owns a 64 x 64
+// output tile (MC = MP = 4), a third fewer LDS operand reads per MFMA than
+// the 64 x 32 wave tile of NT = 2 BP, at 2 waves per SIMD.
+template <int BC, int BP, int NT = 2 * BP> struct HaloCfg {
   static constexpr int HB = BC <= 64 ? 1 : 2;
-  static constexpr int OCC = BP == 128 ? (BC <= 64 ? 3 : 2) : (BC <= 64 ? 4 : 2);   // min waves / SIMD
+  static constexpr int OCC = NT == BP ? 2 : BP == 128 ? (BC <= 64 ? 3 : 2) : (BC <= 64 ? 4 : 2);   // min waves / SIMD
 };
 
-template <int BC, int W, int MODE, int BP>
-__global__ __launch_bounds__(2 * BP, (HaloCfg<BC, BP>::OCC)) void igemm3_halo_kernel(IgemmArgs a) {
+template <int BC, int W, int MODE, int BP, int NT = 2 * BP>
+__global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_kernel(IgemmArgs a) {
   using T = bf16_t;
-  using G = HaloGeom<W, BP>;
-  constexpr int HB = HaloCfg<BC, BP>::HB;
-  constexpr int NT = 2 * BP, NWAVE = NT / 64;
+  using G = HaloGeom<W, BP, NT>;
+  constexpr int HB = HaloCfg<BC, BP, NT>::HB;
+  constexpr int NWAVE = NT / 64;
   // wave grid: WC (channel) x WP (pixel) waves; a wave owns WCH channels
   // (64, or all 16 for the narrow NCHW image-grad tile)
   constexpr int WC = BC >= 64 ? BC / 64 : 1, WP = NWAVE / WC, WCH = BC / WC;
@@ -967,17 +970,17 @@ int halo_bc(const rr_igemm_desc *d) {
   return 0;
 }
 
-template <int BC, int BP>
+template <int BC, int BP, int NT = 2 * BP>
 int launch_halo(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   a.ncblk = (a.cout + BC - 1) / BC;
   const long long nblk = (long long)(a.P / BP) * a.ncblk;
   if (nblk > 0x7fffffffLL) return RR_EUNSUPPORTED;
-  const dim3 grid((unsigned)nblk), block(2 * BP);
+  const dim3 grid((unsigned)nblk), block(NT);
   switch (d->w) {
-    case 64: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 64, RR_CONV3X3, BP>), grid, block, 0, st, a); break;
-    case 32: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 32, RR_CONV3X3, BP>), grid, block, 0, st, a); break;
-    case 16: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 16, RR_CONV3X3, BP>), grid, block, 0, st, a); break;
-    default: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 8, RR_CONV3X3, BP>), grid, block, 0, st, a); break;
+    case 64: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 64, RR_CONV3X3, BP, NT>), grid, block, 0, st, a); break;
+    case 32: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 32, RR_CONV3X3, BP, NT>), grid, block, 0, st, a); break;
+    case 16: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 16, RR_CONV3X3, BP, NT>), grid, block, 0, st, a); break;
+    default: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 8, RR_CONV3X3, BP, NT>), grid, block, 0, st, a); break;
   }
   RR_CHECK_LAUNCH();
   return RR_OK;
@@ -993,7 +996,11 @@ int dispatch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
       if (hb == 16) return launch_halo<16, 128>(d, a, st);
     } else {
       if (hb == 128) return launch_halo<128, 256>(d, a, st);
-      if (hb == 64) return launch_halo<64, 256>(d, a, st);
+      if (hb == 64) {
+        const char *e = getenv("RR_HALO_NT");      // A/B switch (per call): 256 = 4-wave tiles
+        if (e && atoi(e) == 256) return launch_halo<64, 256, 256>(d, a, st);
+        return launch_halo<64, 256>(d, a, st);
+      }
       if (hb == 16) return launch_halo<16, 256>(d, a, st);
     }
   }
