@@ -302,14 +302,23 @@ __device__ __forceinline__ f32x4 bwd_gm(const BnBwd &a, long long e, int c, f32x
 // ---- 8-channel forms (C % 8 == 0, C / 8 divides 256): a thread's channel
 // group is fixed for the whole grid-stride walk, so the per-channel
 // coefficients live in registers and every access is a 16-B vector.
+//
+// MASK 4 / 5 (nbn = 2, the residual tail with a BN shortcut): as 1 / 3, but
+// the ReLU mask is recomputed from the two pre-BN tensors the kernel reads
+// anyway, with the forward's own expression (affine_act8_kernel /
+// affine_act_pool_kernel: v = t0*s0 + b0; q = t1*s1 + b1; v += q; relu), so
+// the block output is not read: out > 0 <=> v > 0.  s8/b8 hold BN0's forward
+// affine, sB/bB BN1's; tA/tB are the row's t0/t1 values.
 template <typename T, int MASK>
 __device__ __forceinline__ void bwd_gm8(const BnBwd &a, long long e, const float *s8,
-                                        const float *b8, float al, float *g, float &ag) {
+                                        const float *b8, float al, float *g, float &ag,
+                                        const float *tA = nullptr, const float *tB = nullptr,
+                                        const float *sB = nullptr, const float *bB = nullptr) {
   f32x4 g0, g1;
   load8<T>((const T *)a.g + e, g0, g1);
   g[0] = g0[0]; g[1] = g0[1]; g[2] = g0[2]; g[3] = g0[3];
   g[4] = g1[0]; g[5] = g1[1]; g[6] = g1[2]; g[7] = g1[3];
-  if constexpr (MASK == 3) {
+  if constexpr (MASK == 3 || MASK == 5) {
     // + the MaxPool2d(2, 2) backward: the pooled grad goes to the window's
     // first max (rr_maxpool2_bwd's routing), added before the ReLU mask
     const int C = a.C;
@@ -328,7 +337,22 @@ __device__ __forceinline__ void bwd_gm8(const BnBwd &a, long long e, const float
       g[j] += ij == k ? pv[j] : 0.f;
     }
   }
-  if constexpr (MASK == 1 || MASK == 3) {
+  if constexpr (MASK == 4 || MASK == 5) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      f32x4 v = f32x4{tA[4 * h], tA[4 * h + 1], tA[4 * h + 2], tA[4 * h + 3]};
+      f32x4 q = f32x4{tB[4 * h], tB[4 * h + 1], tB[4 * h + 2], tB[4 * h + 3]};
+      const f32x4 sv = f32x4{s8[4 * h], s8[4 * h + 1], s8[4 * h + 2], s8[4 * h + 3]};
+      const f32x4 bv = f32x4{b8[4 * h], b8[4 * h + 1], b8[4 * h + 2], b8[4 * h + 3]};
+      const f32x4 sq = f32x4{sB[4 * h], sB[4 * h + 1], sB[4 * h + 2], sB[4 * h + 3]};
+      const f32x4 bq = f32x4{bB[4 * h], bB[4 * h + 1], bB[4 * h + 2], bB[4 * h + 3]};
+      v = v * sv + bv;
+      q = q * sq + bq;
+      v += q;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) g[4 * h + k] = fmaxf(v[k], 0.f) > 0.f ? g[4 * h + k] : 0.f;
+    }
+  } else if constexpr (MASK == 1 || MASK == 3) {
     f32x4 m0, m1;
     load8<T>((const T *)a.aux + e, m0, m1);
     const float m[8] = {m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
@@ -356,12 +380,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwd a, float *__r
   const int R = 256 / TPR;
   const int tr = threadIdx.x / TPR, tc = threadIdx.x % TPR;
   const int c = tc * 8;
-  float m0[8], i0[8], m1[8], i1[8], s8[8], b8[8];
+  constexpr bool AFF = MASK == 2 || MASK >= 4, REC = MASK >= 4;
+  float m0[8], i0[8], m1[8], i1[8], s8[8], b8[8], sB[8], bB[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     m0[k] = a.mean0[c + k]; i0[k] = a.inv0[c + k];
     m1[k] = NBN == 2 ? a.mean1[c + k] : 0.f; i1[k] = NBN == 2 ? a.inv1[c + k] : 0.f;
-    s8[k] = MASK == 2 ? a.aff_s[c + k] : 0.f; b8[k] = MASK == 2 ? a.aff_b[c + k] : 0.f;
+    s8[k] = AFF ? a.aff_s[c + k] : 0.f; b8[k] = AFF ? a.aff_b[c + k] : 0.f;
+    sB[k] = REC ? a.aff_s[a.C + c + k] : 0.f; bB[k] = REC ? a.aff_b[a.C + c + k] : 0.f;
   }
   const float al = MASK == 2 ? a.alpha[0] : 0.f;
   float s[3][8];
@@ -372,19 +398,23 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwd a, float *__r
   const long long r1 = min(a.P, r0 + rows_per_block);
   for (long long r = r0 + tr; r < r1; r += R) {
     const long long e = r * a.C + c;
-    float gm[8];
-    bwd_gm8<T, MASK>(a, e, s8, b8, al, gm, asum);
+    float gm[8], t0[8], t1[8];
     f32x4 u0, u1;
     load8<T>((const T *)a.t0 + e, u0, u1);
-    const float t0[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+    t0[0] = u0[0]; t0[1] = u0[1]; t0[2] = u0[2]; t0[3] = u0[3];
+    t0[4] = u1[0]; t0[5] = u1[1]; t0[6] = u1[2]; t0[7] = u1[3];
+    if constexpr (NBN == 2) {
+      load8<T>((const T *)a.t1 + e, u0, u1);
+      t1[0] = u0[0]; t1[1] = u0[1]; t1[2] = u0[2]; t1[3] = u0[3];
+      t1[4] = u1[0]; t1[5] = u1[1]; t1[6] = u1[2]; t1[7] = u1[3];
+    }
+    bwd_gm8<T, MASK>(a, e, s8, b8, al, gm, asum, t0, t1, sB, bB);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       s[0][k] += gm[k];
       s[1][k] += gm[k] * ((t0[k] - m0[k]) * i0[k]);
     }
     if constexpr (NBN == 2) {
-      load8<T>((const T *)a.t1 + e, u0, u1);
-      const float t1[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
 #pragma unroll
       for (int k = 0; k < 8; ++k) s[2][k] += gm[k] * ((t1[k] - m1[k]) * i1[k]);
     }
@@ -414,7 +444,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(BnBwd a, const float
                                                             T *dt0, T *dt1, T *gmo) {
   const int G = a.C / 8;
   const int c = (threadIdx.x % G) * 8;   // fixed: G divides the grid stride
-  float cf[2][3][8], mu[2][8], iv[2][8], s8[8], b8[8];
+  constexpr bool AFF = MASK == 2 || MASK >= 4, REC = MASK >= 4;
+  float cf[2][3][8], mu[2][8], iv[2][8], s8[8], b8[8], sB[8], bB[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
 #pragma unroll
@@ -424,22 +455,28 @@ __global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(BnBwd a, const float
     }
     mu[0][k] = a.mean0[c + k]; iv[0][k] = a.inv0[c + k];
     mu[1][k] = NBN == 2 ? a.mean1[c + k] : 0.f; iv[1][k] = NBN == 2 ? a.inv1[c + k] : 0.f;
-    s8[k] = MASK == 2 ? a.aff_s[c + k] : 0.f; b8[k] = MASK == 2 ? a.aff_b[c + k] : 0.f;
+    s8[k] = AFF ? a.aff_s[c + k] : 0.f; b8[k] = AFF ? a.aff_b[c + k] : 0.f;
+    sB[k] = REC ? a.aff_s[a.C + c + k] : 0.f; bB[k] = REC ? a.aff_b[a.C + c + k] : 0.f;
   }
   const float al = MASK == 2 ? a.alpha[0] : 0.f;
   const long long rows = a.P;
   const long long stride = ((long long)gridDim.x * blockDim.x) / G;
   for (long long r = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / G; r < rows; r += stride) {
     const long long e = r * a.C + c;
-    float gm[8], ag = 0.f;
-    bwd_gm8<T, MASK>(a, e, s8, b8, al, gm, ag);
-    if constexpr (GMO)
-      store8<T>(gmo + e, f32x4{gm[0], gm[1], gm[2], gm[3]}, f32x4{gm[4], gm[5], gm[6], gm[7]});
+    float gm[8], ag = 0.f, tv[2][8];
 #pragma unroll
     for (int b = 0; b < NBN; ++b) {
       f32x4 u0, u1;
       load8<T>((const T *)(b == 0 ? a.t0 : a.t1) + e, u0, u1);
-      const float t[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+      tv[b][0] = u0[0]; tv[b][1] = u0[1]; tv[b][2] = u0[2]; tv[b][3] = u0[3];
+      tv[b][4] = u1[0]; tv[b][5] = u1[1]; tv[b][6] = u1[2]; tv[b][7] = u1[3];
+    }
+    bwd_gm8<T, MASK>(a, e, s8, b8, al, gm, ag, tv[0], tv[NBN - 1], sB, bB);
+    if constexpr (GMO)
+      store8<T>(gmo + e, f32x4{gm[0], gm[1], gm[2], gm[3]}, f32x4{gm[4], gm[5], gm[6], gm[7]});
+#pragma unroll
+    for (int b = 0; b < NBN; ++b) {
+      const float *t = tv[b];
       float o[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -758,8 +795,10 @@ extern "C" int rr_bn_bwd_blocks(const rr_bnbwd_desc *d) {
 static int bnbwd_check(const rr_bnbwd_desc *d) {
   if (!d || d->P <= 0 || d->C <= 0 || d->C % 4 || d->C / 4 > 256) return RR_EINVAL;
   if (d->nbn != 1 && d->nbn != 2) return RR_EINVAL;
-  if (d->mask_kind < 0 || d->mask_kind > 3) return RR_EINVAL;
-  if (d->mask_kind == 3) {
+  if (d->mask_kind < 0 || d->mask_kind > 5) return RR_EINVAL;
+  if (d->mask_kind >= 4 && (d->nbn != 2 || d->C % 8 || 256 % (d->C / 8)))
+    return RR_EUNSUPPORTED;                 // recomputed mask: BN shortcut, 8-channel kernels
+  if (d->mask_kind == 3 || d->mask_kind == 5) {
     if (!d->pool_dy || !d->pool_idx || d->h <= 0 || d->w <= 0 || d->h % 2 || d->w % 2 ||
         d->P % ((long long)d->h * d->w) || d->C % 8 || 256 % (d->C / 8) || d->P > 0x7fffffffLL)
       return RR_EUNSUPPORTED;               // 8-channel kernels only
@@ -787,8 +826,9 @@ extern "C" int rr_bn_bwd_reduce(const rr_bnbwd_desc *d, const void *g, const voi
   int rc = bnbwd_check(d);
   if (rc) return rc;
   if (!g || !t0 || !mean0 || !invstd0 || !partial) return RR_EINVAL;
-  if (d->mask_kind && !aux) return RR_EINVAL;
+  if (d->mask_kind && d->mask_kind < 4 && !aux) return RR_EINVAL;
   if (d->mask_kind == 2 && (!aff_s || !aff_b || !alpha)) return RR_EINVAL;
+  if (d->mask_kind >= 4 && (!aff_s || !aff_b)) return RR_EINVAL;
   if (d->nbn == 2 && (!t1 || !mean1 || !invstd1)) return RR_EINVAL;
   const BnBwd a = make_bnbwd(d, g, aux, aff_s, aff_b, alpha, t0, mean0, invstd0, t1, mean1, invstd1);
   const int blocks = reduce_blocks(d->P);
@@ -807,7 +847,8 @@ extern "C" int rr_bn_bwd_reduce(const rr_bnbwd_desc *d, const void *g, const voi
       case 0: RR_RED8(TT, 0, 1); break; case 1: RR_RED8(TT, 0, 2); break; \
       case 2: RR_RED8(TT, 1, 1); break; case 3: RR_RED8(TT, 1, 2); break; \
       case 4: RR_RED8(TT, 2, 1); break; case 5: RR_RED8(TT, 2, 2); break; \
-      case 6: RR_RED8(TT, 3, 1); break; default: RR_RED8(TT, 3, 2); break; \
+      case 6: RR_RED8(TT, 3, 1); break; case 7: RR_RED8(TT, 3, 2); break; \
+      case 9: RR_RED8(TT, 4, 2); break; default: RR_RED8(TT, 5, 2); break; \
     }
     if (d->dtype == RR_BF16) { RR_RED8_T(bf16_t) } else { RR_RED8_T(float) }
 #undef RR_RED8_T
@@ -852,6 +893,7 @@ extern "C" int rr_bn_bwd_apply(const rr_bnbwd_desc *d, const void *g, const void
   int rc = bnbwd_check(d);
   if (rc) return rc;
   if (!g || !t0 || !coef || !dt0 || (d->nbn == 2 && (!t1 || !dt1))) return RR_EINVAL;
+  if (d->mask_kind >= 4 && (!aff_s || !aff_b || gm_out)) return RR_EINVAL;
   const BnBwd a = make_bnbwd(d, g, aux, aff_s, aff_b, alpha, t0, mean0, invstd0, t1, mean1, invstd1);
   hipStream_t st = (hipStream_t)stream;
   if (d->C % 8 == 0 && 256 % (d->C / 8) == 0) {
@@ -862,7 +904,8 @@ extern "C" int rr_bn_bwd_apply(const rr_bnbwd_desc *d, const void *g, const void
     else { if (gm_out) RR_APP8(TT, M, 2, true); else RR_APP8(TT, M, 2, false); }
 #define RR_APP8_T(TT)                                                           \
     if (d->mask_kind == 0) { RR_APP8_M(TT, 0) } else if (d->mask_kind == 1) { RR_APP8_M(TT, 1) } \
-    else if (d->mask_kind == 2) { RR_APP8_M(TT, 2) } else { RR_APP8_M(TT, 3) }
+    else if (d->mask_kind == 2) { RR_APP8_M(TT, 2) } else if (d->mask_kind == 3) { RR_APP8_M(TT, 3) } \
+    else if (d->mask_kind == 4) { RR_APP8(TT, 4, 2, false); } else { RR_APP8(TT, 5, 2, false); }
     if (d->dtype == RR_BF16) { RR_APP8_T(bf16_t) } else { RR_APP8_T(float) }
 #undef RR_APP8_T
 #undef RR_APP8_M

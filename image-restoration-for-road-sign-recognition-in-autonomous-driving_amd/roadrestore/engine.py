@@ -337,7 +337,7 @@ def resblock_forward(blk, x1, x2, n, h, w, wc, dt, training, need_bwd, pool=Fals
         ss, shs, ms, is_ = _bn_affine(sc1, sts, sc0.bias, P, training)
         res, rsc, rsh = s, ss, shs
         if need_bwd:
-            S.update(s=s, ms=ms, is_=is_, pks=pks)
+            S.update(s=s, ms=ms, is_=is_, pks=pks, s2=s2, sh2=sh2, ss=ss, shs=shs)
     else:
         if x2 is not None:
             raise RuntimeError("identity shortcut with a concatenated input")
@@ -379,8 +379,13 @@ def resblock_backward(blk, S, g_out, sink, pool=None):
     gx1 = gx2 = None
     if has_sc:
         sc0, sc1 = blk.shortcut[0], blk.shortcut[1]
+        # the ReLU mask from t2 and s as the forward formed the output (mask
+        # kind 4/5): one tensor read fewer in both BN-backward passes
+        rec = None
+        if _RECOMPUTE_MASK and cout % 8 == 0 and 256 % (cout // 8) == 0:
+            rec = (torch.stack((S.s2, S.ss)), torch.stack((S.sh2, S.shs)))
         r = ops.bn_backward(g_out, S.t2, S.m2, S.i2, bn2.weight, mask_kind=1, aux=S.out, pool=pool,
-                            t1=S.s, mean1=S.ms, inv1=S.is_, gamma1=sc1.weight,
+                            recompute=rec, t1=S.s, mean1=S.ms, inv1=S.is_, gamma1=sc1.weight,
                             outs=dict(dgamma0=sink[bn2.weight], dbeta0=sink[bn2.bias],
                                       dgamma1=sink[sc1.weight], dbeta1=sink[sc1.bias]))
         dt2, ds = r["dt0"], r["dt1"]
@@ -500,6 +505,9 @@ _FUSED_POOL = os.environ.get("RR_FUSED_POOL", "1") != "0"
 _FUSED_POOL_BWD = os.environ.get("RR_FUSED_POOL_BWD", "1") != "0"
 # A/B switch: dec1's concat dgrad as two 64 -> 64 row-streaming launches
 _SPLIT_DGRAD = os.environ.get("RR_SPLIT_DGRAD", "1") != "0"
+# A/B switch: the BN-shortcut tail's ReLU mask recomputed from t2 and the
+# shortcut's pre-BN output (read anyway) instead of read from the block output
+_RECOMPUTE_MASK = os.environ.get("RR_BN_RECOMPUTE_MASK", "1") != "0"
 
 
 def resunet_backward(m, S, g_out, sink):

@@ -320,22 +320,31 @@ def affine_act_pool(x, scale, shift, res=None, res_scale=None, res_shift=None, r
 
 def bn_backward(g, t0, mean0, inv0, gamma0, *, mask_kind=0, aux=None, aff_s=None, aff_b=None,
                 alpha=None, t1=None, mean1=None, inv1=None, gamma1=None, want_gm=False,
-                gm_out=None, outs=None, pool=None):
+                gm_out=None, outs=None, pool=None, recompute=None):
     """Full BN backward (reduce + finalize + apply) for one or two BNs that
     share the upstream gradient.  Returns dict with dt0, dt1, gm, dgamma0,
     dbeta0, dgamma1, dbeta1, dalpha.  ``pool=(dy_pool, idx)`` with
     mask_kind 1: the 2x2 max-pool backward is added to g before the ReLU mask
-    (mask kind 3, g: [n, h, w, C])."""
+    (mask kind 3, g: [n, h, w, C]).  ``recompute=(aff_s2, aff_b2)`` with
+    mask_kind 1 and two BNs: the ReLU mask is recomputed from t0, t1 with the
+    forward affines ([2, C] each: BN0's then BN1's scale / shift) instead of
+    read from ``aux`` (mask kind 4, or 5 with ``pool``)."""
     Cc = g.shape[-1]
     P = g.numel() // Cc
     nbn = 2 if t1 is not None else 1
     dev = g.device
     d = BnBwdDesc(rr_dtype(g.dtype), P, Cc, mask_kind, nbn, 0, 0, None, None)
+    if recompute is not None:
+        if mask_kind != 1 or nbn != 2 or want_gm or gm_out is not None:
+            raise ValueError("recomputed ReLU mask needs mask_kind 1, two BNs and no gm output")
+        aff_s, aff_b = (x.contiguous() for x in recompute)
+        aux = None
+        d.mask_kind = 4
     if pool is not None:
         if mask_kind != 1 or g.dim() != 4:
             raise ValueError("pool backward fusion needs the ReLU mask and an [n, h, w, C] grad")
         pdy, pidx = pool
-        d.mask_kind, d.h, d.w = 3, g.shape[1], g.shape[2]
+        d.mask_kind, d.h, d.w = 5 if recompute is not None else 3, g.shape[1], g.shape[2]
         d.pool_dy, d.pool_idx = _p(pdy.contiguous()), _p(pidx)
     blocks = lib().rr_bn_bwd_blocks(C.byref(d))
     part = torch.empty(blocks * Cc * 3 + blocks, dtype=torch.float32, device=dev)

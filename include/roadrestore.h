@@ -194,7 +194,12 @@ typedef struct {
   int32_t mask_kind;    /* 0 none, 1 ReLU (aux = ReLU output), 2 PReLU (aux = t),
                            3 ReLU + MaxPool2d(2,2) backward: g + unpool(pool_dy, pool_idx)
                            before the mask (the encoder block output feeds both the
-                           skip concat and the pool, 14:125-131) */
+                           skip concat and the pool, 14:125-131),
+                           4 / 5 as 1 / 3 with nbn = 2 (residual tail with a BN
+                           shortcut, 14:107-115) but the ReLU mask recomputed from
+                           t0, t1 as the forward computed the block output:
+                           relu(t0*aff_s[c] + aff_b[c] + (t1*aff_s[C+c] + aff_b[C+c]));
+                           aux unused, aff_s / aff_b are [2][C], no gm_out */
   int32_t nbn;          /* 1 or 2 */
   int32_t h, w;         /* mask_kind 3: the [P] rows are [n][h][w] pixels (h, w even) */
   const void *pool_dy;  /* mask_kind 3: [n][h/2][w/2][C] grad of the pooled output */

@@ -549,6 +549,39 @@ def test_bn_backward_pool_fused(dev, dt, nbn):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("pool", [False, True])
+@pytest.mark.parametrize("C", [64, 256])
+def test_bn_backward_recomputed_mask(dev, dt, pool, C):
+    """mask kind 4 / 5: the BN-shortcut tail's ReLU mask recomputed from t0,
+    t1 and the forward affines equals the mask read from the block output the
+    forward kernels (rr_affine_act / rr_affine_act_pool) wrote -- every output
+    bit for bit"""
+    from roadrestore import ops
+    n, h, w = 2, 8, 12
+    t0 = rnd(n, h, w, C, seed=21).to(dev, dt)
+    t1 = rnd(n, h, w, C, seed=22).to(dev, dt)
+    s0, b0 = rnd(C, seed=23).to(dev), rnd(C, seed=24).to(dev)
+    s1, b1 = rnd(C, seed=25).to(dev), rnd(C, seed=26).to(dev)
+    if pool:
+        out, pooled, idx = ops.affine_act_pool(t0, s0, b0, res=t1, res_scale=s1, res_shift=b1, relu=True)
+        pl = (rnd(n, h // 2, w // 2, C, seed=27).to(dev, dt), idx)
+    else:
+        out = ops.affine_act(t0, s0, b0, res=t1, res_scale=s1, res_shift=b1, relu=True)
+        pl = None
+    assert 0.2 < (out.float() > 0).float().mean().item() < 0.8
+    g = rnd(n, h, w, C, seed=28).to(dev, dt)
+    m0, i0 = rnd(C, seed=29).to(dev), (rnd(C, seed=30).abs() + 0.5).to(dev)
+    m1, i1 = rnd(C, seed=31).to(dev), (rnd(C, seed=32).abs() + 0.5).to(dev)
+    gam0, gam1 = rnd(C, seed=33).to(dev), rnd(C, seed=34).to(dev)
+    kw = dict(mask_kind=1, aux=out, t1=t1, mean1=m1, inv1=i1, gamma1=gam1, pool=pl)
+    ref = ops.bn_backward(g, t0, m0, i0, gam0, **kw)
+    got = ops.bn_backward(g, t0, m0, i0, gam0,
+                          recompute=(torch.stack((s0, s1)), torch.stack((b0, b1))), **kw)
+    for k in ("dt0", "dt1", "dgamma0", "dbeta0", "dgamma1", "dbeta1"):
+        assert torch.equal(got[k], ref[k]), k
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("count", [4096, 4093])
 @pytest.mark.parametrize("kind", [0, 1])
 def test_loss_vector_and_scalar_paths(dev, dt, count, kind):
