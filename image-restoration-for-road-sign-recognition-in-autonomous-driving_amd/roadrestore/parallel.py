@@ -32,6 +32,20 @@ class _UniqueId(ctypes.Structure):
     _fields_ = [("internal", ctypes.c_char * 128)]     # NCCL_UNIQUE_ID_BYTES
 
 
+def uid_to_bytes(uid):
+    """The raw 128 bytes of an ncclUniqueId (reading the c_char field would
+    stop at the first NUL)."""
+    return ctypes.string_at(ctypes.addressof(uid), ctypes.sizeof(uid))
+
+
+def uid_from_bytes(raw):
+    if len(raw) != ctypes.sizeof(_UniqueId):
+        raise RuntimeError("RcclComm: bad unique id")
+    uid = _UniqueId()
+    ctypes.memmove(ctypes.addressof(uid), raw, len(raw))
+    return uid
+
+
 class RcclComm:
     """A communicator of its own on the RCCL library torch ships (rccl.h:
     ncclGetUniqueId / ncclCommInitRank / ncclAllReduce), for the gradient
@@ -64,12 +78,9 @@ class RcclComm:
         uid = _UniqueId()
         if self.rank == 0:
             self._check(lib.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
-        # raw 128 bytes (the c_char field itself reads as NUL-terminated bytes)
-        obj = [ctypes.string_at(ctypes.addressof(uid), 128) if self.rank == 0 else None]
+        obj = [uid_to_bytes(uid) if self.rank == 0 else None]
         dist.broadcast_object_list(obj, src=0, group=process_group)
-        if len(obj[0]) != 128:
-            raise RuntimeError("RcclComm: bad unique id from rank 0")
-        ctypes.memmove(ctypes.addressof(uid), obj[0], 128)
+        uid = uid_from_bytes(obj[0])
         self.comm = ctypes.c_void_p()
         with torch.cuda.device(device):
             self._check(lib.ncclCommInitRank(ctypes.byref(self.comm), self.world, uid, self.rank),

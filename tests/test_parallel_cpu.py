@@ -101,3 +101,15 @@ def test_bucket_plan_contiguous_with_small_tail():
     ids = set().union(*(b[2] for b in dp.buckets))
     assert ids == {id(p) for p in layout if id(p) not in zs}
     assert (dp.buckets[-1][1] - dp.buckets[-1][0]) * 4 <= 4 * 2 ** 20
+
+
+def test_rccl_unique_id_bytes_round_trip():
+    """RcclComm ships ncclUniqueId as its raw 128 bytes: NULs inside the id
+    survive (the c_char field alone would cut the id at the first NUL)."""
+    from roadrestore.parallel import _UniqueId, uid_from_bytes, uid_to_bytes
+    raw = bytes([0, 1, 0, 255] * 32)
+    uid = uid_from_bytes(raw)
+    assert uid_to_bytes(uid) == raw
+    assert uid_to_bytes(_UniqueId()) == bytes(128)
+    with pytest.raises(RuntimeError):
+        uid_from_bytes(raw[:100])
