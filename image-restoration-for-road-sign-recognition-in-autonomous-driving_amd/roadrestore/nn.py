@@ -185,10 +185,27 @@ class _RRNet(tnn.Module):
             x = x.float()
         return x.contiguous()
 
+    def _empty_forward(self, x, need):
+        """An empty batch, as torch runs the reference modules on one: an empty
+        output; train-mode BNs count the batch (nn.BatchNorm2d increments
+        num_batches_tracked before F.batch_norm) and keep their running stats
+        (ATen returns early on empty input); every parameter gets a zero grad."""
+        if self.training:
+            for m in self.modules():
+                if isinstance(m, BatchNorm2d):
+                    m.num_batches_tracked.add_(1)
+        cout = self.conv_block[0].out_channels if isinstance(self, ResidualBlock) else 3
+        out = x.new_zeros((0, cout) + tuple(x.shape[2:]))
+        if need:
+            out = out + sum(p.sum() * 0 for p in self.parameters() if p.requires_grad)
+        return out
+
     def forward(self, x):
         x = self._check_input(x)
         params = [p for p in self.parameters()]
         need = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        if x.shape[0] == 0:
+            return self._empty_forward(x, need)
         if not need:
             out, _ = self._rr_forward(x, need_bwd=False)
             return out

@@ -417,6 +417,34 @@ def test_hip_graph_dp_step_with_rccl_matches_eager(dev):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("training", [False, True])
+def test_resunet_empty_batch(dev, training):
+    """An empty batch behaves as the reference modules do under torch (the
+    oracle restatement here): an empty [0, 3, H, W] output; in train mode
+    every BN counts the batch and keeps its running stats; backward gives
+    zero parameter grads"""
+    import roadrestore as rr
+    from oracle import reference_cpu as R, seeded as S
+    sd = S.model_state_dict("resunet", seed=0)
+    m = rr.ResUNet().to(dev)
+    m.load_state_dict(sd)
+    m.train(training)
+    x = torch.rand(0, 3, 64, 64)
+    p = {k: v.clone() for k, v in sd.items()}
+    ref = R.resunet_forward(p, x, training=training)
+    if training:
+        out = m(x.to(dev))
+        out.sum().backward()
+        g = m.res2.conv_block[0].weight.grad
+        assert g is not None and not g.abs().any()
+    else:
+        with torch.no_grad():
+            out = m(x.to(dev))
+    assert out.shape == ref.shape == (0, 3, 64, 64)
+    for k, v in m.state_dict().items():
+        assert torch.equal(v.cpu(), p[k]), k
+
+
 def test_running_loss_on_device(dev):
     """RunningLoss (14:246 `run_loss += loss.item()` without the per-step
     sync): fp64 device sum, count, mean; reset; also inside a HIP graph"""
