@@ -28,12 +28,9 @@ __global__ __launch_bounds__(256) void bn_finalize_direct_kernel(
   __shared__ double red[2][256];
   const int c = blockIdx.x, t = threadIdx.x;
   if (nbt && c == 0 && t == 0) nbt[0] += 1;
-  double s1 = 0.0, s2 = 0.0;
-  for (int b = t; b < rows; b += 256) {
-    const float *p = part + ((long long)b * C + c) * 2;
-    s1 += p[0];
-    s2 += p[1];
-  }
+  double s[2] = {0.0, 0.0};
+  rr_fixed_sum<2>(part + ((long long)t * C + c) * 2, 256LL * C * 2, rr_trips(t, rows, 256), s);
+  double s1 = s[0], s2 = s[1];
   red[0][t] = s1;
   red[1][t] = s2;
   __syncthreads();
@@ -72,14 +69,9 @@ __global__ void bn_finalize_kernel(int C, int blocks, double count, const double
   if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
   const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
-  double s1 = 0.0, s2 = 0.0;
-  if (c < C) {
-    for (int b = sl; b < blocks; b += 16) {
-      const double *p = part + ((long long)b * C + c) * 2;
-      s1 += p[0];
-      s2 += p[1];
-    }
-  }
+  double s[2] = {0.0, 0.0};
+  if (c < C) rr_fixed_sum<2>(part + ((long long)sl * C + c) * 2, 16LL * C * 2, rr_trips(sl, blocks, 16), s);
+  double s1 = s[0], s2 = s[1];
   red[0][sl][cl] = s1;
   red[1][sl][cl] = s2;
   __syncthreads();
@@ -557,11 +549,9 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
     float *dg0, float *db0, float *dg1, float *db1, float *dalpha, float *coef) {
   __shared__ double red[3][256];
   const int c = blockIdx.x, t = threadIdx.x;
-  double s0 = 0, s1 = 0, s2 = 0;
-  for (int b = t; b < blocks; b += 256) {
-    const PT *p = part + ((long long)b * C + c) * 3;
-    s0 += p[0]; s1 += p[1]; s2 += p[2];
-  }
+  double s[3] = {0, 0, 0};
+  rr_fixed_sum<3>(part + ((long long)t * C + c) * 3, 256LL * C * 3, rr_trips(t, blocks, 256), s);
+  double s0 = s[0], s1 = s[1], s2 = s[2];
   red[0][t] = s0; red[1][t] = s1; red[2][t] = s2;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
@@ -589,9 +579,9 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
   }
   if (blockIdx.x == 0 && apart && dalpha) {
     __syncthreads();
-    double v = 0;
-    for (int b = t; b < ablocks; b += 256) v += apart[b];
-    red[0][t] = v;
+    double v[1] = {0};
+    rr_fixed_sum<1>(apart + t, 256, rr_trips(t, ablocks, 256), v);
+    red[0][t] = v[0];
     __syncthreads();
     if (t == 0) {
       double tt = 0;
@@ -671,9 +661,9 @@ __global__ void colsum_finalize(int C, int blocks, const float *__restrict__ par
   __shared__ double red[16][17];
   const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
-  double s = 0;
-  if (c < C)
-    for (int b = sl; b < blocks; b += 16) s += part[(long long)b * C + c];
+  double sv[1] = {0};
+  if (c < C) rr_fixed_sum<1>(part + (long long)sl * C + c, 16LL * C, rr_trips(sl, blocks, 16), sv);
+  double s = sv[0];
   red[sl][cl] = s;
   __syncthreads();
   if (sl == 0 && c < C) {

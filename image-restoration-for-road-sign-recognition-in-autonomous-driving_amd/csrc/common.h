@@ -135,6 +135,36 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f) {
   return (t + n) >> f.s;
 }
 
+// Fixed-order strided fp64 sums of NC interleaved components:
+//   for (i = 0; i < n; ++i) s[k] += p[i * stride + k]
+// with the loads of U iterations issued before their adds.  The add order is
+// the plain loop's (bitwise-equal result); the plain loop compiles to one
+// load -> wait -> add per iteration, i.e. one L2/HBM latency per row, which
+// is what held the small finalize launches at 6-18 us.
+template <int NC, int U = (NC == 1 ? 16 : 8), typename T>
+__device__ __forceinline__ void rr_fixed_sum(const T *__restrict__ p, long long stride, long long n,
+                                             double (&s)[NC]) {
+  long long i = 0;
+  for (; i + U <= n; i += U) {
+    T v[U][NC];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < NC; ++k) v[u][k] = p[(i + u) * stride + k];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < NC; ++k) s[k] += (double)v[u][k];
+  }
+  for (; i < n; ++i)
+#pragma unroll
+    for (int k = 0; k < NC; ++k) s[k] += (double)p[i * stride + k];
+}
+// iterations of `for (i = first; i < end; i += step)`
+__device__ __forceinline__ long long rr_trips(long long first, long long end, long long step) {
+  return first < end ? (end - first + step - 1) / step : 0;
+}
+
 // Deterministic column reduction of fp32 partials: in [rows][cols] ->
 // out [chunks][cols] in fp64 (fixed order).  grid (ceil(cols/64), chunks),
 // 256 threads = 64 columns x 4 row lanes.  Feeds the finalize kernels so
@@ -146,10 +176,9 @@ __global__ static void rr_colreduce_kernel(const float *__restrict__ in, int row
   const int c = blockIdx.x * 64 + tc;
   const long long r0 = (long long)blockIdx.y * rows_per_chunk;
   const long long r1 = min((long long)rows, r0 + rows_per_chunk);
-  double s = 0.0;
-  if (c < cols)
-    for (long long r = r0 + l; r < r1; r += 4) s += in[r * cols + c];
-  red[l][tc] = s;
+  double s[1] = {0.0};
+  if (c < cols) rr_fixed_sum<1>(in + (r0 + l) * cols + c, 4LL * cols, rr_trips(r0 + l, r1, 4), s);
+  red[l][tc] = s[0];
   __syncthreads();
   if (l == 0 && c < cols) out[(long long)blockIdx.y * cols + c] = red[0][tc] + red[1][tc] + red[2][tc] + red[3][tc];
 }

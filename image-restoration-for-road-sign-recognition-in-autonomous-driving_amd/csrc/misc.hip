@@ -332,8 +332,9 @@ __global__ void conv_in_wgrad_act_finalize(int chunks, const double *__restrict_
   const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over 64 * 32 + 1
   const int cols = 64 * 32 + 32;
   if (i > 64 * 32) return;
-  double s = 0;
-  for (int b = 0; b < chunks; ++b) s += part[(long long)b * cols + i];
+  double sv[1] = {0};
+  rr_fixed_sum<1>(part + i, cols, chunks, sv);
+  const double s = sv[0];
   if (i == 64 * 32) {
     if (dalpha) dalpha[0] = (float)s;
     return;
@@ -349,8 +350,9 @@ __global__ void conv_in_wgrad_finalize(int cout, int kk, int blocks, const doubl
   if (i >= cout * 32) return;
   const int co = i / 32, j = i % 32;
   if (j > kk) return;
-  double s = 0;
-  for (int b = 0; b < blocks; ++b) s += part[(long long)b * cout * 32 + i];
+  double sv[1] = {0};
+  rr_fixed_sum<1>(part + i, (long long)cout * 32, blocks, sv);
+  const double s = sv[0];
   if (j < kk) dw[(long long)co * kk + j] = (float)s;
   else if (db) db[co] = (float)s;
 }
@@ -739,11 +741,15 @@ __global__ void conv_out_bwd_finalize(int cin, int cout, int blocks, const doubl
   if (i >= cout * cin + cout) return;
   double s = 0;
   if (i < cout * cin) {
-    for (int b = 0; b < blocks; ++b) s += part[(long long)b * (cout + 1) * cin + i];
+    double sv[1] = {0};
+    rr_fixed_sum<1>(part + i, (long long)(cout + 1) * cin, blocks, sv);
+    s = sv[0];
     if (dw) dw[i] = (float)s;
   } else {
     const int co = i - cout * cin;
-    for (int b = 0; b < blocks; ++b) s += part[((long long)b * (cout + 1) + cout) * cin + co];
+    double sv[1] = {0};
+    rr_fixed_sum<1>(part + (long long)cout * cin + co, (long long)(cout + 1) * cin, blocks, sv);
+    s = sv[0];
     if (db) db[co] = (float)s;
   }
 }
@@ -922,9 +928,9 @@ __global__ void prelu_bwd_kernel(long long count, const T *__restrict__ dy, cons
 
 __global__ void sum_partials(int n, const float *__restrict__ part, float *out, int accumulate) {
   __shared__ double red[256];
-  double s = 0;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) s += part[i];
-  red[threadIdx.x] = s;
+  double s[1] = {0};
+  rr_fixed_sum<1>(part + threadIdx.x, blockDim.x, rr_trips(threadIdx.x, n, blockDim.x), s);
+  red[threadIdx.x] = s[0];
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
@@ -1060,9 +1066,9 @@ __global__ void loss_bwd8_kernel(int kind, long long count, const T *__restrict_
 __global__ void loss_finalize(int blocks, const float *__restrict__ part, float *out, double scale,
                               int accumulate) {
   __shared__ double red[256];
-  double s = 0;
-  for (int i = threadIdx.x; i < blocks; i += blockDim.x) s += part[i];
-  red[threadIdx.x] = s;
+  double s[1] = {0};
+  rr_fixed_sum<1>(part + threadIdx.x, blockDim.x, rr_trips(threadIdx.x, blocks, blockDim.x), s);
+  red[threadIdx.x] = s[0];
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
