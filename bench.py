@@ -86,7 +86,7 @@ class KernelProbe:
         return agg
 
 
-PMC_TRAFFIC = os.path.join(REPO, "profiles", "r1g_pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(REPO, "profiles", "r1h_pmc_traffic.json")
 
 
 def _norm_sym(sym):
@@ -290,7 +290,7 @@ def main():
                 "unit": "TFLOP/s", "frac": round(ach / pk, 4), "traffic": traffic,
                 "traffic_note": "HBM bytes per launch, rocprofv3 FETCH_SIZE x2 (gfx950) + "
                                 "WRITE_SIZE in separate --pmc passes of this bench "
-                                "(profiles/r1g_pmc_traffic.json)" if traffic else None,
+                                "(profiles/r1h_pmc_traffic.json)" if traffic else None,
                 "launches": cnt, "avg_launch_ms": round(ms / cnt, 4),
                 "flop_per_launch": fl / cnt}
         tot_fl = sum(v[1] for v in agg.values())

@@ -300,12 +300,13 @@ def simple_unet_backward(m, S, g_out, sink):
 # ---------------------------------------------------------------------------
 # ResidualBlock (14:96-115) and ResUNet (14:117-186)
 
-def _bn_affine(bn, st, bias, count, training):
+def _bn_affine(bn, st, bias, count, training, out=None):
     if training:
         if bn.momentum is None:
             raise NotImplementedError("BatchNorm2d(momentum=None) is not supported")
         return ops.bn_finalize(st, count, bias, bn.weight, bn.bias, bn.running_mean,
-                               bn.running_var, bn.momentum, bn.eps, bn.num_batches_tracked)
+                               bn.running_var, bn.momentum, bn.eps, bn.num_batches_tracked,
+                               out=out)
     s, b = ops.bn_eval_affine(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
     return s, b, None, None
 
@@ -327,17 +328,26 @@ def resblock_forward(blk, x1, x2, n, h, w, wc, dt, training, need_bwd, pool=Fals
     a1 = ops.affine_act(t1, s1, sh1, alpha=pr.weight)
     pk2 = wc.conv(c2.weight, dt, dgrad=need_bwd)
     t2, _, st2 = ops.igemm(RR_CONV3X3, a1, None, n, h, w, pk2[0], cout, bias=c2.bias, stats=training)
-    s2, sh2, m2, i2 = _bn_affine(bn2, st2, c2.bias, P, training)
+    has_sc = block_has_shortcut(blk)
+    # (scale, shift) of bn2 and the shortcut BN as rows of two [2, C] buffers:
+    # the backward's recomputed ReLU mask reads them as pairs (no stack copy)
+    pair = None
+    if has_sc and training and need_bwd and _RECOMPUTE_MASK:
+        pair = (torch.empty(2, cout, dtype=torch.float32, device=x1.device),
+                torch.empty(2, cout, dtype=torch.float32, device=x1.device))
+    s2, sh2, m2, i2 = _bn_affine(bn2, st2, c2.bias, P, training,
+                                 out=(pair[0][0], pair[1][0]) if pair else None)
     S = Bag(x1=x1, x2=x2, n=n, h=h, w=w)
-    if block_has_shortcut(blk):
+    if has_sc:
         sc0, sc1 = blk.shortcut[0], blk.shortcut[1]
         pks = wc.conv(sc0.weight, dt, dgrad=need_bwd)
         s, _, sts = ops.igemm(RR_CONV1X1, x1, x2, n, h, w, pks[0], cout, bias=sc0.bias,
                               stats=training)
-        ss, shs, ms, is_ = _bn_affine(sc1, sts, sc0.bias, P, training)
+        ss, shs, ms, is_ = _bn_affine(sc1, sts, sc0.bias, P, training,
+                                      out=(pair[0][1], pair[1][1]) if pair else None)
         res, rsc, rsh = s, ss, shs
         if need_bwd:
-            S.update(s=s, ms=ms, is_=is_, pks=pks, s2=s2, sh2=sh2, ss=ss, shs=shs)
+            S.update(s=s, ms=ms, is_=is_, pks=pks, s2=s2, sh2=sh2, ss=ss, shs=shs, pair=pair)
     else:
         if x2 is not None:
             raise RuntimeError("identity shortcut with a concatenated input")
@@ -393,7 +403,8 @@ def resblock_backward(blk, S, g_out, sink, pool=None):
         # kind 4/5): one tensor read fewer in both BN-backward passes
         rec = None
         if _RECOMPUTE_MASK and cout % 8 == 0 and 256 % (cout // 8) == 0:
-            rec = (torch.stack((S.s2, S.ss)), torch.stack((S.sh2, S.shs)))
+            rec = S.pair if S.get("pair") is not None else (torch.stack((S.s2, S.ss)),
+                                                             torch.stack((S.sh2, S.shs)))
         r = ops.bn_backward(g_out, S.t2, S.m2, S.i2, bn2.weight, mask_kind=1, aux=S.out, pool=pool,
                             recompute=rec, t1=S.s, mean1=S.ms, inv1=S.is_, gamma1=sc1.weight,
                             outs=dict(dgamma0=sink[bn2.weight], dbeta0=sink[bn2.bias],

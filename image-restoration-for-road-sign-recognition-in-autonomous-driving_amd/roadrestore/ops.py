@@ -266,12 +266,20 @@ def wgrad(mode, dy, x1, x2, n, h, w, cout, dw=None, accumulate=False, dw_shape=N
 # batch norm
 
 def bn_finalize(st, count, bias, gamma, beta, running_mean, running_var, momentum=0.1,
-                eps=1e-5, num_batches_tracked=None):
+                eps=1e-5, num_batches_tracked=None, out=None):
+    """``out=(scale, shift)``: caller-provided fp32 [C] outputs (e.g. rows of
+    one [2, C] buffer that a later kernel reads as a pair)."""
     blocks, Cc = st.shape[0], st.shape[1]
     dev = st.device
-    scale = torch.empty(Cc, dtype=torch.float32, device=dev)
-    shift = torch.empty_like(scale)
-    mean = torch.empty_like(scale)
+    if out is not None:
+        scale, shift = out
+        if scale.numel() != Cc or shift.numel() != Cc or not (scale.is_contiguous()
+                                                               and shift.is_contiguous()):
+            raise ValueError("bn_finalize: out must be two contiguous fp32 [C] tensors")
+    else:
+        scale = torch.empty(Cc, dtype=torch.float32, device=dev)
+        shift = torch.empty_like(scale)
+    mean = torch.empty(Cc, dtype=torch.float32, device=dev)
     inv = torch.empty_like(scale)
     ws = _ws(lib().rr_bn_finalize_workspace(Cc, blocks), dev)
     lib().check(lib().rr_bn_finalize(Cc, blocks, int(count), _p(st), _p(bias), _p(gamma), _p(beta),
