@@ -346,6 +346,39 @@ def test_bn_train_fwd_bwd(dev, dt):
     close(r["dalpha"].cpu(), alp.grad, dt, scale=alp.grad.abs().max().item())
 
 
+@pytest.mark.parametrize("rows,C", [(1, 64), (37, 64), (2071, 128), (8192, 64), (9001, 32)])
+def test_bn_finalize_partials_and_pair_out(dev, rows, C):
+    """Statistics finalize from raw per-tile partials [rows][C][2]: the direct
+    path (<= 8192 rows) and the column-reduce path, with row counts that end
+    inside and outside a batch of in-flight loads (rr_fixed_sum); against an
+    fp64 torch sum, and ``out=`` rows of a [2, C] pair equal to the default
+    outputs bit for bit."""
+    import roadrestore as rr
+    g = torch.Generator().manual_seed(rows * 7 + C)
+    st = torch.randn(rows, C, 2, generator=g)
+    st[..., 1] = st[..., 1].abs() * 4.0 + 2.0
+    count = rows * 16
+    bias, gamma, beta = (torch.randn(C, generator=g) for _ in range(3))
+    s64 = st.double().sum(0)
+    mean_acc = s64[:, 0] / count
+    var = (s64[:, 1] / count - mean_acc ** 2).clamp_min(0)
+    inv = 1.0 / torch.sqrt(var + 1e-5)
+    want_scale = (gamma.double() * inv).float()
+    want_shift = (beta.double() - (mean_acc + bias.double()) * gamma.double() * inv).float()
+    outs = []
+    for pair in (None, (torch.empty(2, C, device=dev), torch.empty(2, C, device=dev))):
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        o = (pair[0][1], pair[1][1]) if pair else None
+        sc, sh, _, _ = rr.ops.bn_finalize(st.to(dev), count, bias.to(dev), gamma.to(dev),
+                                          beta.to(dev), rm, rv, 0.1, 1e-5, out=o)
+        if pair:
+            assert sc.data_ptr() == pair[0][1].data_ptr() and sh.data_ptr() == pair[1][1].data_ptr()
+        outs.append((sc.cpu(), sh.cpu()))
+    torch.testing.assert_close(outs[0][0], want_scale, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(outs[0][1], want_shift, rtol=1e-6, atol=1e-6)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("C,h,w", [(64, 8, 10), (12, 9, 11), (128, 7, 6)])
 def test_maxpool(dev, dt, C, h, w):
