@@ -83,3 +83,16 @@ def test_cpu_tensors_rejected():
     m = rr.ResUNet()
     with pytest.raises(RuntimeError, match="GPU"):
         m(torch.zeros(1, 3, 64, 64))
+
+
+def test_bn_finalize_out_validated_before_launch():
+    """``out=`` must be two contiguous fp32 [C] tensors; checked on the host
+    before any launch (no GPU needed)."""
+    import torch
+    import roadrestore as rr
+    st = torch.zeros(4, 8, 2)
+    z = torch.zeros(8)
+    with pytest.raises(ValueError, match="out"):
+        rr.ops.bn_finalize(st, 64, None, z, z, z, z, out=(torch.empty(7), torch.empty(8)))
+    with pytest.raises(ValueError, match="out"):
+        rr.ops.bn_finalize(st, 64, None, z, z, z, z, out=(torch.empty(8, 2)[:, 0], torch.empty(8)))
