@@ -681,8 +681,11 @@ int reduce_blocks(long long P) {
 
 }  // namespace
 
+// the direct path (<= RR_BN_DIRECT_ROWS partial rows) reads the partials in
+// place and needs no workspace
+#define RR_BN_DIRECT_ROWS 8192
 extern "C" size_t rr_bn_finalize_workspace(int C, int blocks) {
-  return rr_colreduce_bytes(blocks, C * 2);
+  return blocks <= RR_BN_DIRECT_ROWS ? 0 : rr_colreduce_bytes(blocks, C * 2);
 }
 
 extern "C" int rr_bn_finalize(int C, int blocks, long long count, const float *part,
@@ -692,15 +695,15 @@ extern "C" int rr_bn_finalize(int C, int blocks, long long count, const float *p
                               float *save_invstd, int64_t *num_batches_tracked, void *ws,
                               size_t ws_bytes, rr_stream stream) {
   if (C <= 0 || blocks <= 0 || count <= 0 || !part || !scale || !shift) return RR_EINVAL;
-  if (!ws || ws_bytes < rr_colreduce_bytes(blocks, C * 2)) return RR_EWORKSPACE;
   hipStream_t st = (hipStream_t)stream;
-  if (blocks <= 8192) {
+  if (blocks <= RR_BN_DIRECT_ROWS) {
     hipLaunchKernelGGL(bn_finalize_direct_kernel, dim3(C), dim3(256), 0, st, C, blocks, (double)count,
                        part, bias, gamma, beta, running_mean, running_var, momentum, eps, scale, shift,
                        save_mean, save_invstd, num_batches_tracked);
     RR_CHECK_LAUNCH();
     return RR_OK;
   }
+  if (!ws || ws_bytes < rr_colreduce_bytes(blocks, C * 2)) return RR_EWORKSPACE;
   const int chunks = rr_colreduce(part, blocks, C * 2, (double *)ws, st);
   if (chunks < 0) return RR_ELAUNCH;
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st,

@@ -271,16 +271,30 @@ def bn_finalize(st, count, bias, gamma, beta, running_mean, running_var, momentu
     one [2, C] buffer that a later kernel reads as a pair)."""
     blocks, Cc = st.shape[0], st.shape[1]
     dev = st.device
+    if st.dtype != torch.float32 or not st.is_contiguous():
+        raise ValueError("bn_finalize: st must be a contiguous fp32 [blocks, C, 2] tensor")
     if out is not None:
         scale, shift = out
-        if scale.numel() != Cc or shift.numel() != Cc or not (scale.is_contiguous()
-                                                               and shift.is_contiguous()):
-            raise ValueError("bn_finalize: out must be two contiguous fp32 [C] tensors")
+        for o in (scale, shift):
+            if (o.numel() != Cc or not o.is_contiguous() or o.dtype != torch.float32
+                    or o.device != dev):
+                raise ValueError("bn_finalize: out must be two contiguous fp32 [C] tensors "
+                                 "on the device of st")
     else:
         scale = torch.empty(Cc, dtype=torch.float32, device=dev)
-        shift = torch.empty_like(scale)
+        shift = torch.empty(Cc, dtype=torch.float32, device=dev)
+    for name, t in (("bias", bias), ("gamma", gamma), ("beta", beta),
+                    ("running_mean", running_mean), ("running_var", running_var)):
+        if t is not None and (t.dtype != torch.float32 or t.numel() != Cc or t.device != dev
+                              or not t.is_contiguous()):
+            raise ValueError(f"bn_finalize: {name} must be a contiguous fp32 [C] tensor on the "
+                             "device of st")
+    if num_batches_tracked is not None and (num_batches_tracked.dtype != torch.int64
+                                            or num_batches_tracked.device != dev):
+        raise ValueError("bn_finalize: num_batches_tracked must be an int64 tensor on the device")
+    _need_cuda(st, scale, shift, bias, gamma, beta, running_mean, running_var, num_batches_tracked)
     mean = torch.empty(Cc, dtype=torch.float32, device=dev)
-    inv = torch.empty_like(scale)
+    inv = torch.empty(Cc, dtype=torch.float32, device=dev)
     ws = _ws(lib().rr_bn_finalize_workspace(Cc, blocks), dev)
     lib().check(lib().rr_bn_finalize(Cc, blocks, int(count), _p(st), _p(bias), _p(gamma), _p(beta),
                                      _p(running_mean), _p(running_var), float(momentum),

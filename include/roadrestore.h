@@ -157,8 +157,10 @@ int rr_bn_finalize(int C, int blocks, long long count, const float *stats_partia
                    float eps, float *scale, float *shift, float *save_mean,
                    float *save_invstd, int64_t *num_batches_tracked, void *ws,
                    size_t ws_bytes, rr_stream stream);
-/* workspace of rr_bn_finalize: the [blocks][C][2] partials are first folded to
- * <= 64 fp64 rows by a parallel fixed-order column reduction */
+/* workspace of rr_bn_finalize: 0 for blocks <= 8192 (one workgroup per channel
+ * sums the raw partials in place; ws may be NULL); above that the
+ * [blocks][C][2] partials are first folded to <= 64 fp64 rows by a parallel
+ * fixed-order column reduction in ws */
 size_t rr_bn_finalize_workspace(int C, int blocks);
 /* eval mode: scale/shift from running stats (17:64 model.eval()) */
 int rr_bn_eval_affine(int C, const float *gamma, const float *beta,

@@ -96,3 +96,15 @@ def test_bn_finalize_out_validated_before_launch():
         rr.ops.bn_finalize(st, 64, None, z, z, z, z, out=(torch.empty(7), torch.empty(8)))
     with pytest.raises(ValueError, match="out"):
         rr.ops.bn_finalize(st, 64, None, z, z, z, z, out=(torch.empty(8, 2)[:, 0], torch.empty(8)))
+    # a bf16 / fp16 out of numel C would be overrun by C fp32 writes
+    for dt in (torch.bfloat16, torch.float16):
+        with pytest.raises(ValueError, match="out"):
+            rr.ops.bn_finalize(st, 64, None, z, z, z, z, out=(torch.empty(8, dtype=dt), torch.empty(8)))
+    # gamma / running stats of the wrong dtype or size
+    with pytest.raises(ValueError, match="gamma"):
+        rr.ops.bn_finalize(st, 64, None, z.double(), z, z, z)
+    with pytest.raises(ValueError, match="running_var"):
+        rr.ops.bn_finalize(st, 64, None, z, z, z, torch.zeros(9))
+    # all-host operands: no host pointer ever reaches a launch
+    with pytest.raises(RuntimeError, match="device"):
+        rr.ops.bn_finalize(st, 64, None, z, z, z, z, out=(torch.empty(8), torch.empty(8)))

@@ -365,15 +365,24 @@ def test_bn_finalize_partials_and_pair_out(dev, rows, C):
     inv = 1.0 / torch.sqrt(var + 1e-5)
     want_scale = (gamma.double() * inv).float()
     want_shift = (beta.double() - (mean_acc + bias.double()) * gamma.double() * inv).float()
+    mean = mean_acc + bias.double()
+    want_rm = (0.1 * mean).float()                               # (1 - m) * 0 + m * mean
+    want_rv = (0.9 + 0.1 * var * count / (count - 1)).float()    # unbiased update
     outs = []
     for pair in (None, (torch.empty(2, C, device=dev), torch.empty(2, C, device=dev))):
         rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        nbt = torch.zeros((), dtype=torch.long, device=dev)
         o = (pair[0][1], pair[1][1]) if pair else None
-        sc, sh, _, _ = rr.ops.bn_finalize(st.to(dev), count, bias.to(dev), gamma.to(dev),
-                                          beta.to(dev), rm, rv, 0.1, 1e-5, out=o)
+        sc, sh, sm, si = rr.ops.bn_finalize(st.to(dev), count, bias.to(dev), gamma.to(dev),
+                                            beta.to(dev), rm, rv, 0.1, 1e-5, nbt, out=o)
         if pair:
             assert sc.data_ptr() == pair[0][1].data_ptr() and sh.data_ptr() == pair[1][1].data_ptr()
         outs.append((sc.cpu(), sh.cpu()))
+        torch.testing.assert_close(rm.cpu(), want_rm, rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(rv.cpu(), want_rv, rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(sm.cpu(), mean.float(), rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(si.cpu(), inv.float(), rtol=1e-6, atol=1e-6)
+        assert nbt.item() == 1
     torch.testing.assert_close(outs[0][0], want_scale, rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(outs[0][1], want_shift, rtol=1e-6, atol=1e-6)
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
