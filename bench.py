@@ -2,16 +2,20 @@
 
 Workload (BASELINE.json metric "images/sec ResUNet fwd+bwd (64x64 GTSRB
 batch)"; config 3 = 14_train_unified_advanced.py unified step, batch 512,
-bf16): one step = ResUNet forward on a 64x64x3 batch, loss = L1 + 0.1 *
-VGG16-features[:16] perceptual (14:238-242), full backward, AdamW(lr 2e-4,
-wd 1e-4) (14:222, 245).  Synthetic GTSRB-shaped data generated on device.
+bf16): one step = the dynamic distortion of a clean 64x64x3 uint8 batch
+(14:31-64, draws and pixels on device) + ToTensor of both images
+(14:199-202), ResUNet forward, loss = L1 + 0.1 * VGG16-features[:16]
+perceptual (14:238-242), full backward, AdamW(lr 2e-4, wd 1e-4) (14:222,
+245).  Synthetic GTSRB-shaped clean images generated on device.  --repeats
+windows of --steps timed steps each; the median window is reported (SURVEY
+§8d: 10 warm-up + 50 timed steps, median of 3).
 With --gpus N (launched by torch.distributed.run) every rank runs the same
 per-GPU batch and gradients are all-reduced over RCCL (weak scaling).
 
 Prints ONE JSON line on rank 0 with the driver's fields plus
   roofline     -- the dominant kernel's algorithmic FLOP rate vs the MFMA peak,
-                  timed with HIP events on the launch stream during the timed
-                  steps;
+                  timed with HIP events on the launch stream over eager steps
+                  run right after the timed windows;
   cpu_baseline -- the CPU restatement of the same step (oracle/, the
                   reference's ATen CPU kernels) on the host cores, bounded
                   sample.
@@ -44,8 +48,10 @@ PEAK = {"bf16": 2516.6, "f32": 157.3}          # dense MFMA TFLOP/s (MI355X_MICR
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--repeats", type=int, default=3,
+                    help="timed windows of --steps steps each; the median window is reported")
     ap.add_argument("--batch", type=int, default=512, help="per-GPU batch")
     ap.add_argument("--size", type=int, default=64)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
@@ -86,7 +92,14 @@ class KernelProbe:
         return agg
 
 
-PMC_TRAFFIC = os.path.join(REPO, "profiles", "r1h_pmc_traffic.json")
+def _latest_pmc():
+    import glob
+    c = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json")),
+               key=lambda f: (len(os.path.basename(f).split("_")[0]), os.path.basename(f)))
+    return c[-1] if c else None
+
+
+PMC_TRAFFIC = _latest_pmc()
 
 
 def _norm_sym(sym):
@@ -99,7 +112,7 @@ def pmc_traffic(sym):
     summary (FETCH_SIZE x2 + WRITE_SIZE, separate passes; tools/pmc_traffic.py)."""
     try:
         tab = json.load(open(PMC_TRAFFIC))
-    except (OSError, ValueError):
+    except (OSError, ValueError, TypeError):
         return None
     key = _norm_sym(sym)
     for k, v in tab.items():
@@ -108,14 +121,39 @@ def pmc_traffic(sym):
     return None
 
 
+def cpu_share():
+    """CPUs this process may use: the affinity mask, capped by a cgroup v2
+    CPU quota (a GPU box grants a share of the host, os.cpu_count() shows all
+    of its CPUs)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(math.ceil(int(quota) / int(period)))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(seconds, size):
     """The CPU restatement of the same unified step (oracle, fp32), timed on
-    the host: a bounded sample of the workload (batch 8)."""
+    the host with every CPU this process may use: a bounded sample of the
+    workload (batch 16)."""
     from oracle import reference_cpu as R
     from oracle import seeded as S
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_share()
     torch.set_num_threads(threads)
-    B = 8
+    B = 16
     sd = S.model_state_dict("resunet")
     p = {k: v.clone().requires_grad_(v.dtype.is_floating_point and "running" not in k)
          for k, v in sd.items()}
@@ -143,9 +181,11 @@ def cpu_baseline(seconds, size):
         if el >= seconds and n >= 2:
             break
     return {"value": round(n * B / el, 3), "unit": "images/sec", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
             "sample": f"{n} unified steps (ResUNet fwd+bwd + L1 + 0.1*perceptual + AdamW) at "
-                      f"batch {B}, {size}x{size}, fp32, oracle/reference_cpu.py on {threads} "
-                      f"host threads ({el:.1f} s)"}
+                      f"batch {B}, {size}x{size}, fp32, oracle/reference_cpu.py (the reference's "
+                      f"ATen CPU kernels) on {threads} threads = this process's CPU share "
+                      f"({el:.1f} s); the distortion (DataLoader workers in 14:213) is not in it"}
 
 
 def main():
@@ -191,15 +231,22 @@ def main():
     use_graph = a.graph == 1 or (a.graph == -1 and (dp is None or dp.rccl is not None))
     opt = rr.AdamW(model.parameters(), lr=2e-4, weight_decay=1e-4, capturable=use_graph)
 
-    # synthetic GTSRB-shaped batch: clean ~ U{0..255}/255, bad = fog + noise
+    # synthetic GTSRB-shaped clean images (uint8 RGB, NHWC as decoded); every
+    # step distorts them on device (14:31-64: draws + fog / noise / motion
+    # blur, rr_distort_random_u8) and applies ToTensor to both (14:199-202,
+    # the resample at 64x64 is the identity) -- the reference's DataLoader
+    # work, inside the timed step and inside the HIP graph
+    from roadrestore import imgproc
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     B, H = a.batch, a.size
-    clean = torch.randint(0, 256, (B, 3, H, H), generator=g, device=dev, dtype=torch.uint8).float() / 255
-    noise = torch.randn((B, 3, H, H), generator=g, device=dev) * math.sqrt(0.02)
-    bad = (clean * 0.5 + 0.45 + noise).clamp_(0, 1)
+    clean_u8 = torch.randint(0, 256, (B, H, H, 3), generator=g, device=dev, dtype=torch.uint8)
+    distort = imgproc.RandomDistortion(dev, seed=1000 + rank)
+    to_tensor = imgproc.Compose([imgproc.Resize((H, H)), imgproc.ToTensor()])
     w_perc = 0.0 if a.no_perceptual else 0.1
 
     def step():
+        bad = to_tensor(distort(clean_u8))
+        clean = to_tensor(clean_u8)
         opt.zero_grad(set_to_none=True)
         out = model(bad)
         loss = rr.unified_loss(out, clean, perc, w_perc, grad_scale=gscale)
@@ -211,11 +258,12 @@ def main():
         step()
     graph = None
     if use_graph:
-        # one whole training step (fwd, L1 + perceptual, bwd, AdamW with the
-        # device-side step count, weight re-packs) as a HIP graph; the
-        # allocator is warmed on the capture side stream first (torch recipe)
-        # (the warmup on the side stream keeps older AccumulateGrad nodes on
-        # the default stream; the mismatch is intentional and harmless here)
+        # one whole training step (data distortion + ToTensor, fwd, L1 +
+        # perceptual, bwd, AdamW with the device-side step count, weight
+        # re-packs) as a HIP graph; the allocator is warmed on the capture
+        # side stream first (torch recipe) (the warmup on the side stream
+        # keeps older AccumulateGrad nodes on the default stream; the mismatch
+        # is intentional and harmless here)
         setw = getattr(torch.autograd.graph, "set_warn_on_accumulate_grad_stream_mismatch", None)
         if setw is not None:
             setw(False)
@@ -236,7 +284,10 @@ def main():
                 loss_g = step()
             torch.cuda.synchronize()
         except Exception as e:                      # pragma: no cover - safety net
-            # a capture that fails the same way on every rank: time eagerly
+            if world > 1:
+                # never time a silently different (eager) N > 1 step
+                raise SystemExit(f"bench: HIP-graph capture of the N={world} step failed "
+                                 f"({type(e).__name__}: {e})")
             print(f"bench: HIP-graph capture failed ({type(e).__name__}: {e}); "
                   "timing eager steps", file=sys.stderr, flush=True)
             graph = None
@@ -247,19 +298,26 @@ def main():
     # the timed region: it times separate eager steps afterwards
     probe = None
     ops.PROBE = None
+    windows = []
+    for _ in range(max(1, a.repeats)):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            if graph is not None:
+                graph.replay()
+            else:
+                loss = step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        windows.append(time.perf_counter() - t0)
     if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        if graph is not None:
-            graph.replay()
-        else:
-            loss = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
+        t = torch.tensor(windows, device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        windows = t.tolist()
+    el = sorted(windows)[len(windows) // 2]          # median window (max over ranks)
     if graph is not None:
         loss = loss_g
     if not a.no_probe:
@@ -270,10 +328,6 @@ def main():
         for _ in range(a.probe_steps):
             step()
         ops.PROBE = None
-    if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = t.item()
     loss_v = float(loss.item())
     if not math.isfinite(loss_v):
         raise RuntimeError(f"non-finite loss {loss_v}")
@@ -290,7 +344,7 @@ def main():
                 "unit": "TFLOP/s", "frac": round(ach / pk, 4), "traffic": traffic,
                 "traffic_note": "HBM bytes per launch, rocprofv3 FETCH_SIZE x2 (gfx950) + "
                                 "WRITE_SIZE in separate --pmc passes of this bench "
-                                "(profiles/r1h_pmc_traffic.json)" if traffic else None,
+                                f"({os.path.relpath(PMC_TRAFFIC, REPO)})" if traffic else None,
                 "launches": cnt, "avg_launch_ms": round(ms / cnt, 4),
                 "flop_per_launch": fl / cnt}
         tot_fl = sum(v[1] for v in agg.values())
@@ -306,10 +360,11 @@ def main():
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "bf16" if dt == torch.bfloat16 else "fp32",
-        "data": "synthetic GTSRB-shaped 64x64x3 (uint8/255 clean, fog t=0.5 + N(0,0.02) noise), "
-                "random-init weights",
-        "config": {"workload": "cfg3: ResUNet unified train step (fwd + L1 + 0.1*VGG16[:16] "
-                               "perceptual + bwd + AdamW), 14_train_unified_advanced.py",
+        "data": "synthetic GTSRB-shaped 64x64x3 uint8 clean images; per step dynamic distortion "
+                "(14:31-64, draws + pixels on device) + ToTensor; random-init weights",
+        "config": {"workload": "cfg3: ResUNet unified train step (dynamic distortion + ToTensor, "
+                               "fwd + L1 + 0.1*VGG16[:16] perceptual + bwd + AdamW), "
+                               "14_train_unified_advanced.py",
                    "global_batch": world * B, "per_gpu_batch": B,
                    "image": [H, H, 3], "parallelism": f"dp{world}",
                    "hip_graph": graph is not None,
@@ -317,6 +372,8 @@ def main():
         "achieved_model_tflops": round(value * (FLOP_STEP_WITH_PERC if w_perc else
                                                 FLOP_RESUNET_FWDBWD) / 1e12, 2),
         "loss": round(loss_v, 6),
+        "repeats": len(windows),
+        "window_ms_per_step": [round(w / a.steps * 1e3, 3) for w in windows],
         "roofline": roof,
         "kernels": kernels,
         "cpu_baseline": None,

@@ -1060,6 +1060,40 @@ static int fill_args(const rr_igemm_desc *d, const void *x1, const void *x2, con
   return RR_OK;
 }
 
+// the kernel rr_igemm would launch for *d (same decisions as rr_igemm /
+// dispatch; bench.py names its roofline kernel and the tests assert the
+// benched schedule with it).  Static strings, never NULL.
+extern "C" const char *rr_igemm_kernel_name(const rr_igemm_desc *d, int bnbwd) {
+  if (!d) return "invalid";
+  if (stream3_blocks(d, bnbwd)) return d->w == 64 ? "stream3_kernel<64>" : "stream3_kernel<32>";
+  if (d->dtype == RR_BF16) {
+    const int hb = halo_bc(d);
+    const int bp = (hb && hb <= 64) ? halo_bp(d) : 256;
+    if (hb) {
+      static const char *names[3][4] = {
+          {"igemm3_halo_kernel<16,8>", "igemm3_halo_kernel<16,16>", "igemm3_halo_kernel<16,32>", "igemm3_halo_kernel<16,64>"},
+          {"igemm3_halo_kernel<64,8>", "igemm3_halo_kernel<64,16>", "igemm3_halo_kernel<64,32>", "igemm3_halo_kernel<64,64>"},
+          {"igemm3_halo_kernel<128,8>", "igemm3_halo_kernel<128,16>", "igemm3_halo_kernel<128,32>", "igemm3_halo_kernel<128,64>"}};
+      const int wi = d->w == 8 ? 0 : d->w == 16 ? 1 : d->w == 32 ? 2 : 3;
+      const int bi = hb == 16 ? 0 : hb == 64 ? 1 : 2;
+      (void)bp;
+      return names[bi][wi];
+    }
+  }
+  const Tile t = pick_tile(d);
+  const bool b = d->dtype == RR_BF16;
+  static const char *tn[2][3][4] = {
+      {{"igemm_kernel<f32,128,128,m0>", "igemm_kernel<f32,128,128,m1>", "igemm_kernel<f32,128,128,m2>", "igemm_kernel<f32,128,128,m3>"},
+       {"igemm_kernel<f32,64,256,m0>", "igemm_kernel<f32,64,256,m1>", "igemm_kernel<f32,64,256,m2>", "igemm_kernel<f32,64,256,m3>"},
+       {"igemm_kernel<f32,64,128,m0>", "igemm_kernel<f32,64,128,m1>", "igemm_kernel<f32,64,128,m2>", "igemm_kernel<f32,64,128,m3>"}},
+      {{"igemm_kernel<bf16,128,128,m0>", "igemm_kernel<bf16,128,128,m1>", "igemm_kernel<bf16,128,128,m2>", "igemm_kernel<bf16,128,128,m3>"},
+       {"igemm_kernel<bf16,64,256,m0>", "igemm_kernel<bf16,64,256,m1>", "igemm_kernel<bf16,64,256,m2>", "igemm_kernel<bf16,64,256,m3>"},
+       {"igemm_kernel<bf16,64,128,m0>", "igemm_kernel<bf16,64,128,m1>", "igemm_kernel<bf16,64,128,m2>", "igemm_kernel<bf16,64,128,m3>"}}};
+  const int ti = t.bc == 128 ? 0 : (t.bp == 256 ? 1 : 2);
+  const int mi = d->mode >= 0 && d->mode <= 3 ? d->mode : 0;
+  return tn[b][ti][mi];
+}
+
 extern "C" int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
                         const void *w, const float *bias, void *y1, void *y2,
                         const void *mask, float *stats_partial, rr_stream stream) {

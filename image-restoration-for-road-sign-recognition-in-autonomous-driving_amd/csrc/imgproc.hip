@@ -350,7 +350,13 @@ struct DistCfg {
   const float *taps;                    // [n][RR_DISTORT_KMAX^2], row-major
   const double *noise;                  // [n][h][w][c] or null -> Philox
   unsigned long long seed;
+  const int *tap_idx;                   // null, or [n]: image i's taps are taps + tap_idx[i] * KMAX^2
+  const unsigned long long *seed_dev;   // null, or the Philox seed in device memory
 };
+
+__device__ __forceinline__ unsigned long long dist_seed(const DistCfg &a) {
+  return a.seed_dev ? *a.seed_dev : a.seed;
+}
 
 __device__ __forceinline__ void philox_round(uint32_t &c0, uint32_t &c1, uint32_t &c2, uint32_t &c3,
                                              uint32_t k0, uint32_t k1) {
@@ -393,7 +399,7 @@ __device__ __forceinline__ uint8_t fog_noise(const DistCfg &a, const rr_distort_
 #pragma clang fp contract(off)
   if (p.flags & RR_DISTORT_FOG) x = x * p.fog_mul + p.fog_add;
   if (p.flags & RR_DISTORT_NOISE) {
-    const double nz = a.noise ? a.noise[e] : p.sigma * philox_normal(a.seed, (unsigned long long)e);
+    const double nz = a.noise ? a.noise[e] : p.sigma * philox_normal(dist_seed(a), (unsigned long long)e);
     return trunc_u8(((double)x + nz) * 255.0);
   }
   return trunc_u8f(x * 255.f);
@@ -437,7 +443,7 @@ __global__ void distort_blur_kernel(DistCfg a) {
     if (!(p.flags & RR_DISTORT_BLUR)) continue;
     const int rem = (int)(q - (long long)img * hw), y = rem / a.w, x = rem % a.w;
     const int k = p.ksize, anc = k / 2;
-    const float *kt = a.taps + (long long)img * RR_DISTORT_KMAX * RR_DISTORT_KMAX;
+    const float *kt = a.taps + (long long)(a.tap_idx ? a.tap_idx[img] : img) * RR_DISTORT_KMAX * RR_DISTORT_KMAX;
     const uint8_t *src = a.tmp + (long long)img * hw * a.c;
     float s[4] = {0.f, 0.f, 0.f, 0.f};
     for (int i = 0; i < k; ++i) {
@@ -460,6 +466,88 @@ __global__ void distort_blur_kernel(DistCfg a) {
   }
 }
 
+// ---------------------------------------------------- on-device draws ----
+// The per-image draws of apply_random_distortions (14:36-58) made on device,
+// so the whole data step is graph-capturable: the same distributions as the
+// reference's Python `random` calls (fog with p 0.5, intensity U(0.3, 0.7),
+// t = 1 - intensity * U(0.8, 1.2), A = 0.9; noise with p 0.5, var U(0.01,
+// 0.03); blur with p 0.5, degree randint(5, 15), angle randint(0, 360)), drawn
+// from Philox4x32-10 keyed by (seed, step) with the image index as counter
+// (the reference's stream is unseeded, so only the distributions can match).
+// The step counter lives in device memory and advances once per call; the
+// blur kernel of (degree, angle) is an index into a table of all 11 x 361
+// kernels built once on the host by rr_motion_blur_kernel.
+constexpr int DRAW_DEG0 = 5, DRAW_NDEG = 11, DRAW_NANG = 361;
+
+__device__ __forceinline__ void philox4(uint32_t c[4], unsigned long long key) {
+  uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    philox_round(c[0], c[1], c[2], c[3], k0, k1);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+__device__ __forceinline__ double u01(uint32_t hi, uint32_t lo) {       // [0, 1), 53 bits
+  return ((((unsigned long long)hi << 21) ^ lo) & ((1ull << 53) - 1)) * 0x1p-53;
+}
+
+__global__ __launch_bounds__(256) void distort_draw_kernel(int n, unsigned long long seed,
+                                                           long long *step, rr_distort_param *prm,
+                                                           int *tap_idx, unsigned long long *noise_seed) {
+#pragma clang fp contract(off)
+  const long long s = *step;
+  const unsigned long long key = seed ^ (0x9E3779B97F4A7C15ull * (unsigned long long)(s + 1));
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    uint32_t a[4] = {(uint32_t)i, 0u, 0x5EED0001u, 0u}, b[4] = {(uint32_t)i, 1u, 0x5EED0001u, 0u};
+    philox4(a, key);
+    philox4(b, key);
+    const double r_fog = u01(a[0], a[1]), r_int = u01(a[2], a[3]);
+    const double r_t = u01(b[0], b[1]), r_noise = u01(b[2], b[3]);
+    uint32_t c[4] = {(uint32_t)i, 2u, 0x5EED0001u, 0u}, d[4] = {(uint32_t)i, 3u, 0x5EED0001u, 0u};
+    philox4(c, key);
+    philox4(d, key);
+    const double r_var = u01(c[0], c[1]), r_blur = u01(c[2], c[3]);
+    const double r_deg = u01(d[0], d[1]), r_ang = u01(d[2], d[3]);
+    rr_distort_param p;
+    p.sigma = 0.0;
+    p.fog_mul = 1.0f;
+    p.fog_add = 0.0f;
+    p.flags = 0;
+    p.ksize = 0;
+    int ti = 0;
+    if (r_fog < 0.5) {
+      const double intensity = 0.3 + (0.7 - 0.3) * r_int;
+      const double t = 1.0 - intensity * (0.8 + (1.2 - 0.8) * r_t);
+      p.flags |= RR_DISTORT_FOG;
+      p.fog_mul = (float)t;
+      p.fog_add = (float)(0.9 * (1.0 - t));
+    }
+    if (r_noise < 0.5) {
+      const double var = 0.01 + (0.03 - 0.01) * r_var;
+      p.flags |= RR_DISTORT_NOISE;
+      p.sigma = sqrt(var);
+    }
+    if (r_blur < 0.5) {
+      const int deg = DRAW_DEG0 + (int)(r_deg * DRAW_NDEG);
+      const int ang = (int)(r_ang * DRAW_NANG);
+      p.flags |= RR_DISTORT_BLUR;
+      p.ksize = deg;
+      ti = (deg - DRAW_DEG0) * DRAW_NANG + ang;
+    }
+    prm[i] = p;
+    tap_idx[i] = ti;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t e[4] = {0xFFFFFFFFu, 0u, 0x5EED0002u, 0u};
+    philox4(e, key);
+    *noise_seed = ((unsigned long long)e[0] << 32) | e[1];
+    *step = s + 1;
+  }
+}
+
 extern "C" size_t rr_distort_workspace(int n, int h, int w, int c) {
   return n > 0 && h > 0 && w > 0 && c > 0 ? (size_t)n * h * w * c : 0;
 }
@@ -470,7 +558,7 @@ extern "C" int rr_distort_u8(int n, int h, int w, int c, int mode, const uint8_t
   if (!in || !out || !params || !taps || !ws || n <= 0 || h <= 0 || w <= 0) return RR_EINVAL;
   if (c < 1 || c > 4 || (mode != 0 && mode != 1)) return RR_EINVAL;
   if (ws_bytes < rr_distort_workspace(n, h, w, c)) return RR_EWORKSPACE;
-  DistCfg a{n, h, w, c, mode, in, out, (uint8_t *)ws, params, taps, noise, seed};
+  DistCfg a{n, h, w, c, mode, in, out, (uint8_t *)ws, params, taps, noise, seed, nullptr, nullptr};
   hipStream_t st = (hipStream_t)stream;
   const long long te = (long long)n * h * w * c, tp = (long long)n * h * w;
   hipLaunchKernelGGL(distort_pre_kernel, dim3(rr_grid_cap((te + 255) / 256, 8192)), dim3(256), 0, st, a);
@@ -523,5 +611,64 @@ extern "C" int rr_motion_blur_kernel(int k, int angle, float *taps) {
   for (int y = 0; y < RR_DISTORT_KMAX; ++y)
     for (int x = 0; x < RR_DISTORT_KMAX; ++x)
       if (y >= k || x >= k) taps[y * RR_DISTORT_KMAX + x] = 0.f;
+  return RR_OK;
+}
+
+// all 11 x 361 motion-blur kernels of the draws above ([deg - 5][angle][KMAX^2])
+extern "C" size_t rr_motion_blur_table_floats(void) {
+  return (size_t)DRAW_NDEG * DRAW_NANG * RR_DISTORT_KMAX * RR_DISTORT_KMAX;
+}
+
+extern "C" int rr_motion_blur_table(float *table) {
+  if (!table) return RR_EINVAL;
+  for (int d = 0; d < DRAW_NDEG; ++d)
+    for (int a = 0; a < DRAW_NANG; ++a) {
+      const int rc = rr_motion_blur_kernel(DRAW_DEG0 + d, a,
+                                           table + ((size_t)d * DRAW_NANG + a) * RR_DISTORT_KMAX * RR_DISTORT_KMAX);
+      if (rc) return rc;
+    }
+  return RR_OK;
+}
+
+// workspace of rr_distort_random_u8: the blur staging image, the n draws, the
+// n tap indices and the step's noise seed
+static size_t draw_off_prm(int n, int h, int w, int c) {
+  return ((size_t)n * h * w * c + 15) / 16 * 16;
+}
+extern "C" size_t rr_distort_random_workspace(int n, int h, int w, int c) {
+  if (n <= 0 || h <= 0 || w <= 0 || c <= 0) return 0;
+  return draw_off_prm(n, h, w, c) + (size_t)n * sizeof(rr_distort_param) + ((size_t)n * 4 + 15) / 16 * 16 + 16;
+}
+
+extern "C" int rr_distort_random_u8(int n, int h, int w, int c, const uint8_t *in, uint8_t *out,
+                                    unsigned long long seed, long long *step, const float *table,
+                                    void *ws, size_t ws_bytes, rr_stream stream) {
+  if (!in || !out || !step || !table || !ws || n <= 0 || h <= 0 || w <= 0) return RR_EINVAL;
+  if (c < 1 || c > 4) return RR_EINVAL;
+  if (ws_bytes < rr_distort_random_workspace(n, h, w, c)) return RR_EWORKSPACE;
+  char *base = (char *)ws;
+  rr_distort_param *prm = (rr_distort_param *)(base + draw_off_prm(n, h, w, c));
+  int *tap_idx = (int *)((char *)prm + (size_t)n * sizeof(rr_distort_param));
+  unsigned long long *nseed = (unsigned long long *)((char *)tap_idx + ((size_t)n * 4 + 15) / 16 * 16);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(distort_draw_kernel, dim3(1), dim3(256), 0, st, n, seed, step, prm, tap_idx, nseed);
+  RR_CHECK_LAUNCH();
+  DistCfg a{n, h, w, c, 0, in, out, (uint8_t *)ws, prm, table, nullptr, 0ull, tap_idx, nseed};
+  const long long te = (long long)n * h * w * c, tp = (long long)n * h * w;
+  hipLaunchKernelGGL(distort_pre_kernel, dim3(rr_grid_cap((te + 255) / 256, 8192)), dim3(256), 0, st, a);
+  RR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(distort_blur_kernel, dim3(rr_grid_cap((tp + 255) / 256, 8192)), dim3(256), 0, st, a);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+// the draws of the last rr_distort_random_u8 call, read back from its
+// workspace (tests): params [n], tap indices [n], noise seed
+extern "C" int rr_distort_random_draws(int n, int h, int w, int c, const void *ws,
+                                       size_t *prm_off, size_t *idx_off, size_t *seed_off) {
+  if (!ws || n <= 0 || !prm_off || !idx_off || !seed_off) return RR_EINVAL;
+  *prm_off = draw_off_prm(n, h, w, c);
+  *idx_off = *prm_off + (size_t)n * sizeof(rr_distort_param);
+  *seed_off = *idx_off + ((size_t)n * 4 + 15) / 16 * 16;
   return RR_OK;
 }

@@ -626,6 +626,33 @@ extern "C" size_t rr_wgrad_workspace(const rr_wgrad_desc *d) {
   return (size_t)p.nsplit * p.CA * p.taps * p.CB * sizeof(float);
 }
 
+// the weight-grad kernel rr_wgrad would launch for *d (same decisions;
+// static strings, never NULL)
+extern "C" const char *rr_wgrad_kernel_name(const rr_wgrad_desc *d) {
+  if (!d) return "invalid";
+  if (swgrad_ok(d)) return d->w == 64 ? "swgrad_kernel<64>" : "swgrad_kernel<32>";
+  if (halo_ok(d)) {
+    switch (d->w) {
+      case 64: return "wgrad3_halo_kernel<64>";
+      case 32: return "wgrad3_halo_kernel<32>";
+      case 16: return "wgrad3_halo_kernel<16>";
+      default: return "wgrad3_halo_kernel<8>";
+    }
+  }
+  const Plan pl = plan_of(d);
+  static const char *tn[2][2][2][4] = {
+      {{{"wgrad_kernel<f32,64,64,m0>", "wgrad_kernel<f32,64,64,m1>", "wgrad_kernel<f32,64,64,m2>", "wgrad_kernel<f32,64,64,m3>"},
+        {"wgrad_kernel<f32,64,128,m0>", "wgrad_kernel<f32,64,128,m1>", "wgrad_kernel<f32,64,128,m2>", "wgrad_kernel<f32,64,128,m3>"}},
+       {{"wgrad_kernel<f32,128,64,m0>", "wgrad_kernel<f32,128,64,m1>", "wgrad_kernel<f32,128,64,m2>", "wgrad_kernel<f32,128,64,m3>"},
+        {"wgrad_kernel<f32,128,128,m0>", "wgrad_kernel<f32,128,128,m1>", "wgrad_kernel<f32,128,128,m2>", "wgrad_kernel<f32,128,128,m3>"}}},
+      {{{"wgrad_kernel<bf16,64,64,m0>", "wgrad_kernel<bf16,64,64,m1>", "wgrad_kernel<bf16,64,64,m2>", "wgrad_kernel<bf16,64,64,m3>"},
+        {"wgrad_kernel<bf16,64,128,m0>", "wgrad_kernel<bf16,64,128,m1>", "wgrad_kernel<bf16,64,128,m2>", "wgrad_kernel<bf16,64,128,m3>"}},
+       {{"wgrad_kernel<bf16,128,64,m0>", "wgrad_kernel<bf16,128,64,m1>", "wgrad_kernel<bf16,128,64,m2>", "wgrad_kernel<bf16,128,64,m3>"},
+        {"wgrad_kernel<bf16,128,128,m0>", "wgrad_kernel<bf16,128,128,m1>", "wgrad_kernel<bf16,128,128,m2>", "wgrad_kernel<bf16,128,128,m3>"}}}};
+  const int mi = d->mode >= 0 && d->mode <= 3 ? d->mode : 0;
+  return tn[d->dtype == RR_BF16][pl.BA == 128][pl.BB == 128][mi];
+}
+
 extern "C" int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
                         const void *x2, float *dw, void *ws, size_t ws_bytes,
                         rr_stream stream) {

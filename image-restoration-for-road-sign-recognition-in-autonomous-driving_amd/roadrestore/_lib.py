@@ -61,6 +61,8 @@ S_ = C.c_size_t
 _SIGS = {
     "rr_igemm": (I_, [C.POINTER(IgemmDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_]),
     "rr_igemm_stat_blocks": (I_, [C.POINTER(IgemmDesc)]),
+    "rr_igemm_kernel_name": (C.c_char_p, [C.POINTER(IgemmDesc), I_]),
+    "rr_wgrad_kernel_name": (C.c_char_p, [C.POINTER(WgradDesc)]),
     "rr_igemm_bnbwd_workspace": (S_, [C.POINTER(IgemmDesc)]),
     "rr_igemm_bnbwd": (I_, [C.POINTER(IgemmDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_, P_, P_]),
     "rr_wgrad_workspace": (S_, [C.POINTER(WgradDesc)]),
@@ -121,6 +123,12 @@ _SIGS = {
     "rr_distort_workspace": (S_, [I_, I_, I_, I_]),
     "rr_distort_u8": (I_, [I_, I_, I_, I_, I_, P_, P_, P_, P_, P_, C.c_ulonglong, P_, S_, P_]),
     "rr_motion_blur_kernel": (I_, [I_, I_, P_]),
+    "rr_motion_blur_table_floats": (S_, []),
+    "rr_motion_blur_table": (I_, [P_]),
+    "rr_distort_random_workspace": (S_, [I_, I_, I_, I_]),
+    "rr_distort_random_u8": (I_, [I_, I_, I_, I_, P_, P_, C.c_ulonglong, P_, P_, P_, S_, P_]),
+    "rr_distort_random_draws": (I_, [I_, I_, I_, I_, P_, C.POINTER(S_), C.POINTER(S_),
+                                     C.POINTER(S_)]),
     "rr_scalar_accumulate": (I_, [P_, P_, P_, P_]),
     "rr_zero": (I_, [P_, S_, P_]),
     "rr_version": (C.c_char_p, []),

@@ -27,6 +27,7 @@ from ._lib import (RR_DISTORT_BLUR, RR_DISTORT_FOG, RR_DISTORT_KMAX, RR_DISTORT_
                    DistortParam)
 
 __all__ = ["Resize", "ToTensor", "Normalize", "Compose", "apply_random_distortions",
+           "RandomDistortion", "motion_blur_table",
            "apply_compound_distortion", "distortion_params", "psnr", "ssim",
            "IMAGENET_MEAN", "IMAGENET_STD"]
 
@@ -138,6 +139,76 @@ def apply_random_distortions(x, rng=None, seed=None, noise=None):
     if seed is None:
         seed = (rng or _random).getrandbits(64)
     return ops.distort_u8(x, params, taps, mode=0, noise=noise, seed=seed)
+
+
+_TABLES = {}
+
+
+def motion_blur_table(device):
+    """Device copy of every motion-blur kernel the draws can pick (degree
+    5..15 x angle 0..360, [11, 361, KMAX, KMAX] fp32), built once on the host
+    by the same restatement of cv2 getRotationMatrix2D + warpAffine."""
+    key = str(device)
+    t = _TABLES.get(key)
+    if t is None:
+        import ctypes as C
+        L = ops.lib()
+        nf = L.rr_motion_blur_table_floats()
+        host = torch.empty(nf, dtype=torch.float32)
+        L.check(L.rr_motion_blur_table(C.c_void_p(host.data_ptr())), "rr_motion_blur_table")
+        t = _TABLES[key] = host.view(11, 361, RR_DISTORT_KMAX, RR_DISTORT_KMAX).to(device)
+    return t
+
+
+class RandomDistortion:
+    """apply_random_distortions (14:31-64) for a whole [n, h, w, c] uint8
+    device batch with the per-image draws made ON DEVICE
+    (rr_distort_random_u8): graph-capturable, so a captured training step
+    re-draws on every replay.  The draws follow the reference's distributions
+    (Philox4x32-10 keyed by (seed, step); the reference's stream is unseeded);
+    the step counter lives in device memory and advances once per call.
+
+    ``last_draws()`` reads the most recent draws back (tests)."""
+
+    def __init__(self, device, seed=0):
+        self.device = torch.device(device)
+        self.seed = int(seed) & (2 ** 64 - 1)
+        self.step = torch.zeros((), dtype=torch.int64, device=self.device)
+        self.table = motion_blur_table(self.device)
+        self._ws = None
+        self._shape = None
+
+    def __call__(self, x, out=None):
+        _check_u8(x)
+        ops._need_cuda(x)
+        n, h, w, c = x.shape
+        x = x.contiguous()
+        L = ops.lib()
+        if self._ws is None or self._shape != (n, h, w, c):
+            self._ws = ops._ws(L.rr_distort_random_workspace(n, h, w, c), self.device)
+            self._shape = (n, h, w, c)
+        if out is None:
+            out = torch.empty_like(x)
+        L.check(L.rr_distort_random_u8(n, h, w, c, x.data_ptr(), out.data_ptr(), self.seed,
+                                       self.step.data_ptr(), self.table.data_ptr(),
+                                       self._ws.data_ptr(), self._ws.numel(), ops.stream()),
+                "rr_distort_random_u8")
+        return out
+
+    def last_draws(self):
+        """-> (params: list of DistortParam, table index [n] int32, noise seed)"""
+        import ctypes as C
+        n, h, w, c = self._shape
+        po, io, so = C.c_size_t(), C.c_size_t(), C.c_size_t()
+        L = ops.lib()
+        L.check(L.rr_distort_random_draws(n, h, w, c, self._ws.data_ptr(), C.byref(po), C.byref(io),
+                                          C.byref(so)), "rr_distort_random_draws")
+        raw = self._ws.cpu()
+        sz = C.sizeof(DistortParam)
+        arr = (DistortParam * n).from_buffer_copy(bytes(raw[po.value:po.value + n * sz].numpy()))
+        idx = raw[io.value:io.value + 4 * n].view(torch.int32).clone()
+        seed = int(raw[so.value:so.value + 8].view(torch.int64).item()) & (2 ** 64 - 1)
+        return list(arr), idx, seed
 
 
 def apply_compound_distortion(x, seed=0, noise=None):

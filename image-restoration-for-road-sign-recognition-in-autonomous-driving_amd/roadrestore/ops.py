@@ -9,7 +9,6 @@ CPU fallback: a missing library or device raises.
 from __future__ import annotations
 
 import ctypes as C
-import os
 
 import torch
 
@@ -51,59 +50,30 @@ def _need_cuda(*ts):
 
 # Optional launch probe (bench.py): probe(kernel_symbol, algorithmic_flops, launch_fn, shape_tag)
 PROBE = None
+# Optional launch log (tests): a list that every igemm / wgrad launch appends
+# (kernel_symbol, shape_tag) to -- the symbol is the library's own choice
+# (rr_igemm_kernel_name / rr_wgrad_kernel_name), so a test can assert the
+# schedule it exercises.
+LAUNCH_LOG = None
 
 
-def _kpick_tile(mode, n, h, w, cout, split):
-    """Mirror of csrc/igemm.hip pick_tile (names the template instance)."""
-    P = n * h * w
-    if cout % 128 == 0 and (split == 0 or split % 128 == 0) and ((P + 127) // 128) * (cout // 128) >= 512:
-        return 128, 128, 2
-    if cout <= 64 and (P + 255) // 256 >= 512:
-        return 64, 256, 1
-    return 64, 128, 2
+def igemm_kernel_name(d, bnbwd=False):
+    """The kernel rr_igemm / rr_igemm_bnbwd launches for descriptor ``d``."""
+    return lib().rr_igemm_kernel_name(C.byref(d), int(bnbwd)).decode()
 
 
-def _khalo_bc(mode, dt, n, h, w, c1, c2, cout, split, out_nchw):
-    """Mirror of csrc/igemm.hip halo_bc: BC of the LDS-halo kernel, or 0."""
-    if os.environ.get("RR_IGEMM_NOHALO", "0") not in ("", "0"):
-        return 0
-    if dt != torch.bfloat16 or mode != RR_CONV3X3 or w not in (8, 16, 32, 64):
-        return 0
-    if out_nchw and (cout > 16 or c2):
-        return 0
-    R = 256 // w
-    if h % 8 or (h % R if R <= h else (R % h or n % (R // h))):
-        return 0
-    if c1 % 64 or c2 % 64:
-        return 0
-    if out_nchw:
-        return 16
-    max64 = int(os.environ.get("RR_HALO_BC64_MAXCIN", "128") or 0)
-    if cout % 128 == 0 and (split == 0 or split % 128 == 0) and c1 + c2 > max64:
-        return 128
-    return 64 if cout % 64 == 0 else 0
+def wgrad_kernel_name(d):
+    """The kernel rr_wgrad launches for descriptor ``d``."""
+    return lib().rr_wgrad_kernel_name(C.byref(d)).decode()
 
 
-def _kstream3(mode, dt, n, h, w, c1, c2, cout, split, out_nchw):
-    """Mirror of csrc/stream3.hip stream3_blocks (probe naming only)."""
-    if os.environ.get("RR_STREAM3", "1") in ("0",):
-        return False
-    if dt != torch.bfloat16 or mode != RR_CONV3X3 or w not in (32, 64):
-        return False
-    if c1 != 64 or c2 or cout != 64 or split or out_nchw:
-        return False
-    return h % (256 // w) == 0 and n * h * w >= 65536
-
-
-def _kswgrad(mode, dt, n, h, w, c1, c2, cout):
-    """Mirror of csrc/swgrad.hip swgrad_ok (probe naming only)."""
-    if os.environ.get("RR_SWGRAD", "1") in ("0",):
-        return False
-    if dt != torch.bfloat16 or mode != RR_CONV3X3 or cout % 64 or cout > 128 or w not in (32, 64):
-        return False
-    if c1 <= 0 or c1 % 64 or c2 % 64 or c1 + c2 > 192 or h % (128 // w):
-        return False
-    return n * h * w >= 128 * 256
+def _launch(sym_fn, flops, launch, tag):
+    if LAUNCH_LOG is not None:
+        LAUNCH_LOG.append((sym_fn(), tag))
+    if PROBE is None:
+        launch()
+    else:
+        PROBE(sym_fn(), flops, launch, tag)
 
 
 def _ws(nbytes, device):
@@ -214,20 +184,9 @@ def igemm(mode, x1, x2, n, h, w, wpack, cout, bias=None, act=0, out=None, out2=N
     def launch():
         lib().check(lib().rr_igemm(C.byref(d), _p(x1), _p(x2), _p(wpack), _p(bias), _p(out),
                                    _p(out2), _p(mask), _p(st), stream()), "rr_igemm")
-    if PROBE is None:
-        launch()
-    else:
-        taps = 9 if mode == RR_CONV3X3 else (4 if mode == RR_CONVT_DOWN else 1)
-        hb = _khalo_bc(mode, dt, n, h, w, c1, c2, cout, split, out_nchw)
-        if _kstream3(mode, dt, n, h, w, c1, c2, cout, split, out_nchw):
-            sym = f"stream3_kernel<{w}>"
-        elif hb:
-            sym = f"igemm3_halo_kernel<{hb},{w}>"
-        else:
-            bc, bp, wc = _kpick_tile(mode, n, h, w, cout, split)
-            sym = f"igemm_kernel<{'bf16' if dt == torch.bfloat16 else 'f32'},{bc},{bp},{wc},mode{mode}>"
-        PROBE(sym, 2.0 * n * h * w * cout * taps * (c1 + c2), launch,
-              f"fwd m{mode} {n}x{h}x{w} c{c1}+{c2}->{cout}")
+    taps = 9 if mode == RR_CONV3X3 else (4 if mode == RR_CONVT_DOWN else 1)
+    _launch(lambda: igemm_kernel_name(d), 2.0 * n * h * w * cout * taps * (c1 + c2), launch,
+            f"fwd m{mode} {n}x{h}x{w} c{c1}+{c2}->{cout}")
     return out, out2, st
 
 
@@ -245,20 +204,12 @@ def wgrad(mode, dy, x1, x2, n, h, w, cout, dw=None, accumulate=False, dw_shape=N
     def launch():
         lib().check(lib().rr_wgrad(C.byref(d), _p(dy), _p(x1), _p(x2), _p(dw), _p(ws),
                                    ws.numel(), stream()), "rr_wgrad")
-    if PROBE is None:
-        launch()
-    else:
-        taps = 9 if mode == RR_CONV3X3 else (4 if mode == RR_CONVT_UP else 1)
-        convT = mode == RR_CONVT_UP
-        CA = c1 if convT else cout
-        CB = cout if convT else c1 + c2
-        ba = 128 if CA % 128 == 0 else 64
-        bb = 128 if (CB % 128 == 0 and (cout if convT else c1) % 128 == 0 and c2 % 128 == 0) else 64
-        sym = f"wgrad_kernel<{'bf16' if dy.dtype == torch.bfloat16 else 'f32'},{ba},{bb},mode{mode}>"
-        if _kswgrad(mode, dy.dtype, n, h, w, c1, c2, cout):
-            sym = f"swgrad_kernel<{w}>"
-        PROBE(sym, 2.0 * CA * CB * taps * n * h * w, launch,
-              f"wgrad m{mode} {n}x{h}x{w} c{c1}+{c2}->{cout}")
+    taps = 9 if mode == RR_CONV3X3 else (4 if mode == RR_CONVT_UP else 1)
+    convT = mode == RR_CONVT_UP
+    CA = c1 if convT else cout
+    CB = cout if convT else c1 + c2
+    _launch(lambda: wgrad_kernel_name(d), 2.0 * CA * CB * taps * n * h * w, launch,
+            f"wgrad m{mode} {n}x{h}x{w} c{c1}+{c2}->{cout}")
     return dw
 
 
@@ -423,20 +374,9 @@ def igemm_bnbwd(mode, dy, n, h, w, wpack, cout, t, mean, inv, aff_s, aff_b, alph
         lib().check(lib().rr_igemm_bnbwd(C.byref(d), _p(dy), _p(wpack), _p(t), _p(mean), _p(inv),
                                          _p(aff_s), _p(aff_b), _p(alpha), _p(out), _p(part),
                                          stream()), "rr_igemm_bnbwd")
-    if PROBE is None:
-        launch()
-    else:
-        taps = 9 if mode == RR_CONV3X3 else 1
-        hb = _khalo_bc(mode, dt, n, h, w, dy.shape[-1], 0, cout, 0, False)
-        if _kstream3(mode, dt, n, h, w, dy.shape[-1], 0, cout, 0, False):
-            sym = f"stream3_kernel<{w}>"
-        elif hb:
-            sym = f"igemm3_halo_kernel<{hb},{w}>"
-        else:
-            bc, bp, wc = _kpick_tile(mode, n, h, w, cout, 0)
-            sym = f"igemm_kernel<{'bf16' if dt == torch.bfloat16 else 'f32'},{bc},{bp},{wc},mode{mode}>"
-        PROBE(sym, 2.0 * n * h * w * cout * taps * dy.shape[-1], launch,
-              f"bnbwd m{mode} {n}x{h}x{w} c{dy.shape[-1]}->{cout}")
+    taps = 9 if mode == RR_CONV3X3 else 1
+    _launch(lambda: igemm_kernel_name(d, bnbwd=True), 2.0 * n * h * w * cout * taps * dy.shape[-1],
+            launch, f"bnbwd m{mode} {n}x{h}x{w} c{dy.shape[-1]}->{cout}")
     return out, part, rows, rows * (cout // 64)
 
 

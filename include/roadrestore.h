@@ -83,6 +83,12 @@ int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
              const void *mask, float *stats_partial, rr_stream stream);
 /* number of row blocks the partial stats buffer holds: [blocks][c_out][2] */
 int rr_igemm_stat_blocks(const rr_igemm_desc *d);
+/* The kernel rr_igemm (bnbwd = 0) or rr_igemm_bnbwd (bnbwd = 1) launches for
+ * *d, e.g. "stream3_kernel<64>", "igemm3_halo_kernel<64,32>",
+ * "igemm_kernel<bf16,128,128,m1>" (m = mode).  Static string, never NULL; no
+ * launch, no device needed.  Used to name the roofline kernel and to assert
+ * which schedule a test exercises. */
+const char *rr_igemm_kernel_name(const rr_igemm_desc *d, int bnbwd);
 
 /* conv dgrad fused with the backward reduce of the BatchNorm2d -> PReLU pair
  * that produced its input (ResidualBlock conv_block[1:3], 14:101-103):
@@ -117,6 +123,9 @@ typedef struct {
 } rr_wgrad_desc;
 
 size_t rr_wgrad_workspace(const rr_wgrad_desc *d);
+/* The weight-grad kernel rr_wgrad launches for *d ("swgrad_kernel<64>",
+ * "wgrad3_halo_kernel<16>", "wgrad_kernel<bf16,128,64,m1>", ...); static string. */
+const char *rr_wgrad_kernel_name(const rr_wgrad_desc *d);
 int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
              const void *x2, float *dw, void *ws, size_t ws_bytes,
              rr_stream stream);
@@ -413,6 +422,28 @@ int rr_distort_u8(int n, int h, int w, int c, int mode, const uint8_t *in,
  * getRotationMatrix2D + warpAffine of np.diag(np.ones(k)), / k, as fp32)
  * into taps[KMAX][KMAX] (row-major, zero outside k x k) */
 int rr_motion_blur_kernel(int k, int angle, float *taps);
+
+/* The whole apply_random_distortions (14:31-64) of a batch on device, graph-
+ * capturable: the per-image draws (the reference's distributions: fog / noise
+ * / blur each with p 0.5, intensity U(0.3, 0.7) x U(0.8, 1.2), var U(0.01,
+ * 0.03), degree randint(5, 15), angle randint(0, 360)) come from
+ * Philox4x32-10 keyed by (seed, *step), image index as counter; *step (device
+ * int64) advances by one per call; the noise field uses a per-step Philox
+ * seed.  `table` is the device copy of rr_motion_blur_table (all 11 x 361
+ * blur kernels).  Then the same fog -> noise -> blur arithmetic as
+ * rr_distort_u8 mode 0.  Replaces the host-side draws of the reference's
+ * DataLoader workers (14:72-84, 213). */
+size_t rr_motion_blur_table_floats(void);
+int rr_motion_blur_table(float *table_host);
+size_t rr_distort_random_workspace(int n, int h, int w, int c);
+int rr_distort_random_u8(int n, int h, int w, int c, const uint8_t *in, uint8_t *out,
+                         unsigned long long seed, long long *step_dev,
+                         const float *table_dev, void *workspace, size_t workspace_bytes,
+                         rr_stream stream);
+/* byte offsets, inside that workspace, of the last call's draws (tests):
+ * rr_distort_param[n], int32 table index[n], uint64 noise seed */
+int rr_distort_random_draws(int n, int h, int w, int c, const void *workspace,
+                            size_t *params_off, size_t *index_off, size_t *seed_off);
 
 /* running loss on device: acc[0] += x[0] (fp64), count[0] += 1 -- the
  * reference's per-step `running_loss += loss.item()` (14:246) without a host

@@ -108,3 +108,23 @@ def test_bn_finalize_out_validated_before_launch():
     # all-host operands: no host pointer ever reaches a launch
     with pytest.raises(RuntimeError, match="device"):
         rr.ops.bn_finalize(st, 64, None, z, z, z, z, out=(torch.empty(8), torch.empty(8)))
+
+
+def test_kernel_selection_for_the_benched_layers():
+    """The library reports which kernel owns each cfg3 layer (B = 512, bf16,
+    64x64 input) -- host-only queries, no launch: the row-streaming conv and
+    weight grad on the 64-channel 64x64 / 32x32 layers, the LDS-halo kernels
+    on the rest."""
+    from roadrestore import ops
+    from roadrestore._lib import RR_BF16, RR_CONV3X3, IgemmDesc, WgradDesc
+    want = {  # (h, c_in1, c_in2, c_out): (fwd, wgrad)
+        (64, 64, 0, 64): ("stream3_kernel<64>", "swgrad_kernel<64>"),
+        (64, 64, 64, 64): ("igemm3_halo_kernel<64,64>", "swgrad_kernel<64>"),
+        (32, 64, 0, 128): ("igemm3_halo_kernel<64,32>", "swgrad_kernel<32>"),
+        (16, 256, 0, 256): ("igemm3_halo_kernel<128,16>", "wgrad3_halo_kernel<16>"),
+        (8, 512, 0, 512): ("igemm3_halo_kernel<128,8>", "wgrad3_halo_kernel<8>"),
+    }
+    for (h, c1, c2, co), (f, wg) in want.items():
+        d = IgemmDesc(RR_BF16, RR_CONV3X3, 512, h, h, c1, c2, co, 0, 0, 0, 1, 0, 1, 0)
+        assert ops.igemm_kernel_name(d) == f, (h, c1, c2, co, ops.igemm_kernel_name(d))
+        assert ops.wgrad_kernel_name(WgradDesc(RR_BF16, RR_CONV3X3, 512, h, h, c1, c2, co, 0)) == wg

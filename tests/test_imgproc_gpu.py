@@ -166,3 +166,63 @@ def test_random_distortions_entry_point(dev):
     y = imgproc.apply_random_distortions(x, rng=random.Random(0))
     assert y.shape == x.shape and y.dtype == torch.uint8
     assert not torch.equal(x, y)
+
+
+def test_random_distortion_draws_on_device(dev):
+    """rr_distort_random_u8 (14:31-64 with the draws made on device): the
+    draws follow the reference's distributions, the blur taps are the table
+    entry of the drawn (degree, angle), the pixels equal rr_distort_u8 given
+    the same draws byte for byte, and the step counter advances per call."""
+    from roadrestore import imgproc, ops
+    from roadrestore._lib import RR_DISTORT_BLUR, RR_DISTORT_FOG, RR_DISTORT_NOISE
+    n = 512
+    x = torch.from_numpy(_batch(n, 64, 64, seed=5)).to(dev)
+    rd = imgproc.RandomDistortion(dev, seed=1234)
+    y1 = rd(x)
+    p1, idx1, s1 = rd.last_draws()
+    y2 = rd(x)
+    p2, idx2, s2 = rd.last_draws()
+    assert rd.step.item() == 2 and s1 != s2 and not torch.equal(y1, y2)
+    table = imgproc.motion_blur_table(dev).view(-1, 15, 15)
+    for params, idx, seed, y in ((p1, idx1, s1, y1), (p2, idx2, s2, y2)):
+        fog = np.array([bool(p.flags & RR_DISTORT_FOG) for p in params])
+        noi = np.array([bool(p.flags & RR_DISTORT_NOISE) for p in params])
+        blu = np.array([bool(p.flags & RR_DISTORT_BLUR) for p in params])
+        for f in (fog, noi, blu):                       # p = 0.5 each: 3.5 sigma band
+            assert abs(f.mean() - 0.5) < 3.5 * 0.5 / np.sqrt(n), f.mean()
+        t = np.array([p.fog_mul for p in params])[fog]
+        assert t.min() >= 1 - 0.7 * 1.2 - 1e-6 and t.max() <= 1 - 0.3 * 0.8 + 1e-6
+        fa = np.array([p.fog_add for p in params])[fog]
+        assert np.allclose(fa, 0.9 * (1 - t), atol=1e-6)
+        sg = np.array([p.sigma for p in params])[noi]
+        assert sg.min() >= 0.1 - 1e-12 and sg.max() <= 0.03 ** 0.5 + 1e-12
+        k = np.array([p.ksize for p in params])[blu]
+        assert k.min() >= 5 and k.max() <= 15 and len(set(k.tolist())) >= 9
+        ang = idx.numpy()[blu] - (k - 5) * 361
+        assert ang.min() >= 0 and ang.max() <= 360
+        taps = table[idx.to(dev).long()]
+        want = ops.distort_u8(x, params, taps, mode=0, seed=seed)
+        assert torch.equal(y, want)
+
+
+def test_random_distortion_in_hip_graph(dev):
+    """Captured once, every replay re-draws (the counter is device state)."""
+    from roadrestore import imgproc
+    x = torch.from_numpy(_batch(64, 32, 32, seed=6)).to(dev)
+    rd = imgproc.RandomDistortion(dev, seed=7)
+    out = torch.empty_like(x)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        rd(x, out=out)                                  # warm-up: workspace allocated
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        rd(x, out=out)
+    seen = []
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        seen.append(out.clone())
+    assert rd.step.item() == 4
+    assert not torch.equal(seen[0], seen[1]) and not torch.equal(seen[1], seen[2])

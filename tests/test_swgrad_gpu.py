@@ -40,9 +40,10 @@ def run(dev, n, h, w, c1, c2, cout, seed, dw=None, accumulate=False):
 @pytest.mark.parametrize("shape", SHAPES)
 def test_swgrad_selected(shape):
     from roadrestore import ops
-    from roadrestore._lib import RR_CONV3X3
+    from roadrestore._lib import RR_BF16, RR_CONV3X3, WgradDesc
     n, h, w, c1, c2, cout = shape
-    assert ops._kswgrad(RR_CONV3X3, torch.bfloat16, n, h, w, c1, c2, cout)
+    d = WgradDesc(RR_BF16, RR_CONV3X3, n, h, w, c1, c2, cout, 0)
+    assert ops.wgrad_kernel_name(d) == f"swgrad_kernel<{w}>"     # the library's own choice
 
 
 @pytest.mark.parametrize("shape", SHAPES)
