@@ -12,14 +12,23 @@ Two batches:
     grads -- asserted from the library's own kernel choice
     (rr_igemm_kernel_name / rr_wgrad_kernel_name via ops.LAUNCH_LOG).
 
-Bounds ("bf16 path"): bf16 keeps 8 significant bits, so every
-conv input / output rounds at 2^-9 relative; through 40 conv layers with BN
-the errors add up to ~1 % relative.  Per quantity (relative L2 vs fp64):
-  restored output                    <= OUT_TOL
-  loss                               <= LOSS_TOL (relative)
-  parameter grads, median over tensors <= GRAD_MED_TOL, every tensor <= GRAD_MAX_TOL
-  10-step loss curve vs the fp32 oracle: every step within CURVE_TOL relative,
-  and the loss change over the 10 steps within CURVE_DELTA_TOL of the oracle's.
+Bounds ("bf16 path").  bf16 keeps 8 significant bits; how much
+error that alone causes in this network is measured, not guessed: the
+bf16-storage emulation oracle (oracle/bf16_emulation.py) evaluates the
+reference step in fp64 with every tensor the HIP path stores rounded to bf16
+at the same point (activations, weights, and the gradient of each stored
+activation).  Its distance to the fp64 oracle is the error of an ideal bf16
+implementation (restored output ~2.4e-2 rel-L2; parameter grads median
+~0.08-0.35 rel-L2 -- the bottleneck BN / PReLU-alpha gradients cancel
+heavily).  The HIP bf16 step must be as accurate as that ideal, per quantity
+against fp64:
+  restored output rel-L2          <= 1.25 x ideal + 1e-3
+  loss relative error             <= 2 x ideal + 1e-4
+  grad rel-L2, median over tensors <= 1.25 x ideal + 1e-3
+  grad rel-L2, 90th percentile     <= 1.5 x ideal + 1e-3
+  grad cosine, median              >= ideal - 0.01
+and the 10-step loss curve tracks the fp32 oracle within CURVE_TOL per step,
+its total change within CURVE_DELTA_TOL of the oracle's.
 """
 import numpy as np
 import pytest
@@ -27,15 +36,11 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-OUT_TOL = 2e-2
-LOSS_TOL = 1e-2
-GRAD_MED_TOL = 4e-2
-GRAD_MAX_TOL = 0.25
 CURVE_TOL = 1e-2
 CURVE_DELTA_TOL = 0.25
 
-# the benched kernels a B >= 16, 64x64 step must route through
-BENCHED = {"stream3_kernel<64>", "swgrad_kernel<64>", "swgrad_kernel<32>",
+# the benched kernels a B >= 64, 64x64 step must route through
+BENCHED = {"stream3_kernel<64>", "stream3_kernel<32>", "swgrad_kernel<64>", "swgrad_kernel<32>",
            "igemm3_halo_kernel<64,32>", "igemm3_halo_kernel<64,16>", "igemm3_halo_kernel<128,16>",
            "igemm3_halo_kernel<128,8>", "igemm3_halo_kernel<64,64>", "wgrad3_halo_kernel<16>",
            "wgrad3_halo_kernel<8>"}
@@ -47,17 +52,20 @@ def _gold(name):
     return np.load(os.path.join(S.GOLDEN_DIR, name + ".npz"))
 
 
-def _oracle(bad, clean, sd, perc_sd, dtype):
-    """One unified step on the CPU oracle in ``dtype`` -> (out, loss, grads)."""
+def _oracle(bad, clean, sd, perc_sd, dtype, emulate_bf16=False):
+    """One unified step on the CPU oracle in ``dtype`` -> (out, loss, grads);
+    ``emulate_bf16``: the bf16-storage emulation (oracle/bf16_emulation.py)."""
     from oracle import reference_cpu as R
+    from oracle import bf16_emulation as E
     p = {k: (v.detach().clone().to(dtype) if v.dtype.is_floating_point else v.clone())
          for k, v in sd.items()}
     for k, v in p.items():
         if v.dtype.is_floating_point and "running" not in k:
             v.requires_grad_(True)
     pp = {k: v.detach().clone().to(dtype) for k, v in perc_sd.items()}
-    out = R.resunet_forward(p, bad.to(dtype), True)
-    loss = R.unified_loss(out, clean.to(dtype), pp)
+    M = E if emulate_bf16 else R
+    out = M.resunet_forward(p, bad.to(dtype), True)
+    loss = M.unified_loss(out, clean.to(dtype), pp)
     loss.backward()
     grads = {k: v.grad.detach().double() for k, v in p.items() if v.requires_grad}
     return out.detach().double(), loss.item(), grads
@@ -88,25 +96,38 @@ def _bf16_step(dev, bad, clean, sd, perc_sd, log=None):
     return m, out.detach().cpu(), loss.item()
 
 
-def _check(m, out, loss, o64, l64, g64, o32, l32, g32, tag):
-    e_out, e_out32 = _rel(out, o64), _rel(o32, o64)
-    e_loss = abs(loss - l64) / abs(l64)
-    errs = []
-    for k, p in m.named_parameters():
-        t = g64[k]
-        if t.norm().item() < 1e-9:         # exactly-zero grads (conv bias before train-mode BN)
-            assert p.grad.double().cpu().norm().item() <= 1e-6 + g32[k].norm().item(), k
+def _grad_errs(grads, g64, check_zero=True):
+    """per-tensor (rel-L2, cosine, name) against fp64; the exactly-zero grads
+    (conv bias before a train-mode BN: the BN subtracts the batch mean) are
+    skipped -- and, for the HIP path (written as exact zeros), checked"""
+    rows = []
+    for k, t in g64.items():
+        g = grads[k].double()
+        if t.norm().item() < 1e-9:
+            if check_zero:
+                assert g.norm().item() <= 1e-6, k
             continue
-        errs.append((_rel(p.grad.cpu(), t), _rel(g32[k], t), k))
-    rel = np.array([e for e, _, _ in errs])
-    print(f"[{tag}] out rel-L2 {e_out:.3e} (fp32 ref {e_out32:.1e})  loss {loss:.6f} vs "
-          f"{l64:.6f} (rel {e_loss:.2e}; fp32 {l32:.6f})  grads rel-L2 median "
-          f"{np.median(rel):.3e} max {rel.max():.3e} over {len(rel)} tensors; worst "
-          f"{sorted(errs, reverse=True)[:4]}")
-    assert e_out <= OUT_TOL, e_out
-    assert e_loss <= LOSS_TOL, e_loss
-    assert np.median(rel) <= GRAD_MED_TOL, np.median(rel)
-    assert rel.max() <= GRAD_MAX_TOL, sorted(errs, reverse=True)[:4]
+        rows.append((_rel(g, t), (g * t).sum().item() / max((g.norm() * t.norm()).item(), 1e-300), k))
+    return rows
+
+
+def _check(m, out, loss, o64, l64, g64, oe, le, ge, tag):
+    ours = _grad_errs({k: p.grad.cpu() for k, p in m.named_parameters()}, g64)
+    ideal = _grad_errs(ge, g64, check_zero=False)   # rounded dt: not exactly 0
+    r_o, r_i = np.array([r[0] for r in ours]), np.array([r[0] for r in ideal])
+    c_o, c_i = np.array([r[1] for r in ours]), np.array([r[1] for r in ideal])
+    e_out, e_out_i = _rel(out, o64), _rel(oe, o64)
+    e_loss, e_loss_i = abs(loss - l64) / abs(l64), abs(le - l64) / abs(l64)
+    print(f"[{tag}] vs fp64, HIP bf16 / ideal bf16: out rel-L2 {e_out:.3e} / {e_out_i:.3e}; "
+          f"loss rel {e_loss:.2e} / {e_loss_i:.2e}; grad rel-L2 median {np.median(r_o):.3e} / "
+          f"{np.median(r_i):.3e}, p90 {np.percentile(r_o, 90):.3e} / {np.percentile(r_i, 90):.3e}; "
+          f"cos median {np.median(c_o):.5f} / {np.median(c_i):.5f} ({len(r_o)} tensors)")
+    print("  worst (HIP):", [(round(e, 3), k) for e, _, k in sorted(ours, reverse=True)[:5]])
+    assert e_out <= 1.25 * e_out_i + 1e-3, (e_out, e_out_i)
+    assert e_loss <= 2.0 * e_loss_i + 1e-4, (e_loss, e_loss_i)
+    assert np.median(r_o) <= 1.25 * np.median(r_i) + 1e-3, (np.median(r_o), np.median(r_i))
+    assert np.percentile(r_o, 90) <= 1.5 * np.percentile(r_i, 90) + 1e-3
+    assert np.median(c_o) >= np.median(c_i) - 0.01, (np.median(c_o), np.median(c_i))
 
 
 def _inputs(B, H, step):
@@ -124,26 +145,27 @@ def test_bf16_unified_step_golden(dev):
     bad, clean = torch.from_numpy(z["bad"]), torch.from_numpy(z["clean"])
     m, out, loss = _bf16_step(dev, bad, clean, sd, perc_sd)
     o64, l64, g64 = _oracle(bad, clean, sd, perc_sd, torch.float64)
-    o32, l32, g32 = _oracle(bad, clean, sd, perc_sd, torch.float32)
+    oe, le, ge = _oracle(bad, clean, sd, perc_sd, torch.float64, emulate_bf16=True)
+    _, l32, _ = _oracle(bad, clean, sd, perc_sd, torch.float32)
     assert abs(l32 - z["loss"][0]) <= 1e-6 * abs(l32)          # oracle pinned to the reference
-    _check(m, out, loss, o64, l64, g64, o32, l32, g32, "B=2 golden")
+    _check(m, out, loss, o64, l64, g64, oe, le, ge, "B=2 golden")
 
 
 def test_bf16_unified_step_benched_schedule(dev):
-    """B=16 at 64x64: the kernels bench.py times own their layers (asserted
-    from the library's own choice), and the step still matches fp64."""
+    """B=64 at 64x64: the kernels bench.py times own their layers (asserted
+    from the library's own choice), and the step is as accurate as ideal bf16."""
     from oracle import seeded as S
     sd = S.model_state_dict("resunet")
     perc_sd = S.seeded_state_dict(S.load_manifest("perceptual"), seed=5)
-    bad, clean = _inputs(16, 64, 0)
+    bad, clean = _inputs(64, 64, 0)
     log = []
     m, out, loss = _bf16_step(dev, bad, clean, sd, perc_sd, log)
     used = {k for k, _ in log}
     print("kernels:", sorted(used))
     assert BENCHED <= used, sorted(BENCHED - used)
     o64, l64, g64 = _oracle(bad, clean, sd, perc_sd, torch.float64)
-    o32, l32, g32 = _oracle(bad, clean, sd, perc_sd, torch.float32)
-    _check(m, out, loss, o64, l64, g64, o32, l32, g32, "B=16 benched")
+    oe, le, ge = _oracle(bad, clean, sd, perc_sd, torch.float64, emulate_bf16=True)
+    _check(m, out, loss, o64, l64, g64, oe, le, ge, "B=64 benched")
 
 
 def test_bf16_loss_curve_10_steps(dev):

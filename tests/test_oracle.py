@@ -107,3 +107,30 @@ def test_cosine_schedule():
         sch.step()
     for e, lr in enumerate(sch_lr):
         assert abs(lr - R.cosine_lr(2e-4, e, 25)) < 1e-12
+
+
+def test_bf16_emulation_is_the_reference_step_without_rounding(monkeypatch):
+    """oracle/bf16_emulation.py is the reference restatement with bf16
+    rounding points inserted: with the rounding switched off it reproduces
+    reference_cpu's unified step exactly (same ops, same order)."""
+    import torch
+    from oracle import bf16_emulation as E, reference_cpu as R, seeded as S
+    monkeypatch.setattr(E, "_rb", lambda x: x)
+    sd = S.model_state_dict("resunet")
+    perc = S.seeded_state_dict(S.load_manifest("perceptual"), seed=5)
+    clean = S.image_batch(1, 32, 32, seed=3)
+    bad = S.fog_noise(clean, seed=4)
+    outs = []
+    for M in (R, E):
+        p = {k: v.clone().requires_grad_(v.dtype.is_floating_point and "running" not in k)
+             for k, v in sd.items()}
+        out = M.resunet_forward(p, bad, True)
+        loss = M.unified_loss(out, clean, perc)
+        loss.backward()
+        outs.append((out.detach(), loss.item(), p["res2.conv_block.0.weight"].grad))
+    assert torch.equal(outs[0][0], outs[1][0]) and outs[0][1] == outs[1][1]
+    assert torch.equal(outs[0][2], outs[1][2])
+    # and with rounding on, it really rounds (differs from fp32)
+    monkeypatch.undo()
+    p = {k: v.clone() for k, v in sd.items()}
+    assert not torch.equal(E.resunet_forward(p, bad, True), outs[0][0])
