@@ -11,8 +11,11 @@ from roadrestore._lib import RR_CONV3X3
 
 dev = torch.device("cuda:0")
 B = int(os.environ.get("B", 512))
-LAYERS = [("res1.c", 64, 64, 0, 64), ("dec1.c1", 64, 64, 64, 64), ("res2.c2", 32, 128, 0, 128),
-          ("res3.c2", 16, 256, 0, 256), ("bott.512", 8, 512, 0, 512)]
+LAYERS = [("dec1.c1", 64, 64, 64, 64), ("res2.c1", 32, 64, 0, 128), ("res2.c2", 32, 128, 0, 128),
+          ("dec2.c1", 32, 128, 64, 64), ("res3.c1", 16, 128, 0, 256), ("res3.c2", 16, 256, 0, 256),
+          ("dec3.c1", 16, 128, 256, 128), ("bott.256", 8, 256, 0, 512), ("bott.512", 8, 512, 0, 512)]
+if os.environ.get("LAYERS"):
+    LAYERS = [l for l in LAYERS if l[0] in os.environ["LAYERS"].split(",")]
 
 
 def timeit(fn, reps=10):

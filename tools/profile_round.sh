@@ -7,7 +7,7 @@ TAG=${1:-r1}
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/prof_$TAG
 rm -rf $OUT && mkdir -p $OUT
-ARGS="--steps 5 --warmup 3 --graph 0 --no-cpu-baseline --no-probe"
+ARGS="--steps 5 --warmup 3 --repeats 1 --graph 0 --no-cpu-baseline --no-probe"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt -- python bench.py $ARGS > $OUT/kt.log 2>&1
 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/fetch -o f -- python bench.py $ARGS > $OUT/fetch.log 2>&1
 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/write -o w -- python bench.py $ARGS > $OUT/write.log 2>&1
