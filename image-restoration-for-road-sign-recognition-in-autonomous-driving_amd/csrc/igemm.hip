@@ -1103,7 +1103,7 @@ extern "C" int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
   hipStream_t st = (hipStream_t)stream;
   if (stream3_blocks(d, 0)) {
     S3Args s{};
-    s.x = a.x1; s.wt = a.wt; s.bias = a.bias; s.y = a.y1;
+    s.x = a.x1; s.x2 = a.x2; s.wt = a.wt; s.bias = a.bias; s.y = a.y1;
     s.mask = d->has_mask ? a.mask : nullptr;
     s.stats = a.stats;
     s.n = d->n; s.h = d->h; s.act = d->act; s.accumulate = d->accumulate;

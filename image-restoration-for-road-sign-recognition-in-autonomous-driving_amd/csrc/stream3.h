@@ -7,7 +7,9 @@
 
 struct S3Args {
   const char *x;             // NHWC bf16 input [n][h][w][64]
-  const char *wt;            // packed bf16 weights [64][9][64] (fwd or dgrad pack)
+  const char *x2;            // second 64-channel source of a concat input (two passes) or null
+  const char *wt;            // packed bf16 weights [64][9][wld] (fwd or dgrad pack)
+  int wld, woff;             // packed row length (c_in) and the pass's channel offset
   const float *bias;         // [64] or null
   char *y;                   // NHWC bf16 output [n][h][w][64]
   const char *mask;          // relu-backward mask (NHWC bf16) or null

@@ -186,7 +186,7 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
         wr[mi][tap][kb] =
-            *reinterpret_cast<const bf16x8 *>(a.wt + ((co * 9 + tap) * 64 + kb * 32 + fq * 8) * 2);
+            *reinterpret_cast<const bf16x8 *>(a.wt + ((co * 9 + tap) * a.wld + a.woff + kb * 32 + fq * 8) * 2);
   }
   float al = 0.f;
   if constexpr (BNBWD) {
@@ -371,12 +371,14 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
           }
           g = gm;
         } else {
+          // ACC: the destination holds the first pass of a two-source (concat)
+          // conv, so the statistics and the bias apply to the sum
+          if constexpr (ACC) g += unpack4(ev0[mi][ni]);
           if constexpr (STATS) {
             r0[mi] += g;
             r1[mi] += g * g;
           }
           if constexpr ((F & F_BIAS) != 0) g += bia;
-          if constexpr (ACC) g += unpack4(ev0[mi][ni]);
           if constexpr ((F & F_RELU) != 0) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) g[j] = fmaxf(g[j], 0.f);
@@ -577,6 +579,20 @@ int s3_flags(const rr_igemm_desc *d, bool bnbwd) {
   }
 }
 
+// second pass of a 64 + 64-channel concat input: accumulate onto the first
+// pass, then the caller's epilogue (bias, statistics, ReLU)
+int s3_concat_flags(const rr_igemm_desc *d) {
+  if (d->accumulate || d->has_mask) return -1;
+  const int f = (d->has_bias ? F_BIAS : 0) | (d->want_stats ? F_STATS : 0) |
+                (d->act == RR_ACT_RELU ? F_RELU : 0);
+  switch (f) {
+    case 0: case F_BIAS: case F_STATS: case F_BIAS | F_STATS: case F_RELU: case F_BIAS | F_RELU:
+      return F_ACC | f;
+    default:
+      return -1;
+  }
+}
+
 template <int W, int MP, int F>
 void launch1(const S3Args &a, int P, hipStream_t st) {
   // the late-epilogue stagger measured faster only for 256-pixel steps
@@ -598,6 +614,11 @@ int launch_w(const S3Args &a, int f, int P, hipStream_t st) {
     case F_ACC: launch1<W, 2, F_ACC>(a, P, st); break;
     case F_MASK: launch1<W, 2, F_MASK>(a, P, st); break;
     case F_ACC | F_MASK: launch1<W, 2, F_ACC | F_MASK>(a, P, st); break;
+    case F_ACC | F_BIAS: launch1<W, 2, F_ACC | F_BIAS>(a, P, st); break;
+    case F_ACC | F_STATS: launch1<W, 2, F_ACC | F_STATS>(a, P, st); break;
+    case F_ACC | F_BIAS | F_STATS: launch1<W, 2, F_ACC | F_BIAS | F_STATS>(a, P, st); break;
+    case F_ACC | F_RELU: launch1<W, 2, F_ACC | F_RELU>(a, P, st); break;
+    case F_ACC | F_BIAS | F_RELU: launch1<W, 2, F_ACC | F_BIAS | F_RELU>(a, P, st); break;
     case F_BNBWD: launch1<W, 2, F_BNBWD>(a, P, st); break;
     default: return RR_EUNSUPPORTED;
   }
@@ -611,9 +632,16 @@ int stream3_blocks(const rr_igemm_desc *d, int bnbwd) {
   const char *e = getenv("RR_STREAM3");
   if (e && !atoi(e)) return 0;
   if (d->dtype != RR_BF16 || d->mode != RR_CONV3X3) return 0;
-  if (d->c_in1 != 64 || d->c_in2 != 0 || d->c_out != 64 || d->out_split || d->out_nchw) return 0;
+  if (d->c_in1 != 64 || d->c_out != 64 || d->out_split || d->out_nchw) return 0;
   if (d->w != 64 && d->w != 32) return 0;
-  if (s3_flags(d, bnbwd != 0) < 0) return 0;
+  if (d->c_in2 == 64) {
+    // concat input (dec1: 64 + 64 -> 64): two passes, the second accumulating
+    // (RR_STREAM3_CONCAT=0: the tiled halo kernel)
+    const char *ec = getenv("RR_STREAM3_CONCAT");
+    if ((ec && !atoi(ec)) || bnbwd || s3_concat_flags(d) < 0) return 0;
+  } else if (d->c_in2 != 0 || s3_flags(d, bnbwd != 0) < 0) {
+    return 0;
+  }
   // eligibility independent of the step size: whole 256-pixel steps (the
   // larger one) and at least one per workgroup
   if (d->h % (256 / d->w)) return 0;
@@ -624,8 +652,21 @@ int stream3_blocks(const rr_igemm_desc *d, int bnbwd) {
 
 int stream3_launch(const rr_igemm_desc *d, const S3Args &a, int bnbwd, hipStream_t st) {
   if (!stream3_blocks(d, bnbwd)) return RR_EUNSUPPORTED;
-  const int f = s3_flags(d, bnbwd != 0);
   const int P = d->n * d->h * d->w;
-  if (d->w == 64) return launch_w<64>(a, f, P, st);
-  return launch_w<32>(a, f, P, st);
+  auto go = [&](const S3Args &x, int f) { return d->w == 64 ? launch_w<64>(x, f, P, st) : launch_w<32>(x, f, P, st); };
+  if (d->c_in2 == 64) {
+    // conv(cat(x1, x2)) = conv(x1, W[:, :64]) + conv(x2, W[:, 64:]): pass 1
+    // writes the x1 half (bf16), pass 2 adds the x2 half and applies the
+    // epilogue to the sum (statistics of the pre-bias sum, as one pass)
+    S3Args p1 = a;
+    p1.x2 = nullptr; p1.bias = nullptr; p1.stats = nullptr; p1.mask = nullptr;
+    p1.wld = 128; p1.woff = 0; p1.accumulate = 0;
+    if (const int rc = go(p1, 0)) return rc;
+    S3Args p2 = a;
+    p2.x = a.x2; p2.x2 = nullptr; p2.wld = 128; p2.woff = 64; p2.accumulate = 1;
+    return go(p2, s3_concat_flags(d));
+  }
+  S3Args p = a;
+  p.wld = 64; p.woff = 0;
+  return go(p, s3_flags(d, bnbwd != 0));
 }

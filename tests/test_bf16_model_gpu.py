@@ -42,7 +42,7 @@ CURVE_DELTA_TOL = 0.25
 # the benched kernels a B >= 64, 64x64 step must route through
 BENCHED = {"stream3_kernel<64>", "stream3_kernel<32>", "swgrad_kernel<64>", "swgrad_kernel<32>",
            "igemm3_halo_kernel<64,32>", "igemm3_halo_kernel<64,16>", "igemm3_halo_kernel<128,16>",
-           "igemm3_halo_kernel<128,8>", "igemm3_halo_kernel<64,64>", "wgrad3_halo_kernel<16>",
+           "igemm3_halo_kernel<128,8>", "wgrad3_halo_kernel<16>",
            "wgrad3_halo_kernel<8>"}
 
 

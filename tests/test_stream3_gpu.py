@@ -152,3 +152,43 @@ def test_stream3_bnbwd(dev, shape, monkeypatch):
         assert rel(got[k], ref[k]) < 2e-2, k
         assert rel(got[k], tiled[k]) < 1e-4, k
     assert rel(got["dt0"], tiled["dt0"]) < 2e-3
+
+
+@pytest.mark.parametrize("shape", [(16, 64, 64), (17, 64, 64), (81, 32, 32)])
+@pytest.mark.parametrize("stats,bias,act", [(True, True, 0), (False, True, 1), (False, False, 0)])
+def test_stream3_concat_two_pass(dev, shape, stats, bias, act, monkeypatch):
+    """64 + 64-channel concat input (ResUNet dec1 conv1, 14:144,174-177):
+    two streaming passes, the second accumulating onto the first's bf16 half
+    and applying bias / statistics / ReLU to the sum.  vs fp32 torch on the
+    concatenation and vs the tiled halo kernel (RR_STREAM3_CONCAT=0); the
+    statistics are of the pre-bias sum, as in one pass (the extra bf16
+    rounding of the first half is within the bf16 tolerance)."""
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    n, h, w = shape
+    x1 = rnd(n, 64, h, w, seed=61).bfloat16().float()
+    x2 = rnd(n, 64, h, w, seed=62).bfloat16().float()
+    wt = (rnd(64, 128, 3, 3, seed=63) / 34.0).bfloat16().float()
+    b = rnd(64, seed=64) if bias else None
+    pre = F.conv2d(torch.cat((x1, x2), 1), wt, None, padding=1)
+    ref = pre + (b[None, :, None, None] if bias else 0)
+    if act:
+        ref = F.relu(ref)
+    wf, _ = rr.ops.pack_conv(wt.to(dev), BF)
+    outs = {}
+    for tag in ("1", "0"):
+        monkeypatch.setenv("RR_STREAM3_CONCAT", tag)
+        d = rr.ops.IgemmDesc(rr.ops.RR_BF16, RR_CONV3X3, n, h, w, 64, 64, 64, 0, act, 0,
+                             int(bias), 0, int(stats), 0)
+        name = rr.ops.igemm_kernel_name(d)
+        assert name == ("stream3_kernel<%d>" % w if tag == "1" else "igemm3_halo_kernel<64,%d>" % w)
+        y, _, st = rr.ops.igemm(RR_CONV3X3, nhwc(x1, dev), nhwc(x2, dev), n, h, w, wf, 64,
+                                bias=b.to(dev) if bias else None, act=act, stats=stats)
+        torch.cuda.synchronize()
+        outs[tag] = (nchw(y), st.double().sum(0).cpu() if stats else None)
+    y, s = outs["1"]
+    assert rel(y, ref) < 6e-3
+    assert rel(y, outs["0"][0]) < 4e-3
+    if stats:
+        assert rel(s[:, 0], pre.double().sum((0, 2, 3))) < 4e-3
+        assert rel(s[:, 1], (pre.double() ** 2).sum((0, 2, 3))) < 4e-3
