@@ -43,6 +43,11 @@ METRIC = "images/sec ResUNet fwd+bwd (64x64 GTSRB batch) at 1/2/4/8 MI355X; PSNR
 FLOP_RESUNET_FWDBWD = 13_698_072_576
 FLOP_STEP_WITH_PERC = 18_270_388_224
 PEAK = {"bf16": 2516.6, "f32": 157.3}          # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0                           # HBM3E (MI355X_MICROARCH.md)
+# back-to-back v_mfma_f32_16x16x32_bf16 on random operands, every CU, 2 waves
+# per SIMD: the clock the chip holds under MFMA load caps what any kernel can
+# reach (tools/mfma_ceiling.hip, profiles/r2a_mfma_ceiling.jsonl)
+MFMA_CEILING = 1995.9
 
 
 def parse():
@@ -66,8 +71,28 @@ def parse():
     return ap.parse_args()
 
 
+def algorithmic_bytes(tag):
+    """Minimal HBM bytes of one conv GEMM launch from its shape tag
+    ("fwd m<mode> NxHxW c<c1>+<c2>-><cout>" / "wgrad m<mode> ..."): every
+    activation operand read once and the output written once, bf16 (weights
+    and epilogue side operands -- accumulate / mask / BN inputs -- not
+    counted, so the achieved rate is a lower bound)."""
+    import re
+    m = re.match(r"(\w+) m(\d) (\d+)x(\d+)x(\d+) c(\d+)\+(\d+)->(\d+)", tag or "")
+    if not m:
+        return None
+    kind, mode, n, h, w, c1, c2, co = m.group(1), *map(int, m.groups()[1:])
+    P = n * h * w
+    if kind == "wgrad":
+        return 2 * P * (c1 + c2 + (co if mode != 2 else 4 * co))
+    if mode == 3:                       # convT down: input on the (2h, 2w) grid
+        return 2 * (4 * P * (c1 + c2) + P * co)
+    return 2 * P * (c1 + c2 + co)       # conv3x3 / 1x1; convT up: 4 taps x co/4
+
+
 class KernelProbe:
-    """HIP-event timing of every igemm / wgrad launch, per kernel symbol."""
+    """HIP-event timing of every igemm / wgrad launch, per kernel symbol:
+    launches, algorithmic FLOP, algorithmic bytes, ms."""
 
     def __init__(self):
         self.rec = []
@@ -83,12 +108,13 @@ class KernelProbe:
     def summary(self):
         torch.cuda.synchronize()
         agg = {}
-        for sym, fl, s, e, _ in self.rec:
+        for sym, fl, s, e, tag in self.rec:
             ms = s.elapsed_time(e)
-            a = agg.setdefault(sym, [0, 0.0, 0.0])
+            a = agg.setdefault(sym, [0, 0.0, 0.0, 0.0])
             a[0] += 1
             a[1] += fl
             a[2] += ms
+            a[3] += algorithmic_bytes(tag) or 0.0
         return agg
 
 
@@ -336,17 +362,27 @@ def main():
     kernels = None
     if probe is not None:
         agg = probe.summary()
-        sym, (cnt, fl, ms) = max(agg.items(), key=lambda kv: kv[1][2])
-        ach = fl / (ms * 1e-3) / 1e12
+        sym, (cnt, fl, ms, by) = max(agg.items(), key=lambda kv: kv[1][2])
+        tflops = fl / (ms * 1e-3) / 1e12
+        gbs = by / (ms * 1e-3) / 1e9
         pk = PEAK["bf16" if dt == torch.bfloat16 else "f32"]
+        # the bound by the kernel's algorithmic intensity vs the ridge point
+        hbm_bound = by > 0 and fl / by < pk * 1e12 / (HBM_PEAK_GBS * 1e9)
         traffic = pmc_traffic(sym)
-        roof = {"bound": "mfma", "kernel": sym, "achieved": round(ach, 2), "peak": pk,
-                "unit": "TFLOP/s", "frac": round(ach / pk, 4), "traffic": traffic,
+        roof = {"bound": "hbm" if hbm_bound else "mfma", "kernel": sym,
+                "achieved": round(gbs if hbm_bound else tflops, 2),
+                "peak": HBM_PEAK_GBS if hbm_bound else pk,
+                "unit": "GB/s" if hbm_bound else "TFLOP/s",
+                "frac": round(gbs / HBM_PEAK_GBS if hbm_bound else tflops / pk, 4),
+                "traffic": traffic,
                 "traffic_note": "HBM bytes per launch, rocprofv3 FETCH_SIZE x2 (gfx950) + "
                                 "WRITE_SIZE in separate --pmc passes of this bench "
                                 f"({os.path.relpath(PMC_TRAFFIC, REPO)})" if traffic else None,
                 "launches": cnt, "avg_launch_ms": round(ms / cnt, 4),
-                "flop_per_launch": fl / cnt}
+                "flop_per_launch": fl / cnt, "algorithmic_bytes_per_launch": by / cnt,
+                "mfma_tflops": round(tflops, 2), "mfma_frac": round(tflops / pk, 4),
+                "hbm_gbs": round(gbs, 1),
+                "mfma_practical_ceiling_tflops": MFMA_CEILING}
         tot_fl = sum(v[1] for v in agg.values())
         tot_ms = sum(v[2] for v in agg.values())
         kernels = {"conv_gemm_ms_per_step": round(tot_ms / a.probe_steps, 3),

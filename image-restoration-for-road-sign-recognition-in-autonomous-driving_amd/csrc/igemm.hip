@@ -32,6 +32,7 @@
 // (the grads of a torch.cat's two halves), convT 2x2 pixel scatter.
 #include "common.h"
 #include "stream3.h"
+#include "stream1.h"
 
 #include <cstdlib>
 #include <type_traits>
@@ -632,7 +633,10 @@ template <int BC, int BP, int NT = 2 * BP> struct HaloCfg {
   static constexpr int OCC = NT == BP ? 2 : BP == 128 ? (BC <= 64 ? 3 : 2) : (BC <= 64 ? 4 : 2);   // min waves / SIMD
 };
 
-template <int BC, int W, int MODE, int BP, int NT = 2 * BP>
+// DBGK (timing diagnostics only, RR_HALO_DBGK; results are wrong): bit0 no
+// barriers in the K loop, bit1 no fragment reads in the K loop (the first
+// stage's fragments reused) -- bounds on what the barriers / LDS reads cost
+template <int BC, int W, int MODE, int BP, int NT = 2 * BP, int DBGK = 0>
 __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_kernel(IgemmArgs a) {
   using T = bf16_t;
   using G = HaloGeom<W, BP, NT>;
@@ -778,6 +782,8 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
 #pragma unroll
     for (int ni = 0; ni < MP; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // DBGK bit1: fragments read once (diagnostics)
+  bf16x8 dfa[(DBGK & 2) ? 2 : 1][MC], dfb[(DBGK & 2) ? 2 : 1][MP];
   // prologue: halo(0), weights(0) into LDS; weights(1) in flight
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -807,12 +813,19 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 fa[MC], fb[MP];
+      if constexpr ((DBGK & 2) != 0) {
 #pragma unroll
-      for (int mi = 0; mi < MC; ++mi)
-        fa[mi] = *reinterpret_cast<const bf16x8 *>(sA + abase[mi] + kk * 4 * WPLANE);
+        for (int mi = 0; mi < MC; ++mi) fa[mi] = dfa[kk][mi];
 #pragma unroll
-      for (int ni = 0; ni < MP; ++ni)
-        fb[ni] = *reinterpret_cast<const bf16x8 *>(sB + bbase[ni] + kk * 4 * G::PLANE);
+        for (int ni = 0; ni < MP; ++ni) fb[ni] = dfb[kk][ni];
+      } else {
+#pragma unroll
+        for (int mi = 0; mi < MC; ++mi)
+          fa[mi] = *reinterpret_cast<const bf16x8 *>(sA + abase[mi] + kk * 4 * WPLANE);
+#pragma unroll
+        for (int ni = 0; ni < MP; ++ni)
+          fb[ni] = *reinterpret_cast<const bf16x8 *>(sB + bbase[ni] + kk * 4 * G::PLANE);
+      }
 #pragma unroll
       for (int mi = 0; mi < MC; ++mi)
 #pragma unroll
@@ -823,14 +836,14 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
     if constexpr (TAP == 8) {
       if (ch + 1 < kch) {
         if constexpr (HB == 1) {
-          __syncthreads();                   // every wave is done reading this chunk's halo
+          if constexpr ((DBGK & 1) == 0) __syncthreads();   // every wave is done reading this chunk's halo
           store_halo(0);
         } else {
           store_halo((ch + 1) & 1);
         }
       }
     }
-    __syncthreads();
+    if constexpr ((DBGK & 1) == 0) __syncthreads();
   };
   auto chunk_even = [&](int ch) __attribute__((always_inline)) {          // 9 ch even: s & 1 == TAP & 1
     stage(ch, std::integral_constant<int, 0>{}, I0{});
@@ -854,6 +867,15 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
     stage(ch, std::integral_constant<int, 7>{}, I0{});
     stage(ch, std::integral_constant<int, 8>{}, I1{});
   };
+  if constexpr ((DBGK & 2) != 0) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int mi = 0; mi < MC; ++mi) dfa[kk][mi] = *reinterpret_cast<const bf16x8 *>(wbuf + abase[mi] + kk * 4 * WPLANE);
+#pragma unroll
+      for (int ni = 0; ni < MP; ++ni) dfb[kk][ni] = *reinterpret_cast<const bf16x8 *>(hbuf + bbase[ni] + kk * 4 * G::PLANE);
+    }
+  }
   // diagnostics (RR_IGEMM_DBG, timing only -- results are wrong): bit1 runs
   // the K loop twice, bit0 skips the epilogue
   const int reps = (a.dbg & 2) ? 2 : 1;
@@ -970,12 +992,35 @@ int halo_bc(const rr_igemm_desc *d) {
   return 0;
 }
 
+template <int BC, int W, int BP, int NT>
+bool launch_halo_dbgk(const rr_igemm_desc *d, IgemmArgs &a, const dim3 &grid, const dim3 &block, hipStream_t st) {
+  const char *e = getenv("RR_HALO_DBGK");
+  const int k = e ? atoi(e) : 0;
+  if (!k || d->w != W) return false;
+  if (k == 1) hipLaunchKernelGGL((igemm3_halo_kernel<BC, W, RR_CONV3X3, BP, NT, 1>), grid, block, 0, st, a);
+  else if (k == 2) hipLaunchKernelGGL((igemm3_halo_kernel<BC, W, RR_CONV3X3, BP, NT, 2>), grid, block, 0, st, a);
+  else hipLaunchKernelGGL((igemm3_halo_kernel<BC, W, RR_CONV3X3, BP, NT, 3>), grid, block, 0, st, a);
+  return true;
+}
+
 template <int BC, int BP, int NT = 2 * BP>
 int launch_halo(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   a.ncblk = (a.cout + BC - 1) / BC;
   const long long nblk = (long long)(a.P / BP) * a.ncblk;
   if (nblk > 0x7fffffffLL) return RR_EUNSUPPORTED;
   const dim3 grid((unsigned)nblk), block(NT);
+  if constexpr (BC == 128 && BP == 256 && NT == 512) {
+    if (launch_halo_dbgk<BC, 8, BP, NT>(d, a, grid, block, st) || launch_halo_dbgk<BC, 16, BP, NT>(d, a, grid, block, st)) {
+      RR_CHECK_LAUNCH();
+      return RR_OK;
+    }
+  }
+  if constexpr (BC == 64 && BP == 256 && NT == 512) {
+    if (launch_halo_dbgk<BC, 32, BP, NT>(d, a, grid, block, st) || launch_halo_dbgk<BC, 16, BP, NT>(d, a, grid, block, st)) {
+      RR_CHECK_LAUNCH();
+      return RR_OK;
+    }
+  }
   switch (d->w) {
     case 64: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 64, RR_CONV3X3, BP, NT>), grid, block, 0, st, a); break;
     case 32: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 32, RR_CONV3X3, BP, NT>), grid, block, 0, st, a); break;
@@ -1015,6 +1060,8 @@ int dispatch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
 extern "C" int rr_igemm_stat_blocks(const rr_igemm_desc *d) {
   if (!d) return RR_EINVAL;
   if (const int sb = stream3_blocks(d, 0)) return sb;
+  S1Plan pl;
+  if (const int g = stream1_plan(d, &pl)) return g;
   const long long P = (long long)d->n * d->h * d->w;
   const int hb = halo_bc(d);
   const int bp = hb ? (hb <= 64 ? halo_bp(d) : 256) : pick_tile(d).bp;
@@ -1066,6 +1113,8 @@ static int fill_args(const rr_igemm_desc *d, const void *x1, const void *x2, con
 extern "C" const char *rr_igemm_kernel_name(const rr_igemm_desc *d, int bnbwd) {
   if (!d) return "invalid";
   if (stream3_blocks(d, bnbwd)) return d->w == 64 ? "stream3_kernel<64>" : "stream3_kernel<32>";
+  S1Plan pl;
+  if (!bnbwd && stream1_plan(d, &pl)) return stream1_name(pl);
   if (d->dtype == RR_BF16) {
     const int hb = halo_bc(d);
     const int bp = (hb && hb <= 64) ? halo_bp(d) : 256;
@@ -1108,6 +1157,14 @@ extern "C" int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
     s.stats = a.stats;
     s.n = d->n; s.h = d->h; s.act = d->act; s.accumulate = d->accumulate;
     return stream3_launch(d, s, 0, st);
+  }
+  S1Plan pl;
+  if (stream1_plan(d, &pl)) {
+    S1Args s{};
+    s.x1 = a.x1; s.x2 = a.x2; s.wt = a.wt; s.bias = a.bias; s.y1 = a.y1; s.y2 = a.y2;
+    s.mask = d->has_mask ? a.mask : nullptr;
+    s.stats = a.stats;
+    return stream1_launch(d, pl, s, st);
   }
   if (d->dtype == RR_BF16) return dispatch<bf16_t>(d, a, st);
   return dispatch<float>(d, a, st);

@@ -128,3 +128,24 @@ def test_kernel_selection_for_the_benched_layers():
         d = IgemmDesc(RR_BF16, RR_CONV3X3, 512, h, h, c1, c2, co, 0, 0, 0, 1, 0, 1, 0)
         assert ops.igemm_kernel_name(d) == f, (h, c1, c2, co, ops.igemm_kernel_name(d))
         assert ops.wgrad_kernel_name(WgradDesc(RR_BF16, RR_CONV3X3, 512, h, h, c1, c2, co, 0)) == wg
+
+
+def _s1name(mode, n, h, w, c1, c2, co, split=0, act=0, acc=0, bias=0, mask=0, stats=0, nchw_=0):
+    from roadrestore import ops
+    from roadrestore._lib import RR_BF16, IgemmDesc
+    return ops.igemm_kernel_name(IgemmDesc(RR_BF16, mode, n, h, w, c1, c2, co, split, act, acc,
+                                           bias, mask, stats, nchw_))
+
+
+def test_stream1_benched_shapes_selected():
+    """host-only: the cfg3 (B = 512) 1x1 / convT layers the planner gives to
+    the streaming kernel"""
+    from roadrestore._lib import RR_CONV1X1, RR_CONVT_DOWN, RR_CONVT_UP
+    assert _s1name(RR_CONV1X1, 512, 32, 32, 64, 0, 128, bias=1, stats=1) == "stream1_kernel<4,2>"
+    assert _s1name(RR_CONV1X1, 512, 64, 64, 64, 64, 64, bias=1, stats=1) == "stream1_kernel<4,4>"
+    assert _s1name(RR_CONV1X1, 512, 64, 64, 64, 0, 128, split=64, acc=1) == "stream1_kernel<8,2>"
+    assert _s1name(RR_CONV1X1, 512, 64, 64, 64, 0, 3, bias=1, nchw_=1) == "stream1_kernel<1,2>"
+    assert _s1name(RR_CONVT_UP, 512, 32, 32, 64, 0, 256, bias=1) == "stream1_kernel<8,2>"
+    assert _s1name(RR_CONVT_DOWN, 512, 32, 32, 64, 0, 64, mask=1).startswith("igemm_kernel")
+    # 8x8 maps (P = 32768) stay on the tiled kernel
+    assert _s1name(RR_CONV1X1, 512, 8, 8, 256, 0, 512, bias=1, stats=1).startswith("igemm_kernel")
