@@ -1523,6 +1523,104 @@ extern "C" int rr_conv_out_bwd(int dtype, int n, int h, int w, int cin, int cout
   return RR_OK;
 }
 
+// ---------------------------------------------------------------------------
+// F.interpolate(x, size=(ho, wo)) default mode 'nearest' (ResUNet skip
+// alignment, 14:169-182): ATen's source index, output == input -> identity,
+// output == 2 input -> o >> 1, else min(floorf(o * (float)in / out), in - 1)
+// in fp32 (as upsample_nearest2d computes it).  NHWC, C % 4 == 0.
+__device__ __forceinline__ int nearest_src(int o, int in, int out) {
+  if (out == in) return o;
+  if (out == 2 * in) return o >> 1;
+  const float scale = (float)in / (float)out;
+  const int s = (int)floorf((float)o * scale);
+  return s < in - 1 ? s : in - 1;
+}
+
+template <typename T>
+__global__ void nearest_fwd_kernel(int n, int hi, int wi, int ho, int wo, int C,
+                                   const T *__restrict__ x, T *__restrict__ y) {
+  const int G = C / 4;
+  const long long total = (long long)n * ho * wo * G;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int g = (int)(i % G);
+    const long long op = i / G;
+    const int ox = (int)(op % wo);
+    const long long t = op / wo;
+    const int oy = (int)(t % ho), nn = (int)(t / ho);
+    const long long ip = ((long long)nn * hi + nearest_src(oy, hi, ho)) * wi + nearest_src(ox, wi, wo);
+    store4<T>(y + op * C + g * 4, load4<T>(x + ip * C + g * 4));
+  }
+}
+
+// backward in gather form (deterministic): dx[iy][ix] = sum of dy over the
+// outputs whose source is (iy, ix), rows then columns in increasing order.
+// The source index is monotone, so those outputs form a contiguous range;
+// it is found by scanning a window around iy * out / in.
+__device__ __forceinline__ void nearest_range(int i, int in, int out, int &lo, int &hi) {
+  int o = (int)(((long long)i * out) / in) - 2;
+  o = o < 0 ? 0 : o;
+  while (o < out && nearest_src(o, in, out) < i) ++o;
+  lo = o;
+  while (o < out && nearest_src(o, in, out) == i) ++o;
+  hi = o;
+}
+
+template <typename T>
+__global__ void nearest_bwd_kernel(int n, int hi, int wi, int ho, int wo, int C,
+                                   const T *__restrict__ dy, T *__restrict__ dx) {
+  const int G = C / 4;
+  const long long total = (long long)n * hi * wi * G;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int g = (int)(i % G);
+    const long long ip = i / G;
+    const int ix = (int)(ip % wi);
+    const long long t = ip / wi;
+    const int iy = (int)(t % hi), nn = (int)(t / hi);
+    int y0, y1, x0, x1;
+    nearest_range(iy, hi, ho, y0, y1);
+    nearest_range(ix, wi, wo, x0, x1);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int oy = y0; oy < y1; ++oy)
+      for (int ox = x0; ox < x1; ++ox)
+        acc += load4<T>(dy + (((long long)nn * ho + oy) * wo + ox) * C + g * 4);
+    store4<T>(dx + ip * C + g * 4, acc);
+  }
+}
+
+extern "C" int rr_nearest_resize(int dtype, int n, int hi, int wi, int ho, int wo, int C,
+                                 const void *x, void *y, rr_stream stream) {
+  if (!x || !y || n < 0 || hi <= 0 || wi <= 0 || ho <= 0 || wo <= 0 || C <= 0 || C % 4) return RR_EINVAL;
+  if (dtype != RR_BF16 && dtype != RR_F32) return RR_EINVAL;
+  const long long total = (long long)n * ho * wo * (C / 4);
+  if (total == 0) return RR_OK;
+  dim3 g(rr_grid_cap((total + 255) / 256, 8192)), b(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(nearest_fwd_kernel<bf16_t>, g, b, 0, st, n, hi, wi, ho, wo, C, (const bf16_t *)x, (bf16_t *)y);
+  else
+    hipLaunchKernelGGL(nearest_fwd_kernel<float>, g, b, 0, st, n, hi, wi, ho, wo, C, (const float *)x, (float *)y);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_nearest_resize_bwd(int dtype, int n, int hi, int wi, int ho, int wo, int C,
+                                     const void *dy, void *dx, rr_stream stream) {
+  if (!dy || !dx || n < 0 || hi <= 0 || wi <= 0 || ho <= 0 || wo <= 0 || C <= 0 || C % 4) return RR_EINVAL;
+  if (dtype != RR_BF16 && dtype != RR_F32) return RR_EINVAL;
+  const long long total = (long long)n * hi * wi * (C / 4);
+  if (total == 0) return RR_OK;
+  dim3 g(rr_grid_cap((total + 255) / 256, 8192)), b(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(nearest_bwd_kernel<bf16_t>, g, b, 0, st, n, hi, wi, ho, wo, C, (const bf16_t *)dy, (bf16_t *)dx);
+  else
+    hipLaunchKernelGGL(nearest_bwd_kernel<float>, g, b, 0, st, n, hi, wi, ho, wo, C, (const float *)dy, (float *)dx);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
 extern "C" int rr_maxpool2_fwd(int dtype, int n, int h, int w, int C, const void *x, void *y,
                                uint8_t *idx, rr_stream stream) {
   if (!x || !y || !idx || C % 4 || h < 2 || w < 2) return RR_EINVAL;

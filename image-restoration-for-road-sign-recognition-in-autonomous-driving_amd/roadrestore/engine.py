@@ -458,14 +458,26 @@ def resunet_block_names():
             "dec1"]
 
 
+def _skip_align(u, h, w):
+    """14:169-182: ``if d.size() != r.size(): d = F.interpolate(d, size=r.shape[2:])``.
+    The reference compares full sizes (channels included), so the nearest
+    resize always runs; at equal spatial sizes it is the identity (no launch
+    here).  Returns (aligned, resized?)."""
+    if u.shape[1] == h and u.shape[2] == w:
+        return u, False
+    return ops.nearest_resize(u, h, w), True
+
+
 def resunet_forward(m, x, wc, dt, training, need_bwd):
     wc.begin()
     n, _, H, W = x.shape
-    if H % 8 or W % 8:
-        raise NotImplementedError(
-            "ResUNet input sizes must be multiples of 8 (the reference's F.interpolate "
-            "alignment branch, 14:169-182, is not implemented on this path)")
-    S = Bag(n=n, H=H, W=W, x=x)
+    if H < 8 or W < 8:
+        raise ValueError("ResUNet needs H, W >= 8 (three 2x2 max-pools, floor mode)")
+    # floor-mode pool sizes (14:155-161)
+    H2, W2 = H // 2, W // 2
+    H3, W3 = H2 // 2, W2 // 2
+    H4, W4 = H3 // 2, W3 // 2
+    S = Bag(n=n, H=H, W=W, x=x, sizes=((H, W), (H2, W2), (H3, W3), (H4, W4)))
     pr = m.enc1[1]
     # conv + PReLU in one pass (the pre-activation kept for the PReLU backward)
     e1, e1pre = ops.first_conv_fwd(x, m.enc1[0].weight, m.enc1[0].bias, dt,
@@ -475,25 +487,28 @@ def resunet_forward(m, x, wc, dt, training, need_bwd):
         S.e1pre = e1pre
     r1, S.res1, (p1, i1) = resblock_forward(m.res1, e1, None, n, H, W, wc, dt, training, need_bwd,
                                             pool=True)
-    r2, S.res2, (p2, i2) = resblock_forward(m.res2, p1, None, n, H // 2, W // 2, wc, dt, training,
+    r2, S.res2, (p2, i2) = resblock_forward(m.res2, p1, None, n, H2, W2, wc, dt, training,
                                             need_bwd, pool=True)
-    r3, S.res3, (p3, i3) = resblock_forward(m.res3, p2, None, n, H // 4, W // 4, wc, dt, training,
+    r3, S.res3, (p3, i3) = resblock_forward(m.res3, p2, None, n, H3, W3, wc, dt, training,
                                             need_bwd, pool=True)
     b = p3
     for i in range(3):
-        b, S[f"bottleneck.{i}"] = resblock_forward(m.bottleneck[i], b, None, n, H // 8, W // 8, wc,
+        b, S[f"bottleneck.{i}"] = resblock_forward(m.bottleneck[i], b, None, n, H4, W4, wc,
                                                    dt, training, need_bwd)
-    u3, pku3 = _convT_up(wc, dt, m.up3, b, n, H // 8, W // 8, need_bwd)
-    d3, S.dec3 = resblock_forward(m.dec3, u3, r3, n, H // 4, W // 4, wc, dt, training, need_bwd)
-    u2, pku2 = _convT_up(wc, dt, m.up2, d3, n, H // 4, W // 4, need_bwd)
-    d2, S.dec2 = resblock_forward(m.dec2, u2, r2, n, H // 2, W // 2, wc, dt, training, need_bwd)
-    u1, pku1 = _convT_up(wc, dt, m.up1, d2, n, H // 2, W // 2, need_bwd)
+    u3, pku3 = _convT_up(wc, dt, m.up3, b, n, H4, W4, need_bwd)
+    u3, al3 = _skip_align(u3, H3, W3)
+    d3, S.dec3 = resblock_forward(m.dec3, u3, r3, n, H3, W3, wc, dt, training, need_bwd)
+    u2, pku2 = _convT_up(wc, dt, m.up2, d3, n, H3, W3, need_bwd)
+    u2, al2 = _skip_align(u2, H2, W2)
+    d2, S.dec2 = resblock_forward(m.dec2, u2, r2, n, H2, W2, wc, dt, training, need_bwd)
+    u1, pku1 = _convT_up(wc, dt, m.up1, d2, n, H2, W2, need_bwd)
+    u1, al1 = _skip_align(u1, H, W)
     d1, S.dec1 = resblock_forward(m.dec1, u1, r1, n, H, W, wc, dt, training, need_bwd)
     out = ops.conv_out_fwd(d1, m.final.weight, m.final.bias,
                            wpack=wc.conv(m.final.weight, dt, dgrad=False)[0])
     if need_bwd:
         S.update(e1=e1, r1=r1, r2=r2, r3=r3, i1=i1, i2=i2, i3=i3, b=b, d3=d3, d2=d2, d1=d1,
-                 pku3=pku3, pku2=pku2, pku1=pku1)
+                 pku3=pku3, pku2=pku2, pku1=pku1, aligned=(al1, al2, al3))
     return out, S
 
 
@@ -547,31 +562,39 @@ def _side_stream(device):
 
 
 def resunet_backward(m, S, g_out, sink):
-    n, H, W = S.n, S.H, S.W
+    n = S.n
+    (H, W), (H2, W2), (H3, W3), (H4, W4) = S.sizes
+    al1, al2, al3 = S.aligned
     g_d1, _, _ = ops.conv_out_bwd(g_out, S.d1, m.final.weight, mask_relu=False,
                                   dw=sink[m.final.weight], db=sink[m.final.bias])
     sink.ready(_params(m.final))
     g_u1, g_r1 = resblock_backward(m.dec1, S.dec1, g_d1, sink)
-    g_d2 = _convT_bwd(m.up1, S.pku1, g_u1, S.d2, n, H // 2, W // 2, sink)
+    if al1:
+        g_u1 = ops.nearest_resize_bwd(g_u1, 2 * H2, 2 * W2)
+    g_d2 = _convT_bwd(m.up1, S.pku1, g_u1, S.d2, n, H2, W2, sink)
     sink.ready(_params(m.up1))
     g_u2, g_r2 = resblock_backward(m.dec2, S.dec2, g_d2, sink)
-    g_d3 = _convT_bwd(m.up2, S.pku2, g_u2, S.d3, n, H // 4, W // 4, sink)
+    if al2:
+        g_u2 = ops.nearest_resize_bwd(g_u2, 2 * H3, 2 * W3)
+    g_d3 = _convT_bwd(m.up2, S.pku2, g_u2, S.d3, n, H3, W3, sink)
     sink.ready(_params(m.up2))
     g_u3, g_r3 = resblock_backward(m.dec3, S.dec3, g_d3, sink)
-    g_b = _convT_bwd(m.up3, S.pku3, g_u3, S.b, n, H // 8, W // 8, sink)
+    if al3:
+        g_u3 = ops.nearest_resize_bwd(g_u3, 2 * H4, 2 * W4)
+    g_b = _convT_bwd(m.up3, S.pku3, g_u3, S.b, n, H4, W4, sink)
     sink.ready(_params(m.up3))
     for i in (2, 1, 0):
         g_b, _ = resblock_backward(m.bottleneck[i], S[f"bottleneck.{i}"], g_b, sink)
-    if _FUSED_POOL_BWD and g_b.dtype == torch.bfloat16:
+    if _FUSED_POOL_BWD and g_b.dtype == torch.bfloat16 and H % 8 == 0 and W % 8 == 0:
         # each encoder block's output fed the skip concat and the pool: the
         # pool backward runs inside that block's tail BN backward
         g_p2, _ = resblock_backward(m.res3, S.res3, g_r3, sink, pool=(g_b, S.i3))
         g_p1, _ = resblock_backward(m.res2, S.res2, g_r2, sink, pool=(g_p2, S.i2))
         g_e1, _ = resblock_backward(m.res1, S.res1, g_r1, sink, pool=(g_p1, S.i1))
     else:
-        ops.maxpool2_bwd(g_b, S.i3, H // 4, W // 4, out=g_r3, accumulate=True)
+        ops.maxpool2_bwd(g_b, S.i3, H3, W3, out=g_r3, accumulate=True)
         g_p2, _ = resblock_backward(m.res3, S.res3, g_r3, sink)
-        ops.maxpool2_bwd(g_p2, S.i2, H // 2, W // 2, out=g_r2, accumulate=True)
+        ops.maxpool2_bwd(g_p2, S.i2, H2, W2, out=g_r2, accumulate=True)
         g_p1, _ = resblock_backward(m.res2, S.res2, g_r2, sink)
         ops.maxpool2_bwd(g_p1, S.i1, H, W, out=g_r1, accumulate=True)
         g_e1, _ = resblock_backward(m.res1, S.res1, g_r1, sink)

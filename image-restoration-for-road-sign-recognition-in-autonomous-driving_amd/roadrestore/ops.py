@@ -22,7 +22,8 @@ __all__ = [
     "prelu_bwd", "conv_out_fwd", "conv_out_bwd", "nchw_to_nhwc", "nhwc_to_nchw",
     "loss_fwd", "loss_bwd", "adamw_", "to_uint8_hwc", "psnr_u8", "argmax_rows",
     "adaptive_avgpool_flatten", "zero_", "resize_bilinear_u8", "ssim_u8", "distort_u8",
-    "motion_blur_kernel", "first_conv_wgrad_act", "affine_act_pool",
+    "motion_blur_kernel", "first_conv_wgrad_act", "affine_act_pool", "nearest_resize",
+    "nearest_resize_bwd",
 ]
 
 
@@ -433,6 +434,27 @@ def maxpool2_fwd(x):
     lib().check(lib().rr_maxpool2_fwd(rr_dtype(x.dtype), n, h, w, Cc, _p(x), _p(y), _p(idx),
                                       stream()), "rr_maxpool2_fwd")
     return y, idx
+
+
+def nearest_resize(x, ho, wo):
+    """F.interpolate(x, size=(ho, wo)) mode 'nearest' (14:169-182), NHWC."""
+    _need_cuda(x)
+    n, hi, wi, Cc = x.shape
+    y = torch.empty((n, ho, wo, Cc), dtype=x.dtype, device=x.device)
+    lib().check(lib().rr_nearest_resize(rr_dtype(x.dtype), n, hi, wi, ho, wo, Cc, _p(x.contiguous()),
+                                        _p(y), stream()), "rr_nearest_resize")
+    return y
+
+
+def nearest_resize_bwd(dy, hi, wi):
+    """gradient of nearest_resize w.r.t. its [n, hi, wi, C] input"""
+    _need_cuda(dy)
+    n, ho, wo, Cc = dy.shape
+    dx = torch.empty((n, hi, wi, Cc), dtype=dy.dtype, device=dy.device)
+    lib().check(lib().rr_nearest_resize_bwd(rr_dtype(dy.dtype), n, hi, wi, ho, wo, Cc,
+                                            _p(dy.contiguous()), _p(dx), stream()),
+                "rr_nearest_resize_bwd")
+    return dx
 
 
 def maxpool2_bwd(dy, idx, h, w, out=None, accumulate=False, mask=None):

@@ -266,6 +266,16 @@ int rr_maxpool2_bwd(int dtype, int n, int h, int w, int C, const void *dy,
                     const uint8_t *idx, void *dx, int accumulate,
                     const void *mask, rr_stream stream);
 
+/* F.interpolate(x, size=(ho, wo)) mode 'nearest' on NHWC [n][hi][wi][C]
+ * (ResUNet decoder skip alignment, 14:169-182; C % 4 == 0): ATen's source
+ * index min(floor(o * (float)hi / ho), hi - 1) (identity / o >> 1 at equal /
+ * doubled sizes), and its backward in deterministic gather form (dx of a
+ * source pixel = the fixed-order sum of dy over the outputs it feeds). */
+int rr_nearest_resize(int dtype, int n, int hi, int wi, int ho, int wo, int C,
+                      const void *x, void *y, rr_stream stream);
+int rr_nearest_resize_bwd(int dtype, int n, int hi, int wi, int ho, int wo, int C,
+                          const void *dy, void *dx, rr_stream stream);
+
 /* first layer: conv3x3 p1 from NCHW fp32 [n][cin][h][w] into NHWC dtype,
  * + bias, act: 0 none, 1 relu, 2 prelu(alpha)  (07:78 enc1.0, 14:122 enc1) */
 int rr_conv_in_fwd(int dtype, int n, int h, int w, int cin, int cout,

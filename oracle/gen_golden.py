@@ -245,5 +245,64 @@ def main():
     print("done")
 
 
+def odd_sizes(m14=None):
+    """ResUNet at input sizes that are not multiples of 8 (14:169-182: the
+    nearest interpolate really resizes the up-conv output), B = 2:
+    eval / train forward, running stats, and one unified step (L1 + 0.1
+    perceptual, 14:235-245) -- loss and grad digests.  60x60: 60 -> 30 -> 15
+    -> 7, up3 14 -> 15; 36x52: 36x52 -> 18x26 -> 9x13 -> 4x6, up3 8x12 -> 9x13."""
+    torch.set_num_threads(8)
+    torch.use_deterministic_algorithms(True)
+    if m14 is None:
+        _install_stubs()
+        m14 = _load("14_train_unified_advanced.py", "ref14")
+    mans = {n: S.load_manifest(n) for n in ("resunet", "perceptual")}
+    perc = m14.VGGPerceptualLoss()
+    perc_sd = S.seeded_state_dict(mans["perceptual"], seed=5)
+    perc.slice.load_state_dict({k[len("slice."):]: v for k, v in perc_sd.items()})
+    for H, W in ((60, 60), (36, 52)):
+        B = 2
+        sd = S.model_state_dict("resunet", seed=0)
+        clean = S.image_batch(B, H, W, seed=70 + H + W)
+        bad = S.fog_noise(clean, seed=80 + H + W)
+        m = m14.ResUNet()
+        m.load_state_dict(sd)
+        m.eval()
+        with torch.no_grad():
+            out_eval = m(bad)
+        _close(R.resunet_forward({k: v.clone() for k, v in sd.items()}, bad, training=False), out_eval)
+        arrays = dict(bad=bad.numpy(), clean=clean.numpy(), out_eval=out_eval.numpy())
+        m.train()
+        opt = torch.optim.AdamW(m.parameters(), lr=2e-4, weight_decay=1e-4)   # 14:222
+        opt.zero_grad()
+        out = m(bad)
+        l_pix = torch.nn.L1Loss()(out, clean)
+        l_perc = perc(out, clean)
+        loss = l_pix + 0.1 * l_perc
+        loss.backward()
+        p = {k: v.clone().requires_grad_(not ("running" in k or "num_batches" in k))
+             for k, v in sd.items()}
+        out_r = R.resunet_forward(p, bad, True)
+        _close(out_r.detach(), out.detach(), 0.0)
+        lr_ = R.unified_loss(out_r, clean, perc_sd)
+        lr_.backward()
+        assert abs(lr_.item() - loss.item()) < 1e-6, (lr_.item(), loss.item())
+        grads = {k: v.grad for k, v in m.named_parameters()}
+        for k in ("enc1.0.weight", "up3.weight", "final.bias"):
+            _close(p[k].grad, grads[k], 1e-5)
+        arrays["out_train"] = out.detach().numpy()
+        run = {k: v for k, v in m.state_dict().items()
+               if k.endswith("running_mean") or k.endswith("running_var")}
+        arrays["running_keys"] = np.array(sorted(run))
+        arrays["running_vals"] = np.concatenate([run[k].numpy().ravel() for k in sorted(run)])
+        arrays["loss"] = np.array([loss.item()])
+        arrays.update({"grad:" + k: v for k, v in digest(grads).items()})
+        save(f"resunet_{H}x{W}.npz", **arrays)
+
+
 if __name__ == "__main__":
-    main()
+    if "--only-odd" in sys.argv:
+        odd_sizes()
+    else:
+        main()
+        odd_sizes()

@@ -645,3 +645,35 @@ def test_loss_vector_and_scalar_paths(dev, dt, count, kind):
     tol = 1e-6 if dt == torch.float32 else 1e-2
     err = (ga.double().cpu() - (base.double().cpu() + gref)).abs().max().item()
     assert err <= tol * max(1.0, base.abs().max().item()), err
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("src,dst", [((7, 7), (15, 15)), ((4, 6), (9, 13)), ((8, 8), (16, 16)),
+                                     ((9, 13), (9, 13)), ((16, 16), (7, 11)), ((5, 3), (17, 10))])
+def test_nearest_resize_fwd_bwd(dev, dt, src, dst):
+    """F.interpolate(size=..., mode='nearest') as the ResUNet skip alignment
+    calls it (14:169-182): forward equal to torch's CPU result bit for bit
+    (a pure gather), backward equal to autograd's scatter-add (exact in fp32:
+    at most 3 addends per source pixel for these ratios; bf16 within one
+    rounding)."""
+    import roadrestore as rr
+    n, C = 3, 64
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(n, C, *src, generator=g)
+    if dt == torch.bfloat16:
+        x = x.bfloat16().float()
+    xr = x.clone().requires_grad_(True)
+    y = F.interpolate(xr, size=dst)
+    dy = torch.randn(y.shape, generator=g)
+    if dt == torch.bfloat16:
+        dy = dy.bfloat16().float()
+    y.backward(dy)
+    xn = x.permute(0, 2, 3, 1).contiguous().to(dev, dt)
+    yo = rr.ops.nearest_resize(xn, *dst)
+    assert torch.equal(yo.float().permute(0, 3, 1, 2).cpu(), y.detach())
+    dx = rr.ops.nearest_resize_bwd(dy.permute(0, 2, 3, 1).contiguous().to(dev, dt), *src)
+    dxc = dx.float().permute(0, 3, 1, 2).cpu()
+    if dt == torch.float32:
+        assert (dxc - xr.grad).abs().max().item() <= 1e-6 * max(1.0, xr.grad.abs().max().item())
+    else:
+        assert (dxc - xr.grad).abs().max().item() <= 1e-2 * max(1.0, xr.grad.abs().max().item())

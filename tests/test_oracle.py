@@ -134,3 +134,24 @@ def test_bf16_emulation_is_the_reference_step_without_rounding(monkeypatch):
     monkeypatch.undo()
     p = {k: v.clone() for k, v in sd.items()}
     assert not torch.equal(E.resunet_forward(p, bad, True), outs[0][0])
+
+
+@pytest.mark.parametrize("hw", ["60x60", "36x52"])
+def test_resunet_oracle_odd_sizes(hw):
+    """The restatement reproduces the reference ResUNet bit for bit at input
+    sizes that trigger the nearest interpolate (14:169-182): eval / train
+    forward and the unified loss, from the committed fixtures."""
+    from oracle import reference_cpu as R
+    from oracle import seeded as S
+    z = gold(f"resunet_{hw}")
+    sd = S.model_state_dict("resunet")
+    bad, clean = torch.from_numpy(z["bad"]), torch.from_numpy(z["clean"])
+    with torch.no_grad():
+        out = R.resunet_forward({k: v.clone() for k, v in sd.items()}, bad, training=False)
+        assert torch.equal(out, torch.from_numpy(z["out_eval"]))
+        p = {k: v.clone() for k, v in sd.items()}
+        out = R.resunet_forward(p, bad, training=True)
+        assert torch.equal(out, torch.from_numpy(z["out_train"]))
+        perc_sd = S.seeded_state_dict(S.load_manifest("perceptual"), seed=5)
+        loss = R.unified_loss(out, clean, perc_sd)
+        assert abs(loss.item() - z["loss"][0]) <= 1e-6 * abs(z["loss"][0])
