@@ -18,15 +18,18 @@ DataLoader workers and in the inference loop).  Here they take a whole
 """
 from __future__ import annotations
 
+import ctypes as C
+import os
 import random as _random
 
 import torch
 
 from . import ops
 from ._lib import (RR_DISTORT_BLUR, RR_DISTORT_FOG, RR_DISTORT_KMAX, RR_DISTORT_NOISE,
-                   DistortParam)
+                   DistortParam, lib)
 
 __all__ = ["Resize", "ToTensor", "Normalize", "Compose", "apply_random_distortions",
+           "encode_png", "write_png",
            "RandomDistortion", "motion_blur_table",
            "apply_compound_distortion", "distortion_params", "psnr", "ssim",
            "IMAGENET_MEAN", "IMAGENET_STD"]
@@ -230,3 +233,48 @@ def psnr(a, b):
 def ssim(a, b):
     """per-image SSIM (08:125, data_range 255, channel_axis=2)"""
     return ops.ssim_u8(a, b)
+
+
+# ---------------------------------------------------------------------------
+# PNG output (17:89-99)
+
+def _host_u8(images):
+    if images.dtype != torch.uint8 or images.dim() != 4 or images.shape[-1] not in (1, 3):
+        raise ValueError("expected an [n, h, w, 1|3] uint8 tensor (rr_to_uint8_hwc layout)")
+    return images.contiguous().cpu() if images.is_cuda else images.contiguous()
+
+
+def encode_png(image, level=1):
+    """One [h, w, c] uint8 RGB (or greyscale) image -> PNG bytes."""
+    if image.dim() == 3:
+        image = image.unsqueeze(0)
+    host = _host_u8(image)
+    _, h, w, c = host.shape
+    need = lib().rr_png_encode(h, w, c, host.data_ptr(), int(level), None, 0)
+    if need < 0:
+        lib().check(int(need), "rr_png_encode")
+    buf = (C.c_uint8 * need)()
+    got = lib().rr_png_encode(h, w, c, host.data_ptr(), int(level), C.addressof(buf), need)
+    if got != need:
+        lib().check(int(got) if got < 0 else -1, "rr_png_encode")
+    return bytes(buf)
+
+
+def write_png(images, paths, level=1, threads=0):
+    """Batched PNG writer for restored images (17:89-99).  ``images``: the
+    [n, h, w, 3] uint8 RGB batch of ops.to_uint8_hwc (device or host).  The
+    reference swaps to BGR and calls cv2.imwrite, which writes the RGB pixels
+    back out; the files here hold the same RGB pixels.  Parent directories are
+    created (17:96)."""
+    host = _host_u8(images)
+    n, h, w, c = host.shape
+    paths = [os.fspath(p) for p in paths]
+    if len(paths) != n:
+        raise ValueError(f"{n} images, {len(paths)} paths")
+    for p in paths:
+        d = os.path.dirname(p)
+        if d:
+            os.makedirs(d, exist_ok=True)
+    arr = (C.c_char_p * max(n, 1))(*[p.encode() for p in paths])
+    lib().check(lib().rr_png_write_batch(n, h, w, c, host.data_ptr(), C.cast(arr, C.c_void_p),
+                                         int(level), int(threads)), "rr_png_write_batch")

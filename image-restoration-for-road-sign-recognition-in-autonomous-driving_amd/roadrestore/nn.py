@@ -14,8 +14,10 @@ unchanged):
 Leaf modules (Conv2d, BatchNorm2d, PReLU, ...) are parameter containers with
 the torch.nn defaults for initialisation; the parent networks run their whole
 forward as one fused HIP schedule and their backward as one hand-written
-reverse schedule (roadrestore.engine).  Nothing here falls back to ATen
-compute: without the HIP library or a device every forward raises.
+reverse schedule (roadrestore.engine), each reached through a registered
+PyTorch custom op (``torch.ops.rr.*``, roadrestore.torch_ops) with its
+autograd formula.  Nothing here falls back to ATen compute: without the HIP
+library or a device every forward raises.
 
 The compute dtype (fp32 default: the parity path; bf16 for throughput) is a
 per-model attribute, ``model.compute_dtype``, or ``RR_COMPUTE_DTYPE``.
@@ -29,6 +31,7 @@ import torch
 import torch.nn as tnn
 
 from . import engine, ops
+from . import torch_ops as _tops
 
 __all__ = ["Conv2d", "ConvTranspose2d", "BatchNorm2d", "PReLU", "ReLU", "MaxPool2d", "Linear",
            "Dropout", "AdaptiveAvgPool2d", "SimpleUNet", "ResidualBlock", "ResUNet",
@@ -140,37 +143,21 @@ class AdaptiveAvgPool2d(_Leaf):
 
 
 # ---------------------------------------------------------------------------
-# network autograd node
-
-class _NetFn(torch.autograd.Function):
-    """One autograd node for a whole network: forward = fused HIP schedule,
-    backward = hand-written reverse schedule writing a flat grad buffer."""
-
-    @staticmethod
-    def forward(ctx, x, net, *params):
-        out, S = net._rr_forward(x, need_bwd=True)
-        ctx.net, ctx.S = net, S
-        ctx.params = params
-        return out
-
-    @staticmethod
-    def backward(ctx, g):
-        net, S = ctx.net, ctx.S
-        views = net._rr_backward(S, g.contiguous())
-        ctx.S = None
-        return (None, None) + tuple(views.pop(id(p), None) for p in ctx.params)
-
+# networks: one custom op (torch.ops.rr.<name>_forward) per call, its
+# registered autograd formula calls rr::<name>_backward (torch_ops.py)
 
 class _RRNet(tnn.Module):
     """Shared plumbing of the restorers."""
 
     _has_bn = True
+    _op = None        # torch.ops.rr.<_op>_forward runs this network
 
     def __init__(self):
         super().__init__()
         self.compute_dtype = default_compute_dtype()
         self._wc = engine.WeightCache()
         self._grad_hook = None
+        self._op_key = _tops.register_module(self)
 
     # data-parallel wrappers install a hook called as grad groups become final
     def set_grad_ready_hook(self, hook):
@@ -206,13 +193,12 @@ class _RRNet(tnn.Module):
         need = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         if x.shape[0] == 0:
             return self._empty_forward(x, need)
-        if not need:
-            out, _ = self._rr_forward(x, need_bwd=False)
-            return out
-        if self._has_bn and not self.training:
+        if need and self._has_bn and not self.training:
             raise NotImplementedError("backward through eval-mode BatchNorm is not implemented; "
                                       "use model.train() or torch.no_grad()")
-        return _NetFn.apply(x, self, *params)
+        fwd = getattr(torch.ops.rr, f"{self._op}_forward")
+        out, _ = fwd(x, params, self._op_key, need)
+        return out
 
     def _make_sink(self, order, zero_params, device):
         return engine.GradSink(order, device, zero_params=zero_params, hook=self._grad_hook)
@@ -228,6 +214,7 @@ class SimpleUNet(_RRNet):
     """07_train_restoration.py:75-120 (verbatim copies at 07adv:65-92, 08:19-46, 13:59-85)."""
 
     _has_bn = False
+    _op = "simple_unet"
 
     def __init__(self):
         super().__init__()
@@ -255,7 +242,7 @@ class SimpleUNet(_RRNet):
         order, zero = self._grad_order()
         sink = self._make_sink(order, zero, g.device)
         engine.simple_unet_backward(self, S, g, sink)
-        return sink.release()
+        return sink.flat
 
 
 class ResidualBlock(_RRNet):
@@ -263,6 +250,8 @@ class ResidualBlock(_RRNet):
 
     As a standalone module its forward takes / returns NCHW fp32 tensors; the
     ResUNet runs its blocks on NHWC activations inside one schedule."""
+
+    _op = "resblock"
 
     def __init__(self, in_c, out_c):
         super().__init__()
@@ -293,11 +282,13 @@ class ResidualBlock(_RRNet):
         sink = self._make_sink(order, zero, g.device)
         gn = ops.nchw_to_nhwc(g, self.compute_dtype)
         engine.resblock_backward(self, S, gn, sink)
-        return sink.release()
+        return sink.flat
 
 
 class ResUNet(_RRNet):
     """14_train_unified_advanced.py:117-186 (copies 15:43-90, 17:29-55)."""
+
+    _op = "resunet"
 
     def __init__(self):
         super().__init__()
@@ -332,7 +323,7 @@ class ResUNet(_RRNet):
         order, zero = self._grad_order()
         sink = self._make_sink(order, zero, g.device)
         engine.resunet_backward(self, S, g, sink)
-        return sink.release()
+        return sink.flat
 
 
 # ---------------------------------------------------------------------------
@@ -376,6 +367,7 @@ class VGG(tnn.Module):
                 tnn.init.constant_(m.bias, 0)
         self.compute_dtype = default_compute_dtype()
         self._wc = engine.WeightCache()
+        self._op_key = _tops.register_module(self)
 
     def forward(self, x):
         """Eval-mode logits (18:46): the classifier is the fixed judge."""
@@ -383,9 +375,8 @@ class VGG(tnn.Module):
             raise RuntimeError("roadrestore networks run on the GPU only (no CPU fallback)")
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
             raise NotImplementedError("VGG16 runs as the frozen judge: use torch.no_grad()")
-        logits = engine.vgg_classifier_forward(self, x.float().contiguous(), self._wc,
-                                               self.compute_dtype)
-        return logits if logits.dtype == torch.float32 else logits.float()
+        return torch.ops.rr.vgg16_logits(x.float().contiguous(), list(self.parameters()),
+                                         self._op_key)
 
 
 def vgg16(weights=None, num_classes=43, **kw):
@@ -395,22 +386,6 @@ def vgg16(weights=None, num_classes=43, **kw):
     if weights is not None:
         raise RuntimeError("pretrained weights need a network download; load a state_dict")
     return VGG(num_classes=num_classes)
-
-
-class _PercFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, y, mod, scale):
-        loss, S, fx, fy = mod._rr_forward(x, y, scale, need_bwd=True)
-        ctx.S, ctx.fx, ctx.fy, ctx.scale = S, fx, fy, scale
-        return loss
-
-    @staticmethod
-    def backward(ctx, g):
-        gpre = ops.loss_bwd(ops.MSE, ctx.fx, ctx.fy, gscale=g.contiguous(), scale=ctx.scale,
-                            mask_a_pos=True)
-        gx = engine.vgg_features_backward_input(ctx.S, gpre)
-        ctx.S = ctx.fx = ctx.fy = None
-        return gx, None, None, None
 
 
 class VGGPerceptualLoss(tnn.Module):
@@ -426,6 +401,7 @@ class VGGPerceptualLoss(tnn.Module):
             p.requires_grad = False
         self.compute_dtype = default_compute_dtype()
         self._wc = engine.WeightCache()
+        self._op_key = _tops.register_module(self)
 
     def _rr_forward(self, x, y, scale, need_bwd):
         fx, S = engine.vgg_features_forward(self.slice, x, self._wc, self.compute_dtype,
@@ -439,69 +415,27 @@ class VGGPerceptualLoss(tnn.Module):
     def forward(self, x, y):
         x = x.float().contiguous()
         y = y.float().contiguous()
-        if torch.is_grad_enabled() and x.requires_grad:
-            return _PercFn.apply(x, y, self, 1.0)
-        return self._rr_forward(x, y, 1.0, need_bwd=False)[0]
-
-
-class _PixFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, a, b, kind):
-        ctx.save_for_backward(a, b)
-        ctx.kind = kind
-        return ops.loss_fwd(kind, a, b)
-
-    @staticmethod
-    def backward(ctx, g):
-        a, b = ctx.saved_tensors
-        return ops.loss_bwd(ctx.kind, a, b, gscale=g.contiguous()), None, None
+        need = torch.is_grad_enabled() and x.requires_grad
+        return torch.ops.rr.perceptual_loss(x, y, self._op_key, need)[0]
 
 
 class L1Loss(tnn.Module):
     """nn.L1Loss (mean) on device tensors (14:219)."""
 
     def forward(self, a, b):
-        return _PixFn.apply(a.float().contiguous(), b.float().contiguous(), ops.L1)
+        return torch.ops.rr.pixel_loss(a.float().contiguous(), b.float().contiguous(), ops.L1)
 
 
 class MSELoss(tnn.Module):
     """nn.MSELoss (mean) on device tensors (07:142)."""
 
     def forward(self, a, b):
-        return _PixFn.apply(a.float().contiguous(), b.float().contiguous(), ops.MSE)
-
-
-class _UnifiedFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, out, clean, perc, w, grad_scale):
-        loss = ops.loss_fwd(ops.L1, out, clean)
-        S = None
-        if w != 0.0:
-            fx, S = engine.vgg_features_forward(perc.slice, out, perc._wc, perc.compute_dtype,
-                                                need_bwd=True)
-            fy, _ = engine.vgg_features_forward(perc.slice, clean, perc._wc, perc.compute_dtype)
-            ops.loss_fwd(ops.MSE, fx, fy, scale=w, out=loss, accumulate=True)
-            ctx.fx, ctx.fy = fx, fy
-        ctx.save_for_backward(out, clean)
-        ctx.S, ctx.w, ctx.gs = S, w, grad_scale
-        return loss
-
-    @staticmethod
-    def backward(ctx, g):
-        out, clean = ctx.saved_tensors
-        g = g.contiguous()
-        gout = ops.loss_bwd(ops.L1, out, clean, gscale=g, scale=ctx.gs)
-        if ctx.S is not None:
-            gpre = ops.loss_bwd(ops.MSE, ctx.fx, ctx.fy, gscale=g, scale=ctx.w * ctx.gs,
-                                mask_a_pos=True)
-            engine.vgg_features_backward_input(ctx.S, gpre, x_grad_out=gout, accumulate=True)
-        ctx.S = ctx.fx = ctx.fy = None
-        return gout, None, None, None, None
+        return torch.ops.rr.pixel_loss(a.float().contiguous(), b.float().contiguous(), ops.MSE)
 
 
 def unified_loss(out, clean, perc, w=0.1, grad_scale=1.0):
     """L1(out, clean) + w * perceptual(out, clean) as ONE autograd node
     (14:238-242) with a single fused gradient; ``grad_scale`` pre-scales the
     backward (1/world_size under data parallelism)."""
-    return _UnifiedFn.apply(out.contiguous(), clean.float().contiguous(), perc, float(w),
-                            float(grad_scale))
+    return torch.ops.rr.unified_loss(out.contiguous(), clean.float().contiguous(), perc._op_key,
+                                     float(w), float(grad_scale))[0]

@@ -266,6 +266,18 @@ int rr_maxpool2_bwd(int dtype, int n, int h, int w, int C, const void *dy,
                     const uint8_t *idx, void *dx, int accumulate,
                     const void *mask, rr_stream stream);
 
+/* PNG encoding of restored uint8 HWC images (17:89-99: cv2.imwrite of the
+ * BGR-swapped array, which stores the RGB pixels).  Host memory, no device:
+ * 8-bit truecolour (c = 3) / greyscale (c = 1), zlib level 0..9, adaptive
+ * per-row filter.  rr_png_encode: one image into out[cap]; returns the PNG
+ * size (the bytes are written only when it fits) or a negative status.
+ * rr_png_write_batch: n images of [h][w][c] into paths[i], on `threads` host
+ * threads (<= 0: all hardware threads). */
+long long rr_png_encode(int h, int w, int c, const uint8_t *hwc, int level, uint8_t *out,
+                        long long cap);
+int rr_png_write_batch(int n, int h, int w, int c, const uint8_t *hwc, const char *const *paths,
+                       int level, int threads);
+
 /* F.interpolate(x, size=(ho, wo)) mode 'nearest' on NHWC [n][hi][wi][C]
  * (ResUNet decoder skip alignment, 14:169-182; C % 4 == 0): ATen's source
  * index min(floor(o * (float)hi / ho), hi - 1) (identity / o >> 1 at equal /

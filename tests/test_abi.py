@@ -149,3 +149,38 @@ def test_stream1_benched_shapes_selected():
     assert _s1name(RR_CONVT_DOWN, 512, 32, 32, 64, 0, 64, mask=1).startswith("igemm_kernel")
     # 8x8 maps (P = 32768) stay on the tiled kernel
     assert _s1name(RR_CONV1X1, 512, 8, 8, 256, 0, 512, bias=1, stats=1).startswith("igemm_kernel")
+
+
+def test_custom_ops_registered_with_fake_shapes():
+    """The hot path is registered as PyTorch custom ops (torch.ops.rr.*) with
+    fake kernels: shapes propagate without a device (torch.compile / meta
+    tracing), and every op the modules call exists."""
+    import torch
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    import roadrestore as rr
+    from roadrestore import torch_ops
+    assert all(hasattr(torch.ops.rr, n) for n in torch_ops.OPS)
+    s = str(torch.ops.rr.resunet_forward.default._schema)
+    assert s.startswith("rr::resunet_forward(Tensor x, Tensor[] params,"), s
+    res, su, blk, vgg = rr.ResUNet(), rr.SimpleUNet(), rr.ResidualBlock(64, 128), rr.vgg16()
+    with FakeTensorMode(allow_non_fake_inputs=True):
+        x = torch.empty(2, 3, 36, 52, device="cuda")
+        out, h = torch.ops.rr.resunet_forward(x, list(res.parameters()), res._op_key, True)
+        assert out.shape == (2, 3, 36, 52) and h.dtype == torch.int64
+        out, _ = torch.ops.rr.simple_unet_forward(torch.empty(2, 3, 64, 64, device="cuda"),
+                                                  list(su.parameters()), su._op_key, False)
+        assert out.shape == (2, 3, 64, 64)
+        out, _ = torch.ops.rr.resblock_forward(torch.empty(2, 64, 16, 16, device="cuda"),
+                                               list(blk.parameters()), blk._op_key, False)
+        assert out.shape == (2, 128, 16, 16)
+        lg = torch.ops.rr.vgg16_logits(torch.empty(5, 3, 224, 224, device="cuda"),
+                                       list(vgg.parameters()), vgg._op_key)
+        assert lg.shape == (5, 43) and lg.dtype == torch.float32
+        assert torch.ops.rr.nearest_resize(torch.empty(2, 4, 6, 128, device="cuda"), 9, 13).shape \
+            == (2, 9, 13, 128)
+        u8 = torch.ops.rr.to_uint8_hwc(torch.empty(2, 3, 8, 8, device="cuda"), True)
+        assert u8.shape == (2, 8, 8, 3) and u8.dtype == torch.uint8
+        assert torch.ops.rr.argmax_rows(torch.empty(7, 43, device="cuda")).shape == (7,)
+        loss, _ = torch.ops.rr.unified_loss(torch.empty(2, 3, 8, 8, device="cuda"),
+                                            torch.empty(2, 3, 8, 8, device="cuda"), 0, 0.1, 1.0)
+        assert loss.shape == ()

@@ -132,3 +132,27 @@ def test_distortion_params_follow_reference_draw_order():
         assert bool(p.flags & RR_DISTORT_BLUR) == blur
         seen.add((fog, noise, blur))
     assert len(seen) == 8                                    # every branch combination drawn
+
+
+@pytest.mark.parametrize("shape", [(3, 64, 64, 3), (2, 224, 224, 3), (1, 37, 53, 3), (2, 5, 7, 1)])
+def test_png_writer_roundtrip(tmp_path, shape):
+    """17:89-99: the restored uint8 images written as PNG (host-side batched
+    encoder in libroadrestore.so, no device needed) decode with Pillow to
+    exactly the same pixels; cv2.imwrite of the BGR-swapped array stores the
+    RGB pixels, so the files carry the RGB buffer."""
+    import numpy as np
+    from PIL import Image
+    from roadrestore import imgproc
+    g = np.random.default_rng(sum(shape))
+    u8 = g.integers(0, 256, size=shape, dtype=np.uint8)
+    u8[0, : shape[1] // 2] = 17                     # flat region: exercises the filters
+    t = torch.from_numpy(u8)
+    paths = [tmp_path / "sub" / f"img{i}.png" for i in range(shape[0])]
+    imgproc.write_png(t, paths, level=1, threads=2)
+    for i, p in enumerate(paths):
+        with Image.open(p) as im:
+            got = np.asarray(im)
+        ref = u8[i, ..., 0] if shape[-1] == 1 else u8[i]
+        assert got.shape == ref.shape and np.array_equal(got, ref)
+    # single-image encoder: same bytes as the batch writer's file
+    assert imgproc.encode_png(t[0], level=1) == paths[0].read_bytes()

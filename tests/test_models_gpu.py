@@ -522,3 +522,38 @@ def test_running_loss_on_device(dev):
         g.replay()
     torch.cuda.synchronize()
     assert rl.steps() == 3 and rl.total() == 6.0
+
+
+def test_reference_loop_through_custom_ops_profiled(dev):
+    """The reference's training step (14:235-246) written as the reference
+    writes it -- separate L1 and perceptual modules, loss.backward(),
+    optimizer.step(), loss.item() -- runs through the registered custom ops:
+    torch.profiler attributes the work to rr::resunet_forward / _backward and
+    the loss ops, and the first step's loss equals the reference's."""
+    import roadrestore as rr
+    from oracle import seeded as S
+    z = gold("resunet_64")
+    m = rr.ResUNet().to(dev)
+    m.load_state_dict(S.model_state_dict("resunet"))
+    m.train()
+    perc = rr.VGGPerceptualLoss().to(dev)
+    perc.load_state_dict(S.seeded_state_dict(S.load_manifest("perceptual"), seed=5))
+    crit = rr.L1Loss()
+    opt = rr.AdamW(m.parameters(), lr=2e-4, weight_decay=1e-4)
+    bad = torch.from_numpy(z["bad"]).to(dev)
+    clean = torch.from_numpy(z["clean"]).to(dev)
+    losses = []
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU]) as prof:
+        for _ in range(2):
+            opt.zero_grad()
+            out = m(bad)
+            loss = crit(out, clean) + 0.1 * perc(out, clean)
+            loss.backward()
+            opt.step()
+            losses.append(loss.item())
+    names = {e.key for e in prof.key_averages()}
+    want = {"rr::resunet_forward", "rr::resunet_backward", "rr::pixel_loss",
+            "rr::pixel_loss_backward", "rr::perceptual_loss", "rr::perceptual_loss_backward"}
+    assert want <= names, sorted(want - names)
+    assert abs(losses[0] - z["loss"][0]) <= 1e-4 * abs(z["loss"][0])
+    assert losses[1] < losses[0]
