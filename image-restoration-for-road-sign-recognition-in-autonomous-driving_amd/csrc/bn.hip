@@ -724,6 +724,32 @@ extern "C" int rr_bn_eval_affine(int C, const float *gamma, const float *beta,
   return RR_OK;
 }
 
+// eval-mode BatchNorm folded into the conv before it (17:84-85 inference):
+// BN(W x + b) = (s W) x + (s b + t) with s, t = rr_bn_eval_affine's scale /
+// shift; w [co][kel] fp32 (torch layout, kel = c_in * k * k)
+__global__ void fold_conv_bn_kernel(int co, int kel, const float *__restrict__ w,
+                                    const float *__restrict__ b, const float *__restrict__ scale,
+                                    const float *__restrict__ shift, float *__restrict__ w_out,
+                                    float *__restrict__ b_out) {
+  const long long total = (long long)co * kel;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i / kel);
+    w_out[i] = w[i] * scale[c];
+    if (i - (long long)c * kel == 0) b_out[c] = (b ? b[c] : 0.f) * scale[c] + shift[c];
+  }
+}
+
+extern "C" int rr_fold_conv_bn(int co, int kel, const float *w, const float *b, const float *scale,
+                               const float *shift, float *w_out, float *b_out, rr_stream stream) {
+  if (co <= 0 || kel <= 0 || !w || !scale || !shift || !w_out || !b_out) return RR_EINVAL;
+  const long long total = (long long)co * kel;
+  hipLaunchKernelGGL(fold_conv_bn_kernel, dim3(rr_grid_cap((total + 255) / 256, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, co, kel, w, b, scale, shift, w_out, b_out);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
 extern "C" int rr_affine_act(int dtype, long long P, int C, const void *x, const float *scale,
                              const float *shift, const float *alpha, const void *res,
                              const float *res_scale, const float *res_shift, int relu, void *y,

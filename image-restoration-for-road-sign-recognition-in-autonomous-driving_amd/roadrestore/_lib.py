@@ -92,6 +92,7 @@ _SIGS = {
     "rr_maxpool2_fwd": (I_, [I_, I_, I_, I_, I_, P_, P_, P_, P_]),
     "rr_nearest_resize": (I_, [I_, I_, I_, I_, I_, I_, I_, P_, P_, P_]),
     "rr_png_encode": (L_, [I_, I_, I_, P_, I_, P_, L_]),
+    "rr_fold_conv_bn": (I_, [I_, I_, P_, P_, P_, P_, P_, P_, P_]),
     "rr_png_write_batch": (I_, [I_, I_, I_, I_, P_, P_, I_, I_]),
     "rr_nearest_resize_bwd": (I_, [I_, I_, I_, I_, I_, I_, I_, P_, P_, P_]),
     "rr_maxpool2_bwd": (I_, [I_, I_, I_, I_, I_, P_, P_, P_, I_, P_, P_]),

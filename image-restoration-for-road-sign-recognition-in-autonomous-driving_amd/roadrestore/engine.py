@@ -72,6 +72,27 @@ class WeightCache:
             self._c[key] = (ver, v)
         return v
 
+    def conv_bn_folded(self, conv, bn, dtype):
+        """Eval: the BN after ``conv`` folded into it -- (packed fwd weights of
+        w * s, fp32 bias b * s + t), s / t the BN eval affine (17:84-85).
+        Cached on the versions of the conv and BN tensors."""
+        deps = [t for t in (conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean,
+                            bn.running_var) if t is not None]
+        from .optim import GENERATION
+        ver = tuple((t.data_ptr(), t._version) for t in deps) + (GENERATION[0], bn.eps)
+        key = (id(conv.weight), dtype, "fold")
+        cap = torch.cuda.is_current_stream_capturing()
+        e = None if cap else self._c.get(key)
+        if e is not None and e[0] == ver:
+            return e[1]
+        s, t = ops.bn_eval_affine(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
+        wf, bf = ops.fold_conv_bn(conv.weight, conv.bias, s, t)
+        pk, _ = ops.pack_conv(wf, dtype, fwd=True, dgrad=False)
+        v = (pk, bf)
+        if not cap:
+            self._c[key] = (ver, v)
+        return v
+
     def begin(self):
         """Start of a forward: one batched re-pack of every planned conv."""
         self._fresh = {}
@@ -315,9 +336,46 @@ def block_has_shortcut(blk):
     return len(blk.shortcut) > 0
 
 
+# A/B switch: eval-mode BN folded into the conv weights (RR_FOLD_BN=0: conv +
+# separate BN affine passes, as in training)
+_FOLD_BN = os.environ.get("RR_FOLD_BN", "1") != "0"
+
+
+def resblock_forward_eval_folded(blk, x1, x2, n, h, w, wc, dt, pool=False):
+    """Inference (17:84-86): every BN folded into the conv before it, so
+      a1  = PReLU(conv1'(x))                    conv1' = BN1 o conv1
+      out = relu(conv2'(a1) + sc'(x))           the shortcut 1x1 accumulates onto
+                                                conv2's output with the ReLU in
+                                                its epilogue (no tail pass)
+      out = relu(conv2'(a1) + x)                identity shortcut: one pass"""
+    cb = blk.conv_block
+    c1, bn1, pr, c2, bn2 = cb[0], cb[1], cb[2], cb[3], cb[4]
+    cout = c1.weight.shape[0]
+    pk1, b1 = wc.conv_bn_folded(c1, bn1, dt)
+    t1, _, _ = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, pk1, cout, bias=b1)
+    one, zero = _unit_affine(cout, x1.device)
+    a1 = ops.affine_act(t1, one, zero, alpha=pr.weight)
+    pk2, b2 = wc.conv_bn_folded(c2, bn2, dt)
+    t2, _, _ = ops.igemm(RR_CONV3X3, a1, None, n, h, w, pk2, cout, bias=b2)
+    if block_has_shortcut(blk):
+        pks, bs = wc.conv_bn_folded(blk.shortcut[0], blk.shortcut[1], dt)
+        out, _, _ = ops.igemm(RR_CONV1X1, x1, x2, n, h, w, pks, cout, bias=bs, out=t2,
+                              accumulate=True, act=RELU)
+    else:
+        if x2 is not None:
+            raise RuntimeError("identity shortcut with a concatenated input")
+        out = ops.affine_act(t2, one, zero, res=x1, relu=True)
+    S = Bag(x1=x1, x2=x2, n=n, h=h, w=w)
+    if pool:
+        return out, S, ops.maxpool2_fwd(out)
+    return out, S
+
+
 def resblock_forward(blk, x1, x2, n, h, w, wc, dt, training, need_bwd, pool=False):
     """-> (out, S), or (out, S, (pooled, idx)) with ``pool`` (the 2x2 max-pool
     that follows the encoder blocks, fused into the residual tail)."""
+    if _FOLD_BN and not training and not need_bwd:
+        return resblock_forward_eval_folded(blk, x1, x2, n, h, w, wc, dt, pool)
     cb = blk.conv_block
     c1, bn1, pr, c2, bn2 = cb[0], cb[1], cb[2], cb[3], cb[4]
     cout = c1.weight.shape[0]

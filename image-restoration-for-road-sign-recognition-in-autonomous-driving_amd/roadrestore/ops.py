@@ -23,7 +23,7 @@ __all__ = [
     "loss_fwd", "loss_bwd", "adamw_", "to_uint8_hwc", "psnr_u8", "argmax_rows",
     "adaptive_avgpool_flatten", "zero_", "resize_bilinear_u8", "ssim_u8", "distort_u8",
     "motion_blur_kernel", "first_conv_wgrad_act", "affine_act_pool", "nearest_resize",
-    "nearest_resize_bwd",
+    "nearest_resize_bwd", "fold_conv_bn",
 ]
 
 
@@ -264,6 +264,18 @@ def bn_eval_affine(gamma, beta, running_mean, running_var, eps=1e-5):
                                         _p(running_var), float(eps), _p(scale), _p(shift),
                                         stream()), "rr_bn_eval_affine")
     return scale, shift
+
+
+def fold_conv_bn(w, b, scale, shift):
+    """eval BN folded into the conv: (w * scale[c], b * scale + shift), fp32"""
+    _need_cuda(w, scale, shift)
+    co = w.shape[0]
+    w = w.contiguous()
+    wf = torch.empty_like(w)
+    bf = torch.empty(co, dtype=torch.float32, device=w.device)
+    lib().check(lib().rr_fold_conv_bn(co, w.numel() // co, _p(w), _p(b), _p(scale), _p(shift),
+                                      _p(wf), _p(bf), stream()), "rr_fold_conv_bn")
+    return wf, bf
 
 
 def affine_act(x, scale, shift, alpha=None, res=None, res_scale=None, res_shift=None, relu=False,

@@ -171,6 +171,12 @@ int rr_bn_finalize(int C, int blocks, long long count, const float *stats_partia
  * [blocks][C][2] partials are first folded to <= 64 fp64 rows by a parallel
  * fixed-order column reduction in ws */
 size_t rr_bn_finalize_workspace(int C, int blocks);
+/* eval-mode BatchNorm folded into the conv that feeds it (inference,
+ * 17:84-85): w_out[c][k] = w[c][k] * scale[c], b_out[c] = b[c] * scale[c] +
+ * shift[c] (scale / shift from rr_bn_eval_affine; b may be NULL); fp32,
+ * torch weight layout [co][kel] */
+int rr_fold_conv_bn(int co, int kel, const float *w, const float *b, const float *scale,
+                    const float *shift, float *w_out, float *b_out, rr_stream stream);
 /* eval mode: scale/shift from running stats (17:64 model.eval()) */
 int rr_bn_eval_affine(int C, const float *gamma, const float *beta,
                       const float *running_mean, const float *running_var,

@@ -557,3 +557,72 @@ def test_reference_loop_through_custom_ops_profiled(dev):
     assert want <= names, sorted(want - names)
     assert abs(losses[0] - z["loss"][0]) <= 1e-4 * abs(z["loss"][0])
     assert losses[1] < losses[0]
+
+
+def _e2e_images(B=6, s0=48):
+    """GTSRB-sized uint8 crops, each with its own tint (so the judge's Top-1
+    varies across the batch)"""
+    rng = np.random.Generator(np.random.PCG64([2024, 5]))
+    imgs = []
+    for i in range(B):
+        base = rng.integers(0, 256, size=(s0, s0, 3)).astype(np.float64)
+        tint = np.array([(i * 70) % 256, (i * 130 + 40) % 256, (255 - i * 40) % 256], dtype=np.float64)
+        imgs.append(np.clip(0.35 * base + 0.65 * tint, 0, 255).astype(np.uint8))
+    return np.stack(imgs)
+
+
+def test_inference_pipeline_fp32_end_to_end(dev):
+    """cfg5 at the reference's precision: Resize((224, 224)) + ToTensor
+    (17:66) -> ResUNet.eval() (BN folded into the convs) -> clamp, x255,
+    uint8 truncation (17:84-90) -> Resize + ToTensor + Normalize(ImageNet)
+    (18:28-32) -> VGG16 43-class logits -> Top-1 (18:46-47), every stage on
+    device, against the oracle composition of the same steps on CPU (PIL-exact
+    resize restatement, reference ResUNet / VGG16 restatements).  The judge's
+    weights (seed 4) give three distinct classes on this batch, margins > 0.3."""
+    import roadrestore as rr
+    from roadrestore import imgproc as T
+    from oracle import reference_cpu as R
+    from oracle import imgproc_cpu as I
+    from oracle import seeded as S
+    imgs = _e2e_images()
+    mean, std = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
+    # oracle composition
+    x = torch.from_numpy(np.stack([I.to_tensor_normalize(I.pil_resize_bilinear(im, 224, 224))
+                                   for im in imgs]))
+    sd = S.model_state_dict("resunet")
+    vsd = S.seeded_state_dict(S.load_manifest("vgg16"), seed=4)
+    with torch.no_grad():
+        out_ref = R.resunet_forward({k: v.clone() for k, v in sd.items()}, x, training=False)
+        u8_ref = R.to_uint8_image(out_ref)
+        xin = torch.from_numpy(np.stack([I.to_tensor_normalize(I.pil_resize_bilinear(u, 224, 224),
+                                                               mean, std) for u in u8_ref]))
+        vgg_ref = R.TorchvisionVGG16(43)
+        vgg_ref.load_state_dict(vsd)
+        vgg_ref.eval()
+        lg_ref = vgg_ref(xin)
+    pred_ref = R.top1(lg_ref)
+    assert len(set(pred_ref.tolist())) >= 3
+    # device pipeline, fp32
+    net = rr.ResUNet().to(dev).eval()
+    net.load_state_dict(sd)
+    judge = rr.vgg16().to(dev).eval()
+    judge.load_state_dict(vsd)
+    pre = T.Compose([T.Resize((224, 224)), T.ToTensor()])
+    judge_pre = T.Compose([T.Resize((224, 224)), T.ToTensor(), T.Normalize(mean, std)])
+    src = torch.from_numpy(imgs).to(dev)
+    with torch.no_grad():
+        xd = pre(src)
+        assert torch.equal(xd.cpu(), x)                    # PIL-exact resize, bit for bit
+        out = net(xd)
+        mae = (out.cpu() - out_ref).abs().mean().item()
+        assert mae <= 1e-4 and (out.cpu() - out_ref).abs().max().item() <= 1e-3, mae
+        u8 = rr.ops.to_uint8_hwc(out)
+        d = u8.cpu().numpy().astype(int) - u8_ref.astype(int)
+        assert np.abs(d).max() <= 1 and (d != 0).mean() < 1e-3
+        # 17:91: the BGR array cv2.imwrite receives
+        bgr = rr.ops.to_uint8_hwc(out, bgr=True)
+        assert torch.equal(bgr, u8.flip(-1))
+        logits = judge(judge_pre(u8))
+    pred = rr.ops.argmax_rows(logits).cpu()
+    assert (logits.cpu() - lg_ref).abs().max().item() <= 1e-3 * max(1.0, lg_ref.abs().max().item())
+    assert torch.equal(pred, pred_ref), (pred.tolist(), pred_ref.tolist())

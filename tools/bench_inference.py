@@ -82,6 +82,15 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     run(a.images, True)
+    # roofline of the two compute stages: hook-counted conv/linear FLOP per
+    # image at 224 over the HIP-event stage times, vs the dense
+    # MFMA peak of the compute dtype (MI355X_MICROARCH.md)
+    peak = 2516.6 if a.dtype == "bf16" else 157.3
+    fl = {"restore": 55_991_599_104 * (a.res / 224) ** 2, "judge": 30_932_688_896}
+    roof = {}
+    for k in ("restore", "judge"):
+        tf = fl[k] * a.images / (stage_ms[k] * 1e-3) / 1e12
+        roof[k] = {"achieved_tflops": round(tf, 1), "peak_tflops": peak, "frac": round(tf / peak, 4)}
     print(json.dumps({
         "config": f"cfg5 end-to-end inference: {a.images} GTSRB-sized {a.size}x{a.size} crops, "
                   f"Resize({a.res}) + ResUNet eval + uint8 + Resize(224)/Normalize + VGG16 Top-1 + PSNR/SSIM",
@@ -91,6 +100,10 @@ def main():
         "data": "synthetic uint8 crops, compound distortion (16:14-37) on device, random-init weights",
         "mean_psnr_db": round(ps.mean().item(), 3), "mean_ssim": round(ss.mean().item(), 4),
         "top1_hist_max": int(torch.bincount(top1, minlength=43).max().item()),
+        "top1_note": "random-init judge: Top-1 collapses to few classes; Top-1 parity with a "
+                     "non-degenerate judge is tests/test_models_gpu.py::"
+                     "test_inference_pipeline_fp32_end_to_end",
+        "roofline": roof, "bn_folded": os.environ.get("RR_FOLD_BN", "1") != "0",
     }))
 
 
