@@ -635,7 +635,10 @@ template <int BC, int BP, int NT = 2 * BP> struct HaloCfg {
 
 // DBGK (timing diagnostics only, RR_HALO_DBGK; results are wrong): bit0 no
 // barriers in the K loop, bit1 no fragment reads in the K loop (the first
-// stage's fragments reused) -- bounds on what the barriers / LDS reads cost
+// stage's fragments reused), bit2 no global loads in the K loop, bit4 no
+// next-chunk halo loads (weights still loaded) -- bounds on what each costs;
+// bit5 alone: the unsplit staging (every wave loads both operands), correct
+// results, for same-box A/B against the role split
 template <int BC, int W, int MODE, int BP, int NT = 2 * BP, int DBGK = 0>
 __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_kernel(IgemmArgs a) {
   using T = bf16_t;
@@ -787,12 +790,26 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
   // prologue: halo(0), weights(0) into LDS; weights(1) in flight
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
-  load_halo(0);
-  load_w(0, I0{});
-  load_w(nst > 1 ? 1 : 0, I1{});
-  store_halo(0);
-  store_w(I0{});
-  __syncthreads();
+  // RS (role split, HB = 2): waves 0-3 stage the weights, waves 4-7 the
+  // next chunk's halo.  vmcnt retires in issue order, so a wave that loaded
+  // the (HBM, long-latency) halo at tap 0 and then waited for its weights
+  // two stages later also waited for the halo: the weight prefetch, not the
+  // MFMAs, then set the pace (tools/halo_dbgk.py: without the halo loads the
+  // K loop ran 9-33% faster).  With separate roles no wave ever waits for a
+  // load of the other kind; every wave still runs the same MFMAs.
+  // weight/halo role split: measured 3 % faster at BC = 64, W = 32 / 16
+  // (r2h_dbgk.jsonl) but 5-7 % slower at BC = 128 (the four weight waves
+  // then carry 2 x 4 loads + LDS stores per stage and become the critical
+  // path); BC = 64 at W = 64 / 8 spills with it (128-VGPR cap)
+  constexpr bool RS = NT == 512 && DBGK == 0 && BC == 64 && (W == 16 || W == 32);
+  if constexpr (!RS) {
+    load_halo(0);
+    load_w(0, I0{});
+    load_w(nst > 1 ? 1 : 0, I1{});
+    store_halo(0);
+    store_w(I0{});
+    __syncthreads();
+  }
 
   // One (chunk, tap) stage s = 9 ch + TAP.  weights(k) live in register set
   // k & 1: stage s loads weights(s + 2) into set s & 1 (freed when weights(s)
@@ -803,8 +820,8 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
     constexpr int TAP = decltype(tapc)::value;
     constexpr int SET = decltype(setc)::value;        // == s & 1
     const int s = ch * 9 + TAP;
-    load_w(s + 2 < nst ? s + 2 : nst - 1, setc);
-    if constexpr (TAP == 0) {
+    if constexpr ((DBGK & 4) == 0) load_w(s + 2 < nst ? s + 2 : nst - 1, setc);
+    if constexpr (TAP == 0 && (DBGK & 20) == 0) {
       if constexpr (HB == 2) load_halo(ch + 1 < kch ? ch + 1 : ch);
       else if (kch > 1) load_halo(ch + 1 < kch ? ch + 1 : ch);   // uniform: kch per launch
     }
@@ -879,13 +896,176 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
   // diagnostics (RR_IGEMM_DBG, timing only -- results are wrong): bit1 runs
   // the K loop twice, bit0 skips the epilogue
   const int reps = (a.dbg & 2) ? 2 : 1;
-  for (int rep = 0; rep < reps; ++rep) {
-    int ch = 0;
-    for (; ch + 2 <= kch; ch += 2) {
-      chunk_even(ch);
-      chunk_odd(ch + 1);
+  if constexpr (!RS) {
+    for (int rep = 0; rep < reps; ++rep) {
+      int ch = 0;
+      for (; ch + 2 <= kch; ch += 2) {
+        chunk_even(ch);
+        chunk_odd(ch + 1);
+      }
+      if (ch < kch) chunk_even(ch);
     }
-    if (ch < kch) chunk_even(ch);
+  } else {
+    // weight waves: half of them at BC = 128 (2 x 4 pieces vs 13 halo
+    // pieces per thread), a quarter at BC = 64 (2 x 4 vs 8: the same
+    // registers as the unsplit kernel, which sits at its 128-VGPR cap)
+    constexpr int WT = (HB == 2 ? NWAVE / 2 : NWAVE / 4) * 64;   // weight threads
+    constexpr int HT = NT - WT;                                   // halo threads
+    constexpr int LH2 = (G::HMAX * 8 + HT - 1) / HT;              // halo pieces per halo thread
+    constexpr int LW2 = (WPIECES + WT - 1) / WT;                  // weight pieces per weight thread
+    constexpr int NU = LH2 > 2 * LW2 ? LH2 : 2 * LW2;
+    constexpr int NPI = LH2 > LW2 ? LH2 : LW2;
+    const bool wrole = tid < WT;                                  // wave-uniform
+    const int lt = wrole ? tid : tid - WT;
+    // per-piece source: halo role -> pixel (-1 = zero padding), weight role
+    // -> byte offset of the weight row (+ this thread's 16-B chunk)
+    int pidx[NPI];
+    V lr[NU];
+#pragma unroll
+    for (int i = 0; i < NPI; ++i) {
+      const int idx = lt + (wrole ? WT : HT) * i;
+      const int r = 8 * (idx >> 6) + (idx & 7);
+      int v = -1;
+      if (wrole) {
+        v = (int)(((long long)(c0 + r < a.cout ? c0 + r : 0) * a.K) * 2 + pj);
+      } else if (r < hrows) {
+        const int im = r / himg, rem = r - (r / himg) * himg;
+        const int hy = rem / (W + 2), hx = rem - (rem / (W + 2)) * (W + 2);
+        const int yy = y0 - 1 + hy, xx = hx - 1;
+        if (yy >= 0 && yy < a.h && xx >= 0 && xx < W) v = ((n0 + im) * a.h + yy) * W + xx;
+      }
+      pidx[i] = v;
+    }
+    auto rs_load_halo = [&](int ch) __attribute__((always_inline)) {
+      const int ci0 = ch * 64;
+      const bool first = ci0 < a.c1;
+      const char *base = first ? a.x1 : a.x2;
+      const long long cs = first ? a.c1 : a.c2;
+      const char *src0 = base + (long long)(first ? ci0 : ci0 - a.c1) * 2 + pj;
+#pragma unroll
+      for (int i = 0; i < LH2; ++i) {
+        const bool ok = pidx[i] >= 0;
+        V v = *reinterpret_cast<const V *>(src0 + (long long)(ok ? pidx[i] : 0) * cs * 2);
+        v.x = ok ? v.x : 0u; v.y = ok ? v.y : 0u; v.z = ok ? v.z : 0u; v.w = ok ? v.w : 0u;
+        lr[i] = v;
+      }
+    };
+    auto rs_store_halo = [&](int buf) __attribute__((always_inline)) {
+      char *d = hbuf + buf * G::HBYTES;
+#pragma unroll
+      for (int i = 0; i < LH2; ++i) {
+        const int idx = lt + HT * i;
+        const int r = 8 * (idx >> 6) + (idx & 7);
+        if (r < hrows) *reinterpret_cast<V *>(d + ((idx >> 3) & 7) * G::PLANE + r * 16) = lr[i];
+      }
+    };
+    auto rs_load_w = [&](int s, auto setc) __attribute__((always_inline)) {
+      constexpr int SET = decltype(setc)::value;
+      const int ch = s / 9, tap = s - (s / 9) * 9;
+      const long long off = ((long long)tap * a.cin + ch * 64) * 2;
+#pragma unroll
+      for (int i = 0; i < LW2; ++i) lr[SET * LW2 + i] = *reinterpret_cast<const V *>(a.wt + pidx[i] + off);
+    };
+    auto rs_store_w = [&](auto setc) __attribute__((always_inline)) {
+      constexpr int SET = decltype(setc)::value;
+      char *d = wbuf + SET * WBYTES;
+#pragma unroll
+      for (int i = 0; i < LW2; ++i) {
+        const int idx = lt + WT * i;
+        const int r = 8 * (idx >> 6) + (idx & 7);
+        if (WPIECES % WT == 0 || idx < WPIECES)
+          *reinterpret_cast<V *>(d + ((idx >> 3) & 7) * WPLANE + r * 16) = lr[SET * LW2 + i];
+      }
+    };
+    // one stage of one role (ROLE 0 weights, 1 halo); SET == s & 1
+    auto rs_stage = [&](int ch, auto tapc, auto setc, auto rolec) __attribute__((always_inline)) {
+      constexpr int TAP = decltype(tapc)::value;
+      constexpr int SET = decltype(setc)::value;
+      constexpr int ROLE = decltype(rolec)::value;
+      const int s = ch * 9 + TAP;
+      if constexpr (ROLE == 0) rs_load_w(s + 2 < nst ? s + 2 : nst - 1, setc);
+      if constexpr (ROLE == 1 && TAP == 0) {
+        if (HB == 2 || kch > 1) rs_load_halo(ch + 1 < kch ? ch + 1 : ch);   // uniform: kch per launch
+      }
+      const char *sA = wbuf + SET * WBYTES;
+      const char *sB = hbuf + (HB == 2 ? (ch & 1) * G::HBYTES : 0) + ((TAP / 3) * (W + 2) + TAP % 3) * 16;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 fa[MC], fb[MP];
+#pragma unroll
+        for (int mi = 0; mi < MC; ++mi)
+          fa[mi] = *reinterpret_cast<const bf16x8 *>(sA + abase[mi] + kk * 4 * WPLANE);
+#pragma unroll
+        for (int ni = 0; ni < MP; ++ni)
+          fb[ni] = *reinterpret_cast<const bf16x8 *>(sB + bbase[ni] + kk * 4 * G::PLANE);
+#pragma unroll
+        for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < MP; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi], fb[ni], acc[mi][ni], 0, 0, 0);
+      }
+      if constexpr (ROLE == 0) {
+        if (s + 1 < nst) rs_store_w(std::integral_constant<int, SET ^ 1>{});
+      }
+      if constexpr (TAP == 8) {
+        if (ch + 1 < kch) {
+          if constexpr (HB == 1) {
+            __syncthreads();                 // every wave is done reading this chunk's halo
+            if constexpr (ROLE == 1) rs_store_halo(0);
+          } else if constexpr (ROLE == 1) {
+            rs_store_halo((ch + 1) & 1);
+          }
+        }
+      }
+      __syncthreads();
+    };
+    auto rs_run = [&](auto rolec) __attribute__((always_inline)) {
+      constexpr int ROLE = decltype(rolec)::value;
+      using R = std::integral_constant<int, ROLE>;
+      auto even = [&](int ch) __attribute__((always_inline)) {
+        rs_stage(ch, std::integral_constant<int, 0>{}, I0{}, R{});
+        rs_stage(ch, std::integral_constant<int, 1>{}, I1{}, R{});
+        rs_stage(ch, std::integral_constant<int, 2>{}, I0{}, R{});
+        rs_stage(ch, std::integral_constant<int, 3>{}, I1{}, R{});
+        rs_stage(ch, std::integral_constant<int, 4>{}, I0{}, R{});
+        rs_stage(ch, std::integral_constant<int, 5>{}, I1{}, R{});
+        rs_stage(ch, std::integral_constant<int, 6>{}, I0{}, R{});
+        rs_stage(ch, std::integral_constant<int, 7>{}, I1{}, R{});
+        rs_stage(ch, std::integral_constant<int, 8>{}, I0{}, R{});
+      };
+      auto odd = [&](int ch) __attribute__((always_inline)) {
+        rs_stage(ch, std::integral_constant<int, 0>{}, I1{}, R{});
+        rs_stage(ch, std::integral_constant<int, 1>{}, I0{}, R{});
+        rs_stage(ch, std::integral_constant<int, 2>{}, I1{}, R{});
+        rs_stage(ch, std::integral_constant<int, 3>{}, I0{}, R{});
+        rs_stage(ch, std::integral_constant<int, 4>{}, I1{}, R{});
+        rs_stage(ch, std::integral_constant<int, 5>{}, I0{}, R{});
+        rs_stage(ch, std::integral_constant<int, 6>{}, I1{}, R{});
+        rs_stage(ch, std::integral_constant<int, 7>{}, I0{}, R{});
+        rs_stage(ch, std::integral_constant<int, 8>{}, I1{}, R{});
+      };
+      // prologue: halo(0) (halo role), weights(0) into LDS and weights(1) in
+      // flight (weight role)
+      if constexpr (ROLE == 1) {
+        rs_load_halo(0);
+        rs_store_halo(0);
+      } else {
+        rs_load_w(0, I0{});
+        rs_load_w(nst > 1 ? 1 : 0, I1{});
+        rs_store_w(I0{});
+      }
+      __syncthreads();
+      for (int rep = 0; rep < reps; ++rep) {
+        int ch = 0;
+        for (; ch + 2 <= kch; ch += 2) {
+          even(ch);
+          odd(ch + 1);
+        }
+        if (ch < kch) even(ch);
+      }
+    };
+    if (wrole) rs_run(I0{});
+    else rs_run(I1{});
   }
   if (a.dbg & 1) {
     float t = 0.f;
@@ -997,9 +1177,12 @@ bool launch_halo_dbgk(const rr_igemm_desc *d, IgemmArgs &a, const dim3 &grid, co
   const char *e = getenv("RR_HALO_DBGK");
   const int k = e ? atoi(e) : 0;
   if (!k || d->w != W) return false;
-  if (k == 1) hipLaunchKernelGGL((igemm3_halo_kernel<BC, W, RR_CONV3X3, BP, NT, 1>), grid, block, 0, st, a);
-  else if (k == 2) hipLaunchKernelGGL((igemm3_halo_kernel<BC, W, RR_CONV3X3, BP, NT, 2>), grid, block, 0, st, a);
-  else hipLaunchKernelGGL((igemm3_halo_kernel<BC, W, RR_CONV3X3, BP, NT, 3>), grid, block, 0, st, a);
+  switch (k) {
+#define DK(v) case v: hipLaunchKernelGGL((igemm3_halo_kernel<BC, W, RR_CONV3X3, BP, NT, v>), grid, block, 0, st, a); break;
+    DK(1) DK(2) DK(3) DK(4) DK(16) DK(32)
+#undef DK
+    default: return false;
+  }
   return true;
 }
 
@@ -1010,7 +1193,8 @@ int launch_halo(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   if (nblk > 0x7fffffffLL) return RR_EUNSUPPORTED;
   const dim3 grid((unsigned)nblk), block(NT);
   if constexpr (BC == 128 && BP == 256 && NT == 512) {
-    if (launch_halo_dbgk<BC, 8, BP, NT>(d, a, grid, block, st) || launch_halo_dbgk<BC, 16, BP, NT>(d, a, grid, block, st)) {
+    if (launch_halo_dbgk<BC, 8, BP, NT>(d, a, grid, block, st) || launch_halo_dbgk<BC, 16, BP, NT>(d, a, grid, block, st) ||
+        launch_halo_dbgk<BC, 32, BP, NT>(d, a, grid, block, st)) {
       RR_CHECK_LAUNCH();
       return RR_OK;
     }
