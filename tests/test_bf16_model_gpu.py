@@ -6,7 +6,7 @@ oracle in fp64 (the 'true' values) and fp32 (the reference's own precision).
 
 Two batches:
   * the golden B=2 64x64 fixture (reference-generated, tests/golden), and
-  * B=16 at 64x64, large enough that the benched kernels own their layers:
+  * B=64 at 64x64, large enough that the benched kernels own their layers:
     the row-streaming conv (stream3, 64 -> 64 at 64x64), the row-streaming
     weight grad (swgrad), the LDS-halo convs at 32/16/8 and the halo weight
     grads -- asserted from the library's own kernel choice
