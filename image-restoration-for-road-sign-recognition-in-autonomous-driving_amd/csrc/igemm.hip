@@ -638,7 +638,9 @@ template <int BC, int BP, int NT = 2 * BP> struct HaloCfg {
 // stage's fragments reused), bit2 no global loads in the K loop, bit4 no
 // next-chunk halo loads (weights still loaded) -- bounds on what each costs;
 // bit5 alone: the unsplit staging (every wave loads both operands), correct
-// results, for same-box A/B against the role split
+// results, for same-box A/B against the role split; bit6 alone: the next
+// chunk's halo issued all at tap 0 (correct results; A/B of the spread);
+// bit7 alone: weights 3 stages ahead at BC = 128 (correct results)
 template <int BC, int W, int MODE, int BP, int NT = 2 * BP, int DBGK = 0>
 __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_kernel(IgemmArgs a) {
   using T = bf16_t;
@@ -726,7 +728,11 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
   const int nst = kch * 9;
   typedef uint4 V;
   V hreg[G::LH];
-  V wr0[LW], wr1[LW];                    // weight register sets (stage parity)
+  // weights prefetched 2 stages ahead (register set = stage parity).  DBGK
+  // bit7 (BC = 128): 3 ahead, register set k % 3 holding W(k) (9 taps per
+  // chunk, so the set is TAP % 3) -- measured no faster (r2i_dbgk.jsonl)
+  constexpr bool W3 = HB == 2 && (DBGK & 128) != 0;
+  V wr0[LW], wr1[LW], wr2[W3 ? LW : 1];
 
   auto load_halo = [&](int ch) __attribute__((always_inline)) {
     const int ci0 = ch * 64;
@@ -738,6 +744,26 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
     for (int i = 0; i < G::LH; ++i) {
       // padding pieces load pixel 0 (valid, L2-hot) and are zeroed by a
       // select: no divergent branch, no pointer merge across address spaces
+      const bool ok = hpix[i] >= 0;
+      V v = *reinterpret_cast<const V *>(src0 + (long long)(ok ? hpix[i] : 0) * cs * 2);
+      v.x = ok ? v.x : 0u; v.y = ok ? v.y : 0u; v.z = ok ? v.z : 0u; v.w = ok ? v.w : 0u;
+      hreg[i] = v;
+    }
+  };
+  // the next chunk's halo, spread over taps 0-6: piece i is issued at tap
+  // 7 i / LH.  Issued all at tap 0 by every workgroup at once it was a
+  // chip-wide burst (256 x ~100 KB) that the in-order vmcnt wait for the
+  // weights two stages later then sat behind
+  auto load_halo_part = [&](int ch, auto tapc) __attribute__((always_inline)) {
+    constexpr int TAP = decltype(tapc)::value;
+    const int ci0 = ch * 64;
+    const bool first = ci0 < a.c1;
+    const char *base = first ? a.x1 : a.x2;
+    const long long cs = first ? a.c1 : a.c2;
+    const char *src0 = base + (long long)(first ? ci0 : ci0 - a.c1) * 2 + pj;
+#pragma unroll
+    for (int i = 0; i < G::LH; ++i) {
+      if ((i * 7) / G::LH != TAP) continue;
       const bool ok = hpix[i] >= 0;
       V v = *reinterpret_cast<const V *>(src0 + (long long)(ok ? hpix[i] : 0) * cs * 2);
       v.x = ok ? v.x : 0u; v.y = ok ? v.y : 0u; v.z = ok ? v.z : 0u; v.w = ok ? v.w : 0u;
@@ -764,18 +790,23 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
         const bool ok = c0 + 8 * (idx >> 6) + (idx & 7) < a.cout;
         v.x = ok ? v.x : 0u; v.y = ok ? v.y : 0u; v.z = ok ? v.z : 0u; v.w = ok ? v.w : 0u;
       }
-      if constexpr (decltype(setc)::value == 0) wr0[i] = v; else wr1[i] = v;
+      if constexpr (decltype(setc)::value == 0) wr0[i] = v;
+      else if constexpr (decltype(setc)::value == 1) wr1[i] = v;
+      else wr2[i] = v;
     }
   };
-  auto store_w = [&](auto setc) __attribute__((always_inline)) {
+  // LDS weight buffer SET (stage parity) <- register set REG
+  auto store_w = [&](auto setc, auto regc) __attribute__((always_inline)) {
     constexpr int SET = decltype(setc)::value;
+    constexpr int REG = decltype(regc)::value;
     char *d = wbuf + SET * WBYTES;
 #pragma unroll
     for (int i = 0; i < LW; ++i) {
       const int idx = tid + NT * i;
       const int r = 8 * (idx >> 6) + (idx & 7);
       if (WPIECES % NT == 0 || idx < WPIECES)
-        *reinterpret_cast<V *>(d + ((idx >> 3) & 7) * WPLANE + r * 16) = SET == 0 ? wr0[i] : wr1[i];
+        *reinterpret_cast<V *>(d + ((idx >> 3) & 7) * WPLANE + r * 16) =
+            REG == 0 ? wr0[i] : (REG == 1 ? wr1[i] : wr2[i < (W3 ? LW : 1) ? i : 0]);
     }
   };
 
@@ -790,6 +821,7 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
   // prologue: halo(0), weights(0) into LDS; weights(1) in flight
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
   // RS (role split, HB = 2): waves 0-3 stage the weights, waves 4-7 the
   // next chunk's halo.  vmcnt retires in issue order, so a wave that loaded
   // the (HBM, long-latency) halo at tap 0 and then waited for its weights
@@ -806,8 +838,9 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
     load_halo(0);
     load_w(0, I0{});
     load_w(nst > 1 ? 1 : 0, I1{});
+    if constexpr (W3) load_w(nst > 2 ? 2 : nst - 1, I2{});
     store_halo(0);
-    store_w(I0{});
+    store_w(I0{}, I0{});
     __syncthreads();
   }
 
@@ -820,8 +853,13 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
     constexpr int TAP = decltype(tapc)::value;
     constexpr int SET = decltype(setc)::value;        // == s & 1
     const int s = ch * 9 + TAP;
-    if constexpr ((DBGK & 4) == 0) load_w(s + 2 < nst ? s + 2 : nst - 1, setc);
-    if constexpr (TAP == 0 && (DBGK & 20) == 0) {
+    if constexpr ((DBGK & 4) == 0) {
+      if constexpr (W3) load_w(s + 3 < nst ? s + 3 : nst - 1, std::integral_constant<int, TAP % 3>{});
+      else load_w(s + 2 < nst ? s + 2 : nst - 1, setc);
+    }
+    if constexpr ((DBGK & 84) == 0 && HB == 2) {       // (BC = 64 at its VGPR cap: spills)
+      if constexpr (TAP < 7) load_halo_part(ch + 1 < kch ? ch + 1 : ch, tapc);
+    } else if constexpr (TAP == 0 && (DBGK & 20) == 0) {
       if constexpr (HB == 2) load_halo(ch + 1 < kch ? ch + 1 : ch);
       else if (kch > 1) load_halo(ch + 1 < kch ? ch + 1 : ch);   // uniform: kch per launch
     }
@@ -849,7 +887,8 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
         for (int ni = 0; ni < MP; ++ni)
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi], fb[ni], acc[mi][ni], 0, 0, 0);
     }
-    if (s + 1 < nst) store_w(std::integral_constant<int, SET ^ 1>{});
+    if (s + 1 < nst)
+      store_w(std::integral_constant<int, SET ^ 1>{}, std::integral_constant<int, W3 ? (TAP + 1) % 3 : (SET ^ 1)>{});
     if constexpr (TAP == 8) {
       if (ch + 1 < kch) {
         if constexpr (HB == 1) {
@@ -1179,7 +1218,7 @@ bool launch_halo_dbgk(const rr_igemm_desc *d, IgemmArgs &a, const dim3 &grid, co
   if (!k || d->w != W) return false;
   switch (k) {
 #define DK(v) case v: hipLaunchKernelGGL((igemm3_halo_kernel<BC, W, RR_CONV3X3, BP, NT, v>), grid, block, 0, st, a); break;
-    DK(1) DK(2) DK(3) DK(4) DK(16) DK(32)
+    DK(1) DK(2) DK(3) DK(4) DK(16) DK(32) DK(64) DK(128) DK(192)
 #undef DK
     default: return false;
   }

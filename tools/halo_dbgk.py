@@ -1,7 +1,10 @@
 """K-loop bounds of the halo igemm (timing only): the loop with the epilogue
 skipped (RR_IGEMM_DBG=1) as built, without its barriers (RR_HALO_DBGK=1),
 without its LDS fragment reads (2), without both (3); full time of the
-unsplit staging (RR_HALO_DBGK=32) beside the weight/halo role split."""
+unsplit staging (RR_HALO_DBGK=32) beside the weight/halo role split, and
+of the next-chunk halo issued all at tap 0 (64) beside its spread over taps,
+and weights 3 stages ahead (128) beside 2 (BC = 128 only; at BC = 64 these
+select the same unsplit kernel, so their spread there is the noise)."""
 import json, os, sys
 R_ = os.path.join(os.path.dirname(__file__), "..")
 sys.path.insert(0, os.path.join(R_, "image-restoration-for-road-sign-recognition-in-autonomous-driving_amd"))
@@ -11,8 +14,8 @@ from roadrestore._lib import RR_CONV3X3
 
 dev = torch.device("cuda:0")
 B = 512
-LAYERS = [("res1.c2", 64, 64, 0, 64), ("res2.c1", 32, 64, 0, 128), ("res2.c2", 32, 128, 0, 128), ("res3.c2", 16, 256, 0, 256),
-          ("bott.512", 8, 512, 0, 512)]
+LAYERS = [("res2.c1", 32, 64, 0, 128), ("res2.c2", 32, 128, 0, 128), ("res3.c2", 16, 256, 0, 256),
+          ("bott.512", 8, 512, 0, 512), ("res3.c1", 16, 128, 0, 256), ("bott.c1", 8, 256, 0, 512)]
 
 
 def timeit(fn, reps=10):
@@ -36,8 +39,9 @@ for name, H, c1, c2, co in LAYERS:
     r = {"layer": name, "kernel": ops.igemm_kernel_name(ops.IgemmDesc(ops.RR_BF16, RR_CONV3X3, B, H, H, c1, c2, co, 0, 0, 0, 0, 0, 1, 0))}
     os.environ["RR_IGEMM_DBG"] = "0"
     r["full_ms"] = round(timeit(lambda: ops.igemm(RR_CONV3X3, x1, None, B, H, H, wf, co, stats=True)), 4)
-    os.environ["RR_HALO_DBGK"] = "32"
-    r["full_unsplit_ms"] = round(timeit(lambda: ops.igemm(RR_CONV3X3, x1, None, B, H, H, wf, co, stats=True)), 4)
+    for k, tag in ((32, "unsplit"), (64, "unsliced"), (128, "w3ahead")):
+        os.environ["RR_HALO_DBGK"] = str(k)
+        r[f"full_{tag}_ms"] = round(timeit(lambda: ops.igemm(RR_CONV3X3, x1, None, B, H, H, wf, co, stats=True)), 4)
     for k in (0,):
         os.environ["RR_IGEMM_DBG"] = "1"
         os.environ["RR_HALO_DBGK"] = str(k)
