@@ -270,9 +270,15 @@ def main():
     to_tensor = imgproc.Compose([imgproc.Resize((H, H)), imgproc.ToTensor()])
     w_perc = 0.0 if a.no_perceptual else 0.1
 
+    # the target's perceptual features F(clean) do not depend on the
+    # distortion or the restorer: started on a side stream, they overlap both
+    prefetch = w_perc != 0.0 and os.environ.get("RR_PERC_PREFETCH", "1") != "0"
+
     def step():
-        bad = to_tensor(distort(clean_u8))
         clean = to_tensor(clean_u8)
+        if prefetch:
+            clean = perc.prefetch_target(clean)
+        bad = to_tensor(distort(clean_u8))
         opt.zero_grad(set_to_none=True)
         out = model(bad)
         loss = rr.unified_loss(out, clean, perc, w_perc, grad_scale=gscale)

@@ -46,9 +46,14 @@ class WeightCache:
     Conv packs are batched: the convs a forward requests are recorded (the
     plan), and ``begin()`` at the start of every later forward re-packs all
     of them in ONE launch (ops.PackBatch) when any is stale or a graph is
-    being captured; the per-layer ``conv()`` calls then hit those packs."""
+    being captured; the per-layer ``conv()`` calls then hit those packs.
 
-    def __init__(self):
+    ``static=True`` (the frozen perceptual VGG, 14:192-193): a capture uses the
+    packs made by the eager forwards before it instead of re-packing in every
+    replay -- weights changed after the capture need a new capture."""
+
+    def __init__(self, static=False):
+        self.static = static
         self._c = {}
         self._plan = {}          # id(w) -> [w, dtype, dgrad], first-request order
         self._batch = None
@@ -64,7 +69,7 @@ class WeightCache:
         cap = torch.cuda.is_current_stream_capturing()
         key = (id(w), dtype, kind)
         ver = self._ver(w, also)
-        e = None if cap else self._c.get(key)
+        e = None if cap and not self.static else self._c.get(key)
         if e is not None and e[0] == ver:
             return e[1]
         v = fn()
@@ -102,6 +107,8 @@ class WeightCache:
         ent = list(self._plan.values())
         keys = [(id(w), dt, "conv+d" if dg else "conv") for w, dt, dg in ent]
         vers = [self._ver(w) for w, _, _ in ent]
+        if cap and self.static and all(self._c.get(k, (None,))[0] == v for k, v in zip(keys, vers)):
+            return                                   # conv() hits the pre-capture packs
         ok = self._batch is not None and self._batch.valid() and \
             self._batch.entries == [tuple(e) for e in ent]
         if not ok and not cap and all(w.is_contiguous() for w, _, _ in ent) and \

@@ -193,11 +193,13 @@ def unified_loss(out: Tensor, clean: Tensor, perceptual: int, w: float,
     loss = ops.loss_fwd(ops.L1, out, clean)
     st = None
     if w != 0.0:
+        fy = perc._target_features(clean)
         fx, S = engine.vgg_features_forward(perc.slice, out, perc._wc, perc.compute_dtype,
                                             need_bwd=True)
-        fy, _ = engine.vgg_features_forward(perc.slice, clean, perc._wc, perc.compute_dtype)
         ops.loss_fwd(ops.MSE, fx, fy, scale=w, out=loss, accumulate=True)
         st = (S, fx, fy)
+    else:
+        perc._join()                 # a prefetched target is not needed, but joins the stream
     return loss, _stash(st)
 
 

@@ -347,11 +347,15 @@ def test_multi_step_training_matches_oracle(dev):
     assert (out - ref).abs().mean().item() <= 1e-3
 
 
-def test_hip_graph_training_step_matches_eager(dev):
+@pytest.mark.parametrize("prefetch", [False, True])
+def test_hip_graph_training_step_matches_eager(dev, prefetch):
     """A whole ResUNet unified training step (fwd, L1 + perceptual, bwd,
     capturable AdamW, weight re-packs) captured in a HIP graph and replayed
     must do exactly what the eager steps do (same kernels, device-side step
-    count for the bias correction)."""
+    count for the bias correction).  ``prefetch``: the captured step starts
+    F(clean) on the perceptual loss's side stream first (bench.py's schedule;
+    the frozen VGG packs come from before the capture) -- same results as the
+    eager steps without it."""
     import roadrestore as rr
     from roadrestore.optim import flatten_parameters
     torch.manual_seed(3)
@@ -371,8 +375,9 @@ def test_hip_graph_training_step_matches_eager(dev):
         opt = rr.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-4, capturable=capturable)
 
         def step():
+            tgt = perc.prefetch_target(clean) if capturable and prefetch else clean
             opt.zero_grad(set_to_none=True)
-            loss = rr.unified_loss(m(bad), clean, perc, 0.1)
+            loss = rr.unified_loss(m(bad), tgt, perc, 0.1)
             loss.backward()
             opt.step()
             return loss
