@@ -433,6 +433,18 @@ __global__ void distort_pre_kernel(DistCfg a) {
 
 // stage 2 (blurred images only): filter2D of tmp, then mode 0: the u8 result
 // ((t / 255) * 255 truncated), mode 1: fog + noise on it
+__device__ __forceinline__ void blur_store(const DistCfg &a, const rr_distort_param &p, long long q,
+                                           const float *s) {
+#pragma clang fp contract(off)
+  for (int c = 0; c < a.c; ++c) {
+    float r = rintf(s[c]);                                   // saturate_cast<uchar>: cvRound
+    r = r < 0.f ? 0.f : (r > 255.f ? 255.f : r);
+    const long long e = q * a.c + c;
+    const float t = (float)(int)r / 255.0f;
+    a.out[e] = a.mode == 0 ? trunc_u8f(t * 255.f) : fog_noise(a, p, t, e);
+  }
+}
+
 __global__ void distort_blur_kernel(DistCfg a) {
 #pragma clang fp contract(off)
   const long long hw = (long long)a.h * a.w, total = hw * a.n;
@@ -456,14 +468,62 @@ __global__ void distort_blur_kernel(DistCfg a) {
         for (int c = 0; c < a.c; ++c) s[c] = s[c] + kv * (float)px[c];
       }
     }
-    for (int c = 0; c < a.c; ++c) {
-      float r = rintf(s[c]);                                 // saturate_cast<uchar>: cvRound
-      r = r < 0.f ? 0.f : (r > 255.f ? 255.f : r);
-      const long long e = q * a.c + c;
-      const float t = (float)(int)r / 255.0f;
-      a.out[e] = a.mode == 0 ? trunc_u8f(t * 255.f) : fog_noise(a, p, t, e);
-    }
+    blur_store(a, p, q, s);
   }
+}
+
+// the same with the image's nonzero taps compacted into LDS first (row-major,
+// so the sums run in the same order: bit-identical) -- for h * w a multiple
+// of 256, where a workgroup's 256 pixels always belong to one image: the
+// per-pixel loop then visits the ~k..2k nonzero taps of the rotated line
+// kernel instead of testing all k * k, with no per-tap global loads
+__global__ __launch_bounds__(256) void distort_blur_tiled_kernel(DistCfg a) {
+#pragma clang fp contract(off)
+  __shared__ float tv[RR_DISTORT_KMAX * RR_DISTORT_KMAX];
+  __shared__ int ti[RR_DISTORT_KMAX * RR_DISTORT_KMAX];
+  __shared__ int wcount[4];
+  const long long hw = (long long)a.h * a.w, total = hw * a.n;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  for (long long q0 = blockIdx.x * 256LL; q0 < total; q0 += (long long)gridDim.x * 256) {
+    const int img = (int)(q0 / hw);                          // uniform: 256 | hw
+    const rr_distort_param p = a.prm[img];
+    if (!(p.flags & RR_DISTORT_BLUR)) continue;              // uniform
+    const int k = p.ksize, anc = k / 2;
+    const float *kt = a.taps + (long long)(a.tap_idx ? a.tap_idx[img] : img) * RR_DISTORT_KMAX * RR_DISTORT_KMAX;
+    const int i = t / (k > 0 ? k : 1), j = t - i * (k > 0 ? k : 1);
+    const float kv = t < k * k ? kt[i * RR_DISTORT_KMAX + j] : 0.f;
+    const bool nz = kv != 0.f;                               // cv2 drops zero taps
+    const unsigned long long m = __ballot(nz);
+    const int pos = __popcll(m & ((1ull << lane) - 1ull));
+    __syncthreads();                                         // the previous image's list is read
+    if (lane == 0) wcount[wv] = __popcll(m);
+    __syncthreads();
+    int off = 0;
+    for (int u = 0; u < wv; ++u) off += wcount[u];
+    if (nz) { tv[off + pos] = kv; ti[off + pos] = (i << 8) | j; }
+    const int nt = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+    __syncthreads();
+    const long long q = q0 + t;
+    const int rem = (int)(q - (long long)img * hw), y = rem / a.w, x = rem % a.w;
+    const uint8_t *src = a.tmp + (long long)img * hw * a.c;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < nt; ++u) {
+      const int ij = ti[u];
+      const float w = tv[u];
+      const int yy = reflect101(y + (ij >> 8) - anc, a.h), xx = reflect101(x + (ij & 255) - anc, a.w);
+      const uint8_t *px = src + ((long long)yy * a.w + xx) * a.c;
+      for (int c = 0; c < a.c; ++c) s[c] = s[c] + w * (float)px[c];
+    }
+    blur_store(a, p, q, s);
+  }
+}
+
+static void launch_blur(const DistCfg &a, long long tp, hipStream_t st) {
+  const char *e = getenv("RR_BLUR_TILED");
+  if (((long long)a.h * a.w) % 256 == 0 && a.c <= 4 && !(e && !atoi(e)))
+    hipLaunchKernelGGL(distort_blur_tiled_kernel, dim3(rr_grid_cap((tp + 255) / 256, 8192)), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(distort_blur_kernel, dim3(rr_grid_cap((tp + 255) / 256, 8192)), dim3(256), 0, st, a);
 }
 
 // ---------------------------------------------------- on-device draws ----
@@ -563,7 +623,7 @@ extern "C" int rr_distort_u8(int n, int h, int w, int c, int mode, const uint8_t
   const long long te = (long long)n * h * w * c, tp = (long long)n * h * w;
   hipLaunchKernelGGL(distort_pre_kernel, dim3(rr_grid_cap((te + 255) / 256, 8192)), dim3(256), 0, st, a);
   RR_CHECK_LAUNCH();
-  hipLaunchKernelGGL(distort_blur_kernel, dim3(rr_grid_cap((tp + 255) / 256, 8192)), dim3(256), 0, st, a);
+  launch_blur(a, tp, st);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }
@@ -657,7 +717,7 @@ extern "C" int rr_distort_random_u8(int n, int h, int w, int c, const uint8_t *i
   const long long te = (long long)n * h * w * c, tp = (long long)n * h * w;
   hipLaunchKernelGGL(distort_pre_kernel, dim3(rr_grid_cap((te + 255) / 256, 8192)), dim3(256), 0, st, a);
   RR_CHECK_LAUNCH();
-  hipLaunchKernelGGL(distort_blur_kernel, dim3(rr_grid_cap((tp + 255) / 256, 8192)), dim3(256), 0, st, a);
+  launch_blur(a, tp, st);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

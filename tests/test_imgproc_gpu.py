@@ -205,6 +205,30 @@ def test_random_distortion_draws_on_device(dev):
         assert torch.equal(y, want)
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+def test_blur_tiled_equals_untiled(dev, mode, monkeypatch):
+    """The LDS-compacted blur (h * w a multiple of 256: nonzero taps listed
+    once per workgroup) is byte-identical to the per-pixel tap scan
+    (RR_BLUR_TILED=0) over every (degree, angle) the draws can produce."""
+    from roadrestore import imgproc, ops
+    from roadrestore._lib import RR_DISTORT_BLUR
+    n = 11 * 24
+    x = torch.from_numpy(_batch(n, 64, 64, seed=31)).to(dev)
+    rd = imgproc.RandomDistortion(dev, seed=77)
+    rd(x)
+    params, _, seed = rd.last_draws()
+    table = imgproc.motion_blur_table(dev).view(-1, 15, 15)
+    idx = torch.tensor([(i % 11) * 361 + (i * 37) % 361 for i in range(n)], device=dev)
+    for i, p in enumerate(params):
+        p.flags |= RR_DISTORT_BLUR
+        p.ksize = 5 + i % 11
+    outs = []
+    for tiled in ("1", "0"):
+        monkeypatch.setenv("RR_BLUR_TILED", tiled)
+        outs.append(ops.distort_u8(x, params, table[idx], mode=mode, seed=seed))
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_random_distortion_in_hip_graph(dev):
     """Captured once, every replay re-draws (the counter is device state)."""
     from roadrestore import imgproc
