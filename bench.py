@@ -272,11 +272,13 @@ def main():
 
     # the target's perceptual features F(clean) do not depend on the
     # distortion or the restorer: started on a side stream, they overlap both
-    prefetch = w_perc != 0.0 and os.environ.get("RR_PERC_PREFETCH", "1") != "0"
+    # (the kernel probe turns it off: per-kernel durations are taken without
+    # a concurrent kernel sharing the chip)
+    prefetch = [w_perc != 0.0 and os.environ.get("RR_PERC_PREFETCH", "1") != "0"]
 
     def step():
         clean = to_tensor(clean_u8)
-        if prefetch:
+        if prefetch[0]:
             clean = perc.prefetch_target(clean)
         bad = to_tensor(distort(clean_u8))
         opt.zero_grad(set_to_none=True)
@@ -357,6 +359,7 @@ def main():
         # (every rank runs these steps: the backward's all-reduces pair up)
         probe = KernelProbe()
         ops.PROBE = probe
+        prefetch[0] = False
         for _ in range(a.probe_steps):
             step()
         ops.PROBE = None

@@ -7,6 +7,9 @@ set -e
 TAG=${1:-r1}
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/prof_$TAG
+# per-kernel durations without the perceptual-target prefetch running
+# concurrently on its side stream (bench.py's probe does the same)
+export RR_PERC_PREFETCH=0
 rm -rf $OUT && mkdir -p $OUT
 ARGS="--steps 5 --warmup 3 --repeats 1 --graph 0 --no-cpu-baseline --no-probe"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt -- python bench.py $ARGS > $OUT/kt.log 2>&1
