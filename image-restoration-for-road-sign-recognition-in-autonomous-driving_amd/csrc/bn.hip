@@ -21,13 +21,46 @@ namespace {
 // [rows][C][2] (no column-reduce launch): one workgroup per channel, 256 row
 // lanes in a fixed order + an LDS tree, then the same per-channel math as
 // bn_finalize_kernel
+struct BnFin {
+  int C, rows;
+  double count;
+  const float *part, *bias, *gamma, *beta;
+  float *rmean, *rvar;
+  float momentum, eps;
+  float *scale, *shift, *smean, *sinv;
+  int64_t *nbt;
+};
+
+__device__ __forceinline__ void bn_finalize_direct_channel(const BnFin &a, int c);
+
 __global__ __launch_bounds__(256) void bn_finalize_direct_kernel(
     int C, int rows, double count, const float *__restrict__ part, const float *bias,
     const float *gamma, const float *beta, float *rmean, float *rvar, float momentum, float eps,
     float *scale, float *shift, float *smean, float *sinv, int64_t *nbt) {
+  const BnFin a{C, rows, count, part, bias, gamma, beta, rmean, rvar, momentum, eps, scale, shift,
+                smean, sinv, nbt};
+  bn_finalize_direct_channel(a, blockIdx.x);
+}
+
+// two BatchNorms finalized by one launch (the residual tail's BN and the
+// shortcut BN, whose statistics are ready together): workgroups [0, A.C)
+// take A's channels, the rest B's
+__global__ __launch_bounds__(256) void bn_finalize_direct2_kernel(BnFin A, BnFin B) {
+  if ((int)blockIdx.x < A.C) bn_finalize_direct_channel(A, blockIdx.x);
+  else bn_finalize_direct_channel(B, blockIdx.x - A.C);
+}
+
+__device__ __forceinline__ void bn_finalize_direct_channel(const BnFin &a, int c) {
+  const int C = a.C, rows = a.rows;
+  const double count = a.count;
+  const float *__restrict__ part = a.part;
+  const float *bias = a.bias, *gamma = a.gamma, *beta = a.beta;
+  float *rmean = a.rmean, *rvar = a.rvar, *scale = a.scale, *shift = a.shift, *smean = a.smean,
+        *sinv = a.sinv;
+  const float momentum = a.momentum, eps = a.eps;
   __shared__ double red[2][256];
-  const int c = blockIdx.x, t = threadIdx.x;
-  if (nbt && c == 0 && t == 0) nbt[0] += 1;
+  const int t = threadIdx.x;
+  if (a.nbt && c == 0 && t == 0) a.nbt[0] += 1;
   double s[2] = {0.0, 0.0};
   rr_fixed_sum<2>(part + ((long long)t * C + c) * 2, 256LL * C * 2, rr_trips(t, rows, 256), s);
   double s1 = s[0], s2 = s[1];
@@ -710,6 +743,26 @@ extern "C" int rr_bn_finalize(int C, int blocks, long long count, const float *p
                      C, chunks, (double)count, (const double *)ws, bias, gamma, beta, running_mean,
                      running_var, momentum, eps, scale, shift, save_mean, save_invstd,
                      num_batches_tracked);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+// two BatchNorms in one launch (direct path only: both with <= 8192 partial
+// rows; else RR_EUNSUPPORTED and the caller finalizes them separately)
+extern "C" int rr_bn_finalize_pair(const rr_bn_finalize_desc *a, const rr_bn_finalize_desc *b,
+                                   rr_stream stream) {
+  if (!a || !b) return RR_EINVAL;
+  for (const rr_bn_finalize_desc *d : {a, b})
+    if (d->C <= 0 || d->blocks <= 0 || d->count <= 0 || !d->part || !d->scale || !d->shift)
+      return RR_EINVAL;
+  if (a->blocks > RR_BN_DIRECT_ROWS || b->blocks > RR_BN_DIRECT_ROWS) return RR_EUNSUPPORTED;
+  auto fin = [](const rr_bn_finalize_desc *d) {
+    return BnFin{d->C, d->blocks, (double)d->count, d->part, d->bias, d->gamma, d->beta,
+                 d->running_mean, d->running_var, d->momentum, d->eps, d->scale, d->shift,
+                 d->save_mean, d->save_invstd, d->num_batches_tracked};
+  };
+  hipLaunchKernelGGL(bn_finalize_direct2_kernel, dim3(a->C + b->C), dim3(256), 0, (hipStream_t)stream,
+                     fin(a), fin(b));
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

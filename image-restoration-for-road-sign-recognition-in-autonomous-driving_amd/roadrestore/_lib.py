@@ -18,6 +18,7 @@ RR_CONV3X3, RR_CONV1X1, RR_CONVT_UP, RR_CONVT_DOWN = 0, 1, 2, 3
 RR_ACT_NONE, RR_ACT_RELU = 0, 1
 
 _STATUS = {0: "ok", -1: "EINVAL", -2: "EUNSUPPORTED", -3: "ELAUNCH", -4: "EWORKSPACE"}
+RR_EUNSUPPORTED = -2
 
 
 class IgemmDesc(C.Structure):
@@ -40,6 +41,15 @@ class BnBwdDesc(C.Structure):
 class DistortParam(C.Structure):
     _fields_ = [("sigma", C.c_double), ("fog_mul", C.c_float), ("fog_add", C.c_float),
                 ("flags", C.c_int32), ("ksize", C.c_int32)]
+
+
+class BnFinalizeDesc(C.Structure):          # mirrors rr_bn_finalize_desc
+    _fields_ = [("C", C.c_int32), ("blocks", C.c_int32), ("count", C.c_int64),
+                ("part", C.c_void_p), ("bias", C.c_void_p), ("gamma", C.c_void_p),
+                ("beta", C.c_void_p), ("running_mean", C.c_void_p), ("running_var", C.c_void_p),
+                ("momentum", C.c_float), ("eps", C.c_float), ("scale", C.c_void_p),
+                ("shift", C.c_void_p), ("save_mean", C.c_void_p), ("save_invstd", C.c_void_p),
+                ("num_batches_tracked", C.c_void_p)]
 
 
 class PackJob(C.Structure):
@@ -74,6 +84,7 @@ _SIGS = {
     "rr_bn_finalize": (I_, [I_, I_, L_, P_, P_, P_, P_, P_, P_, F_, F_, P_, P_, P_, P_, P_, P_,
                             S_, P_]),
     "rr_bn_finalize_workspace": (S_, [I_, I_]),
+    "rr_bn_finalize_pair": (I_, [C.POINTER(BnFinalizeDesc), C.POINTER(BnFinalizeDesc), P_]),
     "rr_bn_eval_affine": (I_, [I_, P_, P_, P_, P_, F_, P_, P_, P_]),
     "rr_affine_act": (I_, [I_, L_, I_, P_, P_, P_, P_, P_, P_, P_, I_, P_, P_]),
     "rr_affine_act_pool": (I_, [I_, I_, I_, I_, I_, P_, P_, P_, P_, P_, P_, I_, P_, P_, P_, P_]),

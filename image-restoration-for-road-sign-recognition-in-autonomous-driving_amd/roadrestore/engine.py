@@ -339,6 +339,16 @@ def _bn_affine(bn, st, bias, count, training, out=None):
     return s, b, None, None
 
 
+# A/B switch: the tail BN and the shortcut BN finalized by one launch
+_PAIR_FINALIZE = os.environ.get("RR_BN_PAIR_FINALIZE", "1") != "0"
+
+
+def _fin_args(bn, st, bias, count, out):
+    return dict(st=st, count=count, bias=bias, gamma=bn.weight, beta=bn.bias,
+                running_mean=bn.running_mean, running_var=bn.running_var, momentum=bn.momentum,
+                eps=bn.eps, num_batches_tracked=bn.num_batches_tracked, out=out)
+
+
 def block_has_shortcut(blk):
     return len(blk.shortcut) > 0
 
@@ -400,22 +410,28 @@ def resblock_forward(blk, x1, x2, n, h, w, wc, dt, training, need_bwd, pool=Fals
     if has_sc and training and need_bwd and _RECOMPUTE_MASK:
         pair = (torch.empty(2, cout, dtype=torch.float32, device=x1.device),
                 torch.empty(2, cout, dtype=torch.float32, device=x1.device))
-    s2, sh2, m2, i2 = _bn_affine(bn2, st2, c2.bias, P, training,
-                                 out=(pair[0][0], pair[1][0]) if pair else None)
+    out2 = (pair[0][0], pair[1][0]) if pair else None
     S = Bag(x1=x1, x2=x2, n=n, h=h, w=w)
     if has_sc:
         sc0, sc1 = blk.shortcut[0], blk.shortcut[1]
         pks = wc.conv(sc0.weight, dt, dgrad=need_bwd)
         s, _, sts = ops.igemm(RR_CONV1X1, x1, x2, n, h, w, pks[0], cout, bias=sc0.bias,
                               stats=training)
-        ss, shs, ms, is_ = _bn_affine(sc1, sts, sc0.bias, P, training,
-                                      out=(pair[0][1], pair[1][1]) if pair else None)
+        outs = (pair[0][1], pair[1][1]) if pair else None
+        if training and _PAIR_FINALIZE and bn2.momentum is not None and sc1.momentum is not None:
+            # both statistics are ready: the two finalizes as one launch
+            (s2, sh2, m2, i2), (ss, shs, ms, is_) = ops.bn_finalize_pair(
+                _fin_args(bn2, st2, c2.bias, P, out2), _fin_args(sc1, sts, sc0.bias, P, outs))
+        else:
+            s2, sh2, m2, i2 = _bn_affine(bn2, st2, c2.bias, P, training, out=out2)
+            ss, shs, ms, is_ = _bn_affine(sc1, sts, sc0.bias, P, training, out=outs)
         res, rsc, rsh = s, ss, shs
         if need_bwd:
             S.update(s=s, ms=ms, is_=is_, pks=pks, s2=s2, sh2=sh2, ss=ss, shs=shs, pair=pair)
     else:
         if x2 is not None:
             raise RuntimeError("identity shortcut with a concatenated input")
+        s2, sh2, m2, i2 = _bn_affine(bn2, st2, c2.bias, P, training, out=out2)
         res, rsc, rsh = x1, None, None
     pooled = None
     if pool and _FUSED_POOL and h % 2 == 0 and w % 2 == 0 and cout % 8 == 0:

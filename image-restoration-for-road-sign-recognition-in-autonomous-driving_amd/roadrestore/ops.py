@@ -256,6 +256,49 @@ def bn_finalize(st, count, bias, gamma, beta, running_mean, running_var, momentu
     return scale, shift, mean, inv
 
 
+def bn_finalize_pair(a, b):
+    """Two bn_finalize calls (keyword dicts of bn_finalize's arguments) as ONE
+    launch (rr_bn_finalize_pair; the residual tail's BN and the shortcut BN).
+    Falls back to two launches when either has > 8192 partial rows."""
+    from ._lib import BnFinalizeDesc, RR_EUNSUPPORTED
+    if a["st"].shape[0] > 8192 or b["st"].shape[0] > 8192:
+        return bn_finalize(**a), bn_finalize(**b)
+    descs, outs = [], []
+    for k in (a, b):
+        st = k["st"]
+        Cc = st.shape[1]
+        dev = st.device
+        if st.dtype != torch.float32 or not st.is_contiguous():
+            raise ValueError("bn_finalize_pair: st must be a contiguous fp32 [blocks, C, 2] tensor")
+        o = k.get("out")
+        scale, shift = o if o is not None else (torch.empty(Cc, dtype=torch.float32, device=dev),
+                                                torch.empty(Cc, dtype=torch.float32, device=dev))
+        mean = torch.empty(Cc, dtype=torch.float32, device=dev)
+        inv = torch.empty(Cc, dtype=torch.float32, device=dev)
+        for name in ("bias", "gamma", "beta", "running_mean", "running_var"):
+            t = k.get(name)
+            if t is not None and (t.dtype != torch.float32 or t.numel() != Cc or t.device != dev
+                                  or not t.is_contiguous()):
+                raise ValueError(f"bn_finalize_pair: {name} must be a contiguous fp32 [C] tensor")
+        for t in (scale, shift):
+            if t.numel() != Cc or t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError("bn_finalize_pair: out must be two contiguous fp32 [C] tensors")
+        _need_cuda(st, scale, shift, k.get("bias"), k.get("gamma"), k.get("beta"),
+                   k.get("running_mean"), k.get("running_var"), k.get("num_batches_tracked"))
+        descs.append(BnFinalizeDesc(Cc, st.shape[0], int(k["count"]), _p(st), _p(k.get("bias")),
+                                    _p(k.get("gamma")), _p(k.get("beta")),
+                                    _p(k.get("running_mean")), _p(k.get("running_var")),
+                                    float(k.get("momentum", 0.1)), float(k.get("eps", 1e-5)),
+                                    _p(scale), _p(shift), _p(mean), _p(inv),
+                                    _p(k.get("num_batches_tracked"))))
+        outs.append((scale, shift, mean, inv))
+    rc = lib().rr_bn_finalize_pair(C.byref(descs[0]), C.byref(descs[1]), stream())
+    if rc == RR_EUNSUPPORTED:
+        return bn_finalize(**a), bn_finalize(**b)
+    lib().check(rc, "rr_bn_finalize_pair")
+    return outs[0], outs[1]
+
+
 def bn_eval_affine(gamma, beta, running_mean, running_var, eps=1e-5):
     Cc = running_mean.numel()
     scale = torch.empty(Cc, dtype=torch.float32, device=running_mean.device)

@@ -166,6 +166,21 @@ int rr_bn_finalize(int C, int blocks, long long count, const float *stats_partia
                    float eps, float *scale, float *shift, float *save_mean,
                    float *save_invstd, int64_t *num_batches_tracked, void *ws,
                    size_t ws_bytes, rr_stream stream);
+/* rr_bn_finalize's arguments as one descriptor */
+typedef struct rr_bn_finalize_desc {
+  int32_t C, blocks;
+  int64_t count;
+  const float *part, *bias, *gamma, *beta;
+  float *running_mean, *running_var;
+  float momentum, eps;
+  float *scale, *shift, *save_mean, *save_invstd;
+  int64_t *num_batches_tracked;
+} rr_bn_finalize_desc;
+/* two rr_bn_finalize calls as ONE launch: the residual tail's BatchNorm and
+ * the shortcut's (14:109-114), whose statistics are ready together.  Direct
+ * path only (blocks <= 8192 for both): else RR_EUNSUPPORTED, nothing done. */
+int rr_bn_finalize_pair(const rr_bn_finalize_desc *a, const rr_bn_finalize_desc *b,
+                        rr_stream stream);
 /* workspace of rr_bn_finalize: 0 for blocks <= 8192 (one workgroup per channel
  * sums the raw partials in place; ws may be NULL); above that the
  * [blocks][C][2] partials are first folded to <= 64 fp64 rows by a parallel

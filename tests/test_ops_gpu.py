@@ -346,6 +346,36 @@ def test_bn_train_fwd_bwd(dev, dt):
     close(r["dalpha"].cpu(), alp.grad, dt, scale=alp.grad.abs().max().item())
 
 
+@pytest.mark.parametrize("rows_a,rows_b,C", [(256, 8192, 64), (37, 2071, 128), (9001, 16, 32)])
+def test_bn_finalize_pair_equals_two_launches(dev, rows_a, rows_b, C):
+    """rr_bn_finalize_pair (tail BN + shortcut BN in one launch) == two
+    rr_bn_finalize calls, bit for bit: scale / shift / mean / invstd, running
+    stats and num_batches_tracked (and the > 8192-row fallback)."""
+    import roadrestore as rr
+    g = torch.Generator().manual_seed(rows_a + rows_b)
+
+    def make(rows):
+        st = torch.randn(rows, C, 2, generator=g)
+        st[..., 1] = st[..., 1].abs() * 4.0 + 2.0
+        return dict(st=st.to(dev), count=rows * 16, bias=torch.randn(C, generator=g).to(dev),
+                    gamma=torch.randn(C, generator=g).to(dev), beta=torch.randn(C, generator=g).to(dev),
+                    running_mean=torch.randn(C, generator=g).to(dev),
+                    running_var=torch.rand(C, generator=g).to(dev) + 0.5, momentum=0.1, eps=1e-5,
+                    num_batches_tracked=torch.zeros((), dtype=torch.long, device=dev))
+
+    a, b = make(rows_a), make(rows_b)
+    a2 = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in a.items()}
+    b2 = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in b.items()}
+    ra, rb = rr.ops.bn_finalize_pair(a, b)
+    sa, sb = rr.ops.bn_finalize(**a2), rr.ops.bn_finalize(**b2)
+    for got, want in ((ra, sa), (rb, sb)):
+        for x, y in zip(got, want):
+            assert torch.equal(x, y)
+    for k in ("running_mean", "running_var", "num_batches_tracked"):
+        assert torch.equal(a[k], a2[k]) and torch.equal(b[k], b2[k]), k
+    assert a["num_batches_tracked"].item() == 1 and b["num_batches_tracked"].item() == 1
+
+
 @pytest.mark.parametrize("rows,C", [(1, 64), (37, 64), (2071, 128), (8192, 64), (9001, 32)])
 def test_bn_finalize_partials_and_pair_out(dev, rows, C):
     """Statistics finalize from raw per-tile partials [rows][C][2]: the direct
