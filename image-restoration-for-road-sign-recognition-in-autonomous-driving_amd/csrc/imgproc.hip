@@ -147,6 +147,32 @@ __global__ void rs_vert_kernel(int n, int rows, int oh, int ow, int ksize, int y
   }
 }
 
+// same-size "resize": Pillow returns a copy of the image (Image.resize with
+// size == self.size), so the passes reduce to the copy / ToTensor (+
+// Normalize) of the input -- one pass instead of horiz + vert + coefficients
+template <int C, int MODE>
+__global__ void rs_same_kernel(long long npix, int hw, const uint8_t *__restrict__ in,
+                               void *__restrict__ out, RsNorm nm, int normalize) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < npix;
+       i += (long long)gridDim.x * blockDim.x) {
+    const uint8_t *src = in + i * C;
+    if constexpr (MODE == 0) {
+      uint8_t *dst = (uint8_t *)out + i * C;
+#pragma unroll
+      for (int c = 0; c < C; ++c) dst[c] = src[c];
+    } else {
+      const long long img = i / hw, px = i - img * hw;
+      float *dst = (float *)out;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        float v = (float)src[c] / 255.0f;                           // ToTensor: .div(255)
+        if (normalize) v = (v - nm.mean[c]) / nm.std[c];          // Normalize: sub_, div_
+        dst[(img * C + c) * hw + px] = v;
+      }
+    }
+  }
+}
+
 struct RsPlan {
   int kh, kv, y_first, rows;
   size_t off_bh, off_kh, off_bv, off_kv, off_tmp, total;
@@ -278,6 +304,27 @@ extern "C" int rr_resize_bilinear_u8(int n, int h, int w, int c, int oh, int ow,
   if (ws_bytes < p.total) return RR_EWORKSPACE;
   if ((mean == nullptr) != (std == nullptr) || (mean && out_kind != 1)) return RR_EINVAL;
   hipStream_t st = (hipStream_t)stream;
+  if (oh == h && ow == w) {
+    RsNorm nm{};
+    for (int i = 0; i < c; ++i) {
+      nm.mean[i] = mean ? mean[i] : 0.f;
+      nm.std[i] = std ? std[i] : 1.f;
+    }
+    const long long np = (long long)n * h * w;
+    const dim3 g(rr_grid_cap((np + 255) / 256, 8192)), b(256);
+#define RS_SAME(CC)                                                                                 \
+  if (out_kind == 0) hipLaunchKernelGGL((rs_same_kernel<CC, 0>), g, b, 0, st, np, h * w, in, out, nm, 0); \
+  else hipLaunchKernelGGL((rs_same_kernel<CC, 1>), g, b, 0, st, np, h * w, in, out, nm, mean != nullptr);
+    switch (c) {
+      case 1: RS_SAME(1) break;
+      case 2: RS_SAME(2) break;
+      case 3: RS_SAME(3) break;
+      default: RS_SAME(4) break;
+    }
+#undef RS_SAME
+    RR_CHECK_LAUNCH();
+    return RR_OK;
+  }
   char *base = (char *)ws;
   RsAxis ah{w, ow, p.kh, (int *)(base + p.off_bh), (int *)(base + p.off_kh)};
   RsAxis av{h, oh, p.kv, (int *)(base + p.off_bv), (int *)(base + p.off_kv)};

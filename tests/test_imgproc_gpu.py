@@ -54,6 +54,17 @@ def test_compose_resize_totensor_normalize_bit_exact(dev):
     y2 = T.Compose([T.Resize((64, 64)), T.ToTensor()])(torch.from_numpy(x).to(dev)).cpu().numpy()
     for i in range(4):
         assert np.array_equal(y2[i], I.to_tensor_normalize(I.pil_resize_bilinear(x[i], 64, 64)))
+    # same size (the bench's ToTensor at 64x64): Pillow returns a copy -> the
+    # single-pass copy / ToTensor (+ Normalize) path
+    x3 = _batch(3, 64, 64, seed=10)
+    for norm in (False, True):
+        ops_ = [T.Resize((64, 64)), T.ToTensor()] + ([T.Normalize(T.IMAGENET_MEAN, T.IMAGENET_STD)] if norm else [])
+        y3 = T.Compose(ops_)(torch.from_numpy(x3).to(dev)).cpu().numpy()
+        for i in range(3):
+            ref = I.pil_resize_bilinear(x3[i], 64, 64)
+            assert np.array_equal(ref, x3[i])
+            want = I.to_tensor_normalize(ref, T.IMAGENET_MEAN, T.IMAGENET_STD) if norm else I.to_tensor_normalize(ref)
+            assert np.array_equal(y3[i], want), (norm, i)
     with pytest.raises(NotImplementedError):
         T.Normalize(T.IMAGENET_MEAN, T.IMAGENET_STD)(torch.zeros(1, 3, 2, 2, device=dev))
 
