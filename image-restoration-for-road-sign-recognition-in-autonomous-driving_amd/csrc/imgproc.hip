@@ -415,7 +415,10 @@ __device__ __forceinline__ void philox_round(uint32_t &c0, uint32_t &c1, uint32_
   c0 = n0; c1 = l1; c2 = n2; c3 = l0;
 }
 
-// standard normal for element e (Philox4x32-10, 2 x 53-bit uniforms, Box-Muller)
+// standard normal for element e (Philox4x32-10, two 24-bit uniforms,
+// Box-Muller in fp32: np.random.normal's stream cannot be reproduced anyway,
+// and the fp32 transcendentals cost a fraction of the fp64 library ones --
+// the noise feeds an fp64 add and a uint8 truncation; |z| <= 5.8)
 __device__ double philox_normal(unsigned long long seed, unsigned long long e) {
   uint32_t c0 = (uint32_t)e, c1 = (uint32_t)(e >> 32), c2 = 0x9E3779B9u, c3 = 0;
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
@@ -425,9 +428,9 @@ __device__ double philox_normal(unsigned long long seed, unsigned long long e) {
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
-  const double u1 = ((((unsigned long long)c0 << 21) ^ c1) & ((1ull << 53) - 1)) * 0x1p-53 + 0x1p-54;
-  const double u2 = ((((unsigned long long)c2 << 21) ^ c3) & ((1ull << 53) - 1)) * 0x1p-53;
-  return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+  const float u1 = (float)((c0 >> 8) + 1) * 0x1p-24f;          // (0, 1]
+  const float u2 = (float)(c2 >> 8) * 0x1p-24f;                // [0, 1)
+  return (double)(sqrtf(-2.f * logf(u1)) * cosf(6.28318530717958648f * u2));
 }
 
 __device__ __forceinline__ uint8_t trunc_u8(double v) {    // np.clip(v, 0, 255).astype(uint8)
