@@ -226,7 +226,8 @@ def test_igemm_bnbwd_fused(dev, dt, n, h, w, C):
 
 
 @pytest.mark.parametrize("acc", [False, True])
-@pytest.mark.parametrize("n,h,w", [(4, 8, 8), (2, 64, 64), (1, 16, 32), (1, 5, 7)])
+@pytest.mark.parametrize("n,h,w", [(4, 8, 8), (2, 64, 64), (1, 16, 32), (1, 5, 7), (3, 40, 16),
+                                   (1, 20, 112)])
 def test_image_grad(dev, n, h, w, acc):
     """Image grad of the perceptual slice's conv1_1 (64 -> 3, 14:189): bf16
     dgrad into fp32 NCHW -- the narrow 16-column halo tile where eligible,
