@@ -579,7 +579,8 @@ template <typename PT>
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
     int C, int blocks, double count, int nbn, const PT *__restrict__ part, int ablocks,
     const float *apart, const float *g0, const float *inv0, const float *g1, const float *inv1,
-    float *dg0, float *db0, float *dg1, float *db1, float *dalpha, float *coef) {
+    float *dg0, float *db0, float *dg1, float *db1, float *dalpha, float *coef, float *dbias0,
+    float *dbias1) {
   __shared__ double red[3][256];
   const int c = blockIdx.x, t = threadIdx.x;
   double s[3] = {0, 0, 0};
@@ -599,15 +600,18 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
     s0 = red[0][0]; s1 = red[1][0]; s2 = red[2][0];
     if (db0) db0[c] = (float)s0;
     if (dg0) dg0[c] = (float)s1;
+    // eval mode: count = +inf, so the batch-statistic terms are exactly 0
     coef[c * 6 + 0] = (g0 ? g0[c] : 1.f) * inv0[c];
     coef[c * 6 + 1] = (float)(s0 / count);
     coef[c * 6 + 2] = (float)(s1 / count);
+    if (dbias0) dbias0[c] = coef[c * 6 + 0] * (float)s0;
     if (nbn == 2) {
       if (db1) db1[c] = (float)s0;
       if (dg1) dg1[c] = (float)s2;
       coef[c * 6 + 3] = (g1 ? g1[c] : 1.f) * inv1[c];
       coef[c * 6 + 4] = (float)(s0 / count);
       coef[c * 6 + 5] = (float)(s2 / count);
+      if (dbias1) dbias1[c] = coef[c * 6 + 3] * (float)s0;
     }
   }
   if (blockIdx.x == 0 && apart && dalpha) {
@@ -864,6 +868,11 @@ extern "C" int rr_bn_bwd_blocks(const rr_bnbwd_desc *d) {
   return reduce_blocks(d->P);
 }
 
+// the sample count of the batch-statistic terms; eval mode: +inf (the terms vanish)
+static double bnbwd_count(const rr_bnbwd_desc *d) {
+  return d->eval ? __builtin_huge_val() : (double)d->P;
+}
+
 static int bnbwd_check(const rr_bnbwd_desc *d) {
   if (!d || d->P <= 0 || d->C <= 0 || d->C % 4 || d->C / 4 > 256) return RR_EINVAL;
   if (d->nbn != 1 && d->nbn != 2) return RR_EINVAL;
@@ -949,9 +958,9 @@ extern "C" int rr_bn_bwd_finalize(const rr_bnbwd_desc *d, const float *partial,
   const int blocks = reduce_blocks(d->P);
   const float *apart = d->mask_kind == 2 ? partial + (size_t)blocks * d->C * 3 : nullptr;
   hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3(d->C), dim3(256), 0,
-                     (hipStream_t)stream, d->C, blocks, (double)d->P, d->nbn, partial, blocks, apart,
+                     (hipStream_t)stream, d->C, blocks, bnbwd_count(d), d->nbn, partial, blocks, apart,
                      gamma0, invstd0, gamma1, invstd1, dgamma0, dbeta0, dgamma1, dbeta1, dalpha,
-                     coef);
+                     coef, d->eval ? d->dbias0 : nullptr, d->eval ? d->dbias1 : nullptr);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }
@@ -1040,8 +1049,9 @@ extern "C" int rr_bn_bwd_finalize_rows(const rr_bnbwd_desc *d, int rows, const f
   const int chunks = rr_colreduce(partial, rows, d->C * 3, (double *)ws, st);
   if (chunks < 0) return RR_ELAUNCH;
   hipLaunchKernelGGL(bn_bwd_finalize_kernel<double>, dim3(d->C), dim3(256), 0, st,
-                     d->C, chunks, (double)d->P, 1, (const double *)ws, arows, apartial, gamma0,
-                     invstd0, nullptr, nullptr, dgamma0, dbeta0, nullptr, nullptr, dalpha, coef);
+                     d->C, chunks, bnbwd_count(d), 1, (const double *)ws, arows, apartial, gamma0,
+                     invstd0, nullptr, nullptr, dgamma0, dbeta0, nullptr, nullptr, dalpha, coef,
+                     d->eval ? d->dbias0 : nullptr, nullptr);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

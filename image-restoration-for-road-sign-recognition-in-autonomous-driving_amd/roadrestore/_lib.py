@@ -35,7 +35,8 @@ class WgradDesc(C.Structure):
 class BnBwdDesc(C.Structure):
     _fields_ = [("dtype", C.c_int32), ("P", C.c_int64), ("C", C.c_int32),
                 ("mask_kind", C.c_int32), ("nbn", C.c_int32), ("h", C.c_int32), ("w", C.c_int32),
-                ("pool_dy", C.c_void_p), ("pool_idx", C.c_void_p)]
+                ("pool_dy", C.c_void_p), ("pool_idx", C.c_void_p), ("eval", C.c_int32),
+                ("dbias0", C.c_void_p), ("dbias1", C.c_void_p)]
 
 
 class DistortParam(C.Structure):

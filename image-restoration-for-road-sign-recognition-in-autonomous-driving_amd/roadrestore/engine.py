@@ -328,15 +328,20 @@ def simple_unet_backward(m, S, g_out, sink):
 # ---------------------------------------------------------------------------
 # ResidualBlock (14:96-115) and ResUNet (14:117-186)
 
-def _bn_affine(bn, st, bias, count, training, out=None):
+def _bn_affine(bn, st, bias, count, training, out=None, need_bwd=False):
+    """-> (scale, shift, mean, invstd).  Eval mode: the running statistics;
+    mean / invstd only when a backward follows (eval-mode BN backward)."""
     if training:
         if bn.momentum is None:
             raise NotImplementedError("BatchNorm2d(momentum=None) is not supported")
         return ops.bn_finalize(st, count, bias, bn.weight, bn.bias, bn.running_mean,
                                bn.running_var, bn.momentum, bn.eps, bn.num_batches_tracked,
                                out=out)
-    s, b = ops.bn_eval_affine(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
-    return s, b, None, None
+    s, b = ops.bn_eval_affine(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, out=out)
+    if not need_bwd:
+        return s, b, None, None
+    inv, _ = ops.bn_eval_affine(None, None, bn.running_mean, bn.running_var, bn.eps)
+    return s, b, bn.running_mean, inv
 
 
 # A/B switch: the tail BN and the shortcut BN finalized by one launch
@@ -399,7 +404,7 @@ def resblock_forward(blk, x1, x2, n, h, w, wc, dt, training, need_bwd, pool=Fals
     P = n * h * w
     pk1 = wc.conv(c1.weight, dt, dgrad=need_bwd)
     t1, _, st1 = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, pk1[0], cout, bias=c1.bias, stats=training)
-    s1, sh1, m1, i1 = _bn_affine(bn1, st1, c1.bias, P, training)
+    s1, sh1, m1, i1 = _bn_affine(bn1, st1, c1.bias, P, training, need_bwd=need_bwd)
     a1 = ops.affine_act(t1, s1, sh1, alpha=pr.weight)
     pk2 = wc.conv(c2.weight, dt, dgrad=need_bwd)
     t2, _, st2 = ops.igemm(RR_CONV3X3, a1, None, n, h, w, pk2[0], cout, bias=c2.bias, stats=training)
@@ -407,7 +412,7 @@ def resblock_forward(blk, x1, x2, n, h, w, wc, dt, training, need_bwd, pool=Fals
     # (scale, shift) of bn2 and the shortcut BN as rows of two [2, C] buffers:
     # the backward's recomputed ReLU mask reads them as pairs (no stack copy)
     pair = None
-    if has_sc and training and need_bwd and _RECOMPUTE_MASK:
+    if has_sc and need_bwd and _RECOMPUTE_MASK:
         pair = (torch.empty(2, cout, dtype=torch.float32, device=x1.device),
                 torch.empty(2, cout, dtype=torch.float32, device=x1.device))
     out2 = (pair[0][0], pair[1][0]) if pair else None
@@ -423,15 +428,16 @@ def resblock_forward(blk, x1, x2, n, h, w, wc, dt, training, need_bwd, pool=Fals
             (s2, sh2, m2, i2), (ss, shs, ms, is_) = ops.bn_finalize_pair(
                 _fin_args(bn2, st2, c2.bias, P, out2), _fin_args(sc1, sts, sc0.bias, P, outs))
         else:
-            s2, sh2, m2, i2 = _bn_affine(bn2, st2, c2.bias, P, training, out=out2)
-            ss, shs, ms, is_ = _bn_affine(sc1, sts, sc0.bias, P, training, out=outs)
+            s2, sh2, m2, i2 = _bn_affine(bn2, st2, c2.bias, P, training, out=out2, need_bwd=need_bwd)
+            ss, shs, ms, is_ = _bn_affine(sc1, sts, sc0.bias, P, training, out=outs,
+                                          need_bwd=need_bwd)
         res, rsc, rsh = s, ss, shs
         if need_bwd:
             S.update(s=s, ms=ms, is_=is_, pks=pks, s2=s2, sh2=sh2, ss=ss, shs=shs, pair=pair)
     else:
         if x2 is not None:
             raise RuntimeError("identity shortcut with a concatenated input")
-        s2, sh2, m2, i2 = _bn_affine(bn2, st2, c2.bias, P, training, out=out2)
+        s2, sh2, m2, i2 = _bn_affine(bn2, st2, c2.bias, P, training, out=out2, need_bwd=need_bwd)
         res, rsc, rsh = x1, None, None
     pooled = None
     if pool and _FUSED_POOL and h % 2 == 0 and w % 2 == 0 and cout % 8 == 0:
@@ -443,7 +449,7 @@ def resblock_forward(blk, x1, x2, n, h, w, wc, dt, training, need_bwd, pool=Fals
             pooled = ops.maxpool2_fwd(out)
     if need_bwd:
         S.update(t1=t1, a1=a1, t2=t2, out=out, s1=s1, sh1=sh1, m1=m1, i1=i1, m2=m2, i2=i2,
-                 pk1=pk1, pk2=pk2)
+                 pk1=pk1, pk2=pk2, eval=not training)
     return (out, S, pooled) if pool else (out, S)
 
 
@@ -468,6 +474,9 @@ def resblock_backward(blk, S, g_out, sink, pool=None):
     cin = c_in1 + c_in2
     has_sc = block_has_shortcut(blk)
     gx1 = gx2 = None
+    # eval-mode BatchNorm: running statistics, no batch-statistic terms, and
+    # the conv biases feeding the BNs get their (non-zero) grads
+    ev = bool(S.get("eval"))
     side = _side_stream(g_out.device) if _WGRAD_SIDE and g_out.is_cuda else None
 
     def wgrad(*args, **kw):
@@ -489,13 +498,15 @@ def resblock_backward(blk, S, g_out, sink, pool=None):
         r = ops.bn_backward(g_out, S.t2, S.m2, S.i2, bn2.weight, mask_kind=1, aux=S.out, pool=pool,
                             recompute=rec, t1=S.s, mean1=S.ms, inv1=S.is_, gamma1=sc1.weight,
                             outs=dict(dgamma0=sink[bn2.weight], dbeta0=sink[bn2.bias],
-                                      dgamma1=sink[sc1.weight], dbeta1=sink[sc1.bias]))
+                                      dgamma1=sink[sc1.weight], dbeta1=sink[sc1.bias]),
+                            eval_mode=ev, dbias=(sink[c2.bias], sink[sc0.bias]) if ev else None)
         dt2, ds = r["dt0"], r["dt1"]
     else:
         gx1 = torch.empty_like(x1)
         r = ops.bn_backward(g_out, S.t2, S.m2, S.i2, bn2.weight, mask_kind=1, aux=S.out, pool=pool,
                             want_gm=True, gm_out=gx1,
-                            outs=dict(dgamma0=sink[bn2.weight], dbeta0=sink[bn2.bias]))
+                            outs=dict(dgamma0=sink[bn2.weight], dbeta0=sink[bn2.bias]),
+                            eval_mode=ev, dbias=(sink[c2.bias], None) if ev else None)
         dt2 = r["dt0"]
     wgrad(RR_CONV3X3, dt2, S.a1, None, n, h, w, cout, dw=sink[c2.weight])
     outs1 = dict(dgamma0=sink[bn1.weight], dbeta0=sink[bn1.bias], dalpha=sink[pr.weight])
@@ -505,11 +516,12 @@ def resblock_backward(blk, S, g_out, sink, pool=None):
         gm1, part, rows, arows = ops.igemm_bnbwd(RR_CONV3X3, dt2, n, h, w, S.pk2[1], cout, S.t1,
                                                  S.m1, S.i1, S.s1, S.sh1, pr.weight)
         r1 = ops.bn_backward_rows(gm1, part, rows, arows, S.t1, S.m1, S.i1, bn1.weight,
-                                  outs=outs1)
+                                  outs=outs1, eval_mode=ev, dbias=(sink[c1.bias],) if ev else None)
     else:
         da1, _, _ = ops.igemm(RR_CONV3X3, dt2, None, n, h, w, S.pk2[1], cout)
         r1 = ops.bn_backward(da1, S.t1, S.m1, S.i1, bn1.weight, mask_kind=2, aux=S.t1,
-                             aff_s=S.s1, aff_b=S.sh1, alpha=pr.weight, outs=outs1)
+                             aff_s=S.s1, aff_b=S.sh1, alpha=pr.weight, outs=outs1,
+                             eval_mode=ev, dbias=(sink[c1.bias], None) if ev else None)
     dt1 = r1["dt0"]
     wgrad(RR_CONV3X3, dt1, x1, x2, n, h, w, cout, dw=sink[c1.weight])
     split = c_in1 if c_in2 else 0

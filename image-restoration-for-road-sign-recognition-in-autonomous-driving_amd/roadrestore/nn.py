@@ -193,9 +193,6 @@ class _RRNet(tnn.Module):
         need = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         if x.shape[0] == 0:
             return self._empty_forward(x, need)
-        if need and self._has_bn and not self.training:
-            raise NotImplementedError("backward through eval-mode BatchNorm is not implemented; "
-                                      "use model.train() or torch.no_grad()")
         fwd = getattr(torch.ops.rr, f"{self._op}_forward")
         out, _ = fwd(x, params, self._op_key, need)
         return out

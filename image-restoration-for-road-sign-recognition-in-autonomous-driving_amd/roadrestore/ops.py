@@ -299,10 +299,16 @@ def bn_finalize_pair(a, b):
     return outs[0], outs[1]
 
 
-def bn_eval_affine(gamma, beta, running_mean, running_var, eps=1e-5):
+def bn_eval_affine(gamma, beta, running_mean, running_var, eps=1e-5, out=None):
+    """Eval-mode BN as scale / shift from the running statistics (gamma /
+    beta None: 1 / 0, so scale = invstd); ``out=(scale, shift)``: fp32 [C]
+    outputs to write."""
     Cc = running_mean.numel()
-    scale = torch.empty(Cc, dtype=torch.float32, device=running_mean.device)
-    shift = torch.empty_like(scale)
+    if out is not None:
+        scale, shift = out
+    else:
+        scale = torch.empty(Cc, dtype=torch.float32, device=running_mean.device)
+        shift = torch.empty_like(scale)
     lib().check(lib().rr_bn_eval_affine(Cc, _p(gamma), _p(beta), _p(running_mean),
                                         _p(running_var), float(eps), _p(scale), _p(shift),
                                         stream()), "rr_bn_eval_affine")
@@ -349,7 +355,7 @@ def affine_act_pool(x, scale, shift, res=None, res_scale=None, res_shift=None, r
 
 def bn_backward(g, t0, mean0, inv0, gamma0, *, mask_kind=0, aux=None, aff_s=None, aff_b=None,
                 alpha=None, t1=None, mean1=None, inv1=None, gamma1=None, want_gm=False,
-                gm_out=None, outs=None, pool=None, recompute=None):
+                gm_out=None, outs=None, pool=None, recompute=None, eval_mode=False, dbias=None):
     """Full BN backward (reduce + finalize + apply) for one or two BNs that
     share the upstream gradient.  Returns dict with dt0, dt1, gm, dgamma0,
     dbeta0, dgamma1, dbeta1, dalpha.  ``pool=(dy_pool, idx)`` with
@@ -357,12 +363,16 @@ def bn_backward(g, t0, mean0, inv0, gamma0, *, mask_kind=0, aux=None, aff_s=None
     (mask kind 3, g: [n, h, w, C]).  ``recompute=(aff_s2, aff_b2)`` with
     mask_kind 1 and two BNs: the ReLU mask is recomputed from t0, t1 with the
     forward affines ([2, C] each: BN0's then BN1's scale / shift) instead of
-    read from ``aux`` (mask kind 4, or 5 with ``pool``)."""
+    read from ``aux`` (mask kind 4, or 5 with ``pool``).  ``eval_mode``:
+    eval-mode BatchNorm (mean / inv = running statistics; no batch-statistic
+    terms); ``dbias=(db0, db1)`` then receive the grads of the conv biases
+    feeding the BNs."""
     Cc = g.shape[-1]
     P = g.numel() // Cc
     nbn = 2 if t1 is not None else 1
     dev = g.device
     d = BnBwdDesc(rr_dtype(g.dtype), P, Cc, mask_kind, nbn, 0, 0, None, None)
+    _set_eval(d, eval_mode, dbias)
     if recompute is not None:
         if mask_kind != 1 or nbn != 2 or want_gm or gm_out is not None:
             raise ValueError("recomputed ReLU mask needs mask_kind 1, two BNs and no gm output")
@@ -436,13 +446,26 @@ def igemm_bnbwd(mode, dy, n, h, w, wpack, cout, t, mean, inv, aff_s, aff_b, alph
     return out, part, rows, rows * (cout // 64)
 
 
-def bn_backward_rows(gm, part, rows, arows, t0, mean0, inv0, gamma0, outs=None):
+def _set_eval(d, eval_mode, dbias):
+    d.eval = int(bool(eval_mode))
+    if eval_mode and dbias is not None:
+        for i, t in enumerate(dbias[:2]):
+            if t is not None:
+                if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != d.C:
+                    raise ValueError("dbias: contiguous fp32 [C] tensors")
+                setattr(d, f"dbias{i}", _p(t))
+
+
+def bn_backward_rows(gm, part, rows, arows, t0, mean0, inv0, gamma0, outs=None, eval_mode=False,
+                     dbias=None):
     """BN backward from precomputed row partials (the rr_igemm_bnbwd epilogue):
-    finalize (fp64 fixed order) + apply with gm already PReLU-masked."""
+    finalize (fp64 fixed order) + apply with gm already PReLU-masked
+    (``eval_mode`` / ``dbias``: as bn_backward)."""
     Cc = gm.shape[-1]
     P = gm.numel() // Cc
     dev = gm.device
     d = BnBwdDesc(rr_dtype(gm.dtype), P, Cc, 0, 1)
+    _set_eval(d, eval_mode, dbias)
     o = outs or {}
     dg0 = o.get("dgamma0")
     if dg0 is None:

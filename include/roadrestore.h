@@ -236,6 +236,14 @@ typedef struct {
   int32_t h, w;         /* mask_kind 3: the [P] rows are [n][h][w] pixels (h, w even) */
   const void *pool_dy;  /* mask_kind 3: [n][h/2][w/2][C] grad of the pooled output */
   const uint8_t *pool_idx; /* mask_kind 3: rr_maxpool2_fwd / rr_affine_act_pool index */
+  int32_t eval;         /* 1: eval-mode BatchNorm (mean / invstd are the running
+                           statistics, which do not depend on the batch): the
+                           finalize drops the mean(gm) and mean(gm * xhat) terms,
+                           so dt = gamma * invstd * gm, and writes the grad of
+                           the conv bias feeding BN i, gamma_i * invstd_i * sum(gm),
+                           to dbias_i (NULL: skipped) -- in training mode that
+                           grad is exactly zero */
+  float *dbias0, *dbias1;
 } rr_bnbwd_desc;
 /* residual tail (as rr_affine_act, without PReLU) over an [n][h][w][C] NHWC
  * activation fused with MaxPool2d(2, 2) (14:125-131): y, the pooled y_pool

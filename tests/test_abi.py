@@ -29,13 +29,36 @@ def test_library_exports_every_header_symbol():
     assert lib.rr_version().startswith(b"roadrestore")
 
 
-def test_descriptor_layouts():
-    from roadrestore._lib import BnBwdDesc, IgemmDesc, WgradDesc
+def test_descriptor_layouts(tmp_path):
+    """The ctypes mirrors of the C descriptors have the C compiler's layout
+    (sizeof / offsetof from include/roadrestore.h, built with gcc here)."""
+    import shutil
+    import subprocess
+    from roadrestore._lib import BnBwdDesc, BnFinalizeDesc, IgemmDesc, PackJob, WgradDesc
     assert ctypes.sizeof(IgemmDesc) == 15 * 4
     assert ctypes.sizeof(WgradDesc) == 9 * 4
-    # int32, pad, int64, 5 x int32, pad, 2 pointers (C layout of rr_bnbwd_desc)
-    assert ctypes.sizeof(BnBwdDesc) == 56
-    assert (BnBwdDesc.h.offset, BnBwdDesc.pool_dy.offset, BnBwdDesc.pool_idx.offset) == (28, 40, 48)
+    checks = [("rr_bnbwd_desc", BnBwdDesc, ["P", "h", "pool_dy", "pool_idx", "eval", "dbias0", "dbias1"]),
+              ("rr_bn_finalize_desc", BnFinalizeDesc, ["count", "part", "momentum", "scale",
+                                                       "num_batches_tracked"]),
+              ("rr_pack_job", PackJob, ["c_out", "begin"])]
+    if shutil.which("gcc") is None:
+        pytest.skip("no C compiler")
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "roadrestore.h"', "int main(void) {"]
+    for cname, _, fields in checks:
+        lines.append(f'  printf("%zu\\n", sizeof({cname}));')
+        lines += [f'  printf("%zu\\n", offsetof({cname}, {f}));' for f in fields]
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "probe.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True,
+                                          text=True).stdout.split()]
+    want = []
+    for _, cls, fields in checks:
+        want.append(ctypes.sizeof(cls))
+        want += [getattr(cls, f).offset for f in fields]
+    assert got == want
 
 
 def test_status_codes_raise():

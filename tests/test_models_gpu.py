@@ -631,3 +631,52 @@ def test_inference_pipeline_fp32_end_to_end(dev):
     pred = rr.ops.argmax_rows(logits).cpu()
     assert (logits.cpu() - lg_ref).abs().max().item() <= 1e-3 * max(1.0, lg_ref.abs().max().item())
     assert torch.equal(pred, pred_ref), (pred.tolist(), pred_ref.tolist())
+
+
+def test_resunet_eval_mode_backward(dev):
+    """Backward through eval-mode BatchNorm (model.eval() with grads, e.g. a
+    fine-tune with frozen statistics): the running statistics normalise, the
+    batch-statistic terms of the BN backward vanish, and the conv biases
+    feeding the BNs get non-zero grads -- against torch autograd through the
+    oracle's eval forward in fp64, on non-trivial running statistics; the
+    running statistics and num_batches_tracked stay unchanged."""
+    import roadrestore as rr
+    from oracle import reference_cpu as R
+    from oracle import seeded as S
+    g = torch.Generator().manual_seed(11)
+    sd = S.model_state_dict("resunet")
+    for k in list(sd):
+        if k.endswith("running_mean"):
+            sd[k] = torch.randn(sd[k].shape, generator=g) * 0.3
+        elif k.endswith("running_var"):
+            sd[k] = torch.rand(sd[k].shape, generator=g) * 1.5 + 0.5
+    bad = torch.rand(2, 3, 32, 32, generator=g)
+    clean = torch.rand(2, 3, 32, 32, generator=g)
+    m = rr.ResUNet().to(dev)
+    m.load_state_dict(sd)
+    m.eval()
+    out = m(bad.to(dev))
+    loss = rr.L1Loss()(out, clean.to(dev))
+    loss.backward()
+    p = {k: v.detach().clone().double() for k, v in sd.items()}
+    for k, v in p.items():
+        if "running" not in k and "num_batches" not in k:
+            v.requires_grad_(True)
+    out_r = R.resunet_forward(p, bad.double(), False)
+    loss_r = R.l1_loss(out_r, clean.double())
+    loss_r.backward()
+    assert (out.detach().cpu().double() - out_r.detach()).abs().max().item() < 1e-4
+    assert abs(loss.item() - loss_r.item()) < 1e-6
+    errs = {}
+    for name, prm in m.named_parameters():
+        ref = p[name].grad
+        errs[name] = ((prm.grad.cpu().double() - ref).norm() / ref.norm().clamp_min(1e-30)).item()
+    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:5]
+    print("eval-mode grads, worst rel-L2 vs fp64:", worst)
+    assert np.median(list(errs.values())) < 1e-4
+    assert max(errs.values()) < 5e-3, worst
+    # the conv biases feeding a BN: zero grads in train mode, not in eval mode
+    assert m.res1.conv_block[0].bias.grad.abs().max().item() > 0
+    for k, v in m.state_dict().items():
+        if "running" in k or "num_batches" in k:
+            assert torch.equal(v.cpu(), sd[k].to(v.dtype)), k
