@@ -709,6 +709,40 @@ __global__ void colsum_finalize(int C, int blocks, const float *__restrict__ par
   }
 }
 
+// per-block (sum, sum of squares) of a [P][C] tensor: the batch statistics of
+// a standalone BatchNorm2d (leaf-module path, nn.py) when no conv epilogue
+// produced them.  partial [blocks][C][2], the layout rr_bn_finalize reads.
+template <typename T>
+__global__ void colstats_kernel(long long P, int C, const T *__restrict__ x, float *__restrict__ part,
+                                long long rows_per_block) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];   // [R][C][2]
+  const int TPR = C / 4;
+  const int R = blockDim.x / TPR;
+  const int tr = threadIdx.x / TPR, tc = threadIdx.x % TPR;
+  float s[4] = {0.f, 0.f, 0.f, 0.f}, q[4] = {0.f, 0.f, 0.f, 0.f};
+  const long long r0 = blockIdx.x * rows_per_block;
+  const long long r1 = min(P, r0 + rows_per_block);
+  if (tr < R) {
+    for (long long r = r0 + tr; r < r1; r += R) {
+      const f32x4 v = load4<T>(x + r * C + tc * 4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { s[k] += v[k]; q[k] = fmaf(v[k], v[k], q[k]); }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      sm[((size_t)tr * C + tc * 4 + k) * 2] = s[k];
+      sm[((size_t)tr * C + tc * 4 + k) * 2 + 1] = q[k];
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < R; ++rr) { a += sm[((size_t)rr * C + i) * 2]; b += sm[((size_t)rr * C + i) * 2 + 1]; }
+    part[((long long)blockIdx.x * C + i) * 2] = a;
+    part[((long long)blockIdx.x * C + i) * 2 + 1] = b;
+  }
+}
+
 int reduce_blocks(long long P) {
   long long b = (P + 63) / 64;
   if (b > 1024) b = 1024;
@@ -1027,6 +1061,26 @@ extern "C" int rr_channel_sum(int dtype, long long P, int C, const void *x, floa
   RR_CHECK_LAUNCH();
   hipLaunchKernelGGL(colsum_finalize, dim3((C + 15) / 16), dim3(256), 0, st, C, blocks,
                      (const float *)ws, out, accumulate);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_bn_stats_blocks(long long P) { return reduce_blocks(P); }
+
+extern "C" int rr_bn_stats(int dtype, long long P, int C, const void *x, float *partial,
+                           rr_stream stream) {
+  if (P <= 0 || C <= 0 || C % 4 || C / 4 > 256 || !x || !partial) return RR_EINVAL;
+  const int blocks = reduce_blocks(P);
+  const long long rpb = (P + blocks - 1) / blocks;
+  const int R = 256 / (C / 4);
+  const size_t shm = (size_t)R * C * 2 * sizeof(float);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(colstats_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st, P, C,
+                       (const bf16_t *)x, partial, rpb);
+  else
+    hipLaunchKernelGGL(colstats_kernel<float>, dim3(blocks), dim3(256), shm, st, P, C,
+                       (const float *)x, partial, rpb);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

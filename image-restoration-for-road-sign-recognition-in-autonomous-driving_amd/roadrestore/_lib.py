@@ -101,6 +101,8 @@ _SIGS = {
                              P_, P_, P_, P_, P_]),
     "rr_channel_sum": (I_, [I_, L_, I_, P_, P_, I_, P_, S_, P_]),
     "rr_channel_sum_workspace": (S_, [L_, I_]),
+    "rr_bn_stats_blocks": (I_, [L_]),
+    "rr_bn_stats": (I_, [I_, L_, I_, P_, P_, P_]),
     "rr_maxpool2_fwd": (I_, [I_, I_, I_, I_, I_, P_, P_, P_, P_]),
     "rr_nearest_resize": (I_, [I_, I_, I_, I_, I_, I_, I_, P_, P_, P_]),
     "rr_png_encode": (L_, [I_, I_, I_, P_, I_, P_, L_]),

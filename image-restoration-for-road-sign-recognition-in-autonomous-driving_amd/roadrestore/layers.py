@@ -1,0 +1,502 @@
+"""Standalone forwards of the leaf modules, as PyTorch custom ops (``rr::``).
+
+The networks (SimpleUNet, ResUNet, ResidualBlock, VGG16, the perceptual loss)
+run their whole forward as one fused HIP schedule and never call their leaf
+modules.  A caller of the reference can still call a leaf or a Sequential of
+leaves on its own -- ``model.enc1(x)`` (14:153), ``vgg.features[:k](x)``
+(11:39, the hidden-state visualiser), ``model.res1.conv_block(x)`` -- and
+these ops make that work, on NCHW fp32 tensors in and out like torch.nn:
+
+  rr::conv2d / rr::conv2d_backward                 nn.Conv2d (3x3 pad 1, 1x1)
+  rr::conv_transpose2d / rr::conv_transpose2d_backward  nn.ConvTranspose2d(k 2, s 2)
+  rr::batch_norm / rr::batch_norm_backward          nn.BatchNorm2d (train: batch
+                                                    statistics + running-stat update; eval)
+  rr::prelu / rr::prelu_backward, rr::relu / rr::relu_backward
+  rr::max_pool2d / rr::max_pool2d_backward          nn.MaxPool2d(2, 2), floor mode
+  rr::linear, rr::adaptive_avg_pool2d               the VGG16 classifier head (forward only)
+
+Each op converts to the NHWC compute layout, launches the same HIP kernels
+the fused schedules use (igemm / wgrad, the first-conv and last-conv kernels,
+bn_stats + bn_finalize + affine_act, bn_backward, maxpool2) and converts back.
+Shapes the kernels do not serve raise NotImplementedError; there is no ATen
+fallback.  ``dtype`` is the compute dtype code (0 fp32, 1 bf16).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from . import ops
+from ._lib import RR_CONV1X1, RR_CONV3X3, RR_CONVT_DOWN, RR_CONVT_UP
+
+__all__ = ["dtype_code", "conv_kind", "OPS"]
+
+_TD = {0: torch.float32, 1: torch.bfloat16}
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return 0
+    if dt == torch.bfloat16:
+        return 1
+    raise TypeError(f"unsupported compute dtype {dt}")
+
+
+def conv_kind(cin, cout, k, padding):
+    """Which kernels run a standalone conv of this shape."""
+    if k == 3 and padding == 1:
+        if cin <= 4 and cout % 4 == 0 and cout <= 64:
+            return "in"          # first-layer kernels (rr_conv_in_fwd / wgrad / dgrad)
+        if cin % 64 == 0 and cout % 64 == 0:
+            return "igemm"
+    if k == 1 and padding == 0:
+        if cin % 64 == 0 and cout % 64 == 0:
+            return "igemm"
+        if cout <= 4 and cin % 4 == 0 and cin <= 64:
+            return "out"         # last-layer kernels (rr_conv_out_fwd / bwd)
+    raise NotImplementedError(
+        f"standalone Conv2d({cin}, {cout}, {k}, padding={padding}): the HIP kernels serve 3x3 "
+        "pad-1 convs with 64-multiple channels or 3 inputs, and 1x1 convs with 64-multiple "
+        "channels or <= 4 outputs (every conv of the reference networks)")
+
+
+def _nhwc(x, dt):
+    return ops.nchw_to_nhwc(x.contiguous(), dt)
+
+
+def _empty_like_nchw(x, c, h, w):
+    return torch.empty((x.shape[0], c, h, w), dtype=torch.float32, device=x.device)
+
+
+# ---------------------------------------------------------------------------
+# Conv2d
+
+@torch.library.custom_op("rr::conv2d", mutates_args=(), device_types="cuda")
+def conv2d(x: Tensor, weight: Tensor, bias: Optional[Tensor], padding: int, dtype: int) -> Tensor:
+    """nn.Conv2d.forward (stride 1): NCHW fp32 -> NCHW fp32"""
+    dt = _TD[dtype]
+    n, cin, h, w = x.shape
+    cout, _, k, _ = weight.shape
+    kind = conv_kind(cin, cout, k, padding)
+    if n == 0:
+        return _empty_like_nchw(x, cout, h, w)
+    weight = weight.contiguous()
+    if kind == "in":
+        return ops.nhwc_to_nchw(ops.conv_in_fwd(x.contiguous(), weight, bias, dt))
+    xn = _nhwc(x, dt)
+    if kind == "out":
+        return ops.conv_out_fwd(xn, weight, bias)
+    pk, _ = ops.pack_conv(weight, dt, fwd=True, dgrad=False)
+    y, _, _ = ops.igemm(RR_CONV3X3 if k == 3 else RR_CONV1X1, xn, None, n, h, w, pk, cout,
+                        bias=bias)
+    return ops.nhwc_to_nchw(y)
+
+
+@conv2d.register_fake
+def _(x, weight, bias, padding, dtype):
+    return x.new_empty((x.shape[0], weight.shape[0], x.shape[2], x.shape[3]))
+
+
+@torch.library.custom_op("rr::conv2d_backward", mutates_args=(), device_types="cuda")
+def conv2d_backward(grad: Tensor, x: Tensor, weight: Tensor, padding: int,
+                    dtype: int) -> Tuple[Tensor, Tensor, Tensor]:
+    """(dx, dweight, dbias) of rr::conv2d"""
+    dt = _TD[dtype]
+    n, cin, h, w = x.shape
+    cout, _, k, _ = weight.shape
+    kind = conv_kind(cin, cout, k, padding)
+    dev = x.device
+    if n == 0:
+        return (torch.zeros_like(x), torch.zeros_like(weight),
+                torch.zeros(cout, dtype=torch.float32, device=dev))
+    weight = weight.contiguous()
+    grad = grad.contiguous()
+    if kind == "in":
+        gn = _nhwc(grad, dt)
+        dw, db = ops.conv_in_wgrad(x.contiguous(), gn, dw_shape=tuple(weight.shape))
+        return ops.conv_in_dgrad(gn, weight, cin), dw, db
+    xn = _nhwc(x, dt)
+    if kind == "out":
+        dx, dw, db = ops.conv_out_bwd(grad, xn, weight, want_dx=True)
+        return ops.nhwc_to_nchw(dx), dw, db
+    mode = RR_CONV3X3 if k == 3 else RR_CONV1X1
+    gn = _nhwc(grad, dt)
+    dw = ops.wgrad(mode, gn, xn, None, n, h, w, cout, dw_shape=tuple(weight.shape))
+    db = ops.channel_sum(gn)
+    _, wd = ops.pack_conv(weight, dt, fwd=False, dgrad=True)
+    dx, _, _ = ops.igemm(mode, gn, None, n, h, w, wd, cin)
+    return ops.nhwc_to_nchw(dx), dw, db
+
+
+@conv2d_backward.register_fake
+def _(grad, x, weight, padding, dtype):
+    return (torch.empty_like(x), torch.empty_like(weight),
+            weight.new_empty((weight.shape[0],)))
+
+
+def _conv_setup(ctx, inputs, output):
+    x, weight, bias, padding, dtype = inputs
+    ctx.save_for_backward(x, weight)
+    ctx.has_bias, ctx.padding, ctx.dtype = bias is not None, padding, dtype
+
+
+def _conv_bwd(ctx, g):
+    x, weight = ctx.saved_tensors
+    dx, dw, db = torch.ops.rr.conv2d_backward(g, x, weight, ctx.padding, ctx.dtype)
+    return dx, dw, (db if ctx.has_bias else None), None, None
+
+
+conv2d.register_autograd(_conv_bwd, setup_context=_conv_setup)
+
+
+# ---------------------------------------------------------------------------
+# ConvTranspose2d(k = 2, stride = 2)
+
+def _check_convT(cin, cout):
+    if cin % 64 or cout % 64:
+        raise NotImplementedError(f"standalone ConvTranspose2d({cin}, {cout}, 2, 2): the HIP "
+                                  "kernels serve 64-multiple channel counts (07:88, 14:143)")
+
+
+@torch.library.custom_op("rr::conv_transpose2d", mutates_args=(), device_types="cuda")
+def conv_transpose2d(x: Tensor, weight: Tensor, bias: Tensor, dtype: int) -> Tensor:
+    """nn.ConvTranspose2d(cin, cout, 2, stride=2).forward: NCHW fp32"""
+    dt = _TD[dtype]
+    n, cin, h, w = x.shape
+    cout = weight.shape[1]
+    _check_convT(cin, cout)
+    if n == 0:
+        return _empty_like_nchw(x, cout, 2 * h, 2 * w)
+    wu, _ = ops.pack_convT(weight.contiguous(), dt, up=True, down=False)
+    y, _, _ = ops.igemm(RR_CONVT_UP, _nhwc(x, dt), None, n, h, w, wu, 4 * cout,
+                        bias=ops.bias_tile4(bias.contiguous()))
+    return ops.nhwc_to_nchw(y)
+
+
+@conv_transpose2d.register_fake
+def _(x, weight, bias, dtype):
+    return x.new_empty((x.shape[0], weight.shape[1], 2 * x.shape[2], 2 * x.shape[3]))
+
+
+@torch.library.custom_op("rr::conv_transpose2d_backward", mutates_args=(), device_types="cuda")
+def conv_transpose2d_backward(grad: Tensor, x: Tensor, weight: Tensor,
+                              dtype: int) -> Tuple[Tensor, Tensor, Tensor]:
+    dt = _TD[dtype]
+    n, cin, h, w = x.shape
+    cout = weight.shape[1]
+    _check_convT(cin, cout)
+    if n == 0:
+        return (torch.zeros_like(x), torch.zeros_like(weight),
+                torch.zeros(cout, dtype=torch.float32, device=x.device))
+    gu = _nhwc(grad, dt)
+    xn = _nhwc(x, dt)
+    dw = ops.wgrad(RR_CONVT_UP, gu, xn, None, n, h, w, cout, dw_shape=tuple(weight.shape))
+    db = ops.channel_sum(gu)
+    _, wd = ops.pack_convT(weight.contiguous(), dt, up=False, down=True)
+    dx, _, _ = ops.igemm(RR_CONVT_DOWN, gu, None, n, h, w, wd, cin)
+    return ops.nhwc_to_nchw(dx), dw, db
+
+
+@conv_transpose2d_backward.register_fake
+def _(grad, x, weight, dtype):
+    return torch.empty_like(x), torch.empty_like(weight), weight.new_empty((weight.shape[1],))
+
+
+def _convT_setup(ctx, inputs, output):
+    x, weight, bias, dtype = inputs
+    ctx.save_for_backward(x, weight)
+    ctx.dtype = dtype
+
+
+def _convT_bwd(ctx, g):
+    x, weight = ctx.saved_tensors
+    dx, dw, db = torch.ops.rr.conv_transpose2d_backward(g, x, weight, ctx.dtype)
+    return dx, dw, db, None
+
+
+conv_transpose2d.register_autograd(_convT_bwd, setup_context=_convT_setup)
+
+
+# ---------------------------------------------------------------------------
+# BatchNorm2d: the op reads / updates the module's running statistics
+# (module state, as in torch_ops: an op that declares mutated arguments
+# cannot carry an autograd formula)
+
+def _bn_module(key):
+    from .torch_ops import _module
+    return _module(key)
+
+
+@torch.library.custom_op("rr::batch_norm", mutates_args=(), device_types="cuda")
+def batch_norm(x: Tensor, weight: Tensor, bias: Tensor, module: int, training: bool,
+               dtype: int) -> Tuple[Tensor, Tensor, Tensor]:
+    """nn.BatchNorm2d.forward -> (y, mean, invstd).  training: batch
+    statistics (biased variance to normalise, unbiased into running_var,
+    num_batches_tracked += 1); eval: the running statistics."""
+    bn = _bn_module(module)
+    dt = _TD[dtype]
+    n, Cc, h, w = x.shape
+    P = n * h * w
+    dev = x.device
+    if training and n > 0 and P == 1:
+        raise ValueError("Expected more than 1 value per channel when training, got input size "
+                         f"{list(x.shape)}")
+    if n == 0:
+        if training:
+            bn.num_batches_tracked.add_(1)
+        z = torch.zeros(Cc, dtype=torch.float32, device=dev)
+        return _empty_like_nchw(x, Cc, h, w), z, z.clone()
+    xn = _nhwc(x, dt)
+    if training:
+        mom = bn.momentum
+        if mom is None:    # cumulative moving average: factor 1 / num_batches_tracked
+            mom = 1.0 / float(int(bn.num_batches_tracked.item()) + 1)
+        scale, shift, mean, inv = ops.bn_finalize(
+            ops.bn_stats(xn), P, None, weight.contiguous(), bias.contiguous(), bn.running_mean,
+            bn.running_var, momentum=mom, eps=bn.eps, num_batches_tracked=bn.num_batches_tracked)
+    else:
+        scale, shift = ops.bn_eval_affine(weight.contiguous(), bias.contiguous(), bn.running_mean,
+                                          bn.running_var, bn.eps)
+        inv, _ = ops.bn_eval_affine(None, None, bn.running_mean, bn.running_var, bn.eps)
+        mean = bn.running_mean.clone()
+    return ops.nhwc_to_nchw(ops.affine_act(xn, scale, shift)), mean, inv
+
+
+@batch_norm.register_fake
+def _(x, weight, bias, module, training, dtype):
+    c = x.shape[1]
+    return torch.empty_like(x), x.new_empty((c,)), x.new_empty((c,))
+
+
+@torch.library.custom_op("rr::batch_norm_backward", mutates_args=(), device_types="cuda")
+def batch_norm_backward(grad: Tensor, x: Tensor, mean: Tensor, invstd: Tensor, weight: Tensor,
+                        training: bool, dtype: int) -> Tuple[Tensor, Tensor, Tensor]:
+    """(dx, dweight, dbias); eval: no batch-statistic terms (dx = g * gamma * invstd)"""
+    dt = _TD[dtype]
+    if x.shape[0] == 0:
+        z = torch.zeros_like(weight)
+        return torch.zeros_like(x), z, z.clone()
+    r = ops.bn_backward(_nhwc(grad, dt), _nhwc(x, dt), mean, invstd, weight.contiguous(),
+                        mask_kind=0, eval_mode=not training)
+    return ops.nhwc_to_nchw(r["dt0"]), r["dgamma0"], r["dbeta0"]
+
+
+@batch_norm_backward.register_fake
+def _(grad, x, mean, invstd, weight, training, dtype):
+    return torch.empty_like(x), torch.empty_like(weight), torch.empty_like(weight)
+
+
+def _bn_setup(ctx, inputs, output):
+    x, weight, bias, module, training, dtype = inputs
+    ctx.save_for_backward(x, output[1], output[2], weight)
+    ctx.training, ctx.dtype = training, dtype
+
+
+def _bn_bwd(ctx, g, g_mean, g_inv):
+    x, mean, inv, weight = ctx.saved_tensors
+    dx, dw, db = torch.ops.rr.batch_norm_backward(g, x, mean, inv, weight, ctx.training,
+                                                  ctx.dtype)
+    return dx, dw, db, None, None, None
+
+
+batch_norm.register_autograd(_bn_bwd, setup_context=_bn_setup)
+
+
+# ---------------------------------------------------------------------------
+# PReLU (one shared alpha) / ReLU
+
+def _unit(Cc, dev):
+    one = torch.ones(Cc, dtype=torch.float32, device=dev)
+    return one, torch.zeros_like(one)
+
+
+def _check_act_channels(Cc):
+    if Cc % 4:
+        raise NotImplementedError(f"standalone activation on {Cc} channels: the HIP kernels take "
+                                  "4-multiple channel counts")
+
+
+@torch.library.custom_op("rr::prelu", mutates_args=(), device_types="cuda")
+def prelu(x: Tensor, alpha: Tensor, dtype: int) -> Tensor:
+    """nn.PReLU (one alpha, 14:103): x > 0 ? x : alpha * x"""
+    _check_act_channels(x.shape[1])
+    if x.shape[0] == 0:
+        return torch.empty_like(x)
+    one, zero = _unit(x.shape[1], x.device)
+    return ops.nhwc_to_nchw(ops.affine_act(_nhwc(x, _TD[dtype]), one, zero, alpha=alpha))
+
+
+@prelu.register_fake
+def _(x, alpha, dtype):
+    return torch.empty_like(x)
+
+
+@torch.library.custom_op("rr::prelu_backward", mutates_args=(), device_types="cuda")
+def prelu_backward(grad: Tensor, x: Tensor, alpha: Tensor, dtype: int) -> Tuple[Tensor, Tensor]:
+    dt = _TD[dtype]
+    if x.shape[0] == 0:
+        return torch.zeros_like(x), torch.zeros_like(alpha)
+    dx, dalpha = ops.prelu_bwd(_nhwc(grad, dt), _nhwc(x, dt), alpha)
+    return ops.nhwc_to_nchw(dx), dalpha.view_as(alpha)
+
+
+@prelu_backward.register_fake
+def _(grad, x, alpha, dtype):
+    return torch.empty_like(x), torch.empty_like(alpha)
+
+
+def _prelu_setup(ctx, inputs, output):
+    x, alpha, dtype = inputs
+    ctx.save_for_backward(x, alpha)
+    ctx.dtype = dtype
+
+
+def _prelu_bwd(ctx, g):
+    x, alpha = ctx.saved_tensors
+    dx, da = torch.ops.rr.prelu_backward(g, x, alpha, ctx.dtype)
+    return dx, da, None
+
+
+prelu.register_autograd(_prelu_bwd, setup_context=_prelu_setup)
+
+
+@torch.library.custom_op("rr::relu", mutates_args=(), device_types="cuda")
+def relu(x: Tensor, dtype: int) -> Tensor:
+    """nn.ReLU"""
+    _check_act_channels(x.shape[1])
+    if x.shape[0] == 0:
+        return torch.empty_like(x)
+    one, zero = _unit(x.shape[1], x.device)
+    return ops.nhwc_to_nchw(ops.affine_act(_nhwc(x, _TD[dtype]), one, zero, relu=True))
+
+
+@relu.register_fake
+def _(x, dtype):
+    return torch.empty_like(x)
+
+
+@torch.library.custom_op("rr::relu_backward", mutates_args=(), device_types="cuda")
+def relu_backward(grad: Tensor, x: Tensor, dtype: int) -> Tensor:
+    """g where x > 0, else 0 (the PReLU backward with alpha = 0)"""
+    dt = _TD[dtype]
+    if x.shape[0] == 0:
+        return torch.zeros_like(x)
+    zero = torch.zeros(1, dtype=torch.float32, device=x.device)
+    dx, _ = ops.prelu_bwd(_nhwc(grad, dt), _nhwc(x, dt), zero)
+    return ops.nhwc_to_nchw(dx)
+
+
+@relu_backward.register_fake
+def _(grad, x, dtype):
+    return torch.empty_like(x)
+
+
+def _relu_setup(ctx, inputs, output):
+    ctx.save_for_backward(inputs[0])
+    ctx.dtype = inputs[1]
+
+
+def _relu_bwd(ctx, g):
+    (x,) = ctx.saved_tensors
+    return torch.ops.rr.relu_backward(g, x, ctx.dtype), None
+
+
+relu.register_autograd(_relu_bwd, setup_context=_relu_setup)
+
+
+# ---------------------------------------------------------------------------
+# MaxPool2d(2, 2), floor mode
+
+@torch.library.custom_op("rr::max_pool2d", mutates_args=(), device_types="cuda")
+def max_pool2d(x: Tensor, dtype: int) -> Tuple[Tensor, Tensor]:
+    """nn.MaxPool2d(2, 2) -> (y NCHW fp32, window argmax NHWC uint8)"""
+    n, Cc, h, w = x.shape
+    if h < 2 or w < 2:
+        raise ValueError(f"MaxPool2d(2, 2): input {list(x.shape)} is smaller than the window")
+    if n == 0:
+        return (_empty_like_nchw(x, Cc, h // 2, w // 2),
+                torch.empty((0, h // 2, w // 2, Cc), dtype=torch.uint8, device=x.device))
+    y, idx = ops.maxpool2_fwd(_nhwc(x, _TD[dtype]))
+    return ops.nhwc_to_nchw(y), idx
+
+
+@max_pool2d.register_fake
+def _(x, dtype):
+    n, c, h, w = x.shape
+    return x.new_empty((n, c, h // 2, w // 2)), x.new_empty((n, h // 2, w // 2, c),
+                                                           dtype=torch.uint8)
+
+
+@torch.library.custom_op("rr::max_pool2d_backward", mutates_args=(), device_types="cuda")
+def max_pool2d_backward(grad: Tensor, idx: Tensor, h: int, w: int, dtype: int) -> Tensor:
+    n, Cc = grad.shape[0], grad.shape[1]
+    if n == 0:
+        return torch.zeros((0, Cc, h, w), dtype=torch.float32, device=grad.device)
+    return ops.nhwc_to_nchw(ops.maxpool2_bwd(_nhwc(grad, _TD[dtype]), idx, h, w))
+
+
+@max_pool2d_backward.register_fake
+def _(grad, idx, h, w, dtype):
+    return grad.new_empty((grad.shape[0], grad.shape[1], h, w))
+
+
+def _pool_setup(ctx, inputs, output):
+    x, dtype = inputs
+    ctx.save_for_backward(output[1])
+    ctx.h, ctx.w, ctx.dtype = x.shape[2], x.shape[3], dtype
+    ctx.mark_non_differentiable(output[1])
+
+
+def _pool_bwd(ctx, g, g_idx):
+    (idx,) = ctx.saved_tensors
+    return torch.ops.rr.max_pool2d_backward(g, idx, ctx.h, ctx.w, ctx.dtype), None
+
+
+max_pool2d.register_autograd(_pool_bwd, setup_context=_pool_setup)
+
+
+# ---------------------------------------------------------------------------
+# the VGG16 classifier head (forward only: the judge is frozen, 18:46)
+
+@torch.library.custom_op("rr::adaptive_avg_pool2d", mutates_args=(), device_types="cuda")
+def adaptive_avg_pool2d(x: Tensor, oh: int, ow: int, dtype: int) -> Tensor:
+    """nn.AdaptiveAvgPool2d((oh, ow)): NCHW fp32 -> [n, C, oh, ow] fp32"""
+    n, Cc = x.shape[0], x.shape[1]
+    if n == 0:
+        return _empty_like_nchw(x, Cc, oh, ow)
+    y = ops.adaptive_avgpool_flatten(_nhwc(x, _TD[dtype]), oh, ow)   # NCHW flatten order
+    return y.view(n, Cc, oh, ow).float()
+
+
+@adaptive_avg_pool2d.register_fake
+def _(x, oh, ow, dtype):
+    return x.new_empty((x.shape[0], x.shape[1], oh, ow))
+
+
+@torch.library.custom_op("rr::linear", mutates_args=(), device_types="cuda")
+def linear(x: Tensor, weight: Tensor, bias: Tensor, dtype: int) -> Tensor:
+    """nn.Linear.forward on [N, in] fp32 (a 1x1 implicit GEMM on a 1x1 map)"""
+    dt = _TD[dtype]
+    n, fin = x.shape
+    fout = weight.shape[0]
+    if fin % 64:
+        raise NotImplementedError(f"standalone Linear({fin}, {fout}): in_features must be a "
+                                  "multiple of 64 (VGG16's 25088 / 4096)")
+    if n == 0:
+        return x.new_empty((0, fout))
+    pk, _ = ops.pack_conv(weight.contiguous().view(fout, fin, 1, 1), dt, fwd=True, dgrad=False)
+    xv = x.contiguous().to(dt).view(n, 1, 1, fin)
+    y, _, _ = ops.igemm(RR_CONV1X1, xv, None, n, 1, 1, pk, fout, bias=bias.contiguous())
+    return y.view(n, fout).float()
+
+
+@linear.register_fake
+def _(x, weight, bias, dtype):
+    return x.new_empty((x.shape[0], weight.shape[0]))
+
+
+OPS = ["conv2d", "conv2d_backward", "conv_transpose2d", "conv_transpose2d_backward",
+       "batch_norm", "batch_norm_backward", "prelu", "prelu_backward", "relu", "relu_backward",
+       "max_pool2d", "max_pool2d_backward", "adaptive_avg_pool2d", "linear"]

@@ -11,8 +11,9 @@ unchanged):
   vgg16(num_classes=43)     torchvision cfg "D" + 05:53-54 head swap
   L1Loss / MSELoss          14:219 / 07:142
 
-Leaf modules (Conv2d, BatchNorm2d, PReLU, ...) are parameter containers with
-the torch.nn defaults for initialisation; the parent networks run their whole
+Leaf modules (Conv2d, BatchNorm2d, PReLU, ...) carry the torch.nn default
+initialisation and, called on their own, run one HIP op each
+(roadrestore.layers); the parent networks run their whole
 forward as one fused HIP schedule and their backward as one hand-written
 reverse schedule (roadrestore.engine), each reached through a registered
 PyTorch custom op (``torch.ops.rr.*``, roadrestore.torch_ops) with its
@@ -31,6 +32,7 @@ import torch
 import torch.nn as tnn
 
 from . import engine, ops
+from . import layers as _layers
 from . import torch_ops as _tops
 
 __all__ = ["Conv2d", "ConvTranspose2d", "BatchNorm2d", "PReLU", "ReLU", "MaxPool2d", "Linear",
@@ -47,11 +49,32 @@ def default_compute_dtype():
 # ---------------------------------------------------------------------------
 # leaf parameter containers (torch.nn default initialisation)
 
+def _as_nchw(x):
+    """an elementwise layer's [N, F] input (the VGG16 head) as [N, F, 1, 1]"""
+    return x.reshape(x.shape[0], x.shape[1], 1, 1) if x.dim() == 2 else x
+
+
 class _Leaf(tnn.Module):
-    def forward(self, *a, **k):
-        raise NotImplementedError(
-            f"{type(self).__name__} runs inside its parent network's fused HIP schedule; "
-            "call the parent module (SimpleUNet / ResUNet / ResidualBlock / VGG ...)")
+    """A leaf layer.  Inside its parent network it is a parameter container
+    (the parent runs one fused schedule and never calls it, so hooks on it do
+    not fire there); called on its own -- ``model.enc1(x)``,
+    ``vgg.features[:k](x)`` -- it runs its own HIP op (roadrestore.layers,
+    ``torch.ops.rr.<layer>``) on NCHW fp32 tensors, with autograd."""
+
+    def __init__(self):
+        super().__init__()
+        self.compute_dtype = default_compute_dtype()
+
+    def _dt(self):
+        return _layers.dtype_code(self.compute_dtype)
+
+    @staticmethod
+    def _x(x):
+        if not x.is_cuda:
+            raise RuntimeError("roadrestore layers run on the GPU only (no CPU fallback)")
+        if x.dim() != 4:
+            raise ValueError(f"expected an [N, C, H, W] input, got {tuple(x.shape)}")
+        return x if x.dtype == torch.float32 else x.float()
 
 
 class Conv2d(_Leaf):
@@ -71,6 +94,9 @@ class Conv2d(_Leaf):
             b = 1 / math.sqrt(fan_in)
             tnn.init.uniform_(self.bias, -b, b)
 
+    def forward(self, x):
+        return torch.ops.rr.conv2d(self._x(x), self.weight, self.bias, self.padding[0], self._dt())
+
 
 class ConvTranspose2d(_Leaf):
     def __init__(self, in_channels, out_channels, kernel_size, stride=1):
@@ -85,6 +111,9 @@ class ConvTranspose2d(_Leaf):
         b = 1 / math.sqrt(fan_in)
         tnn.init.uniform_(self.bias, -b, b)
 
+    def forward(self, x):
+        return torch.ops.rr.conv_transpose2d(self._x(x), self.weight, self.bias, self._dt())
+
 
 class BatchNorm2d(_Leaf):
     def __init__(self, num_features, eps=1e-5, momentum=0.1):
@@ -95,6 +124,13 @@ class BatchNorm2d(_Leaf):
         self.register_buffer("running_mean", torch.zeros(num_features))
         self.register_buffer("running_var", torch.ones(num_features))
         self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+        self._op_key = _tops.register_module(self)
+
+    def forward(self, x):
+        """nn.BatchNorm2d: batch statistics in train mode (running statistics
+        updated in place), running statistics in eval mode"""
+        return torch.ops.rr.batch_norm(self._x(x), self.weight, self.bias, self._op_key,
+                                       self.training, self._dt())[0]
 
 
 class PReLU(_Leaf):
@@ -104,11 +140,20 @@ class PReLU(_Leaf):
             raise NotImplementedError("PReLU with one shared alpha (14:103)")
         self.weight = tnn.Parameter(torch.full((1,), float(init)))
 
+    def forward(self, x):
+        x4 = self._x(_as_nchw(x))
+        return torch.ops.rr.prelu(x4, self.weight, self._dt()).view(x.shape)
+
 
 class ReLU(_Leaf):
     def __init__(self, inplace=False):
         super().__init__()
         self.inplace = inplace
+
+    def forward(self, x):
+        """a new tensor also for inplace=True (the value torch returns)"""
+        x4 = self._x(_as_nchw(x))
+        return torch.ops.rr.relu(x4, self._dt()).view(x.shape)
 
 
 class MaxPool2d(_Leaf):
@@ -117,6 +162,9 @@ class MaxPool2d(_Leaf):
         if kernel_size != 2 or (stride or 2) != 2:
             raise NotImplementedError("only MaxPool2d(2, 2)")
         self.kernel_size, self.stride = 2, 2
+
+    def forward(self, x):
+        return torch.ops.rr.max_pool2d(self._x(x), self._dt())[0]
 
 
 class Linear(_Leaf):
@@ -129,17 +177,46 @@ class Linear(_Leaf):
         b = 1 / math.sqrt(in_features)
         tnn.init.uniform_(self.bias, -b, b)
 
+    def forward(self, x):
+        """forward only (the VGG16 head is the frozen judge, 18:46)"""
+        if not x.is_cuda:
+            raise RuntimeError("roadrestore layers run on the GPU only (no CPU fallback)")
+        if torch.is_grad_enabled() and (x.requires_grad or self.weight.requires_grad
+                                        or self.bias.requires_grad):
+            raise NotImplementedError("Linear runs forward-only (frozen VGG16 judge): use "
+                                      "torch.no_grad() or freeze its parameters")
+        lead = x.shape[:-1]
+        y = torch.ops.rr.linear(x.float().reshape(-1, x.shape[-1]), self.weight, self.bias,
+                                self._dt())
+        return y.view(*lead, -1)
+
 
 class Dropout(_Leaf):
     def __init__(self, p=0.5):
         super().__init__()
         self.p = p
 
+    def forward(self, x):
+        """eval (the judge, 18:46): the identity.  Training-mode dropout
+        (VGG16 training, 05) is out of scope."""
+        if self.training and self.p > 0:
+            raise NotImplementedError("training-mode Dropout is out of scope (eval: identity)")
+        return x
+
 
 class AdaptiveAvgPool2d(_Leaf):
     def __init__(self, output_size):
         super().__init__()
         self.output_size = output_size
+
+    def forward(self, x):
+        """forward only (the frozen judge's head)"""
+        x = self._x(x)
+        if torch.is_grad_enabled() and x.requires_grad:
+            raise NotImplementedError("AdaptiveAvgPool2d runs forward-only (frozen VGG16 judge)")
+        o = self.output_size
+        oh, ow = (o, o) if isinstance(o, int) else o
+        return torch.ops.rr.adaptive_avg_pool2d(x, oh, ow, self._dt())
 
 
 # ---------------------------------------------------------------------------

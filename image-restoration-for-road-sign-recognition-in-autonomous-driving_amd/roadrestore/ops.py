@@ -23,7 +23,7 @@ __all__ = [
     "loss_fwd", "loss_bwd", "adamw_", "to_uint8_hwc", "psnr_u8", "argmax_rows",
     "adaptive_avgpool_flatten", "zero_", "resize_bilinear_u8", "ssim_u8", "distort_u8",
     "motion_blur_kernel", "first_conv_wgrad_act", "affine_act_pool", "nearest_resize",
-    "nearest_resize_bwd", "fold_conv_bn",
+    "nearest_resize_bwd", "fold_conv_bn", "bn_stats",
 ]
 
 
@@ -500,6 +500,17 @@ def channel_sum(x, out=None, accumulate=False):
     lib().check(lib().rr_channel_sum(rr_dtype(x.dtype), P, Cc, _p(x), _p(out), int(accumulate),
                                      _p(ws), ws.numel(), stream()), "rr_channel_sum")
     return out
+
+
+def bn_stats(x):
+    """(sum, sum of squares) partials [blocks, C, 2] of an NHWC tensor, for
+    ``bn_finalize(st, count=P, ...)`` (a standalone BatchNorm2d)."""
+    _need_cuda(x)
+    Cc = x.shape[-1]
+    P = x.numel() // Cc
+    st = torch.empty((lib().rr_bn_stats_blocks(P), Cc, 2), dtype=torch.float32, device=x.device)
+    lib().check(lib().rr_bn_stats(rr_dtype(x.dtype), P, Cc, _p(x), _p(st), stream()), "rr_bn_stats")
+    return st
 
 
 # ---------------------------------------------------------------------------

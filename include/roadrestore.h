@@ -286,6 +286,14 @@ int rr_channel_sum(int dtype, long long P, int C, const void *x, float *out,
                    int accumulate, void *ws, size_t ws_bytes, rr_stream stream);
 size_t rr_channel_sum_workspace(long long P, int C);
 
+/* per-block (sum, sum of squares) partials [blocks][C][2] of an NHWC [P][C]
+   tensor, blocks = rr_bn_stats_blocks(P): the batch statistics of a
+   standalone train-mode BatchNorm2d (torch.nn.BatchNorm2d.forward, the
+   leaf-module path of 14:100-104 when called on its own), finalized by
+   rr_bn_finalize with count = P */
+int rr_bn_stats_blocks(long long P);
+int rr_bn_stats(int dtype, long long P, int C, const void *x, float *partial, rr_stream stream);
+
 /* MaxPool2d(2,2) floor mode (07:82, 14:125): y and 1-byte argmax (0..3) */
 int rr_maxpool2_fwd(int dtype, int n, int h, int w, int C, const void *x,
                     void *y, uint8_t *idx, rr_stream stream);

@@ -1,0 +1,224 @@
+"""Leaf modules called on their own (roadrestore.layers, torch.ops.rr.<layer>)
+against torch.nn.functional in fp64 on the CPU, the plain PyTorch reference of
+the same layer.  Covers what a caller of the reference does outside the fused
+network schedules: ``model.enc1(x)`` (14:153), ``block.conv_block(x)``
+(14:114), ``vgg.features[:k](x)`` (11:39), the VGG16 head.
+
+Tolerances (fp32 compute): relative L2 <= 1e-5 for outputs and input / weight
+grads (fp32 MFMA accumulation over K <= 1152 terms); running statistics within
+1e-6 relative.  bf16 compute: relative L2 <= 1e-2."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import roadrestore as rr
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _leaf_grads(mod, x, g, dev):
+    xd = x.to(dev).requires_grad_(True)
+    y = mod(xd)
+    y.backward(g.to(dev))
+    return y, xd.grad
+
+
+@pytest.mark.parametrize("cin,cout,k,hw", [(3, 64, 3, (16, 16)), (64, 128, 3, (12, 20)),
+                                           (128, 64, 3, (8, 8)), (64, 128, 1, (10, 6)),
+                                           (64, 3, 1, (16, 16)), (384, 128, 3, (8, 8))])
+def test_conv2d_leaf(dev, cin, cout, k, hw):
+    torch.manual_seed(cin + cout + k)
+    m = rr.Conv2d(cin, cout, k, padding=k // 2).to(dev)
+    x = torch.randn(2, cin, *hw)
+    g = torch.randn(2, cout, *hw)
+    y, gx = _leaf_grads(m, x, g, dev)
+    w, b = m.weight.detach().cpu().double().requires_grad_(True), \
+        m.bias.detach().cpu().double().requires_grad_(True)
+    xr = x.double().requires_grad_(True)
+    yr = F.conv2d(xr, w, b, padding=k // 2)
+    yr.backward(g.double())
+    assert rel(y, yr) <= 1e-5
+    assert rel(gx, xr.grad) <= 1e-5
+    assert rel(m.weight.grad, w.grad) <= 1e-5
+    assert rel(m.bias.grad, b.grad) <= 1e-5
+
+
+def test_conv2d_leaf_bf16(dev):
+    torch.manual_seed(7)
+    m = rr.Conv2d(64, 128, 3, padding=1).to(dev)
+    m.compute_dtype = torch.bfloat16
+    x = torch.randn(4, 64, 16, 16)
+    y = m(x.to(dev))
+    yr = F.conv2d(x.double(), m.weight.detach().cpu().double(), m.bias.detach().cpu().double(),
+                  padding=1)
+    assert rel(y, yr) <= 1e-2
+
+
+def test_conv_transpose2d_leaf(dev):
+    torch.manual_seed(3)
+    m = rr.ConvTranspose2d(128, 64, 2, stride=2).to(dev)
+    x = torch.randn(2, 128, 6, 10)
+    g = torch.randn(2, 64, 12, 20)
+    y, gx = _leaf_grads(m, x, g, dev)
+    w = m.weight.detach().cpu().double().requires_grad_(True)
+    b = m.bias.detach().cpu().double().requires_grad_(True)
+    xr = x.double().requires_grad_(True)
+    yr = F.conv_transpose2d(xr, w, b, stride=2)
+    yr.backward(g.double())
+    assert rel(y, yr) <= 1e-5
+    assert rel(gx, xr.grad) <= 1e-5
+    assert rel(m.weight.grad, w.grad) <= 1e-5
+    assert rel(m.bias.grad, b.grad) <= 1e-5
+
+
+@pytest.mark.parametrize("training", [True, False])
+@pytest.mark.parametrize("C,hw", [(64, (16, 16)), (128, (5, 7)), (12, (9, 9))])
+def test_batchnorm_leaf(dev, training, C, hw):
+    torch.manual_seed(C)
+    m = rr.BatchNorm2d(C).to(dev)
+    with torch.no_grad():
+        m.weight.copy_(torch.rand(C) + 0.5)
+        m.bias.copy_(torch.randn(C))
+        m.running_mean.copy_(torch.randn(C) * 0.1)
+        m.running_var.copy_(torch.rand(C) + 0.5)
+    rm0, rv0 = m.running_mean.cpu().double(), m.running_var.cpu().double()
+    m.train(training)
+    x = torch.randn(3, C, *hw) * 2 + 0.5
+    g = torch.randn(3, C, *hw)
+    y, gx = _leaf_grads(m, x, g, dev)
+    w = m.weight.detach().cpu().double().requires_grad_(True)
+    b = m.bias.detach().cpu().double().requires_grad_(True)
+    xr = x.double().requires_grad_(True)
+    rm, rv = rm0.clone(), rv0.clone()
+    yr = F.batch_norm(xr, rm, rv, w, b, training=training, momentum=0.1, eps=1e-5)
+    yr.backward(g.double())
+    assert rel(y, yr) <= 1e-5
+    assert rel(gx, xr.grad) <= 1e-5
+    assert rel(m.weight.grad, w.grad) <= 1e-5
+    assert rel(m.bias.grad, b.grad) <= 1e-5
+    assert rel(m.running_mean, rm) <= 1e-6
+    assert rel(m.running_var, rv) <= 1e-6
+    assert int(m.num_batches_tracked) == (1 if training else 0)
+
+
+def test_batchnorm_leaf_rejects_single_value_per_channel(dev):
+    m = rr.BatchNorm2d(64).to(dev)
+    with pytest.raises(ValueError, match="more than 1 value"):
+        m(torch.randn(1, 64, 1, 1, device=dev))
+
+
+def test_prelu_relu_leaves(dev):
+    torch.manual_seed(5)
+    x = torch.randn(2, 64, 9, 11)
+    x[0, 0, 0, :4] = 0.0                        # the x == 0 boundary: slope branch
+    g = torch.randn_like(x)
+    p = rr.PReLU().to(dev)
+    with torch.no_grad():
+        p.weight.fill_(0.3)
+    y, gx = _leaf_grads(p, x, g, dev)
+    a = torch.full((1,), 0.3, dtype=torch.float64, requires_grad=True)
+    xr = x.double().requires_grad_(True)
+    yr = F.prelu(xr, a)
+    yr.backward(g.double())
+    assert rel(y, yr) <= 1e-6 and rel(gx, xr.grad) <= 1e-6
+    assert rel(p.weight.grad, a.grad) <= 1e-5
+    r = rr.ReLU(inplace=True).to(dev)
+    y, gx = _leaf_grads(r, x, g, dev)
+    xr = x.double().requires_grad_(True)
+    yr = F.relu(xr)
+    yr.backward(g.double())
+    assert rel(y, yr) <= 1e-6 and rel(gx, xr.grad) <= 1e-6
+
+
+@pytest.mark.parametrize("hw", [(16, 16), (17, 15)])
+def test_maxpool_leaf(dev, hw):
+    torch.manual_seed(11)
+    x = torch.randn(2, 64, *hw)
+    g = torch.randn(2, 64, hw[0] // 2, hw[1] // 2)
+    y, gx = _leaf_grads(rr.MaxPool2d(2, 2), x, g, dev)
+    xr = x.double().requires_grad_(True)
+    yr = F.max_pool2d(xr, 2, 2)
+    yr.backward(g.double())
+    assert torch.equal(y.cpu().double(), yr.detach())
+    assert torch.equal(gx.cpu().double(), xr.grad)
+
+
+def _ref_resunet_enc1(sd, x):
+    return F.prelu(F.conv2d(x, sd["enc1.0.weight"], sd["enc1.0.bias"], padding=1),
+                   sd["enc1.1.weight"])
+
+
+def test_resunet_submodules_called_directly(dev):
+    """model.enc1(x) and model.res1.conv_block(x) (train mode: batch
+    statistics, running statistics updated) as the reference's modules."""
+    torch.manual_seed(0)
+    m = rr.ResUNet().to(dev)
+    sd = {k: v.detach().cpu().double() for k, v in m.state_dict().items()}
+    x = torch.randn(2, 3, 16, 16)
+    e1 = m.enc1(x.to(dev))
+    e1r = _ref_resunet_enc1(sd, x.double())
+    assert rel(e1, e1r) <= 1e-5
+    cb = m.res1.conv_block
+    t = cb(e1.detach())
+    p = "res1.conv_block."
+    rm1, rv1 = sd[p + "1.running_mean"].clone(), sd[p + "1.running_var"].clone()
+    rm2, rv2 = sd[p + "4.running_mean"].clone(), sd[p + "4.running_var"].clone()
+    h = F.conv2d(e1r, sd[p + "0.weight"], sd[p + "0.bias"], padding=1)
+    h = F.batch_norm(h, rm1, rv1, sd[p + "1.weight"], sd[p + "1.bias"], training=True)
+    h = F.prelu(h, sd[p + "2.weight"])
+    h = F.conv2d(h, sd[p + "3.weight"], sd[p + "3.bias"], padding=1)
+    tr = F.batch_norm(h, rm2, rv2, sd[p + "4.weight"], sd[p + "4.bias"], training=True)
+    assert rel(t, tr) <= 1e-4
+    assert rel(cb[1].running_var, rv1) <= 1e-5 and rel(cb[4].running_mean, rm2) <= 1e-5
+
+
+def test_vgg_feature_slices_and_head(dev):
+    """vgg.features[:k](x) (11:39) layer by layer against F, and the head
+    (avgpool -> flatten -> classifier) against the fused judge's logits."""
+    torch.manual_seed(1)
+    v = rr.vgg16(num_classes=43).to(dev).eval()
+    x = torch.rand(2, 3, 32, 32)
+    sd = {k: val.detach().cpu().double() for k, val in v.state_dict().items()}
+    with torch.no_grad():
+        f = v.features[:10](x.to(dev))
+    h = x.double()
+    for i, mod in enumerate(list(v.features)[:10]):
+        if isinstance(mod, rr.Conv2d):
+            h = F.conv2d(h, sd[f"features.{i}.weight"], sd[f"features.{i}.bias"], padding=1)
+        elif isinstance(mod, rr.ReLU):
+            h = F.relu(h)
+        else:
+            h = F.max_pool2d(h, 2, 2)
+    assert rel(f, h) <= 1e-5
+    with torch.no_grad():
+        feats = v.features(x.to(dev))
+        logits = v.classifier(torch.flatten(v.avgpool(feats), 1))
+        fused = v(x.to(dev))
+    assert rel(logits, fused) <= 1e-5
+    # gradient through a feature slice (a hidden-state saliency map)
+    xg = x.to(dev).requires_grad_(True)
+    v.features[:4](xg).sum().backward()
+    xr = x.double().requires_grad_(True)
+    hr = F.relu(F.conv2d(xr, sd["features.0.weight"], sd["features.0.bias"], padding=1))
+    hr = F.relu(F.conv2d(hr, sd["features.2.weight"], sd["features.2.bias"], padding=1))
+    hr.sum().backward()
+    assert rel(xg.grad, xr.grad) <= 1e-5
+
+
+def test_bn_stats_partials(dev):
+    """rr_bn_stats: per-block (sum, sum of squares), summed over blocks,
+    against fp64 (ragged row count, bf16 input)."""
+    torch.manual_seed(2)
+    for P, C, dt in ((2071, 64, torch.float32), (37, 12, torch.float32),
+                     (70001, 128, torch.bfloat16)):
+        x = torch.randn(P, C).to(dt)
+        st = rr.ops.bn_stats(x.to(dev))
+        s = st.double().sum(0).cpu()
+        xd = x.double()
+        assert rel(s[:, 0], xd.sum(0)) <= 1e-5
+        assert rel(s[:, 1], (xd * xd).sum(0)) <= 1e-6
