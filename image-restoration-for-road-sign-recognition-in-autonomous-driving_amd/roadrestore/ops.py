@@ -610,7 +610,8 @@ def first_conv_fwd(x_nchw, wt, b, dtype, wpack, act=0, alpha=None, want_pre=Fals
         return y, (pre if want_pre else None)
     if act == 1 and want_pre:
         pre, _, _ = igemm(RR_CONV1X1, col, None, n, h, w, wpack, cout)
-        y = torch.clamp_min(pre, 0)
+        one = torch.ones(cout, dtype=torch.float32, device=x_nchw.device)
+        y = affine_act(pre, one, torch.zeros_like(one), relu=True)
         return y, pre
     y, _, _ = igemm(RR_CONV1X1, col, None, n, h, w, wpack, cout, act=act)
     return y, (y if (want_pre and not act) else None)
