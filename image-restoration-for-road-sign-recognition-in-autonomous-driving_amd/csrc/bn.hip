@@ -421,6 +421,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwd a, float *__r
   float asum = 0.f;
   const long long r0 = blockIdx.x * rows_per_block;
   const long long r1 = min(a.P, r0 + rows_per_block);
+  // 2 rows per trip: the second row's loads issue before the first row's
+  // math (no stores in the loop, so nothing orders them); same add order
+#pragma unroll 2
   for (long long r = r0 + tr; r < r1; r += R) {
     const long long e = r * a.C + c;
     float gm[8], t0[8], t1[8];
@@ -677,6 +680,7 @@ __global__ void colsum_kernel(long long P, int C, const T *__restrict__ x, float
   const long long r0 = blockIdx.x * rows_per_block;
   const long long r1 = min(P, r0 + rows_per_block);
   if (tr < R) {
+#pragma unroll 4
     for (long long r = r0 + tr; r < r1; r += R) {
       const f32x4 v = load4<T>(x + r * C + tc * 4);
 #pragma unroll
@@ -723,6 +727,7 @@ __global__ void colstats_kernel(long long P, int C, const T *__restrict__ x, flo
   const long long r0 = blockIdx.x * rows_per_block;
   const long long r1 = min(P, r0 + rows_per_block);
   if (tr < R) {
+#pragma unroll 4
     for (long long r = r0 + tr; r < r1; r += R) {
       const f32x4 v = load4<T>(x + r * C + tc * 4);
 #pragma unroll

@@ -479,7 +479,7 @@ __global__ __launch_bounds__(256) void conv_in_mfma_kernel(int n, int h, int w,
                                                            bf16_t *__restrict__ y_pre,
                                                            bf16_t *__restrict__ y_act) {
   constexpr int SR = 68;                       // fp32 staging row (floats), padded
-  __shared__ __attribute__((aligned(16))) float stg[4][64 * SR];
+  __shared__ __attribute__((aligned(16))) float stg[4][32 * SR];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const long long hw = (long long)h * w;
   const long long P = (long long)n * hw;
@@ -536,33 +536,41 @@ __global__ __launch_bounds__(256) void conv_in_mfma_kernel(int n, int h, int w,
       acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi], fb, f32x4{0.f, 0.f, 0.f, 0.f},
                                                            0, 0, 0);
   }
-  // stage: pixel ni*16 + fr, channels 16 mi + 4 q .. +3
+  // epilogue in two halves of 32 pixels (ni 0-1, then 2-3): a 32-row fp32
+  // staging tile per wave (35 KB per workgroup instead of 70) lets 4
+  // workgroups share a CU instead of 2.  Stage: pixel ni*16 + fr, channels
+  // 16 mi + 4 q .. +3
   float *sw = stg[wv];
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-      *reinterpret_cast<f32x4 *>(sw + (ni * 16 + fr) * SR + mi * 16 + q * 4) = acc[mi][ni];
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS writes landed
   // negative-side slope: 1 (none), 0 (ReLU), alpha (PReLU)
   const float slope = act == 2 ? alpha[0] : (act == 1 ? 0.f : 1.f);
   const int rows = (int)min(64LL, P - p0);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int r = i * 8 + (lane >> 3), c8 = (lane & 7) * 8;
-    if (r < rows) {
-      const long long p = p0 + r;
-      const f32x4 v0 = *reinterpret_cast<const f32x4 *>(sw + r * SR + c8);
-      const f32x4 v1 = *reinterpret_cast<const f32x4 *>(sw + r * SR + c8 + 4);
-      if (y_pre) store8<bf16_t>(y_pre + p * 64 + c8, v0, v1);
-      if (y_act) {
-        f32x4 a0, a1;
+  for (int half = 0; half < 2; ++half) {
+    if (half) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // first half read back
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          a0[k] = v0[k] > 0.f ? v0[k] : slope * v0[k];
-          a1[k] = v1[k] > 0.f ? v1[k] : slope * v1[k];
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj)
+        *reinterpret_cast<f32x4 *>(sw + (nj * 16 + fr) * SR + mi * 16 + q * 4) = acc[mi][half * 2 + nj];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS writes landed
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rl = i * 8 + (lane >> 3), c8 = (lane & 7) * 8;
+      const int r = half * 32 + rl;
+      if (r < rows) {
+        const long long p = p0 + r;
+        const f32x4 v0 = *reinterpret_cast<const f32x4 *>(sw + rl * SR + c8);
+        const f32x4 v1 = *reinterpret_cast<const f32x4 *>(sw + rl * SR + c8 + 4);
+        if (y_pre) store8<bf16_t>(y_pre + p * 64 + c8, v0, v1);
+        if (y_act) {
+          f32x4 a0, a1;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            a0[k] = v0[k] > 0.f ? v0[k] : slope * v0[k];
+            a1[k] = v1[k] > 0.f ? v1[k] : slope * v1[k];
+          }
+          store8<bf16_t>(y_act + p * 64 + c8, a0, a1);
         }
-        store8<bf16_t>(y_act + p * 64 + c8, a0, a1);
       }
     }
   }
