@@ -473,18 +473,37 @@ __global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(BnBwd a, const float
   const int G = a.C / 8;
   const int c = (threadIdx.x % G) * 8;   // fixed: G divides the grid stride
   constexpr bool AFF = MASK == 2 || MASK >= 4, REC = MASK >= 4;
-  float cf[2][3][8], mu[2][8], iv[2][8], s8[8], b8[8], sB[8], bB[8];
+  // dt = c0 (gm - c1 - (t - mu) inv c2) folded to dt = A gm + B t + D: three
+  // per-channel constants per BN in registers instead of five (the NBN = 2
+  // variants sat at 162-172 VGPRs, 2-3 waves per SIMD)
+  // the recomputed-mask affines (MASK 4/5: four per channel) are read from
+  // LDS per row instead of held in registers
+  float fA[2][8], fB[2][8], fD[2][8], s8[8], b8[8], sB[8], bB[8];
+  __shared__ __attribute__((aligned(16))) float rcs[REC ? 4 * 1024 : 4];
+  if constexpr (REC) {
+    for (int i = threadIdx.x; i < a.C; i += blockDim.x) {
+      rcs[i] = a.aff_s[i]; rcs[1024 + i] = a.aff_b[i];
+      rcs[2048 + i] = a.aff_s[a.C + i]; rcs[3072 + i] = a.aff_b[a.C + i];
+    }
+    __syncthreads();
+  }
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      cf[0][j][k] = coef[(c + k) * 6 + j];
-      cf[1][j][k] = NBN == 2 ? coef[(c + k) * 6 + 3 + j] : 0.f;
+    for (int b = 0; b < 2; ++b) {
+      float c0 = 0.f, c1 = 0.f, c2 = 0.f, mu = 0.f, iv = 0.f;
+      if (b < NBN) {
+        c0 = coef[(c + k) * 6 + 3 * b]; c1 = coef[(c + k) * 6 + 3 * b + 1];
+        c2 = coef[(c + k) * 6 + 3 * b + 2];
+        mu = (b == 0 ? a.mean0 : a.mean1)[c + k]; iv = (b == 0 ? a.inv0 : a.inv1)[c + k];
+      }
+      const float q = c0 * c2 * iv;
+      fA[b][k] = c0;
+      fB[b][k] = -q;
+      fD[b][k] = fmaf(q, mu, -c0 * c1);
     }
-    mu[0][k] = a.mean0[c + k]; iv[0][k] = a.inv0[c + k];
-    mu[1][k] = NBN == 2 ? a.mean1[c + k] : 0.f; iv[1][k] = NBN == 2 ? a.inv1[c + k] : 0.f;
-    s8[k] = AFF ? a.aff_s[c + k] : 0.f; b8[k] = AFF ? a.aff_b[c + k] : 0.f;
-    sB[k] = REC ? a.aff_s[a.C + c + k] : 0.f; bB[k] = REC ? a.aff_b[a.C + c + k] : 0.f;
+    s8[k] = AFF && !REC ? a.aff_s[c + k] : 0.f; b8[k] = AFF && !REC ? a.aff_b[c + k] : 0.f;
+    sB[k] = 0.f; bB[k] = 0.f;
   }
   const float al = MASK == 2 ? a.alpha[0] : 0.f;
   const long long rows = a.P;
@@ -499,7 +518,19 @@ __global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(BnBwd a, const float
       tv[b][0] = u0[0]; tv[b][1] = u0[1]; tv[b][2] = u0[2]; tv[b][3] = u0[3];
       tv[b][4] = u1[0]; tv[b][5] = u1[1]; tv[b][6] = u1[2]; tv[b][7] = u1[3];
     }
-    bwd_gm8<T, MASK>(a, e, s8, b8, al, gm, ag, tv[0], tv[NBN - 1], sB, bB);
+    if constexpr (REC) {
+      float l[4][8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 u = *reinterpret_cast<const f32x4 *>(rcs + 1024 * j + c);
+        const f32x4 v = *reinterpret_cast<const f32x4 *>(rcs + 1024 * j + c + 4);
+        l[j][0] = u[0]; l[j][1] = u[1]; l[j][2] = u[2]; l[j][3] = u[3];
+        l[j][4] = v[0]; l[j][5] = v[1]; l[j][6] = v[2]; l[j][7] = v[3];
+      }
+      bwd_gm8<T, MASK>(a, e, l[0], l[1], al, gm, ag, tv[0], tv[NBN - 1], l[2], l[3]);
+    } else {
+      bwd_gm8<T, MASK>(a, e, s8, b8, al, gm, ag, tv[0], tv[NBN - 1], sB, bB);
+    }
     if constexpr (GMO)
       store8<T>(gmo + e, f32x4{gm[0], gm[1], gm[2], gm[3]}, f32x4{gm[4], gm[5], gm[6], gm[7]});
 #pragma unroll
@@ -507,10 +538,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(BnBwd a, const float
       const float *t = tv[b];
       float o[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float xh = (t[k] - mu[b][k]) * iv[b][k];
-        o[k] = cf[b][0][k] * (gm[k] - cf[b][1][k] - xh * cf[b][2][k]);
-      }
+      for (int k = 0; k < 8; ++k) o[k] = fmaf(fB[b][k], t[k], fmaf(fA[b][k], gm[k], fD[b][k]));
       store8<T>((b == 0 ? dt0 : dt1) + e, f32x4{o[0], o[1], o[2], o[3]}, f32x4{o[4], o[5], o[6], o[7]});
     }
   }
