@@ -4,7 +4,8 @@ without its LDS fragment reads (2), without both (3); full time of the
 unsplit staging (RR_HALO_DBGK=32) beside the weight/halo role split, and
 of the next-chunk halo issued all at tap 0 (64) beside its spread over taps,
 and weights 3 stages ahead (128) beside 2 (BC = 128 only; at BC = 64 these
-select the same unsplit kernel, so their spread there is the noise)."""
+select the same unsplit kernel, so their spread there is the noise).
+DBGK_LIST=0,32,1,2,3 (env) picks the K-loop variants timed without the epilogue."""
 import json, os, sys
 R_ = os.path.join(os.path.dirname(__file__), "..")
 sys.path.insert(0, os.path.join(R_, "image-restoration-for-road-sign-recognition-in-autonomous-driving_amd"))
@@ -42,7 +43,7 @@ for name, H, c1, c2, co in LAYERS:
     for k, tag in ((32, "unsplit"), (64, "unsliced"), (128, "w3ahead")):
         os.environ["RR_HALO_DBGK"] = str(k)
         r[f"full_{tag}_ms"] = round(timeit(lambda: ops.igemm(RR_CONV3X3, x1, None, B, H, H, wf, co, stats=True)), 4)
-    for k in (0,):
+    for k in [int(v) for v in os.environ.get("DBGK_LIST", "0").split(",")]:
         os.environ["RR_IGEMM_DBG"] = "1"
         os.environ["RR_HALO_DBGK"] = str(k)
         t = timeit(lambda: ops.igemm(RR_CONV3X3, x1, None, B, H, H, wf, co, stats=True))
