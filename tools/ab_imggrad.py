@@ -1,0 +1,46 @@
+"""Timing of the perceptual image gradient (VGG conv1_1 dgrad, 64 -> 3 channels,
+NCHW fp32 out accumulated onto the L1 grad; the igemm3_halo_kernel<16,64>
+tile) at B = 512, 64x64: the 256-pixel tile (2 workgroups per CU by LDS) vs
+the 128-pixel tile (RR_HALO_BP=128, 4 per CU)."""
+import json
+import os
+import sys
+
+R_ = os.path.join(os.path.dirname(__file__), "..")
+sys.path.insert(0, os.path.join(R_, "image-restoration-for-road-sign-recognition-in-autonomous-driving_amd"))
+import torch  # noqa: E402
+from roadrestore import ops  # noqa: E402
+from roadrestore._lib import RR_CONV3X3  # noqa: E402
+
+dev = torch.device("cuda:0")
+B, H = 512, 64
+
+
+def timeit(fn, reps=20):
+    for _ in range(3):
+        fn()
+    ts = []
+    for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record(); fn(); e.record()
+        ts.append((s, e))
+    torch.cuda.synchronize()
+    v = sorted(s.elapsed_time(e) for s, e in ts)
+    return v[len(v) // 2]
+
+
+g = torch.randn(B, H, H, 64, device=dev).bfloat16()
+w = torch.randn(64, 3, 3, 3, device=dev) * 0.1
+_, wd = ops.pack_conv(w, torch.bfloat16)
+out = torch.zeros(B, 3, H, H, device=dev)
+ref = None
+r = {}
+for tag, env in (("bp256", {}), ("bp128", {"RR_HALO_BP": "128"}), ("bp256_again", {})):
+    os.environ.pop("RR_HALO_BP", None)
+    os.environ.update(env)
+    y = ops.conv_in_dgrad(g, w, 3, wpack_dgrad=wd)
+    ref = y if ref is None else ref
+    r[tag + "_equal"] = bool(torch.equal(y, ref))
+    r[tag + "_ms"] = round(timeit(lambda: ops.conv_in_dgrad(g, w, 3, out=out, accumulate=True,
+                                                            wpack_dgrad=wd)), 4)
+print(json.dumps(r), flush=True)
