@@ -658,7 +658,11 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
   constexpr int MAIN = HB * G::HBYTES + 2 * WBYTES;
   constexpr int SROW = BC + 4;
   constexpr int STG = BP * SROW * 4 + 2 * NT * 4 * 2 + 256;
-  constexpr int SMEM = MAIN > STG ? MAIN : STG;
+  // the persistent image-grad tile (BC < 64, below): halo + all 9 taps' weights
+  constexpr int ONE_BYTES = BC < 64 ? G::HBYTES + 9 * WBYTES : 0;
+  static_assert(BC >= 64 || STG <= G::HBYTES, "image-grad staging tile aliases the halo only");
+  constexpr int SMEM0 = MAIN > STG ? MAIN : STG;
+  constexpr int SMEM = SMEM0 > ONE_BYTES ? SMEM0 : ONE_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   char *const hbuf = smem;                                      // [HB][HBYTES]
   char *const wbuf = smem + HB * G::HBYTES;                     // [2][WBYTES]
@@ -727,6 +731,116 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
   const int kch = a.cin / 64;
   const int nst = kch * 9;
   typedef uint4 V;
+
+  // Persistent image-grad tile (BC < 64: conv1_1's dgrad into the NCHW fp32
+  // image grad, one 64-channel K chunk, one column block).  The one-shot
+  // tile was bound by its halo load (a ~50 KB gather, then 4 MFMAs per wave
+  // per tap): here each workgroup walks tiles blockIdx.x + k gridDim.x with
+  // the NEXT tile's halo loading into registers while the current one
+  // computes and stores; the 9 taps' weights (9 x 2 KB) are staged once.
+  if constexpr (BC < 64 && DBGK == 0) {
+    const int ntile = a.P / BP;
+    if (kch == 1 && a.ncblk == 1 && !(a.dbg & 3) && (int)gridDim.x < ntile) {
+      char *const wall = smem + G::HBYTES;
+      for (int i = tid; i < 9 * WPIECES; i += NT) {
+        const int tp = i / WPIECES, idx = i - tp * WPIECES;
+        const int r = 8 * (idx >> 6) + (idx & 7), j = (idx >> 3) & 7;
+        const bool ok = r < a.cout;
+        V v = *reinterpret_cast<const V *>(a.wt + ((long long)(ok ? r : 0) * a.K +
+                                                   (long long)tp * a.cin) * 2 + j * 16);
+        if (!ok) v = V{0u, 0u, 0u, 0u};
+        *reinterpret_cast<V *>(wall + tp * WBYTES + j * WPLANE + r * 16) = v;
+      }
+      V hr[G::LH];
+      const char *src0 = a.x1 + pj;
+      auto load_h = [&](int t) __attribute__((always_inline)) {
+        const int q0 = t * BP;
+        const int tn0 = q0 / hw;
+        const int ty0 = (q0 - tn0 * hw) / W;
+#pragma unroll
+        for (int i = 0; i < G::LH; ++i) {
+          const int idx = tid + NT * i;
+          const int r = 8 * (idx >> 6) + (idx & 7);
+          int pix = -1;
+          if (r < hrows) {
+            const int im = r / himg, rem = r - (r / himg) * himg;
+            const int hy = rem / (W + 2), hx = rem - (rem / (W + 2)) * (W + 2);
+            const int yy = ty0 - 1 + hy, xx = hx - 1;
+            if (yy >= 0 && yy < a.h && xx >= 0 && xx < W) pix = ((tn0 + im) * a.h + yy) * W + xx;
+          }
+          const bool ok = pix >= 0;
+          V v = *reinterpret_cast<const V *>(src0 + (long long)(ok ? pix : 0) * a.c1 * 2);
+          v.x = ok ? v.x : 0u; v.y = ok ? v.y : 0u; v.z = ok ? v.z : 0u; v.w = ok ? v.w : 0u;
+          hr[i] = v;
+        }
+      };
+      float *const stg = reinterpret_cast<float *>(smem);          // aliases the halo
+      float *const yo = reinterpret_cast<float *>(a.y1);
+      const int ncol = min(BC, a.cout);
+      int t = (int)blockIdx.x;
+      load_h(t);
+      for (; t < ntile; t += (int)gridDim.x) {
+#pragma unroll
+        for (int i = 0; i < G::LH; ++i) {
+          const int idx = tid + NT * i;
+          const int r = 8 * (idx >> 6) + (idx & 7);
+          if (r < hrows) *reinterpret_cast<V *>(hbuf + ((idx >> 3) & 7) * G::PLANE + r * 16) = hr[i];
+        }
+        __syncthreads();                                   // halo(t) (and the weights) visible
+        const int tn = t + (int)gridDim.x;
+        if (tn < ntile) load_h(tn);                        // next tile's halo in flight
+        f32x4 acc[MC][MP];
+#pragma unroll
+        for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < MP; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) {
+          const char *sA = wall + tp * WBYTES;
+          const char *sB = hbuf + ((tp / 3) * (W + 2) + tp % 3) * 16;
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            bf16x8 fa[MC], fb[MP];
+#pragma unroll
+            for (int mi = 0; mi < MC; ++mi)
+              fa[mi] = *reinterpret_cast<const bf16x8 *>(sA + abase[mi] + kk * 4 * WPLANE);
+#pragma unroll
+            for (int ni = 0; ni < MP; ++ni)
+              fb[ni] = *reinterpret_cast<const bf16x8 *>(sB + bbase[ni] + kk * 4 * G::PLANE);
+#pragma unroll
+            for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+              for (int ni = 0; ni < MP; ++ni)
+                acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi], fb[ni], acc[mi][ni], 0, 0, 0);
+          }
+        }
+        __syncthreads();                                   // every wave done reading halo(t)
+#pragma unroll
+        for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < MP; ++ni) {
+            const int r = wp * (BP / WP) + ni * 16 + frow;
+            const int col = wc * WCH + mi * 16 + fq * 4;
+            *reinterpret_cast<f32x4 *>(stg + r * SROW + col) = acc[mi][ni];
+          }
+        __syncthreads();
+        const int q0 = t * BP;
+        for (int i = tid; i < ncol * BP; i += NT) {
+          const int cl = i / BP, r = i - (i / BP) * BP;
+          const int p = q0 + r;
+          const int nn = p / hw, rem = p - nn * hw;
+          float v = stg[r * SROW + cl] + (a.bias ? a.bias[cl] : 0.f);
+          const long long o = ((long long)nn * a.cout + cl) * hw + rem;
+          if (a.accumulate) v += yo[o];
+          if (a.act == RR_ACT_RELU) v = fmaxf(v, 0.f);
+          yo[o] = v;
+        }
+        __syncthreads();                                   // staging read before halo(t+1) lands
+      }
+      return;
+    }
+  }
+
   V hreg[G::LH];
   // weights prefetched 2 stages ahead (register set = stage parity).  DBGK
   // bit7 (BC = 128): 3 ahead, register set k % 3 holding W(k) (9 taps per
@@ -1230,7 +1344,15 @@ int launch_halo(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   a.ncblk = (a.cout + BC - 1) / BC;
   const long long nblk = (long long)(a.P / BP) * a.ncblk;
   if (nblk > 0x7fffffffLL) return RR_EUNSUPPORTED;
-  const dim3 grid((unsigned)nblk), block(NT);
+  dim3 grid((unsigned)nblk), block(NT);
+  // the image-grad tile runs persistent (2 workgroups per CU, each walking
+  // tiles with the next halo in flight) when it has one K chunk
+  // (RR_IMGGRAD_PERSIST=0: one tile per workgroup, for A/B)
+  if constexpr (BC < 64) {
+    const char *e = getenv("RR_IMGGRAD_PERSIST");            // per call (A/B)
+    const bool persist = !(e && atoi(e) == 0);
+    if (persist && a.cin == 64 && a.ncblk == 1 && !a.dbg && nblk > 512) grid = dim3(512);
+  }
   if constexpr (BC == 128 && BP == 256 && NT == 512) {
     if (launch_halo_dbgk<BC, 8, BP, NT>(d, a, grid, block, st) || launch_halo_dbgk<BC, 16, BP, NT>(d, a, grid, block, st) ||
         launch_halo_dbgk<BC, 32, BP, NT>(d, a, grid, block, st)) {

@@ -1,7 +1,8 @@
 """Timing of the perceptual image gradient (VGG conv1_1 dgrad, 64 -> 3 channels,
 NCHW fp32 out accumulated onto the L1 grad; the igemm3_halo_kernel<16,64>
-tile) at B = 512, 64x64: the 256-pixel tile (2 workgroups per CU by LDS) vs
-the 128-pixel tile (RR_HALO_BP=128, 4 per CU)."""
+tile) at B = 512, 64x64: the persistent tile walk with the next halo in
+flight (default) vs one tile per workgroup (RR_IMGGRAD_PERSIST=0) vs the
+128-pixel one-shot tile (RR_HALO_BP=128); outputs must be bit-identical."""
 import json
 import os
 import sys
@@ -35,8 +36,11 @@ _, wd = ops.pack_conv(w, torch.bfloat16)
 out = torch.zeros(B, 3, H, H, device=dev)
 ref = None
 r = {}
-for tag, env in (("bp256", {}), ("bp128", {"RR_HALO_BP": "128"}), ("bp256_again", {})):
+for tag, env in (("persist", {}), ("one_shot", {"RR_IMGGRAD_PERSIST": "0"}),
+                 ("bp128", {"RR_HALO_BP": "128", "RR_IMGGRAD_PERSIST": "0"}), ("persist_again", {}),
+                 ("one_shot_again", {"RR_IMGGRAD_PERSIST": "0"})):
     os.environ.pop("RR_HALO_BP", None)
+    os.environ.pop("RR_IMGGRAD_PERSIST", None)
     os.environ.update(env)
     y = ops.conv_in_dgrad(g, w, 3, wpack_dgrad=wd)
     ref = y if ref is None else ref
