@@ -9,8 +9,11 @@ perceptual (14:238-242), full backward, AdamW(lr 2e-4, wd 1e-4) (14:222,
 245).  Synthetic GTSRB-shaped clean images generated on device.  --repeats
 windows of --steps timed steps each; the median window is reported (SURVEY
 §8d: 10 warm-up + 50 timed steps, median of 3).
-With --gpus N (launched by torch.distributed.run) every rank runs the same
-per-GPU batch and gradients are all-reduced over RCCL (weak scaling).
+With --gpus N every rank runs the same per-GPU batch and gradients are
+all-reduced over RCCL (weak scaling).  Launched by torch.distributed.run
+(WORLD_SIZE set) it is one rank; run directly (``python bench.py --gpus 8``)
+it starts the N ranks itself through torch.distributed.run and exits with
+their status; a WORLD_SIZE that disagrees with --gpus is an error.
 
 Prints ONE JSON line on rank 0 with the driver's fields plus
   roofline     -- the dominant kernel's algorithmic FLOP rate vs the MFMA peak,
@@ -135,16 +138,24 @@ def _norm_sym(sym):
 
 def pmc_traffic(sym):
     """HBM bytes per launch of ``sym`` from the committed rocprofv3 PMC
-    summary (FETCH_SIZE x2 + WRITE_SIZE, separate passes; tools/pmc_traffic.py)."""
+    summary (FETCH_SIZE x2 + WRITE_SIZE, separate passes; tools/pmc_traffic.py):
+    the launch-weighted average over every template variant the probe counts
+    under ``sym`` (the same launches as ``algorithmic_bytes_per_launch``),
+    plus the per-variant table.  Returns (bytes or None, {variant: bytes})."""
     try:
         tab = json.load(open(PMC_TRAFFIC))
     except (OSError, ValueError, TypeError):
-        return None
+        return None, {}
     key = _norm_sym(sym)
+    per, tot, n = {}, 0.0, 0
     for k, v in tab.items():
         if _norm_sym(k).startswith(key):
-            return v["hbm_bytes_per_launch"]
-    return None
+            c = int(v.get("launches_per_pass", 1))
+            per[k.lstrip(":")] = {"hbm_bytes_per_launch": v["hbm_bytes_per_launch"],
+                                   "launches_per_pass": c}
+            tot += v["hbm_bytes_per_launch"] * c
+            n += c
+    return (round(tot / n) if n else None), per
 
 
 def cpu_share():
@@ -214,8 +225,37 @@ def cpu_baseline(seconds, size):
                       f"({el:.1f} s); the distortion (DataLoader workers in 14:213) is not in it"}
 
 
+def launch_plan(gpus, argv, env):
+    """How ``bench.py --gpus N`` runs: None = this process is the (only or
+    already launched) rank; else the command that starts N rank processes
+    (torch.distributed.run, one rank per GPU, rendezvous on 127.0.0.1).
+    Raises SystemExit when an outer launcher's WORLD_SIZE disagrees with
+    --gpus (a bench line must never claim N GPUs it did not run on)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus and env.get("RR_BENCH_DP1") != "1":
+            raise SystemExit(f"bench: WORLD_SIZE={ws} but --gpus {gpus}")
+        return None
+    if gpus <= 1:
+        return None
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
+            "--nproc-per-node", str(gpus), "--master-addr", "127.0.0.1",
+            "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
 def main():
     a = parse()
+    # --gpus N without an outer launcher: start the N ranks here, before this
+    # process touches the GPU (a child process, never an exec), and exit
+    # with the launcher's status
+    cmd = launch_plan(a.gpus, sys.argv[1:], os.environ)
+    if cmd is not None:
+        import subprocess
+        raise SystemExit(subprocess.call(cmd))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
@@ -377,16 +417,18 @@ def main():
         pk = PEAK["bf16" if dt == torch.bfloat16 else "f32"]
         # the bound by the kernel's algorithmic intensity vs the ridge point
         hbm_bound = by > 0 and fl / by < pk * 1e12 / (HBM_PEAK_GBS * 1e9)
-        traffic = pmc_traffic(sym)
+        traffic, traffic_per = pmc_traffic(sym)
         roof = {"bound": "hbm" if hbm_bound else "mfma", "kernel": sym,
                 "achieved": round(gbs if hbm_bound else tflops, 2),
                 "peak": HBM_PEAK_GBS if hbm_bound else pk,
                 "unit": "GB/s" if hbm_bound else "TFLOP/s",
                 "frac": round(gbs / HBM_PEAK_GBS if hbm_bound else tflops / pk, 4),
                 "traffic": traffic,
-                "traffic_note": "HBM bytes per launch, rocprofv3 FETCH_SIZE x2 (gfx950) + "
+                "traffic_note": "HBM bytes per launch, launch-weighted over the kernel's "
+                                "variants (traffic_variants): rocprofv3 FETCH_SIZE x2 (gfx950) + "
                                 "WRITE_SIZE in separate --pmc passes of this bench "
                                 f"({os.path.relpath(PMC_TRAFFIC, REPO)})" if traffic else None,
+                "traffic_variants": traffic_per or None,
                 "launches": cnt, "avg_launch_ms": round(ms / cnt, 4),
                 "flop_per_launch": fl / cnt, "algorithmic_bytes_per_launch": by / cnt,
                 "mfma_tflops": round(tflops, 2), "mfma_frac": round(tflops / pk, 4),

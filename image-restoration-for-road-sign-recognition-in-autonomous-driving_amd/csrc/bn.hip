@@ -57,10 +57,14 @@ __device__ __forceinline__ void bn_finalize_direct_channel(const BnFin &a, int c
   const float *bias = a.bias, *gamma = a.gamma, *beta = a.beta;
   float *rmean = a.rmean, *rvar = a.rvar, *scale = a.scale, *shift = a.shift, *smean = a.smean,
         *sinv = a.sinv;
-  const float momentum = a.momentum, eps = a.eps;
+  // momentum < 0: cumulative moving average (nn.BatchNorm2d(momentum=None)),
+  // factor 1 / (num_batches_tracked + 1) read on the device; the count is then
+  // incremented by a separate launch after this one (bn_nbt_inc_kernel)
+  const bool cum = a.momentum < 0.f;
+  const float eps = a.eps;
   __shared__ double red[2][256];
   const int t = threadIdx.x;
-  if (a.nbt && c == 0 && t == 0) a.nbt[0] += 1;
+  if (a.nbt && !cum && c == 0 && t == 0) a.nbt[0] += 1;
   double s[2] = {0.0, 0.0};
   rr_fixed_sum<2>(part + ((long long)t * C + c) * 2, 256LL * C * 2, rr_trips(t, rows, 256), s);
   double s1 = s[0], s2 = s[1];
@@ -85,6 +89,7 @@ __device__ __forceinline__ void bn_finalize_direct_channel(const BnFin &a, int c
     shift[c] = (float)(bt - mean * g * inv);
     if (smean) smean[c] = (float)mean;
     if (sinv) sinv[c] = (float)inv;
+    const double momentum = cum ? 1.0 / (double)(a.nbt[0] + 1) : (double)a.momentum;
     if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
     if (rvar) {
       const double unb = count > 1 ? var * count / (count - 1) : var;
@@ -93,13 +98,16 @@ __device__ __forceinline__ void bn_finalize_direct_channel(const BnFin &a, int c
   }
 }
 
+__global__ void bn_nbt_inc_kernel(int64_t *nbt) { nbt[0] += 1; }
+
 __global__ void bn_finalize_kernel(int C, int blocks, double count, const double *__restrict__ part,
                                    const float *bias, const float *gamma, const float *beta,
                                    float *rmean, float *rvar, float momentum, float eps,
                                    float *scale, float *shift, float *smean, float *sinv,
                                    int64_t *nbt) {
   __shared__ double red[2][16][17];
-  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
+  const bool cum = momentum < 0.f;                  // as in bn_finalize_direct_channel
+  if (nbt && !cum && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
   const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
   double s[2] = {0.0, 0.0};
@@ -121,10 +129,11 @@ __global__ void bn_finalize_kernel(int C, int blocks, double count, const double
     shift[c] = (float)(bt - mean * g * inv);
     if (smean) smean[c] = (float)mean;
     if (sinv) sinv[c] = (float)inv;
-    if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+    const double mom = cum ? 1.0 / (double)(nbt[0] + 1) : (double)momentum;
+    if (rmean) rmean[c] = (float)((1.0 - mom) * rmean[c] + mom * mean);
     if (rvar) {
       const double unb = count > 1 ? var * count / (count - 1) : var;
-      rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+      rvar[c] = (float)((1.0 - mom) * rvar[c] + mom * unb);
     }
   }
 }
@@ -799,22 +808,28 @@ extern "C" int rr_bn_finalize(int C, int blocks, long long count, const float *p
                               float *save_invstd, int64_t *num_batches_tracked, void *ws,
                               size_t ws_bytes, rr_stream stream) {
   if (C <= 0 || blocks <= 0 || count <= 0 || !part || !scale || !shift) return RR_EINVAL;
+  const bool cum = momentum < 0.f;
+  if (cum && !num_batches_tracked) return RR_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   if (blocks <= RR_BN_DIRECT_ROWS) {
     hipLaunchKernelGGL(bn_finalize_direct_kernel, dim3(C), dim3(256), 0, st, C, blocks, (double)count,
                        part, bias, gamma, beta, running_mean, running_var, momentum, eps, scale, shift,
                        save_mean, save_invstd, num_batches_tracked);
     RR_CHECK_LAUNCH();
-    return RR_OK;
+  } else {
+    if (!ws || ws_bytes < rr_colreduce_bytes(blocks, C * 2)) return RR_EWORKSPACE;
+    const int chunks = rr_colreduce(part, blocks, C * 2, (double *)ws, st);
+    if (chunks < 0) return RR_ELAUNCH;
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st,
+                       C, chunks, (double)count, (const double *)ws, bias, gamma, beta, running_mean,
+                       running_var, momentum, eps, scale, shift, save_mean, save_invstd,
+                       num_batches_tracked);
+    RR_CHECK_LAUNCH();
   }
-  if (!ws || ws_bytes < rr_colreduce_bytes(blocks, C * 2)) return RR_EWORKSPACE;
-  const int chunks = rr_colreduce(part, blocks, C * 2, (double *)ws, st);
-  if (chunks < 0) return RR_ELAUNCH;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st,
-                     C, chunks, (double)count, (const double *)ws, bias, gamma, beta, running_mean,
-                     running_var, momentum, eps, scale, shift, save_mean, save_invstd,
-                     num_batches_tracked);
-  RR_CHECK_LAUNCH();
+  if (cum) {
+    hipLaunchKernelGGL(bn_nbt_inc_kernel, dim3(1), dim3(1), 0, st, num_batches_tracked);
+    RR_CHECK_LAUNCH();
+  }
   return RR_OK;
 }
 
@@ -827,6 +842,7 @@ extern "C" int rr_bn_finalize_pair(const rr_bn_finalize_desc *a, const rr_bn_fin
     if (d->C <= 0 || d->blocks <= 0 || d->count <= 0 || !d->part || !d->scale || !d->shift)
       return RR_EINVAL;
   if (a->blocks > RR_BN_DIRECT_ROWS || b->blocks > RR_BN_DIRECT_ROWS) return RR_EUNSUPPORTED;
+  if (a->momentum < 0.f || b->momentum < 0.f) return RR_EUNSUPPORTED;   // cumulative: rr_bn_finalize
   auto fin = [](const rr_bn_finalize_desc *d) {
     return BnFin{d->C, d->blocks, (double)d->count, d->part, d->bias, d->gamma, d->beta,
                  d->running_mean, d->running_var, d->momentum, d->eps, d->scale, d->shift,

@@ -8,6 +8,14 @@
 //     22-bit fixed point, an 8-bit clip after each pass.  Optionally fused with
 //     ToTensor (x / 255 in fp32) and Normalize ((x - mean) / std in fp32, 18:31)
 //     into an NCHW fp32 batch.
+//   * rr_cv_resize_linear_u8: cv2.resize(img, (ow, oh)) INTER_LINEAR, the
+//     clean side of the 08 PSNR leg (08:118-119) -- OpenCV's own fixed-point
+//     bilinear (resize.cpp resizeGeneric_ + HResizeLinear / VResizeLinear),
+//     not Pillow's: 11-bit weights from float source coordinates, an exact
+//     int32 horizontal pass, the vertical pass as the x86 SIMD body computes
+//     it (VResizeLinearVec_32s8u) with the scalar 22-bit rounding on the row
+//     tail; bit-equal to oracle/imgproc_cpu.cv_resize_linear (parity vs cv2
+//     itself unpinned: cv2 is not installed).
 //   * rr_ssim_u8: skimage structural_similarity(a, b, data_range=255,
 //     channel_axis=2) (08:125): 7x7 uniform window, sample covariance
 //     (49/48), K1 = .01, K2 = .03, mean of S over the interior (3-pixel border
@@ -279,6 +287,65 @@ __global__ __launch_bounds__(SS_T) void ssim_kernel(int h, int w, int C, const u
   if (threadIdx.x == 0) chan_mean[blockIdx.x] = red[0] / ((double)(h - 6) * (w - 6));
 }
 
+// ---------------------------------------------------------- cv resize ----
+// resize.cpp's coefficient of output coordinate d: float source position
+// (d + 0.5) * scale - 0.5 evaluated in double then rounded to float (no FMA:
+// contraction would change the rounding), its floor and fraction
+__device__ __forceinline__ void cvr_coord(int d, double scale, int *i, float *f) {
+#pragma clang fp contract(off)
+  const double v = ((double)d + 0.5) * scale - 0.5;
+  const float fv = (float)v;
+  const float fl = floorf(fv);
+  *i = (int)fl;
+  *f = fv - fl;
+}
+
+__device__ __forceinline__ int cvr_round(float v) { return __float2int_rn(v); }   // cvRound
+
+// one thread per output pixel, C channels; vec_end = first row element
+// (x * C + ch) of the scalar tail
+template <int C>
+__global__ void cv_resize_linear_kernel(int n, int h, int w, int oh, int ow, double sx_scale,
+                                        double sy_scale, int vec_end,
+                                        const uint8_t *__restrict__ in, uint8_t *__restrict__ out) {
+#pragma clang fp contract(off)
+  const long long total = (long long)n * oh * ow;
+  for (long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x; q < total;
+       q += (long long)gridDim.x * blockDim.x) {
+    const int x = (int)(q % ow);
+    const long long r = q / ow;
+    const int y = (int)(r % oh);
+    const int im = (int)(r / oh);
+    int sx, sy;
+    float fx, fy;
+    cvr_coord(x, sx_scale, &sx, &fx);
+    if (sx < 0) { sx = 0; fx = 0.f; }
+    if (sx >= w - 1) { sx = w - 1; fx = 0.f; }
+    const int a0 = cvr_round((1.f - fx) * 2048.f), a1 = cvr_round(fx * 2048.f);
+    const int sx1 = sx + 1 < w ? sx + 1 : w - 1;
+    cvr_coord(y, sy_scale, &sy, &fy);
+    const int b0 = cvr_round((1.f - fy) * 2048.f), b1 = cvr_round(fy * 2048.f);
+    const int r0 = sy < 0 ? 0 : (sy > h - 1 ? h - 1 : sy);
+    const int r1 = sy + 1 < 0 ? 0 : (sy + 1 > h - 1 ? h - 1 : sy + 1);
+    const uint8_t *p0 = in + ((long long)im * h + r0) * w * C;
+    const uint8_t *p1 = in + ((long long)im * h + r1) * w * C;
+    uint8_t *o = out + q * C;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int s0 = (int)p0[sx * C + c] * a0 + (int)p0[sx1 * C + c] * a1;
+      const int s1 = (int)p1[sx * C + c] * a0 + (int)p1[sx1 * C + c] * a1;
+      int v;
+      if (x * C + c < vec_end) {
+        // v_mul_hi on the int16-packed S >> 4, then v_rshr_pack_u<2>
+        v = ((((s0 >> 4) * b0) >> 16) + (((s1 >> 4) * b1) >> 16) + 2) >> 2;
+      } else {
+        v = (int)(((long long)s0 * b0 + (long long)s1 * b1 + (1LL << 21)) >> 22);
+      }
+      o[c] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+    }
+  }
+}
+
 __global__ void ssim_chan_mean_kernel(int n, int C, const double *__restrict__ chan_mean,
                                       double *__restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -355,6 +422,38 @@ extern "C" int rr_resize_bilinear_u8(int n, int h, int w, int c, int oh, int ow,
     default: RS_LAUNCH(4) break;
   }
 #undef RS_LAUNCH
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_cv_resize_linear_u8(int n, int h, int w, int c, int oh, int ow,
+                                      const uint8_t *in, uint8_t *out, int simd_lanes,
+                                      rr_stream stream) {
+  if (n < 0 || h <= 0 || w <= 0 || oh <= 0 || ow <= 0 || c < 1 || c > 4) return RR_EINVAL;
+  if (simd_lanes <= 0) simd_lanes = 16;
+  if ((simd_lanes & 1) != 0) return RR_EINVAL;
+  if (n == 0) return RR_OK;
+  if (!in || !out) return RR_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  if (oh == h && ow == w) {                               // cv::resize: same size -> copy
+    const hipError_t e = hipMemcpyAsync(out, in, (size_t)n * h * w * c, hipMemcpyDeviceToDevice, st);
+    return e == hipSuccess ? RR_OK : RR_ELAUNCH;
+  }
+  // hal::resize: scale = 1 / inv_scale, inv_scale = dst / src (double)
+  const double sxs = 1.0 / ((double)ow / (double)w), sys = 1.0 / ((double)oh / (double)h);
+  // VResizeLinearVec_32s8u: x <= width - lanes in full vectors, then
+  // x < width - lanes / 2 in half vectors; the rest scalar
+  const int width = ow * c;
+  int ve = (width / simd_lanes) * simd_lanes;
+  while (ve < width - simd_lanes / 2) ve += simd_lanes / 2;
+  const long long total = (long long)n * oh * ow;
+  const dim3 g(rr_grid_cap((total + 255) / 256, 8192)), b(256);
+  switch (c) {
+    case 1: hipLaunchKernelGGL(cv_resize_linear_kernel<1>, g, b, 0, st, n, h, w, oh, ow, sxs, sys, ve, in, out); break;
+    case 2: hipLaunchKernelGGL(cv_resize_linear_kernel<2>, g, b, 0, st, n, h, w, oh, ow, sxs, sys, ve, in, out); break;
+    case 3: hipLaunchKernelGGL(cv_resize_linear_kernel<3>, g, b, 0, st, n, h, w, oh, ow, sxs, sys, ve, in, out); break;
+    default: hipLaunchKernelGGL(cv_resize_linear_kernel<4>, g, b, 0, st, n, h, w, oh, ow, sxs, sys, ve, in, out); break;
+  }
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

@@ -1151,18 +1151,23 @@ __global__ void adamw_kernel(long long count, float *__restrict__ p, const float
 // double from the same float betas the host path uses
 __global__ void adamw_step_inc_kernel(int64_t *step) { *step += 1; }
 
+// The learning rate is read from the device too (*lr_dev, a 1-element fp32
+// tensor that torch's LR schedulers update in place with fill_), so a
+// scheduler.step() between graph replays takes effect (14:223, 248).
 __global__ void adamw_dev_kernel(long long count, float *__restrict__ p, const float *__restrict__ g,
-                                 float *__restrict__ m, float *__restrict__ v, float lr, float b1,
+                                 float *__restrict__ m, float *__restrict__ v,
+                                 const float *__restrict__ lr_dev, float b1,
                                  float b2, float eps, float wd, int decoupled,
                                  const int64_t *__restrict__ step_dev) {
-  __shared__ float bc[2];
+  __shared__ float bc[3];
   if (threadIdx.x == 0) {
     const double st = (double)*step_dev;
     bc[0] = (float)(1.0 - pow((double)b1, st));
     bc[1] = (float)sqrt(1.0 - pow((double)b2, st));
+    bc[2] = *lr_dev;
   }
   __syncthreads();
-  const float bc1 = bc[0], sbc2 = bc[1];
+  const float bc1 = bc[0], sbc2 = bc[1], lr = bc[2];
   const float step = lr / bc1;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < count;
        i += (long long)gridDim.x * blockDim.x) {
@@ -1826,15 +1831,16 @@ extern "C" int rr_adamw(long long count, float *param, const float *grad, float 
 }
 
 extern "C" int rr_adamw_dev(long long count, float *param, const float *grad, float *m, float *v,
-                            float lr, float beta1, float beta2, float eps, float weight_decay,
-                            int decoupled, int64_t *step_dev, rr_stream stream) {
-  if (count <= 0 || !param || !grad || !m || !v || !step_dev) return RR_EINVAL;
+                            const float *lr_dev, float beta1, float beta2, float eps,
+                            float weight_decay, int decoupled, int64_t *step_dev,
+                            rr_stream stream) {
+  if (count <= 0 || !param || !grad || !m || !v || !step_dev || !lr_dev) return RR_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(adamw_step_inc_kernel, dim3(1), dim3(1), 0, st, step_dev);
   RR_CHECK_LAUNCH();
   dim3 g(rr_grid_cap((count + 255) / 256, 8192)), b(256);
-  hipLaunchKernelGGL(adamw_dev_kernel, g, b, 0, st, count, param, grad, m, v, lr, beta1, beta2, eps,
-                     weight_decay, decoupled, step_dev);
+  hipLaunchKernelGGL(adamw_dev_kernel, g, b, 0, st, count, param, grad, m, v, lr_dev, beta1, beta2,
+                     eps, weight_decay, decoupled, step_dev);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

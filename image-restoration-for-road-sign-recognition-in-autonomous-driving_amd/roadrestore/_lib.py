@@ -129,13 +129,14 @@ _SIGS = {
     "rr_loss_fwd": (I_, [I_, I_, L_, P_, P_, P_, F_, I_, P_, S_, P_]),
     "rr_loss_workspace": (S_, [L_]),
     "rr_loss_bwd": (I_, [I_, I_, L_, P_, P_, P_, F_, P_, P_, I_, I_, P_]),
-    "rr_adamw_dev": (I_, [L_, P_, P_, P_, P_, F_, F_, F_, F_, F_, I_, P_, P_]),
+    "rr_adamw_dev": (I_, [L_, P_, P_, P_, P_, P_, F_, F_, F_, F_, I_, P_, P_]),
     "rr_adamw": (I_, [L_, P_, P_, P_, P_, F_, F_, F_, F_, F_, I_, I_, P_]),
     "rr_to_uint8_hwc": (I_, [I_, I_, I_, I_, P_, P_, I_, P_]),
     "rr_psnr_u8": (I_, [I_, L_, P_, P_, P_, P_]),
     "rr_argmax_rows": (I_, [I_, I_, P_, P_, P_]),
     "rr_adaptive_avgpool_flatten": (I_, [I_, I_, I_, I_, I_, I_, I_, P_, P_, P_]),
     "rr_resize_workspace": (S_, [I_, I_, I_, I_, I_, I_]),
+    "rr_cv_resize_linear_u8": (I_, [I_, I_, I_, I_, I_, I_, P_, P_, I_, P_]),
     "rr_resize_bilinear_u8": (I_, [I_, I_, I_, I_, I_, I_, P_, I_, P_, P_, P_, P_, S_, P_]),
     "rr_ssim_workspace": (S_, [I_, I_]),
     "rr_ssim_u8": (I_, [I_, I_, I_, I_, P_, P_, P_, P_, S_, P_]),

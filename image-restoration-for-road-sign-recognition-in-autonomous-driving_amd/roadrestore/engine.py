@@ -161,6 +161,14 @@ class WeightCache:
     def clear(self):
         self._c.clear()
 
+    def drop_folds(self):
+        """Forget the eval-mode folded conv+BN weights.  Called on every switch
+        to eval mode: train-mode forwards (also HIP-graph replays, where no
+        host code runs to bump version counters) may have moved the running
+        statistics since the fold was made."""
+        for k in [k for k in self._c if k[2] == "fold"]:
+            del self._c[k]
+
 
 # ---------------------------------------------------------------------------
 # gradient sink

@@ -14,6 +14,8 @@ DataLoader workers and in the inference loop).  Here they take a whole
   device (Philox4x32-10) instead of ``np.random.normal``.
 * ``apply_compound_distortion`` -- 16:14-37 (blur 10 @ 45 deg, fog 0.5, noise
   var 0.02).
+* ``cv_resize`` -- ``cv2.resize(img, (224, 224))`` of the 08 PSNR leg's
+  clean image (08:118-119): OpenCV's INTER_LINEAR, which is not PIL's.
 * ``psnr`` / ``ssim`` -- 08:123-125 (skimage semantics, data_range 255).
 """
 from __future__ import annotations
@@ -31,7 +33,7 @@ from ._lib import (RR_DISTORT_BLUR, RR_DISTORT_FOG, RR_DISTORT_KMAX, RR_DISTORT_
 __all__ = ["Resize", "ToTensor", "Normalize", "Compose", "apply_random_distortions",
            "encode_png", "write_png",
            "RandomDistortion", "motion_blur_table",
-           "apply_compound_distortion", "distortion_params", "psnr", "ssim",
+           "apply_compound_distortion", "distortion_params", "psnr", "ssim", "cv_resize",
            "IMAGENET_MEAN", "IMAGENET_STD"]
 
 IMAGENET_MEAN = (0.485, 0.456, 0.406)      # 18:31
@@ -223,6 +225,21 @@ def apply_compound_distortion(x, seed=0, noise=None):
     p = DistortParam(0.02 ** 0.5, t, A * (1 - t), RR_DISTORT_FOG | RR_DISTORT_NOISE | RR_DISTORT_BLUR, 10)
     taps = ops.motion_blur_kernel(10, 45).unsqueeze(0).expand(n, -1, -1).contiguous()
     return ops.distort_u8(x, [p] * n, taps, mode=1, noise=noise, seed=seed)
+
+
+def cv_resize(x, size):
+    """``cv2.resize(img, (w, h))`` (default INTER_LINEAR) of an [n, h, w, c]
+    uint8 device batch (c <= 4): the clean image of the 08 PSNR leg
+    (08:118-119; OpenCV's fixed-point bilinear, not PIL's, see
+    rr_cv_resize_linear_u8).  ``size`` = (w, h) in cv2's order."""
+    _check_u8(x)
+    ow, oh = size
+    n, h, w, c = x.shape
+    x = x.contiguous()
+    out = torch.empty((n, oh, ow, c), dtype=torch.uint8, device=x.device)
+    lib().check(lib().rr_cv_resize_linear_u8(n, h, w, c, oh, ow, x.data_ptr(), out.data_ptr(),
+                                              0, ops.stream()), "rr_cv_resize_linear_u8")
+    return out
 
 
 def psnr(a, b):

@@ -251,8 +251,8 @@ def batch_norm(x: Tensor, weight: Tensor, bias: Tensor, module: int, training: b
     xn = _nhwc(x, dt)
     if training:
         mom = bn.momentum
-        if mom is None:    # cumulative moving average: factor 1 / num_batches_tracked
-            mom = 1.0 / float(int(bn.num_batches_tracked.item()) + 1)
+        if mom is None:    # cumulative moving average: factor 1 / num_batches_tracked,
+            mom = -1.0     # read on the device by the finalize (no host sync)
         scale, shift, mean, inv = ops.bn_finalize(
             ops.bn_stats(xn), P, None, weight.contiguous(), bias.contiguous(), bn.running_mean,
             bn.running_var, momentum=mom, eps=bn.eps, num_batches_tracked=bn.num_batches_tracked)

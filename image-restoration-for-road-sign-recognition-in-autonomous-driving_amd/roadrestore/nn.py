@@ -236,6 +236,12 @@ class _RRNet(tnn.Module):
         self._grad_hook = None
         self._op_key = _tops.register_module(self)
 
+    def train(self, mode=True):
+        super().train(mode)
+        if not mode:
+            self._wc.drop_folds()      # running statistics may have moved (graph replays too)
+        return self
+
     # data-parallel wrappers install a hook called as grad groups become final
     def set_grad_ready_hook(self, hook):
         self._grad_hook = hook
@@ -548,6 +554,8 @@ class MSELoss(tnn.Module):
 def unified_loss(out, clean, perc, w=0.1, grad_scale=1.0):
     """L1(out, clean) + w * perceptual(out, clean) as ONE autograd node
     (14:238-242) with a single fused gradient; ``grad_scale`` pre-scales the
-    backward (1/world_size under data parallelism)."""
+    backward (1/world_size under data parallelism).  Under ``torch.no_grad()``
+    (the validation loss, 14:253-263) no backward state is kept."""
+    need = torch.is_grad_enabled() and out.requires_grad
     return torch.ops.rr.unified_loss(out.contiguous(), clean.float().contiguous(), perc._op_key,
-                                     float(w), float(grad_scale))[0]
+                                     float(w), float(grad_scale), need)[0]

@@ -253,7 +253,20 @@ def bn_finalize(st, count, bias, gamma, beta, running_mean, running_var, momentu
                                      float(eps), _p(scale), _p(shift), _p(mean), _p(inv),
                                      _p(num_batches_tracked), _p(ws), ws.numel(), stream()),
                 "rr_bn_finalize")
+    _bump_running(running_mean, running_var)
     return scale, shift, mean, inv
+
+
+def _bump_running(*ts):
+    """The finalize updated the running statistics through raw pointers: bump
+    their version counters so caches keyed on them (the eval-mode conv+BN
+    fold, engine.WeightCache.conv_bn_folded) see the update.  Under a HIP-graph
+    capture nothing host-side runs on replay; nn._RRNet.train(False) drops the
+    folds for that case."""
+    ts = [t for t in ts if t is not None]
+    inc = getattr(torch.autograd.graph, "increment_version", None)
+    if ts and inc is not None and not torch.cuda.is_current_stream_capturing():
+        inc(ts)
 
 
 def bn_finalize_pair(a, b):
@@ -296,6 +309,8 @@ def bn_finalize_pair(a, b):
     if rc == RR_EUNSUPPORTED:
         return bn_finalize(**a), bn_finalize(**b)
     lib().check(rc, "rr_bn_finalize_pair")
+    for k in (a, b):
+        _bump_running(k.get("running_mean"), k.get("running_var"))
     return outs[0], outs[1]
 
 

@@ -9,6 +9,12 @@ the network's backward into one flat buffer in the same order) each tile one
 contiguous span, a step is a single kernel over every parameter; otherwise
 one launch per parameter.  The learning-rate schedule is host arithmetic:
 torch.optim.lr_scheduler.CosineAnnealingLR works unchanged (14:223, 248).
+
+``capturable=True`` (HIP-graph replay of the whole step): the step count AND
+the learning rate live on the device.  Each group's ``lr`` becomes a
+1-element fp32 device tensor; torch's LR schedulers update a tensor lr in
+place (``fill_``), which the captured ``rr_adamw_dev`` launch reads on every
+replay, so ``scheduler.step()`` between replays takes effect.
 """
 from __future__ import annotations
 
@@ -72,10 +78,33 @@ class _FusedAdamBase(torch.optim.Optimizer):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
         self._gstate = {}
-        # capturable: the step count lives on the device (rr_adamw_dev) so a
-        # HIP-graph replay of optimizer.step() advances the bias correction;
-        # the learning rate is then fixed at capture time
+        # capturable: the step count and the learning rate live on the device
+        # (rr_adamw_dev) so a HIP-graph replay of optimizer.step() advances the
+        # bias correction and follows the LR schedule
         self.capturable = capturable
+        if capturable:
+            for group in self.param_groups:
+                self._lr_to_device(group)
+
+    @staticmethod
+    def _lr_to_device(group):
+        """group["lr"] as a 1-element fp32 tensor on the parameters' device
+        (once the parameters are on a GPU); returns it or None"""
+        lr = group["lr"]
+        dev = next((p.device for p in group["params"] if p.is_cuda), None)
+        if dev is None:
+            return None
+        if not (isinstance(lr, torch.Tensor) and lr.is_cuda and lr.dtype == torch.float32
+                and lr.numel() == 1 and lr.device == dev):
+            lr = torch.full((1,), float(lr), dtype=torch.float32, device=dev)
+            group["lr"] = lr
+        return lr
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        if self.capturable:
+            for group in self.param_groups:
+                self._lr_to_device(group)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -116,9 +145,10 @@ class _FusedAdamBase(torch.optim.Optimizer):
                     if "step_dev" not in gstate:
                         gstate["step_dev"] = torch.full((1,), step - 1, dtype=torch.int64,
                                                         device=ps[0].device)
+                    lr_dev = self._lr_to_device(group)
                     lib().check(lib().rr_adamw_dev(
                         total, pspan[0][0], gspan[0][0], gstate["m"].data_ptr(),
-                        gstate["v"].data_ptr(), float(group["lr"]), float(b1), float(b2),
+                        gstate["v"].data_ptr(), lr_dev.data_ptr(), float(b1), float(b2),
                         float(group["eps"]), float(group["weight_decay"]), int(self.decoupled),
                         gstate["step_dev"].data_ptr(), ops.stream()), "rr_adamw_dev")
                 else:

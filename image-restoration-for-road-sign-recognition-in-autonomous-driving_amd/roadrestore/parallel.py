@@ -17,7 +17,10 @@ the all-reduces are bare ncclAllReduce calls on a communicator of our own
 capturable: the side stream forks from and joins the capturing stream and
 the collectives are recorded into the graph (bench.py captures it at every N).  The
 1/world_size average is folded into the loss gradient (``grad_scale``), the
-exactly-zero gradients (conv biases before a train-mode BN) are not sent.
+exactly-zero gradients (conv biases before a train-mode BN) are not sent in
+train mode.  In eval mode (a fine-tune with frozen BatchNorm statistics)
+those biases have real gradients, so the zero section of the flat buffer goes
+out as one more bucket once the backward is done.
 """
 from __future__ import annotations
 
@@ -128,6 +131,7 @@ class DataParallel:
         # ~bucket_mb (they overlap the rest of the backward)
         self.buckets = []          # (start, end, param-id set)
         start = sum(p.numel() for p in layout if id(p) in zs)
+        self.zero_span = (0, start)
         items, off = [], start
         for p in layout:
             if id(p) in zs:
@@ -182,18 +186,26 @@ class DataParallel:
             if bi in self._launched or not ids <= self._done:
                 continue
             self._launched.add(bi)
-            view = sink.flat[a:b]
-            if self.rccl is not None:
-                self.comm_stream.wait_stream(torch.cuda.current_stream())
-                self.rccl.all_reduce_(view, self.comm_stream)   # joined in finish()
-            elif self.comm_stream is not None:
-                self.comm_stream.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(self.comm_stream):
-                    self._pending.append(dist.all_reduce(view, group=self.pg, async_op=True))
-            else:
-                self._pending.append(dist.all_reduce(view, group=self.pg, async_op=True))
+            self._reduce(sink.flat[a:b])
         if len(self._launched) == len(self.buckets):
+            # eval mode: the conv biases feeding a BN have real gradients
+            # (written during the backward, which is complete once the last
+            # bucket is ready), so the zero section is exchanged too
+            a, b = self.zero_span
+            if b > a and not self.model.training:
+                self._reduce(sink.flat[a:b])
             self.finish()
+
+    def _reduce(self, view):
+        if self.rccl is not None:
+            self.comm_stream.wait_stream(torch.cuda.current_stream())
+            self.rccl.all_reduce_(view, self.comm_stream)   # joined in finish()
+        elif self.comm_stream is not None:
+            self.comm_stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self.comm_stream):
+                self._pending.append(dist.all_reduce(view, group=self.pg, async_op=True))
+        else:
+            self._pending.append(dist.all_reduce(view, group=self.pg, async_op=True))
 
     def finish(self):
         """Join every outstanding bucket (the optimizer reads the grads next)."""

@@ -24,7 +24,13 @@ BatchNorm running statistics in place, as nn.BatchNorm2d does (module state,
 not an op argument: an op with mutated arguments cannot carry an autograd
 formula).
 The forward's saved state (activations, packed weights) lives in a per-process
-table under an int64 handle tensor that the backward op consumes; a status
+table under an int64 handle tensor that the backward op consumes.  The entry
+lives exactly as long as that handle: the autograd node keeps the handle, so a
+graph dropped without a backward (an exception, an eval pass with grads on)
+frees the state with the graph (``weakref.finalize`` on the handle), and a
+forward run where no backward can follow stores nothing.  The backward pops
+the entry (saved state is freed by the backward, as autograd frees saved
+tensors; a second backward through a ``retain_graph`` graph raises).  A status
 from the C ABI becomes a RuntimeError (``_lib.check``), as ATen's shape errors
 do.  There is no CPU or ATen fallback: the real kernels need a HIP device.
 """
@@ -61,9 +67,21 @@ def _module(key: int):
 
 
 def _stash(state) -> Tensor:
+    """a handle tensor owning ``state``: the table entry goes with the handle"""
     h = next(_HANDLES)
     _SAVED[h] = state
-    return torch.tensor(h, dtype=torch.int64)
+    t = torch.tensor(h, dtype=torch.int64)
+    weakref.finalize(t, _SAVED.pop, h, None)
+    return t
+
+
+def _no_state() -> Tensor:
+    return torch.tensor(0, dtype=torch.int64)
+
+
+def saved_state_count() -> int:
+    """live forward states (diagnostics / tests)"""
+    return len(_SAVED)
 
 
 def _unstash(handle: Tensor):
@@ -95,7 +113,7 @@ def _net_op(prefix, doc):
             need_backward: bool) -> Tuple[Tensor, Tensor]:
         net = _module(module)
         out, S = net._rr_forward(x, need_bwd=need_backward)
-        return out, (_stash(S) if need_backward else torch.tensor(0, dtype=torch.int64))
+        return out, (_stash(S) if need_backward else _no_state())
 
     @fwd.register_fake
     def _(x, params, module, need_backward):
@@ -185,26 +203,28 @@ pixel_loss.register_autograd(_pix_bwd, setup_context=_pix_setup)
 
 @torch.library.custom_op("rr::unified_loss", mutates_args=(), device_types="cuda")
 def unified_loss(out: Tensor, clean: Tensor, perceptual: int, w: float,
-                 grad_scale: float) -> Tuple[Tensor, Tensor]:
+                 grad_scale: float, need_backward: bool) -> Tuple[Tensor, Tensor]:
     """L1(out, clean) + w * mean((F(out) - F(clean))^2), F = VGG16
-    features[:16] (14:238-242), one fused node; the handle carries the
-    feature-stack state for rr::unified_loss_backward"""
+    features[:16] (14:238-242), one fused node; with ``need_backward`` the
+    handle carries the feature-stack state for rr::unified_loss_backward
+    (without it -- the no-grad validation loss of 14:253-263 -- nothing is
+    kept)"""
     perc = _module(perceptual)
     loss = ops.loss_fwd(ops.L1, out, clean)
     st = None
     if w != 0.0:
         fy = perc._target_features(clean)
         fx, S = engine.vgg_features_forward(perc.slice, out, perc._wc, perc.compute_dtype,
-                                            need_bwd=True)
+                                            need_bwd=need_backward)
         ops.loss_fwd(ops.MSE, fx, fy, scale=w, out=loss, accumulate=True)
         st = (S, fx, fy)
     else:
         perc._join()                 # a prefetched target is not needed, but joins the stream
-    return loss, _stash(st)
+    return loss, (_stash(st) if need_backward else _no_state())
 
 
 @unified_loss.register_fake
-def _(out, clean, perceptual, w, grad_scale):
+def _(out, clean, perceptual, w, grad_scale, need_backward):
     return out.new_empty(()), torch.empty((), dtype=torch.int64)
 
 
@@ -227,15 +247,17 @@ def _(grad, out, clean, handle, w, grad_scale):
 
 
 def _uni_setup(ctx, inputs, output):
-    out, clean, _, w, gs = inputs
+    out, clean, _, w, gs, need = inputs
     ctx.save_for_backward(out, clean)
-    ctx.handle, ctx.w, ctx.gs = output[1], w, gs
+    ctx.handle, ctx.w, ctx.gs, ctx.need = output[1], w, gs, need
 
 
 def _uni_bwd(ctx, g, g_handle):
+    if not ctx.need:
+        raise RuntimeError("rr::unified_loss: run with need_backward=True to differentiate")
     out, clean = ctx.saved_tensors
     return torch.ops.rr.unified_loss_backward(g, out, clean, ctx.handle, ctx.w, ctx.gs), None, \
-        None, None, None
+        None, None, None, None
 
 
 unified_loss.register_autograd(_uni_bwd, setup_context=_uni_setup)
@@ -246,7 +268,7 @@ def perceptual_loss(x: Tensor, y: Tensor, perceptual: int, need_backward: bool) 
     """VGGPerceptualLoss.forward (14:194-196)"""
     perc = _module(perceptual)
     loss, S, fx, fy = perc._rr_forward(x, y, 1.0, need_bwd=need_backward)
-    return loss, (_stash((S, fx, fy)) if need_backward else torch.tensor(0, dtype=torch.int64))
+    return loss, (_stash((S, fx, fy)) if need_backward else _no_state())
 
 
 @perceptual_loss.register_fake
@@ -255,25 +277,28 @@ def _(x, y, perceptual, need_backward):
 
 
 @torch.library.custom_op("rr::perceptual_loss_backward", mutates_args=(), device_types="cuda")
-def perceptual_loss_backward(grad: Tensor, handle: Tensor) -> Tensor:
+def perceptual_loss_backward(grad: Tensor, handle: Tensor, x: Tensor) -> Tensor:
+    """dL/dx of VGGPerceptualLoss; ``x`` is the forward's input (its shape)"""
     S, fx, fy = _unstash(handle)
     gpre = ops.loss_bwd(ops.MSE, fx, fy, gscale=grad.contiguous(), scale=1.0, mask_a_pos=True)
     return engine.vgg_features_backward_input(S, gpre)
 
 
 @perceptual_loss_backward.register_fake
-def _(grad, handle):
-    raise RuntimeError("rr::perceptual_loss_backward has no shape without its forward state")
+def _(grad, handle, x):
+    return torch.empty_like(x)
 
 
 def _perc_setup(ctx, inputs, output):
     ctx.handle, ctx.need = output[1], inputs[3]
+    ctx.save_for_backward(inputs[0])
 
 
 def _perc_bwd(ctx, g, g_handle):
     if not ctx.need:
         raise RuntimeError("rr::perceptual_loss: run with need_backward=True to differentiate")
-    return torch.ops.rr.perceptual_loss_backward(g, ctx.handle), None, None, None
+    x, = ctx.saved_tensors
+    return torch.ops.rr.perceptual_loss_backward(g, ctx.handle, x), None, None, None
 
 
 perceptual_loss.register_autograd(_perc_bwd, setup_context=_perc_setup)

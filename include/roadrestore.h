@@ -159,6 +159,9 @@ int rr_bias_tile4(int c_out, const float *b, float *b4, rr_stream stream);
  * bias is that conv's bias (may be NULL).  Writes scale/shift (the affine the
  * apply kernels use), save_mean / save_invstd (for backward) and updates the
  * running stats in place (unbiased var), like F.batch_norm(training=True).
+ * momentum < 0: the cumulative moving average of nn.BatchNorm2d(momentum=None),
+ * factor 1 / (num_batches_tracked + 1) read on the device (num_batches_tracked
+ * required; no host synchronisation, graph-capturable).
  */
 int rr_bn_finalize(int C, int blocks, long long count, const float *stats_partial,
                    const float *bias, const float *gamma, const float *beta,
@@ -415,10 +418,12 @@ int rr_adamw(long long count, float *param, const float *grad, float *m,
              float *v, float lr, float beta1, float beta2, float eps,
              float weight_decay, int decoupled, int step, rr_stream stream);
 /* capturable AdamW/Adam (HIP graphs): *step_dev is incremented on the stream
- * first, then the update reads it; bias corrections as above, on device. */
+ * first, then the update reads it; bias corrections as above, on device.  The
+ * learning rate is *lr_dev (fp32, device): the LR schedule of 14:223, 248
+ * (CosineAnnealingLR.step() per epoch) writes it between graph replays. */
 int rr_adamw_dev(long long count, float *param, const float *grad, float *m, float *v,
-                 float lr, float beta1, float beta2, float eps, float weight_decay,
-                 int decoupled, int64_t *step_dev, rr_stream stream);
+                 const float *lr_dev, float beta1, float beta2, float eps,
+                 float weight_decay, int decoupled, int64_t *step_dev, rr_stream stream);
 
 /* inference post-processing (17:84-92): clamp(0,1)*255 -> uint8 HWC */
 int rr_to_uint8_hwc(int n, int c, int h, int w, const float *x, uint8_t *out,
@@ -446,6 +451,17 @@ int rr_resize_bilinear_u8(int n, int h, int w, int c, int oh, int ow,
                           const uint8_t *in, int out_kind, const float *mean,
                           const float *std, void *out, void *workspace,
                           size_t workspace_bytes, rr_stream stream);
+
+/* cv2.resize(img, (ow, oh)) with the default INTER_LINEAR, the clean image of
+ * the 08 PSNR leg (08_run_inference.py:118-119): OpenCV's fixed-point
+ * bilinear (resize.cpp resizeGeneric_, HResizeLinear / VResizeLinear; 11-bit
+ * weights, the vertical pass as the x86 SIMD body VResizeLinearVec_32s8u
+ * rounds, simd_lanes = its u8 vector width, 0 = 16), batched over [n][h][w][c]
+ * uint8 (c <= 4) -> [n][oh][ow][c]; same size = copy.  Parity vs cv2 itself
+ * is unpinned (cv2 is not installed where this was built). */
+int rr_cv_resize_linear_u8(int n, int h, int w, int c, int oh, int ow,
+                           const uint8_t *in, uint8_t *out, int simd_lanes,
+                           rr_stream stream);
 
 /* skimage structural_similarity(a, b, data_range=255, channel_axis=2)
  * (08_run_inference.py:125) per image of [n][h][w][c] uint8, fp64 out[n] */

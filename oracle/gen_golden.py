@@ -300,9 +300,122 @@ def odd_sizes(m14=None):
         save(f"resunet_{H}x{W}.npz", **arrays)
 
 
+# the 08 PSNR leg: GTSRB-like original sizes (distorted input, clean image)
+SIZES_08 = ((41, 47), (64, 58), (30, 33))
+
+
+def _u8_image(h, w, seed):
+    """A smooth synthetic road-sign-like uint8 RGB image (gradients + a disc +
+    mild noise) at an original (pre-resize) size."""
+    rng = np.random.Generator(np.random.PCG64([seed, 13]))
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+    img = np.stack([120 + 100 * np.sin(xx / 7 + c) * np.cos(yy / 9 - c) for c in range(3)], -1)
+    disc = ((yy - h / 2) ** 2 + (xx - w / 2) ** 2) < (min(h, w) / 3) ** 2
+    img[disc] = [200, 30, 40]
+    img += rng.normal(0, 12, img.shape)
+    return np.clip(img, 0, 255).astype(np.uint8)
+
+
+def extra(m07adv=None, m08=None):
+    """Round-3 fixtures.
+
+    simpleunet_08.npz -- the cfg2 PSNR leg of 08_run_inference.py:86-125 on
+    three images of GTSRB-like original sizes: PIL Resize(224) + ToTensor of
+    the distorted RGB input (08:73-76, Pillow itself), the REFERENCE
+    SimpleUNet (08:19-46) forward at batch 1 in eval mode (08:92-93),
+    clamp / x255 / uint8 truncation / RGB->BGR (08:96-100); the clean image
+    (BGR as cv2.imread gives it) resized with cv2.resize(224, 224)
+    (08:118-119) -- restated (oracle.imgproc_cpu.cv_resize_linear; cv2 is not
+    installed: parity vs cv2 unpinned) -- and PSNR / SSIM (08:123-125;
+    skimage restated: unpinned vs skimage).
+
+    simpleunet_07adv.npz -- one step of the perceptual U-Net trainer
+    07_train_restoration_advanced.py:143-157: the REFERENCE SimpleUNet and
+    VGGPerceptualLoss (07adv:95-112, slice on the seeded cfg-D weights),
+    loss = L1 + 0.1 * perceptual, Adam lr 2e-4 (07adv:19, 23, 136): loss,
+    its parts, grad digests, post-Adam digests."""
+    from PIL import Image
+    from oracle import imgproc_cpu as I
+    torch.set_num_threads(8)
+    torch.use_deterministic_algorithms(True)
+    if m07adv is None or m08 is None:
+        _install_stubs()
+        m07adv = _load("07_train_restoration_advanced.py", "ref07adv")
+        m08 = _load("08_run_inference.py", "ref08")
+    sd = S.model_state_dict("simpleunet", seed=0)
+
+    # ---- 08: SimpleUNet inference + PSNR/SSIM vs the cv2-resized clean ----
+    m = m08.SimpleUNet()
+    m.load_state_dict(sd)
+    m.eval()
+    arrays, outs, cleans, ps, ss = {}, [], [], [], []
+    for i, (h, w) in enumerate(SIZES_08):
+        clean_rgb = _u8_image(h, w, seed=200 + i)
+        rng = np.random.Generator(np.random.PCG64([300 + i, 17]))
+        dist = np.clip(clean_rgb.astype(np.float64) * 0.5 + 0.9 * 255 * 0.5 +
+                       rng.normal(0, 0.14 * 255, clean_rgb.shape), 0, 255).astype(np.uint8)
+        pil = Image.fromarray(dist, "RGB").resize((224, 224), Image.BILINEAR)   # Resize((224,224))
+        x = torch.from_numpy(np.asarray(pil).copy()).permute(2, 0, 1).float().div(255)  # ToTensor
+        with torch.no_grad():
+            out = m(x.unsqueeze(0))                                               # 08:92-93
+        _close(R.simple_unet_forward({k: v.clone() for k, v in sd.items()}, x.unsqueeze(0)), out)
+        o = torch.clamp(out, 0, 1).squeeze().permute(1, 2, 0).numpy()            # 08:96-97
+        out_bgr = np.ascontiguousarray((o * 255).astype(np.uint8)[:, :, ::-1])   # 08:98-100
+        clean_bgr = np.ascontiguousarray(clean_rgb[:, :, ::-1])                  # cv2.imread
+        clean224 = I.cv_resize_linear(clean_bgr, 224, 224)                       # 08:119
+        arrays[f"dist_{i}"] = dist
+        arrays[f"clean_bgr_{i}"] = clean_bgr
+        arrays[f"out_sum_{i}"] = np.array([out.double().sum().item()])
+        outs.append(out_bgr)
+        cleans.append(clean224)
+        ps.append(R.psnr_u8(clean224, out_bgr))                                  # 08:123
+        ss.append(I.ssim(clean224, out_bgr))                                     # 08:125
+    arrays.update(out_bgr=np.stack(outs), clean224=np.stack(cleans), psnr=np.array(ps),
+                  ssim=np.array(ss), sizes=np.array(SIZES_08))
+    save("simpleunet_08.npz", **arrays)
+    print("08 leg: PSNR", ps, "SSIM", ss)
+
+    # ---- 07adv: SimpleUNet + L1 + 0.1 perceptual, Adam lr 2e-4 -------------
+    man = S.load_manifest("perceptual")
+    perc_sd = S.seeded_state_dict(man, seed=5)
+    perc = m07adv.VGGPerceptualLoss()
+    perc.slice.load_state_dict({k[len("slice."):]: v for k, v in perc_sd.items()})
+    assert [[k, list(v.shape)] for k, v in perc.state_dict().items()] == man
+    B, H = 2, 64
+    clean = S.image_batch(B, H, H, seed=400)
+    bad = S.fog_noise(clean, seed=401)
+    m = m07adv.SimpleUNet()
+    m.load_state_dict(sd)
+    m.train()
+    opt = torch.optim.Adam(m.parameters(), lr=m07adv.LEARNING_RATE)          # 07adv:136
+    opt.zero_grad()
+    out = m(bad)                                                              # 07adv:147
+    l_pix = torch.nn.L1Loss()(out, clean)                                     # 07adv:150
+    l_perc = perc(out, clean)                                                 # 07adv:151
+    loss = l_pix + m07adv.LAMBDA_PERCEPTUAL * l_perc                          # 07adv:154
+    loss.backward()
+    grads = {k: v.grad for k, v in m.named_parameters()}
+    p = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    lr_ = R.unified_loss(R.simple_unet_forward(p, bad), clean, perc_sd)
+    lr_.backward()
+    assert abs(lr_.item() - loss.item()) < 1e-6, (lr_.item(), loss.item())
+    for k in ("enc1.0.weight", "up1.weight", "final.bias"):
+        _close(p[k].grad, grads[k], 1e-5)
+    opt.step()
+    save("simpleunet_07adv.npz", bad=bad.numpy(), clean=clean.numpy(),
+         loss=np.array([loss.item()]), l_pix=np.array([l_pix.item()]),
+         l_perc=np.array([l_perc.item()]), lr=np.array([m07adv.LEARNING_RATE]),
+         **{"grad:" + k: v for k, v in digest(grads).items()},
+         **{"post:" + k: v for k, v in digest(dict(m.named_parameters())).items()})
+    print("07adv step: loss", loss.item())
+
+
 if __name__ == "__main__":
     if "--only-odd" in sys.argv:
         odd_sizes()
+    elif "--only-extra" in sys.argv:
+        extra()
     else:
         main()
         odd_sizes()
+        extra()

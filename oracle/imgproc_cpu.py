@@ -11,6 +11,22 @@ module, as the checker.  The product (``roadrestore``) never imports it.
   ``normalize_coeffs_8bpc``, ``ImagingResampleHorizontal_8bpc`` /
   ``Vertical_8bpc``, ``ImagingResampleInner``).  Restated in numpy; pinned
   against the installed Pillow itself (tests/test_imgproc_cpu.py).
+* ``cv_resize_linear``     ``cv2.resize(img, (224, 224))`` (default
+  ``INTER_LINEAR``) on the uint8 clean image of the 08 PSNR leg
+  (08_run_inference.py:118-119) -- OpenCV's OWN algorithm, not Pillow's:
+  OpenCV 4.x ``imgproc/src/resize.cpp`` ``hal::resize`` -> ``resizeGeneric_``
+  with ``HResizeLinear<uchar, int, short, 2048>`` and ``VResizeLinear<uchar,
+  int, short, FixedPtCast<int, uchar, 22>>``: float source coordinates
+  ``(d + 0.5) * scale - 0.5`` with ``scale = 1 / (dst / src)`` in double,
+  border clamping, 11-bit coefficients ``saturate_cast<short>(c * 2048)``
+  (round half to even), an exact int32 horizontal pass, and the vertical
+  pass as the x86 SIMD body ``VResizeLinearVec_32s8u`` computes it
+  (``((S0 >> 4) * b0 >> 16) + ((S1 >> 4) * b1 >> 16)``, then ``(v + 2) >> 2``
+  saturated) for the elements it covers, the scalar ``(v + 2^21) >> 22`` for
+  the row tail.  cv2 is not installed here: **parity vs cv2 is unpinned**
+  (the IPP path, off by default for non-exact resizes, and other SIMD
+  widths are not reproduced; at 224 x 3 = 672 row elements the scalar tail
+  is empty for 16- and 32-lane vectors).
 * ``to_tensor_normalize``  ``ToTensor`` (``.float().div(255)``) and
   ``Normalize`` (``sub_(mean).div_(std)``, fp32) (18:29-31).
 * ``ssim``                 skimage ``structural_similarity(a, b,
@@ -100,6 +116,66 @@ def pil_resize_bilinear(img: np.ndarray, oh: int, ow: int) -> np.ndarray:
     if oh != h:
         out = _pass(out, bv, kv, axis=0)
     return out
+
+
+CV_COEF_BITS = 11
+CV_COEF_SCALE = 1 << CV_COEF_BITS
+
+
+def _cv_linear_coeffs(src: int, dst: int):
+    """resize.cpp's per-output source index and 11-bit weights (xofs / ialpha,
+    yofs / ibeta): (index [dst] int64, w0 [dst] int64, w1 [dst] int64).  The x
+    axis clamps the index and zeroes the fraction at the borders; the y axis
+    keeps the raw index (rows are clamped when fetched) and its weights."""
+    scale = 1.0 / (float(dst) / float(src))          # hal::resize: 1. / inv_scale
+    d = np.arange(dst, dtype=np.float64)
+    f = ((d + 0.5) * scale - 0.5).astype(np.float32)  # (float)((dx+0.5)*scale_x - 0.5)
+    i = np.floor(f).astype(np.int64)                  # cvFloor
+    f = (f - i.astype(np.float32)).astype(np.float32)
+    return i, f
+
+
+def _cv_round_short(v: np.ndarray) -> np.ndarray:
+    return np.rint(v.astype(np.float32)).astype(np.int64)   # cvRound: half to even
+
+
+def cv_resize_linear(img: np.ndarray, oh: int, ow: int, simd_lanes: int = 16) -> np.ndarray:
+    """[H, W, C] uint8 -> [oh, ow, C] uint8 as cv2.resize(img, (ow, oh))
+    (INTER_LINEAR); see the module docstring.  ``simd_lanes``: the u8 vector
+    width of the vertical pass (16 = SSE2/NEON baseline)."""
+    h, w, cn = img.shape
+    if (h, w) == (oh, ow):
+        return img.copy()                                # cv::resize: same size -> copy
+    sx, fx = _cv_linear_coeffs(w, ow)
+    lo, hi = sx < 0, sx >= w - 1
+    fx = np.where(lo | hi, np.float32(0), fx).astype(np.float32)
+    sx = np.where(lo, 0, np.where(hi, w - 1, sx))
+    a0 = _cv_round_short((np.float32(1) - fx) * np.float32(CV_COEF_SCALE))
+    a1 = _cv_round_short(fx * np.float32(CV_COEF_SCALE))
+    sx1 = np.minimum(sx + 1, w - 1)                      # weight 0 where clamped
+    src = img.astype(np.int64)
+    # horizontal: D[y][dx][c] = S[y][sx][c] * a0 + S[y][sx + 1][c] * a1 (int32)
+    hz = src[:, sx, :] * a0[None, :, None] + src[:, sx1, :] * a1[None, :, None]
+    sy, fy = _cv_linear_coeffs(h, oh)
+    b0 = _cv_round_short((np.float32(1) - fy) * np.float32(CV_COEF_SCALE))
+    b1 = _cv_round_short(fy * np.float32(CV_COEF_SCALE))
+    r0 = np.clip(sy, 0, h - 1)
+    r1 = np.clip(sy + 1, 0, h - 1)
+    s0 = hz[r0].reshape(oh, ow * cn)
+    s1 = hz[r1].reshape(oh, ow * cn)
+    b0c, b1c = b0[:, None], b1[:, None]
+    # VResizeLinearVec_32s8u: 16-bit fixed point (v_mul_hi = (a * b) >> 16)
+    vec = ((((s0 >> 4) * b0c) >> 16) + (((s1 >> 4) * b1c) >> 16) + 2) >> 2
+    # scalar tail: FixedPtCast<int, uchar, 22>
+    sca = (s0 * b0c + s1 * b1c + (1 << 21)) >> 22
+    width = ow * cn
+    x = np.arange(width)
+    nv = (width // simd_lanes) * simd_lanes              # x <= width - lanes loop
+    half = simd_lanes // 2
+    while nv < width - half:                             # x < width - lanes/2 loop
+        nv += half
+    out = np.where(x[None, :] < nv, vec, sca)
+    return np.clip(out, 0, 255).astype(np.uint8).reshape(oh, ow, cn)
 
 
 def to_tensor_normalize(img_u8: np.ndarray, mean=None, std=None) -> np.ndarray:

@@ -205,5 +205,32 @@ def test_custom_ops_registered_with_fake_shapes():
         assert u8.shape == (2, 8, 8, 3) and u8.dtype == torch.uint8
         assert torch.ops.rr.argmax_rows(torch.empty(7, 43, device="cuda")).shape == (7,)
         loss, _ = torch.ops.rr.unified_loss(torch.empty(2, 3, 8, 8, device="cuda"),
-                                            torch.empty(2, 3, 8, 8, device="cuda"), 0, 0.1, 1.0)
+                                            torch.empty(2, 3, 8, 8, device="cuda"), 0, 0.1, 1.0,
+                                            True)
         assert loss.shape == ()
+        g = torch.ops.rr.perceptual_loss_backward(torch.empty((), device="cuda"),
+                                                  torch.empty((), dtype=torch.int64),
+                                                  torch.empty(2, 3, 8, 8, device="cuda"))
+        assert g.shape == (2, 3, 8, 8)
+
+
+def test_saved_forward_state_lives_with_its_handle():
+    """The forward state table (torch_ops._SAVED) holds an entry only while
+    its handle tensor lives: the autograd node keeps the handle, so a graph
+    dropped without a backward frees the state; a handle never kept (no
+    backward possible) frees it at once; the backward pops it."""
+    import gc
+    from roadrestore import torch_ops as T
+    n0 = T.saved_state_count()
+    hs = [T._stash(("state", i)) for i in range(50)]
+    assert T.saved_state_count() == n0 + 50
+    del hs
+    gc.collect()
+    assert T.saved_state_count() == n0
+    h = T._stash("x")
+    assert T._unstash(h) == "x" and T.saved_state_count() == n0
+    with pytest.raises(RuntimeError, match="already consumed"):
+        T._unstash(h)
+    del h
+    gc.collect()
+    assert T.saved_state_count() == n0

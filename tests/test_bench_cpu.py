@@ -1,0 +1,53 @@
+"""bench.py's multi-GPU launch contract, on CPU (no GPU is touched):
+``python bench.py --gpus N`` with no outer launcher starts N rank processes
+itself (torch.distributed.run, rendezvous on 127.0.0.1) and a WORLD_SIZE that
+disagrees with --gpus is refused, so a bench line can never report n_gpus
+other than the ranks that ran (VERDICT r2 "Next round" item 2)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def test_launch_plan_single_and_outer_launcher():
+    import bench
+    assert bench.launch_plan(1, ["--gpus", "1"], {}) is None
+    # launched by torch.distributed.run (the driver's N > 1 form): one rank
+    assert bench.launch_plan(4, ["--gpus", "4"], {"WORLD_SIZE": "4"}) is None
+    with pytest.raises(SystemExit):
+        bench.launch_plan(8, ["--gpus", "8"], {"WORLD_SIZE": "1"})
+    with pytest.raises(SystemExit):
+        bench.launch_plan(1, [], {"WORLD_SIZE": "2"})
+
+
+def test_self_launch_maps_ranks(tmp_path):
+    """The command --gpus N builds starts N processes with RANK / LOCAL_RANK
+    0..N-1 and WORLD_SIZE N on 127.0.0.1 (each rank later binds cuda:LOCAL_RANK):
+    run here with a stand-in script in place of bench.py."""
+    import bench
+    cmd = bench.launch_plan(2, ["--gpus", "2", "--steps", "3"], {})
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "2"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "2", "--steps", "3"]
+    probe = tmp_path / "probe.py"
+    probe.write_text(
+        "import json, os, sys\n"
+        "r = int(os.environ['RANK'])\n"
+        f"open(os.path.join({str(tmp_path)!r}, f'r{{r}}.json'), 'w').write(json.dumps(\n"
+        "    {k: os.environ[k] for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR')}\n"
+        "    | {'argv': sys.argv[1:]}))\n")
+    i = cmd.index(os.path.abspath(bench.__file__))
+    cmd = cmd[:i] + [str(probe)] + cmd[i + 1:]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    subprocess.run(cmd, check=True, env=env, timeout=120, capture_output=True)
+    got = [json.loads((tmp_path / f"r{r}.json").read_text()) for r in range(2)]
+    for r, g in enumerate(got):
+        assert g["RANK"] == str(r) and g["LOCAL_RANK"] == str(r)
+        assert g["WORLD_SIZE"] == "2" and g["MASTER_ADDR"] == "127.0.0.1"
+        assert g["argv"] == ["--gpus", "2", "--steps", "3"]

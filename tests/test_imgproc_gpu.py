@@ -261,3 +261,20 @@ def test_random_distortion_in_hip_graph(dev):
         seen.append(out.clone())
     assert rd.step.item() == 4
     assert not torch.equal(seen[0], seen[1]) and not torch.equal(seen[1], seen[2])
+
+
+@pytest.mark.parametrize("h,w,oh,ow,c", [
+    (41, 47, 224, 224, 3), (64, 58, 224, 224, 3), (30, 33, 224, 224, 3), (250, 180, 224, 224, 3),
+    (224, 224, 64, 64, 3), (37, 53, 50, 61, 3), (9, 11, 5, 4, 1), (20, 30, 33, 47, 4),
+    (64, 64, 64, 64, 3), (1, 1, 7, 5, 3)])
+def test_cv_resize_linear_bit_exact(dev, h, w, oh, ow, c):
+    """cv2.resize INTER_LINEAR (08:119, the PSNR leg's clean image) on device
+    equals the oracle restatement bit for bit (up / down / anisotropic /
+    1-pixel; 1, 3, 4 channels; scalar row tails at widths not a multiple of
+    the vector width)."""
+    import roadrestore as rr
+    x = _batch(3, h, w, c, seed=h * w + c)
+    y = rr.imgproc.cv_resize(torch.from_numpy(x).to(dev), (ow, oh)).cpu().numpy()
+    assert y.shape == (3, oh, ow, c)
+    for i in range(3):
+        assert np.array_equal(y[i], I.cv_resize_linear(x[i], oh, ow)), i

@@ -106,6 +106,25 @@ def test_batchnorm_leaf(dev, training, C, hw):
     assert int(m.num_batches_tracked) == (1 if training else 0)
 
 
+def test_batchnorm_leaf_cumulative_momentum_none(dev):
+    """nn.BatchNorm2d(momentum=None): cumulative moving average, factor
+    1 / num_batches_tracked, computed on the device (no host sync, so it also
+    runs inside a HIP-graph capture): equal to torch over 3 batches."""
+    import torch.nn as tnn
+    torch.manual_seed(9)
+    C = 32
+    m = rr.BatchNorm2d(C, momentum=None).to(dev).train()
+    ref = tnn.BatchNorm2d(C, momentum=None).double().train()
+    for i in range(3):
+        x = torch.randn(4, C, 6, 5) * (i + 1) + i
+        with torch.no_grad():
+            m(x.to(dev))
+            ref(x.double())
+    assert int(m.num_batches_tracked) == 3
+    assert rel(m.running_mean, ref.running_mean) <= 1e-6
+    assert rel(m.running_var, ref.running_var) <= 1e-6
+
+
 def test_batchnorm_leaf_rejects_single_value_per_channel(dev):
     m = rr.BatchNorm2d(64).to(dev)
     with pytest.raises(ValueError, match="more than 1 value"):

@@ -1,0 +1,141 @@
+"""Boundary hygiene on the GPU:
+
+* the forward state a network / loss op saves for its backward is freed with
+  the autograd graph (50 grad-enabled forwards without a backward leave
+  device memory flat), and the no-grad validation loss (14:253-263) saves
+  nothing;
+* the eval-mode conv+BN fold follows the running statistics after train-mode
+  forwards that took no optimizer step (BN recalibration);
+* ``torch.library.opcheck`` (schema, autograd registration, fake kernels) on
+  every ``rr::`` op, with real inputs."""
+import gc
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _mem(dev):
+    gc.collect()
+    torch.cuda.synchronize(dev)
+    return torch.cuda.memory_allocated(dev)
+
+
+def test_forward_without_backward_frees_state(dev):
+    import roadrestore as rr
+    from roadrestore import torch_ops as T
+    torch.manual_seed(0)
+    m = rr.ResUNet().to(dev)
+    m.train()
+    perc = rr.VGGPerceptualLoss().to(dev)
+    x = torch.rand(8, 3, 32, 32, device=dev)
+    n0 = T.saved_state_count()
+    out = m(x)                                   # warm the caches / allocator
+    loss = rr.unified_loss(out, x, perc, 0.1)
+    del out, loss
+    base = _mem(dev)
+    for _ in range(50):
+        out = m(x)                               # grads enabled, output dropped
+        loss = rr.unified_loss(out, x, perc, 0.1)
+        del out, loss
+    assert T.saved_state_count() == n0
+    grown = _mem(dev) - base
+    assert grown <= 4 << 20, grown               # flat (one step's state is ~100 MB here)
+    with torch.no_grad():                        # the validation loss (14:253-263)
+        for _ in range(10):
+            rr.unified_loss(m(x), x, perc, 0.1)
+    assert T.saved_state_count() == n0
+    # an exception between forward and backward: the graph dies with the frame
+    try:
+        out = m(x)
+        raise ValueError("boom")
+    except ValueError:
+        pass
+    del out
+    gc.collect()
+    assert T.saved_state_count() == n0
+    # the normal path still works and consumes its state
+    out = m(x)
+    rr.unified_loss(out, x, perc, 0.1).backward()
+    assert T.saved_state_count() == n0
+
+
+def test_eval_fold_follows_running_stats_without_optimizer_step(dev):
+    """eval forward -> train-mode forwards with no optimizer step (the
+    running statistics move) -> eval forward: the folded conv+BN weights
+    must be re-made from the new statistics (keyed on tensor
+    versions the finalize never bumped)."""
+    import roadrestore as rr
+    from oracle import reference_cpu as R
+    from oracle import seeded as S
+    sd = S.model_state_dict("resunet")
+    m = rr.ResUNet().to(dev)
+    m.load_state_dict(sd)
+    x = S.fog_noise(S.image_batch(2, 32, 32, seed=3), seed=4)
+    m.eval()
+    with torch.no_grad():
+        out0 = m(x.to(dev)).cpu()
+    m.train()
+    with torch.no_grad():
+        for _ in range(3):
+            m(x.to(dev) * 0.5)                   # BN recalibration, no step
+    m.eval()
+    with torch.no_grad():
+        out1 = m(x.to(dev)).cpu()
+    cur = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    ref = R.resunet_forward(cur, x, training=False)
+    assert (out1 - ref).abs().mean().item() <= 1e-4
+    assert (out0 - out1).abs().max().item() > 1e-3      # the statistics really moved
+
+
+def _opcheck(op, args, utils=("test_schema", "test_autograd_registration", "test_faketensor")):
+    torch.library.opcheck(op, args, test_utils=utils)
+
+
+def test_opcheck_every_rr_op(dev):
+    """torch.library.opcheck on every rr:: op with real device inputs."""
+    import roadrestore as rr
+    from roadrestore import ops
+    torch.manual_seed(0)
+    x = torch.rand(2, 3, 16, 16, device=dev)
+    y = torch.rand(2, 3, 16, 16, device=dev)
+    m = rr.ResUNet().to(dev).train()
+    su = rr.SimpleUNet().to(dev).train()
+    blk = rr.ResidualBlock(64, 128).to(dev).train()
+    perc = rr.VGGPerceptualLoss().to(dev)
+    vgg = rr.vgg16().to(dev).eval()
+    o = torch.ops.rr
+    # networks: forward (need_backward False: opcheck runs the op repeatedly)
+    _opcheck(o.resunet_forward.default, (x, list(m.parameters()), m._op_key, False))
+    _opcheck(o.simple_unet_forward.default, (x, list(su.parameters()), su._op_key, False))
+    xb = torch.rand(2, 64, 8, 8, device=dev)
+    _opcheck(o.resblock_forward.default, (xb, list(blk.parameters()), blk._op_key, False))
+    # their backward ops take a live handle: one forward per call
+    for net, xin in ((m, x), (su, x), (blk, xb)):
+        pre = net._op
+        fwd = getattr(o, f"{pre}_forward").default
+        bwd = getattr(o, f"{pre}_backward").default
+        out, h = fwd(xin, list(net.parameters()), net._op_key, True)
+        _opcheck(bwd, (torch.ones_like(out), h, net._op_key), utils=("test_schema",
+                                                                      "test_faketensor"))
+    # losses
+    _opcheck(o.pixel_loss.default, (x, y, ops.L1))
+    _opcheck(o.pixel_loss_backward.default, (torch.ones((), device=dev), x, y, ops.MSE))
+    _opcheck(o.unified_loss.default, (x, y, perc._op_key, 0.1, 1.0, False))
+    _opcheck(o.perceptual_loss.default, (x, y, perc._op_key, False))
+    loss, h = o.unified_loss(x, y, perc._op_key, 0.1, 1.0, True)
+    _opcheck(o.unified_loss_backward.default, (torch.ones((), device=dev), x, y, h, 0.1, 1.0),
+             utils=("test_schema", "test_faketensor"))
+    loss, h = o.perceptual_loss(x, y, perc._op_key, True)
+    _opcheck(o.perceptual_loss_backward.default, (torch.ones((), device=dev), h, x),
+             utils=("test_schema", "test_faketensor"))
+    # judge and post-processing
+    with torch.no_grad():
+        _opcheck(o.vgg16_logits.default, (torch.rand(2, 3, 32, 32, device=dev),
+                                          list(vgg.parameters()), vgg._op_key))
+    _opcheck(o.nearest_resize.default, (torch.rand(2, 5, 7, 64, device=dev), 9, 13))
+    _opcheck(o.to_uint8_hwc.default, (x, True))
+    u8 = o.to_uint8_hwc(x, False)
+    _opcheck(o.psnr_u8.default, (u8, o.to_uint8_hwc(y, False)))
+    _opcheck(o.argmax_rows.default, (torch.rand(7, 43, device=dev),))

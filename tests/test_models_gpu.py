@@ -2,6 +2,8 @@
 the REFERENCE classes (oracle/gen_golden.py) on the same seeded weights and
 inputs.  Tolerances (fp32 path): restored image MAE <= 1e-4 (BASELINE.json
 north star) and max |err| <= 1e-3; PSNR within 0.01 dB; Top-1 identical."""
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -31,6 +33,10 @@ def _oracle_step(kind, bad, clean, sd, perc_sd, dtype):
     if kind == "simpleunet":
         loss = R.mse_loss(R.simple_unet_forward(p, bad), clean)
         lr, wd, dec = 1e-3, 0.0, False
+    elif kind == "simpleunet_perc":                 # 07adv:143-157
+        pp = {k: v.detach().clone().to(dtype) for k, v in perc_sd.items()}
+        loss = R.unified_loss(R.simple_unet_forward(p, bad), clean, pp)
+        lr, wd, dec = 2e-4, 0.0, False
     else:
         pp = {k: v.detach().clone().to(dtype) for k, v in perc_sd.items()}
         loss = R.unified_loss(R.resunet_forward(p, bad, True), clean, pp)
@@ -146,6 +152,73 @@ def test_simpleunet_train_step_golden(dev):
     _check_grads(m, z, g32, g64)
     opt.step()
     _check_post(m, p32, p64, 1e-3)
+
+
+def test_simpleunet_perceptual_step_07adv_golden(dev):
+    """07_train_restoration_advanced.py:143-157: SimpleUNet, loss = L1 + 0.1 *
+    VGG16[:16] perceptual (07adv:95-112), Adam lr 2e-4 -- one step against
+    the fixture the reference's own classes produced (loss, fp64-anchored
+    grads, post-Adam parameters)."""
+    import roadrestore as rr
+    from oracle import seeded as S
+    z = gold("simpleunet_07adv")
+    m = rr.SimpleUNet().to(dev)
+    m.load_state_dict(S.model_state_dict("simpleunet"))
+    m.train()
+    perc_sd = S.seeded_state_dict(S.load_manifest("perceptual"), seed=5)
+    perc = rr.VGGPerceptualLoss().to(dev)
+    perc.load_state_dict(perc_sd)
+    bad, clean = torch.from_numpy(z["bad"]).to(dev), torch.from_numpy(z["clean"]).to(dev)
+    lr = float(z["lr"][0])
+    opt = rr.Adam(m.parameters(), lr=lr)                            # 07adv:136
+    opt.zero_grad()
+    loss = rr.unified_loss(m(bad), clean, perc, 0.1)                # 07adv:147-154
+    loss.backward()
+    assert abs(loss.item() - z["loss"][0]) <= 1e-5 * max(1, abs(z["loss"][0]))
+    args = ("simpleunet_perc", torch.from_numpy(z["bad"]), torch.from_numpy(z["clean"]),
+            S.model_state_dict("simpleunet"), perc_sd)
+    l32, g32, p32 = _oracle_step(*args, torch.float32)
+    _, g64, p64 = _oracle_step(*args, torch.float64)
+    assert abs(l32 - z["loss"][0]) <= 1e-6 * abs(l32)
+    _check_grads(m, z, g32, g64)
+    opt.step()
+    _check_post(m, p32, p64, lr)
+
+
+def test_simpleunet_08_psnr_leg_golden(dev):
+    """cfg2's PSNR leg, 08_run_inference.py:86-125, all on device: PIL
+    Resize(224) + ToTensor of the distorted image, SimpleUNet eval forward
+    (batch 1, 08:92-93), clamp / x255 / uint8 truncation / BGR, the clean
+    image through cv2.resize(224, 224) (OpenCV INTER_LINEAR, restated:
+    parity vs cv2 unpinned), PSNR and SSIM -- against the fixture the
+    reference SimpleUNet produced.  Bounds: uint8 output within one level on
+    < 0.1 % of the values (truncation boundaries under a different fp32
+    summation order), the resized clean image exact, PSNR within 0.01 dB
+    (BASELINE.json north star), SSIM within 1e-3."""
+    import roadrestore as rr
+    from oracle import seeded as S
+    T = rr.imgproc
+    z = gold("simpleunet_08")
+    m = rr.SimpleUNet().to(dev)
+    m.load_state_dict(S.model_state_dict("simpleunet"))
+    m.eval()
+    tf = T.Compose([T.Resize((224, 224)), T.ToTensor()])
+    for i in range(len(z["sizes"])):
+        dist = torch.from_numpy(z[f"dist_{i}"]).unsqueeze(0).to(dev)
+        with torch.no_grad():
+            out = m(tf(dist))                                       # 08:88-93
+        assert abs(out.double().sum().item() - z[f"out_sum_{i}"][0]) <= 1e-4 * out.numel()
+        u8 = rr.ops.to_uint8_hwc(out, bgr=True)                     # 08:96-100
+        ref = z["out_bgr"][i].astype(int)
+        mism = u8[0].cpu().numpy().astype(int) - ref
+        assert np.abs(mism).max() <= 1 and (mism != 0).mean() < 1e-3, (i, (mism != 0).mean())
+        clean = torch.from_numpy(z[f"clean_bgr_{i}"]).unsqueeze(0).to(dev)
+        c224 = T.cv_resize(clean, (224, 224))                       # 08:119
+        assert np.array_equal(c224[0].cpu().numpy(), z["clean224"][i])
+        ps = T.psnr(c224, u8).item()                                # 08:123
+        ss = T.ssim(c224, u8).item()                                # 08:125
+        assert abs(ps - z["psnr"][i]) <= 0.01, (i, ps, z["psnr"][i])
+        assert abs(ss - z["ssim"][i]) <= 1e-3, (i, ss, z["ssim"][i])
 
 
 def test_resunet_forward_golden(dev):
@@ -402,6 +475,66 @@ def test_hip_graph_training_step_matches_eager(dev, prefetch):
     for (na, pa), (nb, pb) in zip(ma.named_parameters(), mb.named_parameters()):
         d = (pa - pb).abs().max().item()
         assert d <= 1e-6 * max(1.0, pa.abs().max().item()), (na, d)
+
+
+def test_hip_graph_step_follows_cosine_lr_schedule(dev):
+    """The LR schedule under HIP-graph replay (14:223, 248): the capturable
+    AdamW keeps lr on the device, CosineAnnealingLR(T_max=25).step() once per
+    "epoch" writes it in place, and the captured step reads it on every replay.
+    3 epochs x 2 replays must match eager steps with the host float lr, epoch
+    by epoch (lr and parameters)."""
+    import roadrestore as rr
+    from roadrestore.optim import flatten_parameters
+    B, H = 2, 16
+    g = torch.Generator(device=dev).manual_seed(11)
+    clean = torch.rand((B, 3, H, H), generator=g, device=dev)
+    bad = (clean * 0.5 + 0.4).clamp(0, 1)
+
+    def make(capturable):
+        torch.manual_seed(13)
+        m = rr.ResUNet().to(dev)
+        m.train()
+        flatten_parameters(m)
+        opt = rr.AdamW(m.parameters(), lr=2e-4, weight_decay=1e-4, capturable=capturable)
+        sch = rr.CosineAnnealingLR(opt, T_max=25)
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            loss = rr.L1Loss()(m(bad), clean)
+            loss.backward()
+            opt.step()
+            return loss
+        return m, opt, sch, step
+
+    ma, oa, sa, step_a = make(False)
+    mb, ob, sb, step_b = make(True)
+    assert isinstance(ob.param_groups[0]["lr"], torch.Tensor) and ob.param_groups[0]["lr"].is_cuda
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step_b()                                   # 1 eager step (epoch 0)
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        step_b()                                   # recorded, not executed
+    step_a()
+    step_a()
+    graph.replay()                                 # epoch 0: steps 1, 2
+    for epoch in range(3):
+        if epoch:
+            for _ in range(2):
+                step_a()
+                graph.replay()
+        sa.step()
+        sb.step()
+        torch.cuda.synchronize()
+        lra, lrb = float(oa.param_groups[0]["lr"]), ob.param_groups[0]["lr"].item()
+        assert abs(lra - lrb) <= 1e-6 * lra, (epoch, lra, lrb)
+        for (na, pa), (nb, pb) in zip(ma.named_parameters(), mb.named_parameters()):
+            d = (pa - pb).abs().max().item()
+            assert d <= 1e-5 * max(1.0, pa.abs().max().item()), (epoch, na, d)
+    # the schedule really moved lr (cosine, 3 epochs of T_max = 25)
+    assert abs(float(oa.param_groups[0]["lr"]) - 2e-4 * (1 + math.cos(math.pi * 3 / 25)) / 2) < 1e-9
 
 
 def test_hip_graph_dp_step_with_rccl_matches_eager(dev):

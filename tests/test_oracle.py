@@ -155,3 +155,69 @@ def test_resunet_oracle_odd_sizes(hw):
         perc_sd = S.seeded_state_dict(S.load_manifest("perceptual"), seed=5)
         loss = R.unified_loss(out, clean, perc_sd)
         assert abs(loss.item() - z["loss"][0]) <= 1e-6 * abs(z["loss"][0])
+
+
+def test_08_psnr_leg_oracle():
+    """cfg2's PSNR leg (08:86-125): the oracle chain -- Pillow Resize(224) +
+    ToTensor, SimpleUNet batch-1 eval forward, uint8 truncation + BGR, the
+    restated cv2.resize(INTER_LINEAR) of the clean image, PSNR / SSIM --
+    reproduces the fixture the REFERENCE SimpleUNet (08:19-46) produced.
+    The cv2 resize and skimage metrics are restatements (parity vs cv2 /
+    skimage unpinned)."""
+    from PIL import Image
+    from oracle import imgproc_cpu as I
+    z = gold("simpleunet_08")
+    sd = S.model_state_dict("simpleunet")
+    for i in range(len(z["sizes"])):
+        dist = z[f"dist_{i}"]
+        x = torch.from_numpy(np.asarray(Image.fromarray(dist, "RGB").resize((224, 224),
+                                                                           Image.BILINEAR)).copy())
+        assert np.array_equal(x.numpy(), I.pil_resize_bilinear(dist, 224, 224))
+        x = x.permute(2, 0, 1).float().div(255).unsqueeze(0)
+        with torch.no_grad():
+            out = R.simple_unet_forward({k: v.clone() for k, v in sd.items()}, x)
+        assert abs(out.double().sum().item() - z[f"out_sum_{i}"][0]) <= 1e-6 * out.numel()
+        u8 = R.to_uint8_image(out)[0][:, :, ::-1]
+        assert np.array_equal(u8, z["out_bgr"][i])
+        c224 = I.cv_resize_linear(z[f"clean_bgr_{i}"], 224, 224)
+        assert np.array_equal(c224, z["clean224"][i])
+        assert abs(R.psnr_u8(c224, u8) - z["psnr"][i]) < 1e-12
+        assert abs(I.ssim(c224, u8) - z["ssim"][i]) < 1e-12
+
+
+def test_cv_resize_oracle_properties():
+    """The OpenCV INTER_LINEAR restatement: same size = copy; a constant image
+    stays constant (weights sum to 2048, both rounding paths exact there);
+    upscaling by 2 keeps every source pixel's value on the grid where the
+    source coordinate lands on it; the SIMD and scalar vertical roundings
+    differ by at most one level."""
+    from oracle import imgproc_cpu as I
+    rng = np.random.default_rng(1)
+    img = rng.integers(0, 256, (13, 17, 3), dtype=np.uint8)
+    assert np.array_equal(I.cv_resize_linear(img, 13, 17), img)
+    for v in (0, 1, 128, 254, 255):
+        c = np.full((9, 11, 3), v, np.uint8)
+        assert np.all(I.cv_resize_linear(c, 224, 224) == v)
+        assert np.all(I.cv_resize_linear(c, 4, 5) == v)
+    a = I.cv_resize_linear(img, 50, 61, simd_lanes=16)
+    b = I.cv_resize_linear(img, 50, 61, simd_lanes=10 ** 6)       # all scalar
+    assert np.abs(a.astype(int) - b.astype(int)).max() <= 1
+
+
+def test_07adv_step_oracle():
+    """07adv:143-157 (SimpleUNet, L1 + 0.1 perceptual, Adam lr 2e-4): the
+    oracle's loss and grads reproduce the reference's fixture."""
+    z = gold("simpleunet_07adv")
+    sd = S.model_state_dict("simpleunet")
+    perc = S.seeded_state_dict(S.load_manifest("perceptual"), seed=5)
+    p = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    bad, clean = torch.from_numpy(z["bad"]), torch.from_numpy(z["clean"])
+    out = R.simple_unet_forward(p, bad)
+    assert abs(R.l1_loss(out, clean).item() - z["l_pix"][0]) <= 1e-7
+    loss = R.unified_loss(out, clean, perc)
+    assert abs(loss.item() - z["loss"][0]) <= 1e-6 * abs(z["loss"][0])
+    loss.backward()
+    for k, v in p.items():
+        idx = z[f"grad:{k}|idx"]
+        assert np.abs(v.grad.reshape(-1)[idx].numpy() - z[f"grad:{k}|val"]).max() <= \
+            1e-5 * (v.grad.abs().max().item() + 1e-30), k

@@ -60,6 +60,16 @@ def _worker(rank, world, port, result_q):
         v = sink[p]
         want = 0.0 if id(p) in {id(z) for z in zero} else float(total * (i + 1))
         ok &= bool(torch.all(v == want))
+    # eval mode (frozen-BN fine-tune): the conv biases feeding a BN carry real
+    # gradients in the zero section, which must be all-reduced as well
+    m.eval()
+    sink = m._make_sink(order, zero, torch.device("cpu"))
+    for i, p in enumerate(sink.order):
+        sink[p].fill_(float(rank + 1) * (i + 1))
+    for g in groups:
+        sink.ready(list(g.parameters()))
+    for i, p in enumerate(sink.order):
+        ok &= bool(torch.all(sink[p] == float(total * (i + 1))))
     result_q.put((rank, same, ok, launched_early, len(dp.buckets), dp.grad_scale))
     dist.destroy_process_group()
 
