@@ -1,0 +1,369 @@
+// conv3r.hip -- tap-reuse 3x3 bf16 convolution: forward, dgrad and the
+// fused BN/PReLU-backward dgrad of the 64-512-channel layers on 8x8, 16x16
+// and 32x32 maps (ResUNet res2 / res3 / dec2 / dec3 / bottleneck,
+// 14_train_unified_advanced.py:96-186; VGG16 conv2_x / conv3_x of the
+// perceptual loss, 14:189-196; SimpleUNet enc2 / bottleneck / dec2,
+// 07:75-120).
+//
+// What bounds the LDS-halo igemm (igemm.hip) on these layers is the LDS
+// port: its 8 waves own 64 x 32 output tiles and re-read a 64 x 64 weight
+// stage and a 32-pixel activation stage from LDS for every 16 MFMAs, ~768 B
+// of fragment reads per MFMA against the ~1 KB the port supplies per MFMA
+// slot, and every (K chunk, tap) stage ends in a barrier.  Here a wave owns
+// 128 output pixels = R whole output rows (W = 16, 32) or the same 8 rows of
+// two images (W = 8), times 64 output channels, and walks the K loop in
+// stages of (32 input channels, tap column dx):
+//
+//   * the halo of the tile (its rows + 1 above / below, zero at the image
+//     edges) for 32 input channels sits in LDS as 1-KB blocks of 16 pixels x
+//     4 channel planes of 8 (block byte = plane * 256 + pixel * 16), so a
+//     B-fragment read (ds_read_b128: lane = pixel l & 15, plane l >> 4) of
+//     16 consecutive pixels at ANY shift hits 16 distinct bank slots;
+//   * per stage the wave loads the A fragments (weights) of the three taps
+//     (dy, dx), dy = 0..2, once (12 reads), then streams its R + 2 halo rows:
+//     halo row ri is read ONCE and feeds output rows ri, ri - 1, ri - 2 (taps
+//     dy = 0, 1, 2) -- 3 x NM MFMAs per fragment read instead of NM;
+//   * the left / right zero padding is not stored: the shifted read of the
+//     edge column is zeroed in registers (one v_cndmask per dword);
+//   * 96 MFMAs per wave per stage (R x NS x NM x 3), one barrier per stage;
+//     LDS fragment traffic ~240 B per MFMA;
+//   * operands arrive by LDS-DMA (global_load_lds_dwordx4) one stage ahead
+//     into double buffers: the next stage's weights (from the packed
+//     [c_out][9][c_in] rows) and, at the first stage of a chunk, the next
+//     chunk's halo (from the NHWC activations; out-of-image rows from the
+//     zero page).  hipcc would drain the DMA (vmcnt(0)) before any ds_read
+//     it cannot separate from a DMA destination, so the fragment reads are
+//     inline asm with counted lgkmcnt waits, and the stage boundary is a
+//     counted vmcnt + raw s_barrier;
+//   * the epilogue stages one 128-pixel group at a time as fp32 [128][BC]
+//     in LDS and reuses the tiled kernels' staged store (igemm_epi.h): BN
+//     statistics (one partial row per 128 pixels), bias, ReLU, accumulate,
+//     ReLU-backward mask, concat split, or the fused BN/PReLU backward.
+//
+// Workgroup: 8 waves = WC channel groups x WP pixel groups; BC = 64 NW
+// channels per wave group.  Geometry per (W, BC) in R3 below.
+#include "common.h"
+#include "conv3r.h"
+
+#include <cstdlib>
+
+namespace {
+
+template <int W, int BC, int NW> struct R3 {
+  static constexpr bool PAIR = W == 8;              // a row unit = the same row of 2 images
+  static constexpr int NS = PAIR ? 1 : W / 16;      // 16-pixel column blocks per row unit
+  static constexpr int R = PAIR ? 8 : 128 / W;      // output rows per wave
+  static constexpr int NM = NW / 16;                // 16-channel MFMA rows per wave
+  static constexpr int WC = BC / NW, WP = 8 / WC;   // wave grid
+  static constexpr int TPX = WP * 128;              // pixels per tile
+  static constexpr int TR = PAIR ? 8 : WP * R;      // tile rows (W >= 16)
+  static constexpr int HS = PAIR ? 8 : (TR < W ? TR : W);       // output rows per halo segment
+  static constexpr int SEG = PAIR ? WP : (TR < W ? 1 : TR / W); // segments (images / pairs)
+  static constexpr int HROWS = SEG * (HS + 2);
+  static constexpr int HBLK = HROWS * NS;           // 1-KB halo blocks per 32-channel chunk
+  static constexpr int HBYTES = HBLK * 1024;
+  static constexpr int WBLK = 3 * (BC / 16);        // weight blocks per stage (3 taps)
+  static constexpr int WBYTES = WBLK * 1024;
+  static constexpr int NHG = (HBLK + 7) / 8;        // halo DMA pieces per wave per chunk
+  static constexpr int NWG = (WBLK + 7) / 8;        // weight DMA pieces per wave per stage
+  static constexpr int SROW = BC + 4;
+  static constexpr int STG = 128 * SROW * 4 + (8 * BC * 2 + 8) * 4 + 256;
+  // [weights x2][halo x2][guard block]: the shifted edge reads stay inside
+  static constexpr int KBYTES = 2 * WBYTES + 2 * HBYTES + 1024;
+  static constexpr int LDS = KBYTES > STG ? KBYTES : STG;
+  static_assert(LDS <= 160 * 1024, "LDS");
+  static_assert(WC * WP == 8 && NM * 16 == NW, "wave grid");
+  static_assert(PAIR || TR % W == 0 || W % TR == 0, "tile rows");
+  static_assert(2 * WBYTES >= 1024, "the edge read of the first halo block stays in LDS");
+};
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+template <int N> __device__ __forceinline__ void vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <int W, int BC, int NW>
+__global__ __launch_bounds__(512) void conv3r_kernel(IgemmArgs a) {
+  using G = R3<W, BC, NW>;
+  constexpr int NS = G::NS, R = G::R, NM = G::NM, WC = G::WC;
+  constexpr int HW = W * W;
+  __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wv % WC, wp = wv / WC;
+  const int frow = lane & 15, fq = lane >> 4;
+
+  // XCD-aware tile order (as igemm3_halo_kernel): XCD b % 8 walks a
+  // contiguous tile range, so column blocks of a pixel tile share its L2
+  int tile = blockIdx.x;
+  if (a.xcd) {
+    const int per = (int)gridDim.x / 8;
+    if ((int)blockIdx.x < per * 8) tile = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
+  }
+  const int cblk = tile % a.ncblk, pblk = tile / a.ncblk;
+  const int c0 = cblk * BC;
+  const int p0 = pblk * G::TPX;
+  const int n0 = p0 / HW;
+  const int ys = G::PAIR || G::TR >= W ? 0 : (p0 - n0 * HW) / W;   // first tile row (one segment)
+
+  const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+  const uint32_t wbase = sbase, hbase = sbase + 2 * G::WBYTES;
+
+  // ---- per-lane DMA sources ----
+  // halo block b = (segment k, halo row hr, column block s): pixel index of
+  // this lane's 16 B (-1: zero padding row)
+  int hpix[G::NHG], hdst[G::NHG];
+#pragma unroll
+  for (int i = 0; i < G::NHG; ++i) {
+    int b = wv + 8 * i;
+    if (b >= G::HBLK) b -= 8;                       // a duplicate of this wave's previous block
+    const int k = b / ((G::HS + 2) * NS);
+    const int rem = b - k * ((G::HS + 2) * NS);
+    const int hr = rem / NS, s = rem - (rem / NS) * NS;
+    int pix = -1;
+    if constexpr (G::PAIR) {
+      const int y = hr - 1;
+      if (y >= 0 && y < W) pix = ((n0 + 2 * k + (frow >> 3)) * W + y) * W + (frow & 7);
+    } else {
+      const int y = ys + hr - 1;
+      if (y >= 0 && y < W) pix = ((n0 + k) * W + y) * W + 16 * s + frow;
+    }
+    hpix[i] = pix;
+    hdst[i] = b * 1024;
+  }
+  // weight block wb = (tap row dy, 16-channel block m): this lane's row
+  int wrow[G::NWG], wdst[G::NWG], wdy[G::NWG];
+#pragma unroll
+  for (int i = 0; i < G::NWG; ++i) {
+    int b = wv + 8 * i;
+    if (b >= G::WBLK) b -= 8;
+    const int dy = b / (BC / 16), m = b - dy * (BC / 16);
+    wrow[i] = (c0 + m * 16 + frow) * a.K * 2 + fq * 16;
+    wdst[i] = b * 1024;
+    wdy[i] = dy;
+  }
+  auto issue_w = [&](int st) __attribute__((always_inline)) {
+    const int ch = st / 3, dx = st - ch * 3;
+    char *dst = smem + (st & 1) * G::WBYTES;
+#pragma unroll
+    for (int i = 0; i < G::NWG; ++i) {
+      const long long off = (long long)wrow[i] + ((wdy[i] * 3 + dx) * a.cin + ch * 32) * 2;
+      __builtin_amdgcn_global_load_lds((const void *)(a.wt + off), LDS_PTR(dst + wdst[i]), 16, 0, 0);
+    }
+  };
+  auto issue_h = [&](int ch) __attribute__((always_inline)) {
+    const int ci0 = ch * 32;
+    const bool first = ci0 < a.c1;                  // uniform
+    const char *base = first ? a.x1 : a.x2;
+    const long long cs = first ? a.c1 : a.c2;
+    const long long cl = first ? ci0 : ci0 - a.c1;
+    const long long zoff = (long long)((uintptr_t)rr_zero_page - (uintptr_t)base) + fq * 16;
+    char *dst = smem + 2 * G::WBYTES + (ch & 1) * G::HBYTES;
+#pragma unroll
+    for (int i = 0; i < G::NHG; ++i) {
+      const long long off = hpix[i] >= 0 ? ((long long)hpix[i] * cs + cl) * 2 + fq * 16 : zoff;
+      __builtin_amdgcn_global_load_lds((const void *)(base + off), LDS_PTR(dst + hdst[i]), 16, 0, 0);
+    }
+  };
+
+  // ---- fragment addressing ----
+  // A: weight block (dy, wc * NM + m) of the stage buffer; the lane reads
+  // its 16 B at lane * 16 (plane fq, row frow)
+  const uint32_t a_lane = wbase + (wc * NM) * 1024 + lane * 16;
+  // B: the wave's first halo row (output row 0 minus 1) ...
+  int hrow0;
+  if constexpr (G::PAIR) {
+    hrow0 = wp * (G::HS + 2);
+  } else {
+    const int r0 = wp * R;                           // first output row of the wave in the tile
+    const int k = r0 / G::HS;
+    hrow0 = k * (G::HS + 2) + (r0 - k * G::HS);
+  }
+  // ... and the lane part of a read at tap column dx (pixel frow + dx - 1)
+  uint32_t loff[3];
+  bool zl[3];                                        // lane reads a padding column at dx
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) {
+    if constexpr (G::PAIR) {
+      const int x = (frow & 7) + dx - 1;
+      const int xc = x < 0 ? 0 : (x > 7 ? 7 : x);
+      loff[dx] = fq * 256 + ((frow >> 3) * 8 + xc) * 16;
+      zl[dx] = x != xc;
+    } else {
+      const int x = frow + dx - 1;                  // -1 / 16: the neighbouring block
+      loff[dx] = x < 0 ? fq * 256 + 240 - 1024 : (x > 15 ? fq * 256 + 1024 : fq * 256 + x * 16);
+      zl[dx] = x < 0 || x > 15;
+    }
+  }
+  const uint32_t b_wave = hbase + hrow0 * NS * 1024;
+
+  f32x4 acc[R][NS][NM];
+#pragma unroll
+  for (int o = 0; o < R; ++o)
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int m = 0; m < NM; ++m) acc[o][s][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int kc = a.cin / 32, nst = 3 * kc;
+  // prologue: chunk 0's halo, stage 0's weights
+  issue_h(0);
+  issue_w(0);
+  vm_barrier<0>();
+
+  for (int st = 0; st < nst; ++st) {
+    const int ch = st / 3, dx = st - ch * 3;       // uniform
+    // operands of the next stage (weights) and of the next chunk (halo)
+    if (st + 1 < nst) issue_w(st + 1);
+    const bool next_h = dx == 0 && ch + 1 < kc;
+    if (next_h) issue_h(ch + 1);
+
+    const uint32_t aa = a_lane + (st & 1) * G::WBYTES;
+    const uint32_t ba = b_wave + (ch & 1) * G::HBYTES +
+                        (dx == 0 ? loff[0] : (dx == 1 ? loff[1] : loff[2]));
+    const bool zlo = dx == 0 && zl[0];               // left padding column (block s = 0)
+    const bool zhi = dx == 2 && zl[2];               // right padding column (block NS - 1)
+    i32x4 af[3][NM];
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int m = 0; m < NM; ++m)
+        asm volatile("ds_read_b128 %0, %1 offset:%2"
+                     : "=v"(af[dy][m]) : "v"(aa), "i"((dy * (BC / 16) + m) * 1024));
+    i32x4 bf[2][NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bf[0][s]) : "v"(ba), "i"(s * 1024));
+#pragma unroll
+    for (int ri = 0; ri < R + 2; ++ri) {
+      if (ri + 1 < R + 2) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+          asm volatile("ds_read_b128 %0, %1 offset:%2"
+                       : "=v"(bf[(ri + 1) & 1][s]) : "v"(ba), "i"(((ri + 1) * NS + s) * 1024));
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+#pragma unroll
+      for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(bf[ri & 1][s]));
+      if (ri == 0) {
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int m = 0; m < NM; ++m) asm volatile("" : "+v"(af[dy][m]));
+      }
+      // the padding columns: zero the shifted edge reads
+      {
+        i32x4 &lo = bf[ri & 1][0];
+        i32x4 &hi = bf[ri & 1][NS - 1];
+        if (G::PAIR) {
+          if (zlo || zhi) lo = i32x4{0, 0, 0, 0};
+        } else {
+          if (zlo) lo = i32x4{0, 0, 0, 0};
+          if (zhi) hi = i32x4{0, 0, 0, 0};
+        }
+      }
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) {
+        const int o = ri - dy;
+        if (o < 0 || o >= R) continue;
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+          for (int m = 0; m < NM; ++m)
+            acc[o][s][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8, af[dy][m]), __builtin_bit_cast(bf16x8, bf[ri & 1][s]),
+                acc[o][s][m], 0, 0, 0);
+      }
+    }
+    // the next stage's weights must have landed; a next chunk's halo (issued
+    // after them) may stay in flight for one more stage
+    if (next_h) vm_barrier<G::NHG>();
+    else vm_barrier<0>();
+  }
+
+  // ---- epilogue: one 128-pixel group (= one wave row of the grid) at a
+  // time as fp32 [128][BC] in LDS, then the staged store ----
+  float *stg = reinterpret_cast<float *>(smem);
+  for (int g = 0; g < G::WP; ++g) {
+    if (wp == g) {
+#pragma unroll
+      for (int o = 0; o < R; ++o)
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+          for (int m = 0; m < NM; ++m) {
+            const int r = G::PAIR ? (frow >> 3) * 64 + o * 8 + (frow & 7) : o * W + 16 * s + frow;
+            const int col = wc * NW + m * 16 + fq * 4;
+            *reinterpret_cast<f32x4 *>(stg + r * G::SROW + col) = acc[o][s][m];
+          }
+    }
+    __syncthreads();
+    store_staged<bf16_t, BC, 128, 512, RR_CONV3X3>(a, stg, c0, p0 + g * 128, p0 / 128 + g, tid);
+    __syncthreads();
+  }
+}
+
+int r3_nw(int bc) { return bc == 64 ? 32 : 64; }
+int r3_tpx(int bc) { return (8 / (bc / r3_nw(bc))) * 128; }
+
+}  // namespace
+
+int conv3r_bc(const rr_igemm_desc *d) {
+  const char *e = getenv("RR_CONV3R");              // A/B switch (per call): 0 = halo kernels
+  if (e && atoi(e) == 0) return 0;
+  if (!d || d->dtype != RR_BF16 || d->mode != RR_CONV3X3 || d->out_nchw) return 0;
+  const int W = d->w;
+  if (d->h != W || !(W == 8 || W == 16 || W == 32)) return 0;
+  if (d->c_in1 <= 0 || d->c_in1 % 32 || d->c_in2 % 32 || d->c_out % 64) return 0;
+  if (d->out_split && (d->out_split % 8 || d->out_split >= d->c_out)) return 0;
+  const int bc = d->c_out % 256 == 0 ? 256 : (d->c_out % 128 == 0 ? 128 : 64);
+  const long long P = (long long)d->n * d->h * d->w;
+  if (P % r3_tpx(bc)) return 0;
+  return bc;
+}
+
+int conv3r_stat_blocks(const rr_igemm_desc *d) {
+  if (!conv3r_bc(d)) return 0;
+  return (int)(((long long)d->n * d->h * d->w) / 128);
+}
+
+template <int BC>
+static int conv3r_go(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
+  constexpr int NW = BC == 64 ? 32 : 64;
+  a.ncblk = a.cout / BC;
+  const long long nblk = ((long long)a.P / (8 / (BC / NW) * 128)) * a.ncblk;
+  if (nblk <= 0 || nblk > 0x7fffffffLL) return RR_EUNSUPPORTED;
+  const dim3 grid((unsigned)nblk), block(512);
+  switch (d->w) {
+    case 32: hipLaunchKernelGGL((conv3r_kernel<32, BC, NW>), grid, block, 0, st, a); break;
+    case 16: hipLaunchKernelGGL((conv3r_kernel<16, BC, NW>), grid, block, 0, st, a); break;
+    default: hipLaunchKernelGGL((conv3r_kernel<8, BC, NW>), grid, block, 0, st, a); break;
+  }
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+int conv3r_launch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
+  switch (conv3r_bc(d)) {
+    case 256: return conv3r_go<256>(d, a, st);
+    case 128: return conv3r_go<128>(d, a, st);
+    case 64: return conv3r_go<64>(d, a, st);
+    default: return RR_EUNSUPPORTED;
+  }
+}
+
+const char *conv3r_name(const rr_igemm_desc *d) {
+  static const char *names[3][3] = {
+      {"conv3r_kernel<8,64>", "conv3r_kernel<16,64>", "conv3r_kernel<32,64>"},
+      {"conv3r_kernel<8,128>", "conv3r_kernel<16,128>", "conv3r_kernel<32,128>"},
+      {"conv3r_kernel<8,256>", "conv3r_kernel<16,256>", "conv3r_kernel<32,256>"}};
+  const int bc = conv3r_bc(d);
+  if (!bc) return "invalid";
+  const int wi = d->w == 8 ? 0 : d->w == 16 ? 1 : 2;
+  const int bi = bc == 64 ? 0 : bc == 128 ? 1 : 2;
+  return names[bi][wi];
+}

@@ -133,24 +133,35 @@ def test_bn_finalize_out_validated_before_launch():
         rr.ops.bn_finalize(st, 64, None, z, z, z, z, out=(torch.empty(8), torch.empty(8)))
 
 
+def rr_stat_blocks(d):
+    import ctypes as C
+    import roadrestore as rr
+    return rr.lib().rr_igemm_stat_blocks(C.byref(d))
+
+
 def test_kernel_selection_for_the_benched_layers():
     """The library reports which kernel owns each cfg3 layer (B = 512, bf16,
     64x64 input) -- host-only queries, no launch: the row-streaming conv and
-    weight grad on the 64-channel 64x64 / 32x32 layers, the LDS-halo kernels
-    on the rest."""
+    weight grad on the 64-channel 64x64 / 32x32 layers, the tap-reuse conv
+    (conv3r) on the wider 32x32 .. 8x8 layers, the LDS-halo weight grads on
+    the 16x16 / 8x8 ones."""
     from roadrestore import ops
     from roadrestore._lib import RR_BF16, RR_CONV3X3, IgemmDesc, WgradDesc
     want = {  # (h, c_in1, c_in2, c_out): (fwd, wgrad)
         (64, 64, 0, 64): ("stream3_kernel<64>", "swgrad_kernel<64>"),
         (64, 64, 64, 64): ("stream3_kernel<64>", "swgrad_kernel<64>"),   # two passes
-        (32, 64, 0, 128): ("igemm3_halo_kernel<64,32>", "swgrad_kernel<32>"),
-        (16, 256, 0, 256): ("igemm3_halo_kernel<128,16>", "wgrad3_halo_kernel<16>"),
-        (8, 512, 0, 512): ("igemm3_halo_kernel<128,8>", "wgrad3_halo_kernel<8>"),
+        (32, 64, 0, 128): ("conv3r_kernel<32,128>", "swgrad_kernel<32>"),
+        (32, 128, 64, 64): ("conv3r_kernel<32,64>", "swgrad_kernel<32>"),
+        (16, 256, 0, 256): ("conv3r_kernel<16,256>", "wgrad3_halo_kernel<16>"),
+        (16, 256, 128, 128): ("conv3r_kernel<16,128>", "wgrad3_halo_kernel<16>"),
+        (8, 512, 0, 512): ("conv3r_kernel<8,256>", "wgrad3_halo_kernel<8>"),
     }
     for (h, c1, c2, co), (f, wg) in want.items():
         d = IgemmDesc(RR_BF16, RR_CONV3X3, 512, h, h, c1, c2, co, 0, 0, 0, 1, 0, 1, 0)
         assert ops.igemm_kernel_name(d) == f, (h, c1, c2, co, ops.igemm_kernel_name(d))
         assert ops.wgrad_kernel_name(WgradDesc(RR_BF16, RR_CONV3X3, 512, h, h, c1, c2, co, 0)) == wg
+        if f.startswith("conv3r"):     # one BN-statistics partial row per 128 pixels
+            assert rr_stat_blocks(d) == 512 * h * h // 128
 
 
 def _s1name(mode, n, h, w, c1, c2, co, split=0, act=0, acc=0, bias=0, mask=0, stats=0, nchw_=0):

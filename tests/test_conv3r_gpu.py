@@ -1,0 +1,199 @@
+"""Tap-reuse 3x3 conv (csrc/conv3r.hip): the bf16 conv of the 64-512-channel
+layers on 32x32 / 16x16 / 8x8 maps (ResUNet res2 / res3 / dec2 / dec3 /
+bottleneck, VGG16 conv2_x / conv3_x; their dgrads with the concat split and
+the fused BN/PReLU backward) vs fp32 torch and vs the LDS-halo kernel it
+replaces (RR_CONV3R=0).  Inputs are bf16-exact, so against fp32 torch the
+only error is the bf16 rounding of the output; vs the halo kernel the same
+fp32 sums in another order, rounded once.  Shapes cover every tile geometry:
+a tile inside an image (W = 32: 16 or 8 rows, top and bottom zero rows),
+whole images (W = 16), image pairs (W = 8), several column blocks, concat
+inputs."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+BF = torch.bfloat16
+
+
+def rnd(*shape, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g)
+
+
+def nhwc(x, dev):
+    return x.permute(0, 2, 3, 1).contiguous().to(dev, BF)
+
+
+def nchw(y):
+    return y.float().permute(0, 3, 1, 2).contiguous().cpu()
+
+
+def rel(a, r):
+    a, r = a.float().cpu(), r.float().cpu()
+    return ((a - r).norm() / r.norm().clamp_min(1e-30)).item()
+
+
+def _desc(n, w, c1, c2, co, split=0, act=0, acc=0, bias=0, mask=0, stats=0):
+    from roadrestore._lib import RR_BF16, RR_CONV3X3, IgemmDesc
+    return IgemmDesc(RR_BF16, RR_CONV3X3, n, w, w, c1, c2, co, split, act, acc, bias, mask,
+                     stats, 0)
+
+
+# (n, w, c1, c2, c_out, kernel)
+SHAPES = [
+    (4, 32, 64, 0, 128, "conv3r_kernel<32,128>"),     # res2.c1 / VGG conv2_1
+    (2, 32, 128, 0, 128, "conv3r_kernel<32,128>"),    # res2.c2 / conv2_2 (fwd + dgrad)
+    (4, 32, 128, 64, 64, "conv3r_kernel<32,64>"),     # dec2.c1 (concat) fwd
+    (2, 32, 128, 0, 256, "conv3r_kernel<32,256>"),    # 8-row tiles in a 32-row image
+    (8, 16, 128, 0, 256, "conv3r_kernel<16,256>"),    # res3.c1 / conv3_1
+    (4, 16, 256, 128, 128, "conv3r_kernel<16,128>"),  # dec3.c1 (concat)
+    (8, 8, 256, 0, 512, "conv3r_kernel<8,256>"),      # bottleneck (2 column blocks)
+    (16, 8, 512, 0, 256, "conv3r_kernel<8,256>"),
+    (8, 8, 128, 0, 128, "conv3r_kernel<8,128>"),
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv3r_selected(dev, shape, monkeypatch):
+    from roadrestore import ops
+    n, w, c1, c2, co, name = shape
+    assert ops.igemm_kernel_name(_desc(n, w, c1, c2, co, bias=1, stats=1)) == name
+    monkeypatch.setenv("RR_CONV3R", "0")
+    assert not ops.igemm_kernel_name(_desc(n, w, c1, c2, co, bias=1, stats=1)).startswith("conv3r")
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv3r_fwd_bias_stats_relu(dev, shape, monkeypatch):
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    n, w, c1, c2, co, _ = shape
+    cin = c1 + c2
+    x = rnd(n, cin, w, w, seed=1).bfloat16().float()
+    wt = (rnd(co, cin, 3, 3, seed=2) / (3 * cin ** 0.5)).bfloat16().float()
+    b = rnd(co, seed=3)
+    pre = F.conv2d(x, wt, None, padding=1)
+    wf, _ = rr.ops.pack_conv(wt.to(dev), BF)
+    x1 = nhwc(x[:, :c1], dev)
+    x2 = nhwc(x[:, c1:], dev) if c2 else None
+    outs = {}
+    for tag in ("1", "0"):
+        monkeypatch.setenv("RR_CONV3R", tag)
+        y, _, st = rr.ops.igemm(RR_CONV3X3, x1, x2, n, w, w, wf, co, bias=b.to(dev), stats=True)
+        yr, _, _ = rr.ops.igemm(RR_CONV3X3, x1, x2, n, w, w, wf, co, bias=b.to(dev), act=1)
+        torch.cuda.synchronize()
+        outs[tag] = (nchw(y), st.double().sum(0).cpu(), nchw(yr), st.shape[0])
+    y, s, yr, rows = outs["1"]
+    assert rows == n * w * w // 128
+    ref = pre + b[None, :, None, None]
+    assert rel(y, ref) < 4e-3
+    assert rel(yr, F.relu(ref)) < 4e-3
+    assert rel(s[:, 0], pre.double().sum((0, 2, 3))) < 1e-5
+    assert rel(s[:, 1], (pre.double() ** 2).sum((0, 2, 3))) < 1e-5
+    assert rel(y, outs["0"][0]) < 2e-3
+    assert rel(s, outs["0"][1]) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(2, 32, 128, 0, 128), (8, 16, 256, 0, 256), (8, 8, 512, 0, 512)])
+@pytest.mark.parametrize("acc,msk", [(True, False), (False, True), (True, True)])
+def test_conv3r_dgrad_epilogues(dev, shape, acc, msk, monkeypatch):
+    """dgrad epilogues: accumulate into y (the shortcut / identity grad), the
+    ReLU-backward mask (VGG dgrads), both."""
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    monkeypatch.setenv("RR_CONV3R", "1")
+    n, w, c1, _, co = shape
+    x = rnd(n, c1, w, w, seed=11).bfloat16().float()
+    wt = (rnd(co, c1, 3, 3, seed=12) / (3 * c1 ** 0.5)).bfloat16().float()
+    y0 = rnd(n, co, w, w, seed=13).bfloat16().float()
+    m = rnd(n, co, w, w, seed=14).bfloat16().float()
+    ref = F.conv2d(x, wt, None, padding=1) + (y0 if acc else 0)
+    if msk:
+        ref = torch.where(m > 0, ref, torch.zeros(()))
+    wf, _ = rr.ops.pack_conv(wt.to(dev), BF)
+    out = nhwc(y0, dev) if acc else None
+    assert rr.ops.igemm_kernel_name(_desc(n, w, c1, 0, co, acc=int(acc), mask=int(msk))) \
+        .startswith("conv3r")
+    y, _, _ = rr.ops.igemm(RR_CONV3X3, nhwc(x, dev), None, n, w, w, wf, co, out=out,
+                           accumulate=acc, mask=nhwc(m, dev) if msk else None)
+    assert rel(nchw(y), ref) < 4e-3
+
+
+@pytest.mark.parametrize("shape,split", [((4, 16, 128, 0, 384), 256), ((4, 32, 64, 0, 192), 64),
+                                         ((4, 32, 64, 0, 192), 128)])
+def test_conv3r_concat_split_dgrad(dev, shape, split, monkeypatch):
+    """the dgrad of a concat-input conv writes the two halves to two tensors
+    (dec3.c1: 128 -> 256 + 128, dec2.c1: 64 -> 128 + 64 / 64 + 128)"""
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    n, w, c1, _, co = shape
+    x = rnd(n, c1, w, w, seed=21).bfloat16().float()
+    wt = (rnd(co, c1, 3, 3, seed=22) / (3 * c1 ** 0.5)).bfloat16().float()
+    ref = F.conv2d(x, wt, None, padding=1)
+    wf, _ = rr.ops.pack_conv(wt.to(dev), BF)
+    outs = {}
+    for tag in ("1", "0"):
+        monkeypatch.setenv("RR_CONV3R", tag)
+        y1, y2, _ = rr.ops.igemm(RR_CONV3X3, nhwc(x, dev), None, n, w, w, wf, co, split=split)
+        torch.cuda.synchronize()
+        outs[tag] = torch.cat((nchw(y1), nchw(y2)), 1)
+    assert rel(outs["1"], ref) < 4e-3
+    assert rel(outs["1"], outs["0"]) < 2e-3
+
+
+@pytest.mark.parametrize("shape", [(2, 32, 128, 0, 128), (8, 16, 256, 0, 256), (8, 8, 512, 0, 512),
+                                   (4, 32, 128, 0, 64)])
+def test_conv3r_bnbwd(dev, shape, monkeypatch):
+    """conv dgrad + BN/PReLU backward reduce fused in the staged epilogue ==
+    the halo kernel's fused path == the unfused sequence."""
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    ops = rr.ops
+    n, w, cg, _, C = shape
+    g2 = nhwc(rnd(n, cg, w, w, seed=51), dev)
+    wt = (rnd(cg, C, 3, 3, seed=52) * (1.0 / (3 * C ** 0.5))).to(dev)
+    _, wd = ops.pack_conv(wt, BF)
+    t1 = nhwc(rnd(n, C, w, w, seed=53) * 2 + 0.3, dev)
+    tf = t1.float().reshape(-1, C)
+    mean = tf.mean(0)
+    inv = 1.0 / torch.sqrt(tf.var(0, unbiased=False) + 1e-5)
+    gamma = (torch.rand(C, generator=torch.Generator().manual_seed(54)) + 0.5).to(dev)
+    beta = (torch.rand(C, generator=torch.Generator().manual_seed(55)) - 0.5).to(dev)
+    s1 = gamma * inv
+    sh1 = beta - mean * s1
+    alpha = torch.tensor([0.23], device=dev)
+    monkeypatch.setenv("RR_CONV3R", "0")
+    da1, _, _ = ops.igemm(RR_CONV3X3, g2, None, n, w, w, wd, C)
+    ref = ops.bn_backward(da1, t1, mean, inv, gamma, mask_kind=2, aux=t1, aff_s=s1, aff_b=sh1,
+                          alpha=alpha)
+    res = {}
+    for tag in ("0", "1"):
+        monkeypatch.setenv("RR_CONV3R", tag)
+        gm, part, rows, arows = ops.igemm_bnbwd(RR_CONV3X3, g2, n, w, w, wd, C, t1, mean, inv, s1,
+                                                sh1, alpha)
+        if tag == "1":
+            assert rows == n * w * w // 128
+            assert ops.igemm_kernel_name(_desc(n, w, cg, 0, C), bnbwd=True).startswith("conv3r")
+        res[tag] = ops.bn_backward_rows(gm, part, rows, arows, t1, mean, inv, gamma)
+    torch.cuda.synchronize()
+    got, halo = res["1"], res["0"]
+    assert rel(got["dt0"], ref["dt0"]) < 2e-2
+    for k in ("dgamma0", "dbeta0", "dalpha"):
+        assert rel(got[k], ref[k]) < 2e-2, k
+        assert rel(got[k], halo[k]) < 1e-4, k
+    assert rel(got["dt0"], halo["dt0"]) < 2e-3
+
+
+def test_conv3r_stats_rows_deterministic(dev, monkeypatch):
+    """fixed tile -> partial-row mapping: two launches give bitwise-equal
+    outputs and statistics"""
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    monkeypatch.setenv("RR_CONV3R", "1")
+    n, w, c, co = 8, 16, 256, 256
+    x = nhwc(rnd(n, c, w, w, seed=31), dev)
+    wf, _ = rr.ops.pack_conv((rnd(co, c, 3, 3, seed=32) / 48).to(dev), BF)
+    a = rr.ops.igemm(RR_CONV3X3, x, None, n, w, w, wf, co, stats=True)
+    b = rr.ops.igemm(RR_CONV3X3, x, None, n, w, w, wf, co, stats=True)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2])

@@ -31,9 +31,10 @@ def test_forward_without_backward_frees_state(dev):
     perc = rr.VGGPerceptualLoss().to(dev)
     x = torch.rand(8, 3, 32, 32, device=dev)
     n0 = T.saved_state_count()
-    out = m(x)                                   # warm the caches / allocator
-    loss = rr.unified_loss(out, x, perc, 0.1)
-    del out, loss
+    for _ in range(3):                           # warm the caches / allocator (the batched
+        out = m(x)                               # weight re-pack is built on the 2nd forward)
+        loss = rr.unified_loss(out, x, perc, 0.1)
+        del out, loss
     base = _mem(dev)
     for _ in range(50):
         out = m(x)                               # grads enabled, output dropped
@@ -111,25 +112,57 @@ def test_opcheck_every_rr_op(dev):
     _opcheck(o.simple_unet_forward.default, (x, list(su.parameters()), su._op_key, False))
     xb = torch.rand(2, 64, 8, 8, device=dev)
     _opcheck(o.resblock_forward.default, (xb, list(blk.parameters()), blk._op_key, False))
-    # their backward ops take a live handle: one forward per call
-    for net, xin in ((m, x), (su, x), (blk, xb)):
-        pre = net._op
-        fwd = getattr(o, f"{pre}_forward").default
-        bwd = getattr(o, f"{pre}_backward").default
-        out, h = fwd(xin, list(net.parameters()), net._op_key, True)
-        _opcheck(bwd, (torch.ones_like(out), h, net._op_key), utils=("test_schema",
-                                                                      "test_faketensor"))
+    # their backward ops consume a live forward handle: a fresh forward per
+    # check (each opcheck utility runs the op for real)
+    for util in ("test_schema", "test_faketensor"):
+        for net, xin in ((m, x), (su, x), (blk, xb)):
+            pre = net._op
+            fwd = getattr(o, f"{pre}_forward").default
+            bwd = getattr(o, f"{pre}_backward").default
+            out, h = fwd(xin, list(net.parameters()), net._op_key, True)
+            _opcheck(bwd, (torch.ones_like(out), h, net._op_key), utils=(util,))
+        loss, h = o.unified_loss(x, y, perc._op_key, 0.1, 1.0, True)
+        _opcheck(o.unified_loss_backward.default, (torch.ones((), device=dev), x, y, h, 0.1, 1.0),
+                 utils=(util,))
+        loss, h = o.perceptual_loss(x, y, perc._op_key, True)
+        _opcheck(o.perceptual_loss_backward.default, (torch.ones((), device=dev), h, x),
+                 utils=(util,))
     # losses
     _opcheck(o.pixel_loss.default, (x, y, ops.L1))
     _opcheck(o.pixel_loss_backward.default, (torch.ones((), device=dev), x, y, ops.MSE))
     _opcheck(o.unified_loss.default, (x, y, perc._op_key, 0.1, 1.0, False))
     _opcheck(o.perceptual_loss.default, (x, y, perc._op_key, False))
-    loss, h = o.unified_loss(x, y, perc._op_key, 0.1, 1.0, True)
-    _opcheck(o.unified_loss_backward.default, (torch.ones((), device=dev), x, y, h, 0.1, 1.0),
-             utils=("test_schema", "test_faketensor"))
-    loss, h = o.perceptual_loss(x, y, perc._op_key, True)
-    _opcheck(o.perceptual_loss_backward.default, (torch.ones((), device=dev), h, x),
-             utils=("test_schema", "test_faketensor"))
+    # leaf layers called on their own (roadrestore.layers)
+    from roadrestore import layers as L
+    f32 = L.dtype_code(torch.float32)
+    xc = torch.rand(2, 64, 8, 8, device=dev)
+    w3 = torch.randn(32, 64, 3, 3, device=dev) * 0.05
+    b3 = torch.randn(32, device=dev)
+    _opcheck(o.conv2d.default, (xc, w3, b3, 1, f32))
+    _opcheck(o.conv2d_backward.default, (torch.rand(2, 32, 8, 8, device=dev), xc, w3, 1, f32))
+    wt = torch.randn(64, 64, 2, 2, device=dev) * 0.05
+    bt = torch.randn(64, device=dev)
+    _opcheck(o.conv_transpose2d.default, (xc, wt, bt, f32))
+    _opcheck(o.conv_transpose2d_backward.default,
+             (torch.rand(2, 64, 16, 16, device=dev), xc, wt, f32))
+    bn = rr.BatchNorm2d(64).to(dev)
+    for training in (True, False):
+        _opcheck(o.batch_norm.default, (xc, bn.weight, bn.bias, bn._op_key, training, f32))
+        yb, mean, inv = o.batch_norm(xc, bn.weight, bn.bias, bn._op_key, training, f32)
+        _opcheck(o.batch_norm_backward.default,
+                 (torch.rand_like(xc), xc, mean, inv, bn.weight, training, f32))
+    alpha = torch.full((1,), 0.25, device=dev)
+    _opcheck(o.prelu.default, (xc - 0.5, alpha, f32))
+    _opcheck(o.prelu_backward.default, (torch.rand_like(xc), xc - 0.5, alpha, f32))
+    _opcheck(o.relu.default, (xc - 0.5, f32))
+    _opcheck(o.relu_backward.default, (torch.rand_like(xc), xc - 0.5, f32))
+    _opcheck(o.max_pool2d.default, (xc, f32))
+    _, idx = o.max_pool2d(xc, f32)
+    _opcheck(o.max_pool2d_backward.default, (torch.rand(2, 64, 4, 4, device=dev), idx, 8, 8, f32))
+    with torch.no_grad():
+        _opcheck(o.adaptive_avg_pool2d.default, (torch.rand(2, 512, 2, 2, device=dev), 7, 7, f32))
+        _opcheck(o.linear.default, (torch.rand(3, 64, device=dev), torch.randn(10, 64, device=dev),
+                                    torch.randn(10, device=dev), f32))
     # judge and post-processing
     with torch.no_grad():
         _opcheck(o.vgg16_logits.default, (torch.rand(2, 3, 32, 32, device=dev),

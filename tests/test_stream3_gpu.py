@@ -44,16 +44,24 @@ def _blocks(n, h, w):
     return rr.lib().rr_igemm_stat_blocks(C.byref(d))
 
 
+def _name(n, h, w):
+    import roadrestore as rr
+    from roadrestore._lib import IgemmDesc, RR_BF16, RR_CONV3X3
+    return rr.ops.igemm_kernel_name(IgemmDesc(RR_BF16, RR_CONV3X3, n, h, w, 64, 0, 64, 0, 0, 0,
+                                              1, 0, 1, 0))
+
+
 @pytest.mark.parametrize("shape", SHAPES)
 def test_stream3_selected(dev, shape, monkeypatch):
     """the streaming kernel owns these shapes (256 partial rows), and the
     RR_STREAM3=0 switch hands them back to the tiled kernel"""
     n, h, w = shape
-    assert _blocks(n, h, w) == 256
-    # too small for one step per workgroup / not whole steps: tiled kernel
-    assert _blocks(n // 2 if n * h * w // 2 < 65536 else 1, h, w) != 256
+    assert _blocks(n, h, w) == 256 and _name(n, h, w).startswith("stream3")
+    # too small for one step per workgroup / not whole steps: a tiled kernel
+    assert not _name(n // 2 if n * h * w // 2 < 65536 else 1, h, w).startswith("stream3")
     monkeypatch.setenv("RR_STREAM3", "0")
-    assert _blocks(n, h, w) == (n * h * w) // 256
+    # 32x32: the tap-reuse conv (128-pixel partial rows); 64x64: the halo kernel
+    assert _blocks(n, h, w) == (n * h * w) // (128 if w == 32 else 256)
 
 
 @pytest.mark.parametrize("shape", SHAPES)
@@ -181,7 +189,8 @@ def test_stream3_concat_two_pass(dev, shape, stats, bias, act, monkeypatch):
         d = rr.ops.IgemmDesc(rr.ops.RR_BF16, RR_CONV3X3, n, h, w, 64, 64, 64, 0, act, 0,
                              int(bias), 0, int(stats), 0)
         name = rr.ops.igemm_kernel_name(d)
-        assert name == ("stream3_kernel<%d>" % w if tag == "1" else "igemm3_halo_kernel<64,%d>" % w)
+        fallback = "conv3r_kernel<32,64>" if w == 32 else "igemm3_halo_kernel<64,%d>" % w
+        assert name == ("stream3_kernel<%d>" % w if tag == "1" else fallback)
         y, _, st = rr.ops.igemm(RR_CONV3X3, nhwc(x1, dev), nhwc(x2, dev), n, h, w, wf, 64,
                                 bias=b.to(dev) if bias else None, act=act, stats=stats)
         torch.cuda.synchronize()
