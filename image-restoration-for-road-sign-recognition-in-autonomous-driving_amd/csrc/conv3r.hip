@@ -28,8 +28,10 @@
 //   * 96 MFMAs per wave per stage (R x NS x NM x 3), one barrier per stage;
 //     LDS fragment traffic ~240 B per MFMA;
 //   * operands arrive by LDS-DMA (global_load_lds_dwordx4) one stage ahead
-//     into double buffers: the next stage's weights (from the packed
-//     [c_out][9][c_in] rows) and, at the first stage of a chunk, the next
+//     into double buffers: the next stage's weights (the 1-KB tiles the pack
+//     writes behind the [c_out][9][c_in] rows, rr_pack_conv: a stage is 3
+//     contiguous runs of whole lines -- gathered from the row layout as
+//     64-B pieces it cost ~14% of the kernel) and, at the first stage of a chunk, the next
 //     chunk's halo (from the NHWC activations; out-of-image rows from the
 //     zero page).  hipcc would drain the DMA (vmcnt(0)) before any ds_read
 //     it cannot separate from a DMA destination, so the fragment reads are
@@ -45,16 +47,18 @@
 #include "common.h"
 #include "conv3r.h"
 
+#include <cstdio>
 #include <cstdlib>
 
 namespace {
 
-template <int W, int BC, int NW> struct R3 {
+template <int W, int BC, int NW, int NWV, int HB> struct R3 {
   static constexpr bool PAIR = W == 8;              // a row unit = the same row of 2 images
   static constexpr int NS = PAIR ? 1 : W / 16;      // 16-pixel column blocks per row unit
   static constexpr int R = PAIR ? 8 : 128 / W;      // output rows per wave
   static constexpr int NM = NW / 16;                // 16-channel MFMA rows per wave
-  static constexpr int WC = BC / NW, WP = 8 / WC;   // wave grid
+  static constexpr int NT = 64 * NWV;               // threads per workgroup
+  static constexpr int WC = BC / NW, WP = NWV / WC; // wave grid
   static constexpr int TPX = WP * 128;              // pixels per tile
   static constexpr int TR = PAIR ? 8 : WP * R;      // tile rows (W >= 16)
   static constexpr int HS = PAIR ? 8 : (TR < W ? TR : W);       // output rows per halo segment
@@ -64,15 +68,17 @@ template <int W, int BC, int NW> struct R3 {
   static constexpr int HBYTES = HBLK * 1024;
   static constexpr int WBLK = 3 * (BC / 16);        // weight blocks per stage (3 taps)
   static constexpr int WBYTES = WBLK * 1024;
-  static constexpr int NHG = (HBLK + 7) / 8;        // halo DMA pieces per wave per chunk
-  static constexpr int NWG = (WBLK + 7) / 8;        // weight DMA pieces per wave per stage
+  static constexpr int NHG = (HBLK + NWV - 1) / NWV;   // halo DMA pieces per wave per chunk
+  static constexpr int NWG = (WBLK + NWV - 1) / NWV;   // weight DMA pieces per wave per stage
   static constexpr int SROW = BC + 4;
-  static constexpr int STG = 128 * SROW * 4 + (8 * BC * 2 + 8) * 4 + 256;
-  // [weights x2][halo x2][guard block]: the shifted edge reads stay inside
-  static constexpr int KBYTES = 2 * WBYTES + 2 * HBYTES + 1024;
-  static constexpr int LDS = KBYTES > STG ? KBYTES : STG;
+  static constexpr int STG = 128 * SROW * 4 + (NWV * BC * 2 + NWV) * 4 + 256;
+  // [weights x2][halo x HB][guard block]: the shifted edge reads stay inside
+  static constexpr int KBYTES = 2 * WBYTES + HB * HBYTES + 1024;
+  static constexpr int BIAS = KBYTES;               // [BC] fp32 bias for the register epilogue
+  static constexpr int LDS = KBYTES + BC * 4 > STG ? KBYTES + BC * 4 : STG;
   static_assert(LDS <= 160 * 1024, "LDS");
-  static_assert(WC * WP == 8 && NM * 16 == NW, "wave grid");
+  static_assert(WC * WP == NWV && NM * 16 == NW, "wave grid");
+  static_assert(HB == 1 || HB == 2, "halo buffers");
   static_assert(PAIR || TR % W == 0 || W % TR == 0, "tile rows");
   static_assert(2 * WBYTES >= 1024, "the edge read of the first halo block stays in LDS");
 };
@@ -83,9 +89,9 @@ template <int N> __device__ __forceinline__ void vm_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-template <int W, int BC, int NW>
-__global__ __launch_bounds__(512) void conv3r_kernel(IgemmArgs a) {
-  using G = R3<W, BC, NW>;
+template <int W, int BC, int NW, int NWV, int HB>
+__global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) {
+  using G = R3<W, BC, NW, NWV, HB>;
   constexpr int NS = G::NS, R = G::R, NM = G::NM, WC = G::WC;
   constexpr int HW = W * W;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
@@ -117,8 +123,8 @@ __global__ __launch_bounds__(512) void conv3r_kernel(IgemmArgs a) {
   int hpix[G::NHG], hdst[G::NHG];
 #pragma unroll
   for (int i = 0; i < G::NHG; ++i) {
-    int b = wv + 8 * i;
-    if (b >= G::HBLK) b -= 8;                       // a duplicate of this wave's previous block
+    int b = wv + NWV * i;
+    if (b >= G::HBLK) b -= NWV;                     // a duplicate of this wave's previous block
     const int k = b / ((G::HS + 2) * NS);
     const int rem = b - k * ((G::HS + 2) * NS);
     const int hr = rem / NS, s = rem - (rem / NS) * NS;
@@ -137,20 +143,23 @@ __global__ __launch_bounds__(512) void conv3r_kernel(IgemmArgs a) {
   int wrow[G::NWG], wdst[G::NWG], wdy[G::NWG];
 #pragma unroll
   for (int i = 0; i < G::NWG; ++i) {
-    int b = wv + 8 * i;
-    if (b >= G::WBLK) b -= 8;
+    int b = wv + NWV * i;
+    if (b >= G::WBLK) b -= NWV;
     const int dy = b / (BC / 16), m = b - dy * (BC / 16);
-    wrow[i] = (c0 + m * 16 + frow) * a.K * 2 + fq * 16;
+    wrow[i] = (c0 / 16 + m) * 1024 + lane * 16;      // block mb of the tiles, this lane's 16 B
     wdst[i] = b * 1024;
     wdy[i] = dy;
   }
+  // the weight tiles follow the [c_out][9][c_in] pack (rr_pack_conv)
+  const char *wtile = a.wt + (long long)a.cout * a.K * 2;
   auto issue_w = [&](int st) __attribute__((always_inline)) {
     const int ch = st / 3, dx = st - ch * 3;
     char *dst = smem + (st & 1) * G::WBYTES;
 #pragma unroll
     for (int i = 0; i < G::NWG; ++i) {
-      const long long off = (long long)wrow[i] + ((wdy[i] * 3 + dx) * a.cin + ch * 32) * 2;
-      __builtin_amdgcn_global_load_lds((const void *)(a.wt + off), LDS_PTR(dst + wdst[i]), 16, 0, 0);
+      // tile (chunk ch, column dx, row dy, block mb): 3 contiguous runs per stage
+      const long long off = (((long long)ch * 3 + dx) * 3 + wdy[i]) * (a.cout / 16) * 1024 + wrow[i];
+      __builtin_amdgcn_global_load_lds((const void *)(wtile + off), LDS_PTR(dst + wdst[i]), 16, 0, 0);
     }
   };
   auto issue_h = [&](int ch) __attribute__((always_inline)) {
@@ -160,7 +169,7 @@ __global__ __launch_bounds__(512) void conv3r_kernel(IgemmArgs a) {
     const long long cs = first ? a.c1 : a.c2;
     const long long cl = first ? ci0 : ci0 - a.c1;
     const long long zoff = (long long)((uintptr_t)rr_zero_page - (uintptr_t)base) + fq * 16;
-    char *dst = smem + 2 * G::WBYTES + (ch & 1) * G::HBYTES;
+    char *dst = smem + 2 * G::WBYTES + (HB == 2 ? (ch & 1) * G::HBYTES : 0);
 #pragma unroll
     for (int i = 0; i < G::NHG; ++i) {
       const long long off = hpix[i] >= 0 ? ((long long)hpix[i] * cs + cl) * 2 + fq * 16 : zoff;
@@ -207,21 +216,36 @@ __global__ __launch_bounds__(512) void conv3r_kernel(IgemmArgs a) {
 #pragma unroll
       for (int m = 0; m < NM; ++m) acc[o][s][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // the bias of the column block for the register epilogue, read before any
+  // DMA is in flight (the compiler's wait for a plain load would drain them)
+  float *lbias = reinterpret_cast<float *>(smem + G::BIAS);
+  if (!a.bpart && tid < BC) lbias[tid] = a.bias ? a.bias[c0 + tid] : 0.f;
+  __builtin_amdgcn_s_waitcnt(0x0F70);               // vmcnt(0) (gfx9 encoding)
+
   const int kc = a.cin / 32, nst = 3 * kc;
   // prologue: chunk 0's halo, stage 0's weights
   issue_h(0);
   issue_w(0);
   vm_barrier<0>();
 
+  // diagnostics (RR_IGEMM_DBG, timing only -- results are wrong): bit2 no
+  // DMA in the K loop, bit3 no MFMAs, bit0 no epilogue, bit4 no weight DMA,
+  // bit5 no halo DMA
+  const bool dbg_nodma = (a.dbg & 4) != 0, dbg_nomfma = (a.dbg & 8) != 0;
   for (int st = 0; st < nst; ++st) {
     const int ch = st / 3, dx = st - ch * 3;       // uniform
     // operands of the next stage (weights) and of the next chunk (halo)
-    if (st + 1 < nst) issue_w(st + 1);
-    const bool next_h = dx == 0 && ch + 1 < kc;
-    if (next_h) issue_h(ch + 1);
+    const bool next_h = HB == 2 && dx == 0 && ch + 1 < kc && !dbg_nodma && !(a.dbg & 32);
+    const bool next_w = st + 1 < nst && !dbg_nodma && !(a.dbg & 16);
+    if (HB == 1 && dx == 0 && ch > 0) {
+      // one halo buffer: every wave is past the previous chunk's last read
+      // (the barrier that ended the last stage); load this chunk's halo
+      if (!dbg_nodma && !(a.dbg & 32)) issue_h(ch);
+      vm_barrier<0>();
+    }
 
     const uint32_t aa = a_lane + (st & 1) * G::WBYTES;
-    const uint32_t ba = b_wave + (ch & 1) * G::HBYTES +
+    const uint32_t ba = b_wave + (HB == 2 ? (ch & 1) * G::HBYTES : 0) +
                         (dx == 0 ? loff[0] : (dx == 1 ? loff[1] : loff[2]));
     const bool zlo = dx == 0 && zl[0];               // left padding column (block s = 0)
     const bool zhi = dx == 2 && zl[2];               // right padding column (block NS - 1)
@@ -266,18 +290,26 @@ __global__ __launch_bounds__(512) void conv3r_kernel(IgemmArgs a) {
           if (zhi) hi = i32x4{0, 0, 0, 0};
         }
       }
+      if (!dbg_nomfma) {
 #pragma unroll
-      for (int dy = 0; dy < 3; ++dy) {
-        const int o = ri - dy;
-        if (o < 0 || o >= R) continue;
+        for (int dy = 0; dy < 3; ++dy) {
+          const int o = ri - dy;
+          if (o < 0 || o >= R) continue;
 #pragma unroll
-        for (int s = 0; s < NS; ++s)
+          for (int s = 0; s < NS; ++s)
 #pragma unroll
-          for (int m = 0; m < NM; ++m)
-            acc[o][s][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                __builtin_bit_cast(bf16x8, af[dy][m]), __builtin_bit_cast(bf16x8, bf[ri & 1][s]),
-                acc[o][s][m], 0, 0, 0);
+            for (int m = 0; m < NM; ++m)
+              acc[o][s][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  __builtin_bit_cast(bf16x8, af[dy][m]), __builtin_bit_cast(bf16x8, bf[ri & 1][s]),
+                  acc[o][s][m], 0, 0, 0);
+        }
       }
+      // the DMA for the next stage / chunk goes out behind the first rows'
+      // MFMAs (issued right after the barrier, every wave of a SIMD would
+      // sit in ~60-cycle issue slots before its first MFMA); the weights
+      // first, the halo (waited for one stage later) last
+      if (ri == 0 && next_w) issue_w(st + 1);
+      if (ri == 1 && next_h) issue_h(ch + 1);
     }
     // the next stage's weights must have landed; a next chunk's halo (issued
     // after them) may stay in flight for one more stage
@@ -285,8 +317,111 @@ __global__ __launch_bounds__(512) void conv3r_kernel(IgemmArgs a) {
     else vm_barrier<0>();
   }
 
-  // ---- epilogue: one 128-pixel group (= one wave row of the grid) at a
-  // time as fp32 [128][BC] in LDS, then the staged store ----
+  if (a.dbg & 1) {
+    float t = 0.f;
+#pragma unroll
+    for (int o = 0; o < R; ++o)
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int m = 0; m < NM; ++m) t += acc[o][s][m][0];
+    if (t == 1234.5f) a.y1[tid] = 1;                  // keep the accumulators live
+    return;
+  }
+  if (!a.bpart) {
+    // ---- register epilogue: lane = 4 NHWC channels of one pixel per
+    // accumulator tile ----
+    const int cb = wc * NW;                         // the wave's first column in the block
+    const int pg = p0 + wp * 128;                   // the wave's 128 pixels
+    if (a.stats) {
+      // per-channel partial sums of the pre-bias accumulator over the wave's
+      // 128 pixels: over (o, s) in registers, then over the 16 pixel lanes
+      // (fixed xor tree), one partial row per 128 pixels
+      f32x4 s1[NM], s2[NM];
+#pragma unroll
+      for (int m = 0; m < NM; ++m) { s1[m] = f32x4{0.f, 0.f, 0.f, 0.f}; s2[m] = s1[m]; }
+#pragma unroll
+      for (int o = 0; o < R; ++o)
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+          for (int m = 0; m < NM; ++m) {
+            s1[m] += acc[o][s][m];
+            s2[m] += acc[o][s][m] * acc[o][s][m];
+          }
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+        for (int m = 0; m < NM; ++m)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            s1[m][j] += __shfl_xor(s1[m][j], off, 64);
+            s2[m][j] += __shfl_xor(s2[m][j], off, 64);
+          }
+      if (frow == 0) {
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+          float *sp = a.stats + ((long long)(pg / 128) * a.cout + c0 + cb + m * 16 + fq * 4) * 2;
+          *reinterpret_cast<f32x4 *>(sp) = f32x4{s1[m][0], s2[m][0], s1[m][1], s2[m][1]};
+          *reinterpret_cast<f32x4 *>(sp + 4) = f32x4{s1[m][2], s2[m][2], s1[m][3], s2[m][3]};
+        }
+      }
+    }
+    f32x4 bv[NM];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) bv[m] = *reinterpret_cast<const f32x4 *>(lbias + cb + m * 16 + fq * 4);
+    const int ld1 = a.split > 0 ? a.split : a.cout;
+    const int ld2 = a.cout - a.split;
+    // 16-B stores: per pair of 16-channel blocks (2p, 2p + 1) one
+    // v_permlane16_swap per dword (odd rows of the first <-> even rows of the
+    // second) leaves lane (row fq, pixel frow) with 8 consecutive channels at
+    // 32 p + {0, 16, 8, 24}[fq]: 4 lanes write a pixel's 64 B (8-B stores
+    // of 32-B pieces were store-issue bound)
+    const int coff = (fq & 1) * 16 + (fq >> 1) * 8;
+#pragma unroll
+    for (int o = 0; o < R; ++o)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const int r = G::PAIR ? (frow >> 3) * 64 + o * 8 + (frow & 7) : o * W + 16 * s + frow;
+        const long long p = pg + r;
+#pragma unroll
+        for (int pp = 0; pp < NM / 2; ++pp) {
+          f32x4 va = acc[o][s][2 * pp] + bv[2 * pp], vb = acc[o][s][2 * pp + 1] + bv[2 * pp + 1];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const auto t = __builtin_amdgcn_permlane16_swap(__float_as_uint(va[j]), __float_as_uint(vb[j]),
+                                                            false, false);
+            va[j] = __uint_as_float(t[0]);
+            vb[j] = __uint_as_float(t[1]);
+          }
+          const int c = c0 + cb + 32 * pp + coff;
+          const bool second = a.split > 0 && c >= a.split;      // uniform per pair (split % 32 == 0)
+          bf16_t *dst = second ? reinterpret_cast<bf16_t *>(a.y2) + p * ld2 + (c - a.split)
+                               : reinterpret_cast<bf16_t *>(a.y1) + p * ld1 + c;
+          if (a.accumulate) {
+            va += load4<bf16_t>(dst);
+            vb += load4<bf16_t>(dst + 4);
+          }
+          if (a.act == RR_ACT_RELU) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { va[j] = fmaxf(va[j], 0.f); vb[j] = fmaxf(vb[j], 0.f); }
+          }
+          if (a.has_mask) {
+            const bf16_t *mp = reinterpret_cast<const bf16_t *>(a.mask) + p * ld1 + c;
+            const f32x4 ma = load4<bf16_t>(mp), mb = load4<bf16_t>(mp + 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              va[j] = ma[j] > 0.f ? va[j] : 0.f;
+              vb[j] = mb[j] > 0.f ? vb[j] : 0.f;
+            }
+          }
+          store8<bf16_t>(dst, va, vb);
+        }
+      }
+    return;
+  }
+  // ---- BN-backward epilogue: one 128-pixel group (= one wave row of the
+  // grid) at a time as fp32 [128][BC] in LDS, then the staged store ----
   float *stg = reinterpret_cast<float *>(smem);
   for (int g = 0; g < G::WP; ++g) {
     if (wp == g) {
@@ -302,13 +437,40 @@ __global__ __launch_bounds__(512) void conv3r_kernel(IgemmArgs a) {
           }
     }
     __syncthreads();
-    store_staged<bf16_t, BC, 128, 512, RR_CONV3X3>(a, stg, c0, p0 + g * 128, p0 / 128 + g, tid);
+    store_staged<bf16_t, BC, 128, G::NT, RR_CONV3X3>(a, stg, c0, p0 + g * 128, p0 / 128 + g, tid);
     __syncthreads();
   }
 }
 
-int r3_nw(int bc) { return bc == 64 ? 32 : 64; }
-int r3_tpx(int bc) { return (8 / (bc / r3_nw(bc))) * 128; }
+// column block and per-wave channels for *d: BC = 256 / 128 / 64 by c_out,
+// except where that leaves fewer than 256 workgroups (one per CU): the
+// 8x8 256-channel layers (B = 512: 128 tiles) take 128 x 32 wave tiles
+struct R3Pick { int bc, nw, nwv, hb; };
+// RR_CONV3R_WG: 4 (default) = 4-wave workgroups, 2 per CU (one's epilogue /
+// DMA waits overlap the other's MFMAs), one halo buffer; 8 = one 8-wave
+// workgroup per CU with double-buffered halo (A/B)
+R3Pick r3_pick(const rr_igemm_desc *d) {
+  const char *e = getenv("RR_CONV3R_WG");
+  const int nwv = e && atoi(e) == 8 ? 8 : 4;
+  const long long P = (long long)d->n * d->h * d->w;
+  if (nwv == 8) {
+    if (d->c_out % 256 == 0) {
+      if (d->w != 8 || (P / 256) * (d->c_out / 256) >= 256 || P % 256) return {256, 64, 8, 2};
+      return {128, 32, 8, 2};
+    }
+    if (d->c_out % 128 == 0) return {128, 64, 8, 2};
+    return {64, 32, 8, 2};
+  }
+  // 4 waves: 128-channel column blocks of 128 x 64 wave tiles (256-pixel
+  // tiles); below 512 workgroups (2 per CU) the 8x8 layers take 128 x 32
+  // wave tiles (128-pixel tiles)
+  if (d->c_out % 128 == 0) {
+    if (d->w == 8 && (P / 256) * (d->c_out / 128) < 512 && P % 128 == 0) return {128, 32, 4, 1};
+    return {128, 64, 4, 1};
+  }
+  return {64, 64, 4, 1};
+}
+int r3_tpx(R3Pick k) { return (k.nwv / (k.bc / k.nw)) * 128; }
 
 }  // namespace
 
@@ -319,11 +481,11 @@ int conv3r_bc(const rr_igemm_desc *d) {
   const int W = d->w;
   if (d->h != W || !(W == 8 || W == 16 || W == 32)) return 0;
   if (d->c_in1 <= 0 || d->c_in1 % 32 || d->c_in2 % 32 || d->c_out % 64) return 0;
-  if (d->out_split && (d->out_split % 8 || d->out_split >= d->c_out)) return 0;
-  const int bc = d->c_out % 256 == 0 ? 256 : (d->c_out % 128 == 0 ? 128 : 64);
+  if (d->out_split && (d->out_split % 32 || d->out_split >= d->c_out)) return 0;
+  const R3Pick k = r3_pick(d);
   const long long P = (long long)d->n * d->h * d->w;
-  if (P % r3_tpx(bc)) return 0;
-  return bc;
+  if (P % r3_tpx(k)) return 0;
+  return k.bc;
 }
 
 int conv3r_stat_blocks(const rr_igemm_desc *d) {
@@ -331,39 +493,47 @@ int conv3r_stat_blocks(const rr_igemm_desc *d) {
   return (int)(((long long)d->n * d->h * d->w) / 128);
 }
 
-template <int BC>
+template <int BC, int NW, int NWV, int HB>
 static int conv3r_go(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
-  constexpr int NW = BC == 64 ? 32 : 64;
   a.ncblk = a.cout / BC;
-  const long long nblk = ((long long)a.P / (8 / (BC / NW) * 128)) * a.ncblk;
+  const long long nblk = ((long long)a.P / (NWV / (BC / NW) * 128)) * a.ncblk;
   if (nblk <= 0 || nblk > 0x7fffffffLL) return RR_EUNSUPPORTED;
-  const dim3 grid((unsigned)nblk), block(512);
+  const dim3 grid((unsigned)nblk), block(64 * NWV);
   switch (d->w) {
-    case 32: hipLaunchKernelGGL((conv3r_kernel<32, BC, NW>), grid, block, 0, st, a); break;
-    case 16: hipLaunchKernelGGL((conv3r_kernel<16, BC, NW>), grid, block, 0, st, a); break;
-    default: hipLaunchKernelGGL((conv3r_kernel<8, BC, NW>), grid, block, 0, st, a); break;
+    case 32: hipLaunchKernelGGL((conv3r_kernel<32, BC, NW, NWV, HB>), grid, block, 0, st, a); break;
+    case 16: hipLaunchKernelGGL((conv3r_kernel<16, BC, NW, NWV, HB>), grid, block, 0, st, a); break;
+    default: hipLaunchKernelGGL((conv3r_kernel<8, BC, NW, NWV, HB>), grid, block, 0, st, a); break;
   }
   RR_CHECK_LAUNCH();
   return RR_OK;
 }
 
 int conv3r_launch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
-  switch (conv3r_bc(d)) {
-    case 256: return conv3r_go<256>(d, a, st);
-    case 128: return conv3r_go<128>(d, a, st);
-    case 64: return conv3r_go<64>(d, a, st);
-    default: return RR_EUNSUPPORTED;
+  if (!conv3r_bc(d)) return RR_EUNSUPPORTED;
+  const R3Pick k = r3_pick(d);
+  if (k.nwv == 8) {
+    if (k.bc == 256) return conv3r_go<256, 64, 8, 2>(d, a, st);
+    if (k.bc == 128 && k.nw == 64) return conv3r_go<128, 64, 8, 2>(d, a, st);
+    if (k.bc == 128) return conv3r_go<128, 32, 8, 2>(d, a, st);
+    return conv3r_go<64, 32, 8, 2>(d, a, st);
   }
+  if (k.bc == 128 && k.nw == 64) return conv3r_go<128, 64, 4, 1>(d, a, st);
+  if (k.bc == 128) return conv3r_go<128, 32, 4, 1>(d, a, st);
+  return conv3r_go<64, 64, 4, 1>(d, a, st);
 }
 
 const char *conv3r_name(const rr_igemm_desc *d) {
-  static const char *names[3][3] = {
-      {"conv3r_kernel<8,64>", "conv3r_kernel<16,64>", "conv3r_kernel<32,64>"},
-      {"conv3r_kernel<8,128>", "conv3r_kernel<16,128>", "conv3r_kernel<32,128>"},
-      {"conv3r_kernel<8,256>", "conv3r_kernel<16,256>", "conv3r_kernel<32,256>"}};
-  const int bc = conv3r_bc(d);
-  if (!bc) return "invalid";
+  if (!conv3r_bc(d)) return "invalid";
+  const R3Pick k = r3_pick(d);
+  static char names[3][4][2][40];
   const int wi = d->w == 8 ? 0 : d->w == 16 ? 1 : 2;
-  const int bi = bc == 64 ? 0 : bc == 128 ? 1 : 2;
-  return names[bi][wi];
+  const int bi = k.bc == 64 ? 0 : k.bc == 256 ? 3 : (k.nw == 64 ? 1 : 2);
+  const int vi = k.nwv == 8;
+  char *n = names[wi][bi][vi];
+  if (!n[0]) {
+    // conv3r_kernel<W,BC> (128 x 64 wave tiles), <W,BC,32> (128 x 32); the
+    // 8-wave one-per-CU variant adds ",w8"
+    snprintf(n, 40, "conv3r_kernel<%d,%d%s%s>", d->w, k.bc, k.nw == 32 ? ",32" : "", vi ? ",w8" : "");
+  }
+  return n;
 }

@@ -15,11 +15,26 @@
 
 namespace {
 
+// The tap-reuse conv's weight tiles (conv3r.hip), written after the
+// [c_out][9][c_in] pack of every bf16 3x3 conv with c_in, c_out multiples of
+// 32: 1-KB A-fragment blocks [32-channel input chunk c][tap column dx][tap
+// row dy][16-row output block mb] of [plane q = (ci % 32) / 8][row co % 16]
+// [ci % 8], so a (chunk, dx) stage of a column block is 3 contiguous runs.
+__host__ __device__ inline bool r3_tiled(int k, int co_n, int ci_n) {
+  return k == 3 && co_n % 32 == 0 && ci_n % 32 == 0;
+}
+__device__ __forceinline__ long long r3_tile_off(int co_n, int co, int ci, int ky, int kx) {
+  const int c = ci >> 5, q = (ci & 31) >> 3, e = ci & 7;
+  return ((((long long)c * 3 + kx) * 3 + ky) * (co_n >> 4) + (co >> 4)) * 512 + q * 128 +
+         (co & 15) * 8 + e;
+}
+
 template <typename T>
 __global__ void pack_conv_kernel(int co_n, int ci_n, int k, const float *__restrict__ w,
                                  T *__restrict__ wf, T *__restrict__ wd) {
   const int kk = k * k;
   const long long total = (long long)co_n * ci_n * kk;
+  const bool tiled = sizeof(T) == 2 && r3_tiled(k, co_n, ci_n);
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const int t = (int)(i % kk);
@@ -27,11 +42,15 @@ __global__ void pack_conv_kernel(int co_n, int ci_n, int k, const float *__restr
     const int ci = (int)(r % ci_n);
     const int co = (int)(r / ci_n);
     const float v = w[i];
-    if (wf) Elt<T>::store(wf, ((long long)co * kk + t) * ci_n + ci, v);
+    const int ky = t / k, kx = t % k;
+    if (wf) {
+      Elt<T>::store(wf, ((long long)co * kk + t) * ci_n + ci, v);
+      if (tiled) Elt<T>::store(wf + total, r3_tile_off(co_n, co, ci, ky, kx), v);
+    }
     if (wd) {
-      const int ky = t / k, kx = t % k;
       const int tf = (k - 1 - ky) * k + (k - 1 - kx);
       Elt<T>::store(wd, ((long long)ci * kk + tf) * co_n + co, v);
+      if (tiled) Elt<T>::store(wd + total, r3_tile_off(ci_n, ci, co, k - 1 - ky, k - 1 - kx), v);
     }
   }
 }
@@ -75,12 +94,19 @@ __global__ __launch_bounds__(256) void pack_conv_batch_kernel(int count, const r
     const rr_pack_job jb = jobs[lo];
     const long long q = e - pb[lo];
     const int k = jb.k, kk = k * k;
+    const long long tot = (long long)jb.c_out * jb.c_in * kk;
+    const bool tiled = sizeof(T) == 2 && r3_tiled(k, jb.c_out, jb.c_in);
     if (phase == 0) {
       if (!jb.w_fwd) continue;
       const int ci = (int)(q % jb.c_in), co = (int)(q / jb.c_in);
       const float *src = jb.w + ((long long)co * jb.c_in + ci) * kk;
       T *dst = (T *)jb.w_fwd + (long long)co * kk * jb.c_in + ci;
       for (int tp = 0; tp < kk; ++tp) Elt<T>::store(dst, (long long)tp * jb.c_in, src[tp]);
+      if (tiled) {
+        T *tl = (T *)jb.w_fwd + tot;
+        for (int tp = 0; tp < kk; ++tp)
+          Elt<T>::store(tl, r3_tile_off(jb.c_out, co, ci, tp / 3, tp % 3), src[tp]);
+      }
     } else {
       if (!jb.w_dgrad) continue;
       const int co = (int)(q % jb.c_out), ci = (int)(q / jb.c_out);
@@ -90,6 +116,11 @@ __global__ __launch_bounds__(256) void pack_conv_batch_kernel(int count, const r
         const int ky = tp / k, kx = tp - ky * k;
         const int tf = (k - 1 - ky) * k + (k - 1 - kx);
         Elt<T>::store(dst, (long long)tf * jb.c_out, src[tp]);
+      }
+      if (tiled) {
+        T *tl = (T *)jb.w_dgrad + tot;
+        for (int tp = 0; tp < kk; ++tp)
+          Elt<T>::store(tl, r3_tile_off(jb.c_in, ci, co, 2 - tp / 3, 2 - tp % 3), src[tp]);
       }
     }
   }
@@ -1277,6 +1308,11 @@ __global__ void adaptive_avgpool_kernel(int n, int h, int w, int C, int oh, int 
   } while (0)
 
 // dtype-generic pointer casts inside the macro are done by the callers below.
+
+extern "C" long long rr_pack_conv_elems(int dtype, int c_out, int c_in, int k) {
+  const long long n = (long long)c_out * c_in * k * k;
+  return dtype == RR_BF16 && r3_tiled(k, c_out, c_in) ? 2 * n : n;
+}
 
 extern "C" int rr_pack_conv(int dtype, int c_out, int c_in, int k, const float *w, void *w_fwd,
                             void *w_dgrad, rr_stream stream) {

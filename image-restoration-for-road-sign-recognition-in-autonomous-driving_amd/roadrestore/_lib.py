@@ -79,6 +79,7 @@ _SIGS = {
     "rr_wgrad_workspace": (S_, [C.POINTER(WgradDesc)]),
     "rr_wgrad": (I_, [C.POINTER(WgradDesc), P_, P_, P_, P_, P_, S_, P_]),
     "rr_pack_conv": (I_, [I_, I_, I_, I_, P_, P_, P_, P_]),
+    "rr_pack_conv_elems": (L_, [I_, I_, I_, I_]),
     "rr_pack_conv_batch": (I_, [I_, I_, P_, L_, P_]),
     "rr_pack_convT": (I_, [I_, I_, I_, P_, P_, P_, P_]),
     "rr_bias_tile4": (I_, [I_, P_, P_, P_]),

@@ -85,14 +85,22 @@ def _ws(nbytes, device):
 # weights
 
 def pack_conv(w: torch.Tensor, dtype: torch.dtype, fwd=True, dgrad=True):
-    """fp32 [co][ci][k][k] -> (fwd [co][k*k][ci], dgrad [ci][k*k flipped][co])."""
+    """fp32 [co][ci][k][k] -> (fwd [co][k*k][ci], dgrad [ci][k*k flipped][co]);
+    bf16 3x3 packs carry the tap-reuse conv's weight tiles behind that
+    layout (rr_pack_conv_elems)."""
     _need_cuda(w)
     co, ci, k, _ = w.shape
-    wf = torch.empty(co * k * k * ci, dtype=dtype, device=w.device) if fwd else None
-    wd = torch.empty(co * k * k * ci, dtype=dtype, device=w.device) if dgrad else None
+    ne = pack_elems(dtype, co, ci, k)
+    wf = torch.empty(ne, dtype=dtype, device=w.device) if fwd else None
+    wd = torch.empty(ne, dtype=dtype, device=w.device) if dgrad else None
     lib().check(lib().rr_pack_conv(rr_dtype(dtype), co, ci, k, _p(w.contiguous()), _p(wf),
                                    _p(wd), stream()), "rr_pack_conv")
     return wf, wd
+
+
+def pack_elems(dtype, co, ci, k):
+    """elements of one conv pack buffer (rr_pack_conv_elems)"""
+    return int(lib().rr_pack_conv_elems(rr_dtype(dtype), co, ci, k))
 
 
 class PackBatch:
@@ -114,8 +122,9 @@ class PackBatch:
             if not w.is_contiguous():
                 raise ValueError("pack batch needs contiguous weights")
             co, ci, k, _ = w.shape
-            wf = torch.empty(co * k * k * ci, dtype=self.dtype, device=w.device)
-            wd = torch.empty(co * k * k * ci, dtype=self.dtype, device=w.device) if dgrad else None
+            ne = pack_elems(self.dtype, co, ci, k)
+            wf = torch.empty(ne, dtype=self.dtype, device=w.device)
+            wd = torch.empty(ne, dtype=self.dtype, device=w.device) if dgrad else None
             self.out.append((wf, wd))
             jobs[j] = PackJob(_p(w), _p(wf), _p(wd), co, ci, k, 0, begin)
             begin += w.numel()

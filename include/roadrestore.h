@@ -77,7 +77,8 @@ typedef struct {
                           grad of the perceptual slice's conv1_1, 14:196) */
 } rr_igemm_desc;
 
-/* packed weights: w[c_out][taps][c_in1+c_in2] in dtype (see rr_pack_*). */
+/* packed weights: w[c_out][taps][c_in1+c_in2] in dtype (see rr_pack_*; a
+ * bf16 3x3 conv the tap-reuse kernel takes also reads the tiles behind it). */
 int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
              const void *w, const float *bias, void *y1, void *y2,
              const void *mask, float *stats_partial, rr_stream stream);
@@ -131,14 +132,19 @@ int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
              rr_stream stream);
 
 /* weight packing (fp32 torch layout -> compute layout/dtype) */
-/* conv [co][ci][k][k] -> fwd [co][k*k][ci] and dgrad [ci][k*k flipped][co] */
+/* conv [co][ci][k][k] -> fwd [co][k*k][ci] and dgrad [ci][k*k flipped][co].
+ * bf16 3x3 convs with c_in, c_out multiples of 32 also get, right after that
+ * layout, the 1-KB weight tiles the tap-reuse conv reads (one contiguous run
+ * per (32-channel chunk, tap column, tap row)): each pack buffer then holds
+ * rr_pack_conv_elems() = 2 * c_out * 9 * c_in elements. */
+long long rr_pack_conv_elems(int dtype, int c_out, int c_in, int k);
 int rr_pack_conv(int dtype, int c_out, int c_in, int k, const float *w,
                  void *w_fwd, void *w_dgrad, rr_stream stream);
 /* convT [ci][co][2][2] -> up [tap*co][ci] and down [ci][tap][co] */
 /* every conv pack of a network in one launch (the per-step re-pack after the
  * optimizer step): jobs[count] in DEVICE memory, job j covering elements
  * [begin, next begin) of a virtual concatenation of the fp32 weights; total =
- * sum of c_out * c_in * k * k.  Same layouts as rr_pack_conv. */
+ * sum of c_out * c_in * k * k.  Same layouts (and tiles) as rr_pack_conv. */
 typedef struct rr_pack_job {
   const float *w;      /* [c_out][c_in][k][k] fp32                         */
   void *w_fwd;         /* [c_out][k*k][c_in] or NULL                       */

@@ -152,9 +152,10 @@ def test_kernel_selection_for_the_benched_layers():
         (64, 64, 64, 64): ("stream3_kernel<64>", "swgrad_kernel<64>"),   # two passes
         (32, 64, 0, 128): ("conv3r_kernel<32,128>", "swgrad_kernel<32>"),
         (32, 128, 64, 64): ("conv3r_kernel<32,64>", "swgrad_kernel<32>"),
-        (16, 256, 0, 256): ("conv3r_kernel<16,256>", "wgrad3_halo_kernel<16>"),
+        (16, 256, 0, 256): ("conv3r_kernel<16,128>", "wgrad3_halo_kernel<16>"),
         (16, 256, 128, 128): ("conv3r_kernel<16,128>", "wgrad3_halo_kernel<16>"),
-        (8, 512, 0, 512): ("conv3r_kernel<8,256>", "wgrad3_halo_kernel<8>"),
+        (8, 512, 0, 512): ("conv3r_kernel<8,128>", "wgrad3_halo_kernel<8>"),
+        (8, 512, 0, 256): ("conv3r_kernel<8,128,32>", "wgrad3_halo_kernel<8>"),
     }
     for (h, c1, c2, co), (f, wg) in want.items():
         d = IgemmDesc(RR_BF16, RR_CONV3X3, 512, h, h, c1, c2, co, 0, 0, 0, 1, 0, 1, 0)

@@ -41,22 +41,41 @@ def _desc(n, w, c1, c2, co, split=0, act=0, acc=0, bias=0, mask=0, stats=0):
                      stats, 0)
 
 
-# (n, w, c1, c2, c_out, kernel)
+# (n, w, c1, c2, c_out, kernel) -- default 4-wave workgroups (2 per CU)
 SHAPES = [
     (4, 32, 64, 0, 128, "conv3r_kernel<32,128>"),     # res2.c1 / VGG conv2_1
     (2, 32, 128, 0, 128, "conv3r_kernel<32,128>"),    # res2.c2 / conv2_2 (fwd + dgrad)
     (4, 32, 128, 64, 64, "conv3r_kernel<32,64>"),     # dec2.c1 (concat) fwd
-    (2, 32, 128, 0, 256, "conv3r_kernel<32,256>"),    # 8-row tiles in a 32-row image
-    (8, 16, 128, 0, 256, "conv3r_kernel<16,256>"),    # res3.c1 / conv3_1
+    (2, 32, 128, 0, 256, "conv3r_kernel<32,128>"),    # 8-row tiles in a 32-row image, 2 blocks
+    (8, 16, 128, 0, 256, "conv3r_kernel<16,128>"),    # res3.c1 / conv3_1
     (4, 16, 256, 128, 128, "conv3r_kernel<16,128>"),  # dec3.c1 (concat)
-    (8, 8, 256, 0, 512, "conv3r_kernel<8,256>"),      # bottleneck (2 column blocks)
-    (16, 8, 512, 0, 256, "conv3r_kernel<8,256>"),
-    (8, 8, 128, 0, 128, "conv3r_kernel<8,128>"),
+    (512, 8, 512, 0, 512, "conv3r_kernel<8,128>"),    # bottleneck at B = 512 (4 column blocks)
+    (512, 8, 512, 0, 256, "conv3r_kernel<8,128,32>"), # 128 x 32 wave tiles: 512 workgroups
+    (8, 8, 256, 0, 512, "conv3r_kernel<8,128,32>"),   # small batch: 128 x 32 tiles
+    (8, 8, 128, 0, 128, "conv3r_kernel<8,128,32>"),
+]
+# the 8-wave, one-per-CU variant (RR_CONV3R_WG=8)
+SHAPES_W8 = [
+    (4, 32, 64, 0, 128, "conv3r_kernel<32,128,w8>"),
+    (4, 32, 128, 64, 64, "conv3r_kernel<32,64,32,w8>"),
+    (2, 32, 128, 0, 256, "conv3r_kernel<32,256,w8>"),
+    (8, 16, 128, 0, 256, "conv3r_kernel<16,256,w8>"),
+    (512, 8, 512, 0, 512, "conv3r_kernel<8,256,w8>"),
+    (8, 8, 256, 0, 512, "conv3r_kernel<8,128,32,w8>"),
 ]
 
 
-@pytest.mark.parametrize("shape", SHAPES)
+@pytest.fixture(params=["4", "8"])
+def wg(request, monkeypatch):
+    monkeypatch.setenv("RR_CONV3R_WG", request.param)
+    return request.param
+
+
+@pytest.mark.parametrize("shape", SHAPES + [s + ("w8",) for s in SHAPES_W8])
 def test_conv3r_selected(dev, shape, monkeypatch):
+    if len(shape) == 7:
+        monkeypatch.setenv("RR_CONV3R_WG", "8")
+        shape = shape[:6]
     from roadrestore import ops
     n, w, c1, c2, co, name = shape
     assert ops.igemm_kernel_name(_desc(n, w, c1, c2, co, bias=1, stats=1)) == name
@@ -64,8 +83,9 @@ def test_conv3r_selected(dev, shape, monkeypatch):
     assert not ops.igemm_kernel_name(_desc(n, w, c1, c2, co, bias=1, stats=1)).startswith("conv3r")
 
 
-@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("shape", SHAPES + SHAPES_W8)
 def test_conv3r_fwd_bias_stats_relu(dev, shape, monkeypatch):
+    monkeypatch.setenv("RR_CONV3R_WG", "8" if shape in SHAPES_W8 else "4")
     import roadrestore as rr
     from roadrestore._lib import RR_CONV3X3
     n, w, c1, c2, co, _ = shape
@@ -95,9 +115,10 @@ def test_conv3r_fwd_bias_stats_relu(dev, shape, monkeypatch):
     assert rel(s, outs["0"][1]) < 1e-5
 
 
-@pytest.mark.parametrize("shape", [(2, 32, 128, 0, 128), (8, 16, 256, 0, 256), (8, 8, 512, 0, 512)])
+@pytest.mark.parametrize("shape", [(2, 32, 128, 0, 128), (8, 16, 256, 0, 256), (8, 8, 512, 0, 512),
+                                   (512, 8, 512, 0, 512), (4, 32, 128, 0, 64)])
 @pytest.mark.parametrize("acc,msk", [(True, False), (False, True), (True, True)])
-def test_conv3r_dgrad_epilogues(dev, shape, acc, msk, monkeypatch):
+def test_conv3r_dgrad_epilogues(dev, shape, acc, msk, wg, monkeypatch):
     """dgrad epilogues: accumulate into y (the shortcut / identity grad), the
     ReLU-backward mask (VGG dgrads), both."""
     import roadrestore as rr
@@ -122,7 +143,7 @@ def test_conv3r_dgrad_epilogues(dev, shape, acc, msk, monkeypatch):
 
 @pytest.mark.parametrize("shape,split", [((4, 16, 128, 0, 384), 256), ((4, 32, 64, 0, 192), 64),
                                          ((4, 32, 64, 0, 192), 128)])
-def test_conv3r_concat_split_dgrad(dev, shape, split, monkeypatch):
+def test_conv3r_concat_split_dgrad(dev, shape, split, wg, monkeypatch):
     """the dgrad of a concat-input conv writes the two halves to two tensors
     (dec3.c1: 128 -> 256 + 128, dec2.c1: 64 -> 128 + 64 / 64 + 128)"""
     import roadrestore as rr
@@ -143,8 +164,8 @@ def test_conv3r_concat_split_dgrad(dev, shape, split, monkeypatch):
 
 
 @pytest.mark.parametrize("shape", [(2, 32, 128, 0, 128), (8, 16, 256, 0, 256), (8, 8, 512, 0, 512),
-                                   (4, 32, 128, 0, 64)])
-def test_conv3r_bnbwd(dev, shape, monkeypatch):
+                                   (4, 32, 128, 0, 64), (512, 8, 512, 0, 256)])
+def test_conv3r_bnbwd(dev, shape, wg, monkeypatch):
     """conv dgrad + BN/PReLU backward reduce fused in the staged epilogue ==
     the halo kernel's fused path == the unfused sequence."""
     import roadrestore as rr
@@ -185,7 +206,7 @@ def test_conv3r_bnbwd(dev, shape, monkeypatch):
     assert rel(got["dt0"], halo["dt0"]) < 2e-3
 
 
-def test_conv3r_stats_rows_deterministic(dev, monkeypatch):
+def test_conv3r_stats_rows_deterministic(dev, wg, monkeypatch):
     """fixed tile -> partial-row mapping: two launches give bitwise-equal
     outputs and statistics"""
     import roadrestore as rr

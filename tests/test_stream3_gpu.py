@@ -61,7 +61,7 @@ def test_stream3_selected(dev, shape, monkeypatch):
     assert not _name(n // 2 if n * h * w // 2 < 65536 else 1, h, w).startswith("stream3")
     monkeypatch.setenv("RR_STREAM3", "0")
     # 32x32: the tap-reuse conv (128-pixel partial rows); 64x64: the halo kernel
-    assert _blocks(n, h, w) == (n * h * w) // (128 if w == 32 else 256)
+    assert _blocks(n, h, w) == (n * h * w) // (128 if w == 32 and h == w else 256)
 
 
 @pytest.mark.parametrize("shape", SHAPES)
