@@ -52,19 +52,29 @@
 
 namespace {
 
-template <int W, int BC, int NW, int NWV, int HB> struct R3 {
-  static constexpr bool PAIR = W == 8;              // a row unit = the same row of 2 images
-  static constexpr int NS = PAIR ? 1 : W / 16;      // 16-pixel column blocks per row unit
-  static constexpr int R = PAIR ? 8 : 128 / W;      // output rows per wave
+template <int W, int BC, int NW, int NWV, int HB, int SG> struct R3 {
+  // SG > 0: row-segment tiles of any H x W (W ignored): TR rows x 16 SG
+  // columns of one image; out-of-image rows / columns are zero in the halo
+  // and masked in the epilogue
+  static constexpr bool SEGM = SG > 0;
+  static constexpr bool PAIR = !SEGM && W == 8;     // a row unit = the same row of 2 images
+  static constexpr int NS = SEGM ? SG : (PAIR ? 1 : W / 16);   // 16-pixel column blocks per row unit
+  static constexpr int R = SEGM ? 8 / SG : (PAIR ? 8 : 128 / W);  // output rows per wave
   static constexpr int NM = NW / 16;                // 16-channel MFMA rows per wave
   static constexpr int NT = 64 * NWV;               // threads per workgroup
   static constexpr int WC = BC / NW, WP = NWV / WC; // wave grid
   static constexpr int TPX = WP * 128;              // pixels per tile
   static constexpr int TR = PAIR ? 8 : WP * R;      // tile rows (W >= 16)
-  static constexpr int HS = PAIR ? 8 : (TR < W ? TR : W);       // output rows per halo segment
-  static constexpr int SEG = PAIR ? WP : (TR < W ? 1 : TR / W); // segments (images / pairs)
+  static constexpr int HS = PAIR ? 8 : (SEGM || TR < W ? TR : W);        // output rows per halo segment
+  static constexpr int SEG = PAIR ? WP : (SEGM || TR < W ? 1 : TR / W);  // segments (images / pairs)
   static constexpr int HROWS = SEG * (HS + 2);
-  static constexpr int HBLK = HROWS * NS;           // 1-KB halo blocks per 32-channel chunk
+  // blocks per halo row: a row-segment tile keeps a side block in front of
+  // each row -- slot 15 = the pixel left of the segment, slot 0 = the pixel
+  // right of the previous row's segment -- so the shifted edge reads land on
+  // real neighbours (or zeros) with no register fix-up; one trailing side
+  // block serves the last row
+  static constexpr int RS = SEGM ? NS + 1 : NS;
+  static constexpr int HBLK = SEGM ? HROWS * RS + 1 : HROWS * NS;  // 1-KB halo blocks per chunk
   static constexpr int HBYTES = HBLK * 1024;
   static constexpr int WBLK = 3 * (BC / 16);        // weight blocks per stage (3 taps)
   static constexpr int WBYTES = WBLK * 1024;
@@ -73,13 +83,15 @@ template <int W, int BC, int NW, int NWV, int HB> struct R3 {
   static constexpr int SROW = BC + 4;
   static constexpr int STG = 128 * SROW * 4 + (NWV * BC * 2 + NWV) * 4 + 256;
   // [weights x2][halo x HB][guard block]: the shifted edge reads stay inside
-  static constexpr int KBYTES = 2 * WBYTES + HB * HBYTES + 1024;
+  // (row-segment tiles read inside their side blocks: no guard)
+  static constexpr int KBYTES = 2 * WBYTES + HB * HBYTES + (SEGM ? 0 : 1024);
   static constexpr int BIAS = KBYTES;               // [BC] fp32 bias for the register epilogue
-  static constexpr int LDS = KBYTES + BC * 4 > STG ? KBYTES + BC * 4 : STG;
-  static_assert(LDS <= 160 * 1024, "LDS");
+  static constexpr int LDS = KBYTES + BC * 4 > STG || SEGM ? KBYTES + BC * 4 : STG;
+  static_assert(LDS <= 160 * 1024 && (NWV != 4 || 2 * LDS <= 160 * 1024), "LDS");
   static_assert(WC * WP == NWV && NM * 16 == NW, "wave grid");
   static_assert(HB == 1 || HB == 2, "halo buffers");
-  static_assert(PAIR || TR % W == 0 || W % TR == 0, "tile rows");
+  static_assert(!SEGM || (SG == 1 || SG == 2), "segment width");
+  static_assert(SEGM || PAIR || TR % W == 0 || W % TR == 0, "tile rows");
   static_assert(2 * WBYTES >= 1024, "the edge read of the first halo block stays in LDS");
 };
 
@@ -89,10 +101,10 @@ template <int N> __device__ __forceinline__ void vm_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-template <int W, int BC, int NW, int NWV, int HB>
+template <int W, int BC, int NW, int NWV, int HB, int SG>
 __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) {
-  using G = R3<W, BC, NW, NWV, HB>;
-  constexpr int NS = G::NS, R = G::R, NM = G::NM, WC = G::WC;
+  using G = R3<W, BC, NW, NWV, HB, SG>;
+  constexpr int NS = G::NS, R = G::R, NM = G::NM, WC = G::WC, RS = G::RS;
   constexpr int HW = W * W;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
 
@@ -111,8 +123,19 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   const int cblk = tile % a.ncblk, pblk = tile / a.ncblk;
   const int c0 = cblk * BC;
   const int p0 = pblk * G::TPX;
-  const int n0 = p0 / HW;
-  const int ys = G::PAIR || G::TR >= W ? 0 : (p0 - n0 * HW) / W;   // first tile row (one segment)
+  int n0, ys, xs = 0;                                // image, first tile row / column
+  if constexpr (G::SEGM) {
+    // pixel tile = (image, row band, column segment), segments fastest
+    const int nseg = (a.w + 16 * NS - 1) / (16 * NS), nband = (a.h + G::TR - 1) / G::TR;
+    const int seg = pblk % nseg, t2 = pblk / nseg;
+    const int band = t2 % nband;
+    n0 = t2 / nband;
+    ys = band * G::TR;
+    xs = seg * 16 * NS;
+  } else {
+    n0 = p0 / HW;
+    ys = G::PAIR || G::TR >= W ? 0 : (p0 - n0 * HW) / W;   // (one segment)
+  }
 
   const uint32_t sbase = (uint32_t)(uintptr_t)smem;
   const uint32_t wbase = sbase, hbase = sbase + 2 * G::WBYTES;
@@ -125,11 +148,21 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   for (int i = 0; i < G::NHG; ++i) {
     int b = wv + NWV * i;
     if (b >= G::HBLK) b -= NWV;                     // a duplicate of this wave's previous block
-    const int k = b / ((G::HS + 2) * NS);
-    const int rem = b - k * ((G::HS + 2) * NS);
-    const int hr = rem / NS, s = rem - (rem / NS) * NS;
+    const int k = b / ((G::HS + 2) * RS);
+    const int rem = b - k * ((G::HS + 2) * RS);
+    const int hr = rem / RS, s = rem - (rem / RS) * RS;
     int pix = -1;
-    if constexpr (G::PAIR) {
+    if constexpr (G::SEGM) {
+      // s = 0: side block (slot 15: left of row hr; slot 0: right of row
+      // hr - 1); s >= 1: columns 16 (s - 1) .. of row hr (one segment: the
+      // trailing side block is row HS + 2)
+      const int hr_ = b / RS, s_ = b - hr_ * RS;
+      int y = ys + hr_ - 1, x = -1;
+      if (s_ > 0) x = xs + 16 * (s_ - 1) + frow;
+      else if (frow == 15) x = xs - 1;
+      else if (frow == 0) { x = xs + 16 * NS; --y; }
+      if (x >= 0 && x < a.w && y >= 0 && y < a.h) pix = (n0 * a.h + y) * a.w + x;
+    } else if constexpr (G::PAIR) {
       const int y = hr - 1;
       if (y >= 0 && y < W) pix = ((n0 + 2 * k + (frow >> 3)) * W + y) * W + (frow & 7);
     } else {
@@ -203,10 +236,10 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     } else {
       const int x = frow + dx - 1;                  // -1 / 16: the neighbouring block
       loff[dx] = x < 0 ? fq * 256 + 240 - 1024 : (x > 15 ? fq * 256 + 1024 : fq * 256 + x * 16);
-      zl[dx] = x < 0 || x > 15;
+      zl[dx] = !G::SEGM && (x < 0 || x > 15);       // (side blocks hold the neighbours)
     }
   }
-  const uint32_t b_wave = hbase + hrow0 * NS * 1024;
+  const uint32_t b_wave = hbase + (hrow0 * RS + (G::SEGM ? 1 : 0)) * 1024;
 
   f32x4 acc[R][NS][NM];
 #pragma unroll
@@ -266,7 +299,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
 #pragma unroll
         for (int s = 0; s < NS; ++s)
           asm volatile("ds_read_b128 %0, %1 offset:%2"
-                       : "=v"(bf[(ri + 1) & 1][s]) : "v"(ba), "i"(((ri + 1) * NS + s) * 1024));
+                       : "=v"(bf[(ri + 1) & 1][s]) : "v"(ba), "i"(((ri + 1) * RS + s) * 1024));
         asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
       } else {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -280,7 +313,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
           for (int m = 0; m < NM; ++m) asm volatile("" : "+v"(af[dy][m]));
       }
       // the padding columns: zero the shifted edge reads
-      {
+      if constexpr (!G::SEGM) {
         i32x4 &lo = bf[ri & 1][0];
         i32x4 &hi = bf[ri & 1][NS - 1];
         if (G::PAIR) {
@@ -328,11 +361,123 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     if (t == 1234.5f) a.y1[tid] = 1;                  // keep the accumulators live
     return;
   }
-  if (!a.bpart) {
+  const int cb = wc * NW;                           // the wave's first column in the block
+  const int srow = pblk * G::WP + wp;               // the wave's statistics / partial row
+  // output pixel of accumulator tile (o, s) for this lane; -1: outside the
+  // image (row-segment tiles)
+  auto pix_at = [&](int o, int s) __attribute__((always_inline)) -> long long {
+    if constexpr (G::SEGM) {
+      const int y = ys + wp * R + o, x = xs + 16 * s + frow;
+      return y < a.h && x < a.w ? ((long long)n0 * a.h + y) * a.w + x : -1LL;
+    } else {
+      return (long long)p0 + wp * 128 +
+             (G::PAIR ? (frow >> 3) * 64 + o * 8 + (frow & 7) : o * W + 16 * s + frow);
+    }
+  };
+  // 16-B stores: per pair of 16-channel blocks (2p, 2p + 1) one
+  // v_permlane16_swap per dword (odd rows of the first <-> even rows of the
+  // second) leaves lane (row fq, pixel frow) with 8 consecutive channels at
+  // 32 p + {0, 16, 8, 24}[fq]: 4 lanes write a pixel's 64 B (8-B stores of
+  // 32-B pieces were store-issue bound)
+  const int coff = (fq & 1) * 16 + (fq >> 1) * 8;
+  auto swap_pair = [&](f32x4 &va, f32x4 &vb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const auto t = __builtin_amdgcn_permlane16_swap(__float_as_uint(va[j]), __float_as_uint(vb[j]),
+                                                      false, false);
+      va[j] = __uint_as_float(t[0]);
+      vb[j] = __uint_as_float(t[1]);
+    }
+  };
+  if constexpr (G::SEGM) {
+    if (a.bpart) {
+      // ---- fused BN -> PReLU backward (rr_igemm_bnbwd; IgemmArgs::bpart)
+      // in registers: the accumulator is dL/d(PReLU out); per lane 8
+      // channels of one pixel per block pair.  The K loop's last barrier
+      // freed the LDS: the channel constants go there ----
+      float *cst = reinterpret_cast<float *>(smem);   // [4][BC] mean, invstd, aff_s, aff_b
+      for (int i = tid; i < BC; i += G::NT) {
+        cst[i] = a.bmean[c0 + i]; cst[BC + i] = a.binv[c0 + i];
+        cst[2 * BC + i] = a.baff_s[c0 + i]; cst[3 * BC + i] = a.baff_b[c0 + i];
+      }
+      __syncthreads();
+      const float al = a.balpha[0];
+      float g0[NM / 2][8], g1[NM / 2][8], sa = 0.f;
+#pragma unroll
+      for (int pp = 0; pp < NM / 2; ++pp)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { g0[pp][j] = 0.f; g1[pp][j] = 0.f; }
+#pragma unroll
+      for (int o = 0; o < R; ++o)
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          const long long p = pix_at(o, s);
+#pragma unroll
+          for (int pp = 0; pp < NM / 2; ++pp) {
+            f32x4 va = acc[o][s][2 * pp], vb = acc[o][s][2 * pp + 1];
+            swap_pair(va, vb);
+            if (p < 0) continue;
+            const int cl = cb + 32 * pp + coff;          // column in the block
+            const long long e = p * a.cout + c0 + cl;
+            const f32x4 t0 = load4<bf16_t>(reinterpret_cast<const bf16_t *>(a.bt) + e);
+            const f32x4 t1 = load4<bf16_t>(reinterpret_cast<const bf16_t *>(a.bt) + e + 4);
+            const float g[8] = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
+            const float t[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+            float gm[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float u = t[j] * cst[2 * BC + cl + j] + cst[3 * BC + cl + j];   // BN out
+              sa += u > 0.f ? 0.f : g[j] * u;
+              gm[j] = u > 0.f ? g[j] : al * g[j];
+              g0[pp][j] += gm[j];
+              g1[pp][j] += gm[j] * ((t[j] - cst[cl + j]) * cst[BC + cl + j]);
+            }
+            store8<bf16_t>(reinterpret_cast<bf16_t *>(a.y1) + e, f32x4{gm[0], gm[1], gm[2], gm[3]},
+                           f32x4{gm[4], gm[5], gm[6], gm[7]});
+          }
+        }
+      // over the 16 pixel lanes (fixed xor tree), then one partial row per
+      // wave row: [srow][cout][3] = (sum gm, sum gm * xhat, 0)
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+        for (int pp = 0; pp < NM / 2; ++pp)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            g0[pp][j] += __shfl_xor(g0[pp][j], off, 64);
+            g1[pp][j] += __shfl_xor(g1[pp][j], off, 64);
+          }
+      if (frow == 0) {
+#pragma unroll
+        for (int pp = 0; pp < NM / 2; ++pp) {
+          f32x4 *bp = reinterpret_cast<f32x4 *>(a.bpart + ((long long)srow * a.cout + c0 + cb + 32 * pp + coff) * 3);
+          bp[0] = f32x4{g0[pp][0], g1[pp][0], 0.f, g0[pp][1]};
+          bp[1] = f32x4{g1[pp][1], 0.f, g0[pp][2], g1[pp][2]};
+          bp[2] = f32x4{0.f, g0[pp][3], g1[pp][3], 0.f};
+          bp[3] = f32x4{g0[pp][4], g1[pp][4], 0.f, g0[pp][5]};
+          bp[4] = f32x4{g1[pp][5], 0.f, g0[pp][6], g1[pp][6]};
+          bp[5] = f32x4{0.f, g0[pp][7], g1[pp][7], 0.f};
+        }
+      }
+      // the PReLU alpha partial: [srow][cout / 64], one value per 64
+      // channels (a 32-channel wave adds its partner's through LDS)
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) sa += __shfl_xor(sa, off, 64);
+      float *ap = a.bapart + (long long)srow * (a.cout / 64) + (c0 + cb) / 64;
+      if constexpr (NW == 64) {
+        if (lane == 0) *ap = sa;
+      } else {
+        float *red = cst + 4 * BC;
+        if (lane == 0) red[wv] = sa;
+        __syncthreads();
+        if (lane == 0 && (wc & 1) == 0) *ap = sa + red[wv + 1];
+      }
+      return;
+    }
+  }
+  if (G::SEGM || !a.bpart) {
     // ---- register epilogue: lane = 4 NHWC channels of one pixel per
     // accumulator tile ----
-    const int cb = wc * NW;                         // the wave's first column in the block
-    const int pg = p0 + wp * 128;                   // the wave's 128 pixels
     if (a.stats) {
       // per-channel partial sums of the pre-bias accumulator over the wave's
       // 128 pixels: over (o, s) in registers, then over the 16 pixel lanes
@@ -343,12 +488,15 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
 #pragma unroll
       for (int o = 0; o < R; ++o)
 #pragma unroll
-        for (int s = 0; s < NS; ++s)
+        for (int s = 0; s < NS; ++s) {
+          const bool ok = !G::SEGM || pix_at(o, s) >= 0;
 #pragma unroll
           for (int m = 0; m < NM; ++m) {
-            s1[m] += acc[o][s][m];
-            s2[m] += acc[o][s][m] * acc[o][s][m];
+            const f32x4 v = ok ? acc[o][s][m] : f32x4{0.f, 0.f, 0.f, 0.f};
+            s1[m] += v;
+            s2[m] += v * v;
           }
+        }
 #pragma unroll
       for (int off = 1; off < 16; off <<= 1)
 #pragma unroll
@@ -361,7 +509,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
       if (frow == 0) {
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
-          float *sp = a.stats + ((long long)(pg / 128) * a.cout + c0 + cb + m * 16 + fq * 4) * 2;
+          float *sp = a.stats + ((long long)srow * a.cout + c0 + cb + m * 16 + fq * 4) * 2;
           *reinterpret_cast<f32x4 *>(sp) = f32x4{s1[m][0], s2[m][0], s1[m][1], s2[m][1]};
           *reinterpret_cast<f32x4 *>(sp + 4) = f32x4{s1[m][2], s2[m][2], s1[m][3], s2[m][3]};
         }
@@ -372,28 +520,16 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     for (int m = 0; m < NM; ++m) bv[m] = *reinterpret_cast<const f32x4 *>(lbias + cb + m * 16 + fq * 4);
     const int ld1 = a.split > 0 ? a.split : a.cout;
     const int ld2 = a.cout - a.split;
-    // 16-B stores: per pair of 16-channel blocks (2p, 2p + 1) one
-    // v_permlane16_swap per dword (odd rows of the first <-> even rows of the
-    // second) leaves lane (row fq, pixel frow) with 8 consecutive channels at
-    // 32 p + {0, 16, 8, 24}[fq]: 4 lanes write a pixel's 64 B (8-B stores
-    // of 32-B pieces were store-issue bound)
-    const int coff = (fq & 1) * 16 + (fq >> 1) * 8;
 #pragma unroll
     for (int o = 0; o < R; ++o)
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        const int r = G::PAIR ? (frow >> 3) * 64 + o * 8 + (frow & 7) : o * W + 16 * s + frow;
-        const long long p = pg + r;
+        const long long p = pix_at(o, s);
 #pragma unroll
         for (int pp = 0; pp < NM / 2; ++pp) {
           f32x4 va = acc[o][s][2 * pp] + bv[2 * pp], vb = acc[o][s][2 * pp + 1] + bv[2 * pp + 1];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const auto t = __builtin_amdgcn_permlane16_swap(__float_as_uint(va[j]), __float_as_uint(vb[j]),
-                                                            false, false);
-            va[j] = __uint_as_float(t[0]);
-            vb[j] = __uint_as_float(t[1]);
-          }
+          swap_pair(va, vb);
+          if (G::SEGM && p < 0) continue;
           const int c = c0 + cb + 32 * pp + coff;
           const bool second = a.split > 0 && c >= a.split;      // uniform per pair (split % 32 == 0)
           bf16_t *dst = second ? reinterpret_cast<bf16_t *>(a.y2) + p * ld2 + (c - a.split)
@@ -420,89 +556,126 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
       }
     return;
   }
-  // ---- BN-backward epilogue: one 128-pixel group (= one wave row of the
-  // grid) at a time as fp32 [128][BC] in LDS, then the staged store ----
-  float *stg = reinterpret_cast<float *>(smem);
-  for (int g = 0; g < G::WP; ++g) {
-    if (wp == g) {
+  if constexpr (!G::SEGM) {
+    // ---- BN-backward epilogue: one 128-pixel group (= one wave row of the
+    // grid) at a time as fp32 [128][BC] in LDS, then the staged store ----
+    float *stg = reinterpret_cast<float *>(smem);
+    for (int g = 0; g < G::WP; ++g) {
+      if (wp == g) {
 #pragma unroll
-      for (int o = 0; o < R; ++o)
+        for (int o = 0; o < R; ++o)
 #pragma unroll
-        for (int s = 0; s < NS; ++s)
+          for (int s = 0; s < NS; ++s)
 #pragma unroll
-          for (int m = 0; m < NM; ++m) {
-            const int r = G::PAIR ? (frow >> 3) * 64 + o * 8 + (frow & 7) : o * W + 16 * s + frow;
-            const int col = wc * NW + m * 16 + fq * 4;
-            *reinterpret_cast<f32x4 *>(stg + r * G::SROW + col) = acc[o][s][m];
-          }
+            for (int m = 0; m < NM; ++m) {
+              const int r = G::PAIR ? (frow >> 3) * 64 + o * 8 + (frow & 7) : o * W + 16 * s + frow;
+              const int col = wc * NW + m * 16 + fq * 4;
+              *reinterpret_cast<f32x4 *>(stg + r * G::SROW + col) = acc[o][s][m];
+            }
+      }
+      __syncthreads();
+      store_staged<bf16_t, BC, 128, G::NT, RR_CONV3X3>(a, stg, c0, p0 + g * 128, p0 / 128 + g, tid);
+      __syncthreads();
     }
-    __syncthreads();
-    store_staged<bf16_t, BC, 128, G::NT, RR_CONV3X3>(a, stg, c0, p0 + g * 128, p0 / 128 + g, tid);
-    __syncthreads();
   }
 }
 
 // column block and per-wave channels for *d: BC = 256 / 128 / 64 by c_out,
 // except where that leaves fewer than 256 workgroups (one per CU): the
-// 8x8 256-channel layers (B = 512: 128 tiles) take 128 x 32 wave tiles
-struct R3Pick { int bc, nw, nwv, hb; };
+// 8x8 256-channel layers (B = 512: 128 tiles) take 128 x 32 wave tiles.
+// sg > 0: row-segment tiles (any H x W)
+struct R3Pick { int bc, nw, nwv, hb, sg; };
+int r3_tpx(R3Pick k) { return (k.nwv / (k.bc / k.nw)) * 128; }
+
+// square 8 / 16 / 32 maps whose pixel count fills whole tiles take the
+// whole-row tiles; everything else (the reference's 224 / 112 / 56 / 28 /
+// 14 maps, odd sizes, small batches) the row-segment tiles: 32-column
+// segments x 4 rows per wave above W = 16, 16 x 8 at W <= 16
 // RR_CONV3R_WG: 4 (default) = 4-wave workgroups, 2 per CU (one's epilogue /
 // DMA waits overlap the other's MFMAs), one halo buffer; 8 = one 8-wave
-// workgroup per CU with double-buffered halo (A/B)
+// workgroup per CU with double-buffered halo (A/B; whole-row tiles only)
 R3Pick r3_pick(const rr_igemm_desc *d) {
+  const long long P = (long long)d->n * d->h * d->w;
+  const int W = d->w;
+  const bool square = d->h == W && (W == 8 || W == 16 || W == 32);
   const char *e = getenv("RR_CONV3R_WG");
   const int nwv = e && atoi(e) == 8 ? 8 : 4;
-  const long long P = (long long)d->n * d->h * d->w;
-  if (nwv == 8) {
-    if (d->c_out % 256 == 0) {
-      if (d->w != 8 || (P / 256) * (d->c_out / 256) >= 256 || P % 256) return {256, 64, 8, 2};
-      return {128, 32, 8, 2};
+  R3Pick k{0, 0, 0, 0, 0};
+  if (square) {
+    if (nwv == 8) {
+      if (d->c_out % 256 == 0) {
+        if (W != 8 || (P / 256) * (d->c_out / 256) >= 256 || P % 256) k = {256, 64, 8, 2, 0};
+        else k = {128, 32, 8, 2, 0};
+      } else if (d->c_out % 128 == 0) {
+        k = {128, 64, 8, 2, 0};
+      } else {
+        k = {64, 32, 8, 2, 0};
+      }
+    } else if (d->c_out % 128 == 0) {
+      // 128-channel column blocks of 128 x 64 wave tiles (256-pixel tiles);
+      // below 512 workgroups (2 per CU) the 8x8 layers take 128 x 32 wave
+      // tiles (128-pixel tiles)
+      if (W == 8 && (P / 256) * (d->c_out / 128) < 512 && P % 128 == 0) k = {128, 32, 4, 1, 0};
+      else k = {128, 64, 4, 1, 0};
+    } else {
+      k = {64, 64, 4, 1, 0};
     }
-    if (d->c_out % 128 == 0) return {128, 64, 8, 2};
-    return {64, 32, 8, 2};
+    if (P % r3_tpx(k) == 0) return k;
   }
-  // 4 waves: 128-channel column blocks of 128 x 64 wave tiles (256-pixel
-  // tiles); below 512 workgroups (2 per CU) the 8x8 layers take 128 x 32
-  // wave tiles (128-pixel tiles)
-  if (d->c_out % 128 == 0) {
-    if (d->w == 8 && (P / 256) * (d->c_out / 128) < 512 && P % 128 == 0) return {128, 32, 4, 1};
-    return {128, 64, 4, 1};
-  }
-  return {64, 64, 4, 1};
+  const char *se = getenv("RR_CONV3R_SEG");          // A/B: force 1 / 2 column blocks per segment
+  const int sg = se && (atoi(se) == 1 || atoi(se) == 2) ? atoi(se) : (W > 16 ? 2 : 1);
+  if (sg == 2) return d->c_out % 128 == 0 ? R3Pick{128, 64, 4, 1, 2} : R3Pick{64, 64, 4, 1, 2};
+  return d->c_out % 128 == 0 ? R3Pick{128, 32, 4, 1, 1} : R3Pick{64, 32, 4, 1, 1};
 }
-int r3_tpx(R3Pick k) { return (k.nwv / (k.bc / k.nw)) * 128; }
+// row-segment tiles: rows per tile, column segments and row bands per image
+int r3_tr(R3Pick k) { return (k.nwv / (k.bc / k.nw)) * (8 / k.sg); }
+long long r3_seg_tiles(const rr_igemm_desc *d, R3Pick k) {
+  const long long nseg = (d->w + 16 * k.sg - 1) / (16 * k.sg), nband = (d->h + r3_tr(k) - 1) / r3_tr(k);
+  return (long long)d->n * nseg * nband;
+}
+// pixel tiles of the launch
+long long r3_ptiles(const rr_igemm_desc *d, R3Pick k) {
+  if (k.sg) return r3_seg_tiles(d, k);
+  return (long long)d->n * d->h * d->w / r3_tpx(k);
+}
 
 }  // namespace
 
 int conv3r_bc(const rr_igemm_desc *d) {
-  const char *e = getenv("RR_CONV3R");              // A/B switch (per call): 0 = halo kernels
-  if (e && atoi(e) == 0) return 0;
+  const char *e = getenv("RR_CONV3R");              // A/B switch (per call): 0 = halo kernels,
+  const int mode = e ? atoi(e) : 1;                 // 2 = whole-row tiles only
+  if (mode == 0) return 0;
   if (!d || d->dtype != RR_BF16 || d->mode != RR_CONV3X3 || d->out_nchw) return 0;
-  const int W = d->w;
-  if (d->h != W || !(W == 8 || W == 16 || W == 32)) return 0;
+  if (d->n <= 0 || d->h <= 0 || d->w <= 0) return 0;
   if (d->c_in1 <= 0 || d->c_in1 % 32 || d->c_in2 % 32 || d->c_out % 64) return 0;
   if (d->out_split && (d->out_split % 32 || d->out_split >= d->c_out)) return 0;
   const R3Pick k = r3_pick(d);
-  const long long P = (long long)d->n * d->h * d->w;
-  if (P % r3_tpx(k)) return 0;
+  if (k.sg && mode == 2) return 0;
+  const long long tiles = r3_ptiles(d, k) * (d->c_out / k.bc);
+  if (tiles <= 0 || tiles > 0x7fffffffLL) return 0;
   return k.bc;
 }
 
 int conv3r_stat_blocks(const rr_igemm_desc *d) {
   if (!conv3r_bc(d)) return 0;
-  return (int)(((long long)d->n * d->h * d->w) / 128);
+  const R3Pick k = r3_pick(d);
+  return (int)(r3_ptiles(d, k) * (k.nwv / (k.bc / k.nw)));   // one row per wave row of a tile
 }
 
-template <int BC, int NW, int NWV, int HB>
+template <int BC, int NW, int NWV, int HB, int SG>
 static int conv3r_go(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   a.ncblk = a.cout / BC;
-  const long long nblk = ((long long)a.P / (NWV / (BC / NW) * 128)) * a.ncblk;
+  const long long nblk = r3_ptiles(d, R3Pick{BC, NW, NWV, HB, SG}) * a.ncblk;
   if (nblk <= 0 || nblk > 0x7fffffffLL) return RR_EUNSUPPORTED;
   const dim3 grid((unsigned)nblk), block(64 * NWV);
-  switch (d->w) {
-    case 32: hipLaunchKernelGGL((conv3r_kernel<32, BC, NW, NWV, HB>), grid, block, 0, st, a); break;
-    case 16: hipLaunchKernelGGL((conv3r_kernel<16, BC, NW, NWV, HB>), grid, block, 0, st, a); break;
-    default: hipLaunchKernelGGL((conv3r_kernel<8, BC, NW, NWV, HB>), grid, block, 0, st, a); break;
+  if constexpr (SG > 0) {
+    hipLaunchKernelGGL((conv3r_kernel<0, BC, NW, NWV, HB, SG>), grid, block, 0, st, a);
+  } else {
+    switch (d->w) {
+      case 32: hipLaunchKernelGGL((conv3r_kernel<32, BC, NW, NWV, HB, 0>), grid, block, 0, st, a); break;
+      case 16: hipLaunchKernelGGL((conv3r_kernel<16, BC, NW, NWV, HB, 0>), grid, block, 0, st, a); break;
+      default: hipLaunchKernelGGL((conv3r_kernel<8, BC, NW, NWV, HB, 0>), grid, block, 0, st, a); break;
+    }
   }
   RR_CHECK_LAUNCH();
   return RR_OK;
@@ -511,25 +684,41 @@ static int conv3r_go(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
 int conv3r_launch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   if (!conv3r_bc(d)) return RR_EUNSUPPORTED;
   const R3Pick k = r3_pick(d);
-  if (k.nwv == 8) {
-    if (k.bc == 256) return conv3r_go<256, 64, 8, 2>(d, a, st);
-    if (k.bc == 128 && k.nw == 64) return conv3r_go<128, 64, 8, 2>(d, a, st);
-    if (k.bc == 128) return conv3r_go<128, 32, 8, 2>(d, a, st);
-    return conv3r_go<64, 32, 8, 2>(d, a, st);
+  if (k.sg == 2) {
+    if (k.bc == 128) return conv3r_go<128, 64, 4, 1, 2>(d, a, st);
+    return conv3r_go<64, 64, 4, 1, 2>(d, a, st);
   }
-  if (k.bc == 128 && k.nw == 64) return conv3r_go<128, 64, 4, 1>(d, a, st);
-  if (k.bc == 128) return conv3r_go<128, 32, 4, 1>(d, a, st);
-  return conv3r_go<64, 64, 4, 1>(d, a, st);
+  if (k.sg == 1) {
+    if (k.bc == 128) return conv3r_go<128, 32, 4, 1, 1>(d, a, st);
+    return conv3r_go<64, 32, 4, 1, 1>(d, a, st);
+  }
+  if (k.nwv == 8) {
+    if (k.bc == 256) return conv3r_go<256, 64, 8, 2, 0>(d, a, st);
+    if (k.bc == 128 && k.nw == 64) return conv3r_go<128, 64, 8, 2, 0>(d, a, st);
+    if (k.bc == 128) return conv3r_go<128, 32, 8, 2, 0>(d, a, st);
+    return conv3r_go<64, 32, 8, 2, 0>(d, a, st);
+  }
+  if (k.bc == 128 && k.nw == 64) return conv3r_go<128, 64, 4, 1, 0>(d, a, st);
+  if (k.bc == 128) return conv3r_go<128, 32, 4, 1, 0>(d, a, st);
+  return conv3r_go<64, 64, 4, 1, 0>(d, a, st);
 }
 
 const char *conv3r_name(const rr_igemm_desc *d) {
   if (!conv3r_bc(d)) return "invalid";
   const R3Pick k = r3_pick(d);
   static char names[3][4][2][40];
+  static char segnames[2][2][40];
+  char *n;
+  if (k.sg) {
+    // conv3r_kernel<s2,BC> (32-column segments), <s1,BC> (16-column)
+    n = segnames[k.sg - 1][k.bc == 128];
+    if (!n[0]) snprintf(n, 40, "conv3r_kernel<s%d,%d>", k.sg, k.bc);
+    return n;
+  }
   const int wi = d->w == 8 ? 0 : d->w == 16 ? 1 : 2;
   const int bi = k.bc == 64 ? 0 : k.bc == 256 ? 3 : (k.nw == 64 ? 1 : 2);
   const int vi = k.nwv == 8;
-  char *n = names[wi][bi][vi];
+  n = names[wi][bi][vi];
   if (!n[0]) {
     // conv3r_kernel<W,BC> (128 x 64 wave tiles), <W,BC,32> (128 x 32); the
     // 8-wave one-per-CU variant adds ",w8"

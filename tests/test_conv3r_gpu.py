@@ -35,10 +35,10 @@ def rel(a, r):
     return ((a - r).norm() / r.norm().clamp_min(1e-30)).item()
 
 
-def _desc(n, w, c1, c2, co, split=0, act=0, acc=0, bias=0, mask=0, stats=0):
+def _desc(n, w, c1, c2, co, split=0, act=0, acc=0, bias=0, mask=0, stats=0, h=None):
     from roadrestore._lib import RR_BF16, RR_CONV3X3, IgemmDesc
-    return IgemmDesc(RR_BF16, RR_CONV3X3, n, w, w, c1, c2, co, split, act, acc, bias, mask,
-                     stats, 0)
+    return IgemmDesc(RR_BF16, RR_CONV3X3, n, w if h is None else h, w, c1, c2, co, split, act, acc,
+                     bias, mask, stats, 0)
 
 
 # (n, w, c1, c2, c_out, kernel) -- default 4-wave workgroups (2 per CU)
@@ -217,4 +217,163 @@ def test_conv3r_stats_rows_deterministic(dev, wg, monkeypatch):
     wf, _ = rr.ops.pack_conv((rnd(co, c, 3, 3, seed=32) / 48).to(dev), BF)
     a = rr.ops.igemm(RR_CONV3X3, x, None, n, w, w, wf, co, stats=True)
     b = rr.ops.igemm(RR_CONV3X3, x, None, n, w, w, wf, co, stats=True)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2])
+
+
+# ---- row-segment tiles (any H x W): the reference's own geometry, 224^2 and
+# its 112 / 56 / 28 / 14 maps (14:202-205, 17:66, 18:28-32), odd sizes,
+# batches that do not fill whole-row tiles ----
+# (n, h, w, c1, c2, c_out, kernel)
+SHAPES_SEG = [
+    (2, 224, 224, 64, 0, 64, "conv3r_kernel<s2,64>"),      # enc1.c2 / VGG conv1_2 at 224
+    (2, 112, 112, 64, 0, 128, "conv3r_kernel<s2,128>"),    # enc2.c1 / conv2_1 (4th segment half out)
+    (2, 56, 56, 128, 0, 256, "conv3r_kernel<s2,128>"),     # enc3.c1 / conv3_1
+    (2, 28, 28, 256, 0, 512, "conv3r_kernel<s2,128>"),     # bottleneck / conv4_1 (partial band)
+    (2, 14, 14, 512, 0, 512, "conv3r_kernel<s1,128>"),     # VGG conv5_x
+    (4, 14, 14, 64, 0, 64, "conv3r_kernel<s1,64>"),
+    (3, 36, 52, 64, 64, 128, "conv3r_kernel<s2,128>"),     # odd sizes, concat input
+    (2, 60, 60, 64, 0, 64, "conv3r_kernel<s2,64>"),        # partial bands of 16 rows
+    (1, 8, 8, 64, 0, 128, "conv3r_kernel<s1,128>"),        # B = 1 8x8: no whole-row tile
+]
+
+
+def _seg_rows(n, h, w, co, name):
+    sg = int(name.split("<s")[1][0])
+    bc = int(name.split(",")[1].rstrip(">"))
+    nw = 64 if sg == 2 else 32
+    wp = 4 // (bc // nw)
+    tr = wp * (8 // sg)
+    return n * -(-w // (16 * sg)) * -(-h // tr) * wp
+
+
+@pytest.mark.parametrize("shape", SHAPES_SEG)
+def test_conv3r_seg_fwd_bias_stats_relu(dev, shape, monkeypatch):
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    n, h, w, c1, c2, co, name = shape
+    monkeypatch.setenv("RR_CONV3R", "1")
+    assert rr.ops.igemm_kernel_name(_desc(n, w, c1, c2, co, bias=1, stats=1, h=h)) == name
+    cin = c1 + c2
+    x = rnd(n, cin, h, w, seed=1).bfloat16().float()
+    wt = (rnd(co, cin, 3, 3, seed=2) / (3 * cin ** 0.5)).bfloat16().float()
+    b = rnd(co, seed=3)
+    pre = F.conv2d(x, wt, None, padding=1)
+    wf, _ = rr.ops.pack_conv(wt.to(dev), BF)
+    x1 = nhwc(x[:, :c1], dev)
+    x2 = nhwc(x[:, c1:], dev) if c2 else None
+    outs = {}
+    for tag in ("1", "0"):
+        monkeypatch.setenv("RR_CONV3R", tag)
+        y, _, st = rr.ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf, co, bias=b.to(dev), stats=True)
+        yr, _, _ = rr.ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf, co, bias=b.to(dev), act=1)
+        torch.cuda.synchronize()
+        outs[tag] = (nchw(y), st.double().sum(0).cpu(), nchw(yr), st.shape[0])
+    y, s, yr, rows = outs["1"]
+    assert rows == _seg_rows(n, h, w, co, name)
+    ref = pre + b[None, :, None, None]
+    assert rel(y, ref) < 4e-3
+    assert rel(yr, F.relu(ref)) < 4e-3
+    assert rel(s[:, 0], pre.double().sum((0, 2, 3))) < 1e-5
+    assert rel(s[:, 1], (pre.double() ** 2).sum((0, 2, 3))) < 1e-5
+    assert rel(y, outs["0"][0]) < 2e-3
+    assert rel(s, outs["0"][1]) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(2, 112, 112, 128, 0, 64), (2, 28, 28, 512, 0, 256),
+                                   (4, 14, 14, 512, 0, 512), (3, 36, 52, 128, 0, 128)])
+@pytest.mark.parametrize("acc,msk", [(True, False), (False, True), (True, True)])
+def test_conv3r_seg_dgrad_epilogues(dev, shape, acc, msk, monkeypatch):
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    monkeypatch.setenv("RR_CONV3R", "1")
+    n, h, w, c1, _, co = shape
+    x = rnd(n, c1, h, w, seed=11).bfloat16().float()
+    wt = (rnd(co, c1, 3, 3, seed=12) / (3 * c1 ** 0.5)).bfloat16().float()
+    y0 = rnd(n, co, h, w, seed=13).bfloat16().float()
+    m = rnd(n, co, h, w, seed=14).bfloat16().float()
+    ref = F.conv2d(x, wt, None, padding=1) + (y0 if acc else 0)
+    if msk:
+        ref = torch.where(m > 0, ref, torch.zeros(()))
+    wf, _ = rr.ops.pack_conv(wt.to(dev), BF)
+    out = nhwc(y0, dev) if acc else None
+    assert rr.ops.igemm_kernel_name(_desc(n, w, c1, 0, co, acc=int(acc), mask=int(msk), h=h)) \
+        .startswith("conv3r_kernel<s")
+    y, _, _ = rr.ops.igemm(RR_CONV3X3, nhwc(x, dev), None, n, h, w, wf, co, out=out,
+                           accumulate=acc, mask=nhwc(m, dev) if msk else None)
+    assert rel(nchw(y), ref) < 4e-3
+
+
+@pytest.mark.parametrize("shape,split", [((2, 56, 56, 128, 0, 384), 256),
+                                         ((2, 224, 224, 64, 0, 128), 64)])
+def test_conv3r_seg_concat_split_dgrad(dev, shape, split, monkeypatch):
+    """dec3.c1 / dec1.c1 dgrads at the 224 geometry: two output tensors"""
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    n, h, w, c1, _, co = shape
+    x = rnd(n, c1, h, w, seed=21).bfloat16().float()
+    wt = (rnd(co, c1, 3, 3, seed=22) / (3 * c1 ** 0.5)).bfloat16().float()
+    ref = F.conv2d(x, wt, None, padding=1)
+    wf, _ = rr.ops.pack_conv(wt.to(dev), BF)
+    monkeypatch.setenv("RR_CONV3R", "1")
+    assert rr.ops.igemm_kernel_name(_desc(n, w, c1, 0, co, split=split, h=h)).startswith("conv3r_kernel<s")
+    y1, y2, _ = rr.ops.igemm(RR_CONV3X3, nhwc(x, dev), None, n, h, w, wf, co, split=split)
+    torch.cuda.synchronize()
+    assert rel(torch.cat((nchw(y1), nchw(y2)), 1), ref) < 4e-3
+
+
+@pytest.mark.parametrize("shape", [(2, 56, 56, 256, 0, 128), (2, 28, 28, 512, 0, 256),
+                                   (4, 14, 14, 512, 0, 512), (4, 14, 14, 128, 0, 64),
+                                   (3, 36, 52, 128, 0, 64), (2, 112, 112, 64, 0, 128)])
+def test_conv3r_seg_bnbwd(dev, shape, monkeypatch):
+    """conv dgrad + BN/PReLU backward reduce in the row-segment kernel's
+    register epilogue == the unfused sequence == the fallback kernel's fused
+    path (partial rows in another grouping: sums to fp32 rounding)"""
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    ops = rr.ops
+    n, h, w, cg, _, C = shape
+    g2 = nhwc(rnd(n, cg, h, w, seed=51), dev)
+    wt = (rnd(cg, C, 3, 3, seed=52) * (1.0 / (3 * C ** 0.5))).to(dev)
+    _, wd = ops.pack_conv(wt, BF)
+    t1 = nhwc(rnd(n, C, h, w, seed=53) * 2 + 0.3, dev)
+    tf = t1.float().reshape(-1, C)
+    mean = tf.mean(0)
+    inv = 1.0 / torch.sqrt(tf.var(0, unbiased=False) + 1e-5)
+    gamma = (torch.rand(C, generator=torch.Generator().manual_seed(54)) + 0.5).to(dev)
+    beta = (torch.rand(C, generator=torch.Generator().manual_seed(55)) - 0.5).to(dev)
+    s1 = gamma * inv
+    sh1 = beta - mean * s1
+    alpha = torch.tensor([0.23], device=dev)
+    monkeypatch.setenv("RR_CONV3R", "0")
+    da1, _, _ = ops.igemm(RR_CONV3X3, g2, None, n, h, w, wd, C)
+    ref = ops.bn_backward(da1, t1, mean, inv, gamma, mask_kind=2, aux=t1, aff_s=s1, aff_b=sh1,
+                          alpha=alpha)
+    res = {}
+    for tag in ("0", "1"):
+        monkeypatch.setenv("RR_CONV3R", tag)
+        gm, part, rows, arows = ops.igemm_bnbwd(RR_CONV3X3, g2, n, h, w, wd, C, t1, mean, inv, s1,
+                                                sh1, alpha)
+        if tag == "1":
+            name = ops.igemm_kernel_name(_desc(n, w, cg, 0, C, h=h), bnbwd=True)
+            assert name.startswith("conv3r_kernel<s"), name
+            assert rows == _seg_rows(n, h, w, C, name)
+        res[tag] = ops.bn_backward_rows(gm, part, rows, arows, t1, mean, inv, gamma)
+    torch.cuda.synchronize()
+    got, halo = res["1"], res["0"]
+    assert rel(got["dt0"], ref["dt0"]) < 2e-2
+    for k in ("dgamma0", "dbeta0", "dalpha"):
+        assert rel(got[k], ref[k]) < 2e-2, k
+        assert rel(got[k], halo[k]) < 1e-4, k
+    assert rel(got["dt0"], halo["dt0"]) < 2e-3
+
+
+def test_conv3r_seg_deterministic(dev, monkeypatch):
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    monkeypatch.setenv("RR_CONV3R", "1")
+    n, h, w, c, co = 2, 56, 56, 128, 256
+    x = nhwc(rnd(n, c, h, w, seed=31), dev)
+    wf, _ = rr.ops.pack_conv((rnd(co, c, 3, 3, seed=32) / 48).to(dev), BF)
+    a = rr.ops.igemm(RR_CONV3X3, x, None, n, h, w, wf, co, stats=True)
+    b = rr.ops.igemm(RR_CONV3X3, x, None, n, h, w, wf, co, stats=True)
     assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2])

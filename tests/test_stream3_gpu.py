@@ -60,8 +60,11 @@ def test_stream3_selected(dev, shape, monkeypatch):
     # too small for one step per workgroup / not whole steps: a tiled kernel
     assert not _name(n // 2 if n * h * w // 2 < 65536 else 1, h, w).startswith("stream3")
     monkeypatch.setenv("RR_STREAM3", "0")
-    # 32x32: the tap-reuse conv (128-pixel partial rows); 64x64: the halo kernel
-    assert _blocks(n, h, w) == (n * h * w) // (128 if w == 32 and h == w else 256)
+    # the tap-reuse conv: 32x32 whole-row tiles (128-pixel partial rows),
+    # else row-segment tiles (4 wave rows of 4 x 32 pixels per 16-row band)
+    seg = n * -(-w // 32) * -(-h // 16) * 4
+    assert _blocks(n, h, w) == ((n * h * w) // 128 if w == 32 and h == w else seg)
+    assert _name(n, h, w) == ("conv3r_kernel<32,64>" if w == 32 and h == w else "conv3r_kernel<s2,64>")
 
 
 @pytest.mark.parametrize("shape", SHAPES)
@@ -189,7 +192,7 @@ def test_stream3_concat_two_pass(dev, shape, stats, bias, act, monkeypatch):
         d = rr.ops.IgemmDesc(rr.ops.RR_BF16, RR_CONV3X3, n, h, w, 64, 64, 64, 0, act, 0,
                              int(bias), 0, int(stats), 0)
         name = rr.ops.igemm_kernel_name(d)
-        fallback = "conv3r_kernel<32,64>" if w == 32 else "igemm3_halo_kernel<64,%d>" % w
+        fallback = "conv3r_kernel<32,64>" if w == 32 else "conv3r_kernel<s2,64>"
         assert name == ("stream3_kernel<%d>" % w if tag == "1" else fallback)
         y, _, st = rr.ops.igemm(RR_CONV3X3, nhwc(x1, dev), nhwc(x2, dev), n, h, w, wf, 64,
                                 bias=b.to(dev) if bias else None, act=act, stats=stats)
