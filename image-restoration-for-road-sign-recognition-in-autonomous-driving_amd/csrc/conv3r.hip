@@ -591,15 +591,17 @@ int r3_tpx(R3Pick k) { return (k.nwv / (k.bc / k.nw)) * 128; }
 // whole-row tiles; everything else (the reference's 224 / 112 / 56 / 28 /
 // 14 maps, odd sizes, small batches) the row-segment tiles: 32-column
 // segments x 4 rows per wave above W = 16, 16 x 8 at W <= 16
-// RR_CONV3R_WG: 4 (default) = 4-wave workgroups, 2 per CU (one's epilogue /
-// DMA waits overlap the other's MFMAs), one halo buffer; 8 = one 8-wave
-// workgroup per CU with double-buffered halo (A/B; whole-row tiles only)
+// workgroups of whole-row tiles: one 8-wave workgroup per CU with a
+// double-buffered halo where c_out % 128 == 0 (measured 5-12% faster on the
+// 128-512-channel layers, profiles/r3i_ab.jsonl), else 4-wave workgroups, 2
+// per CU (one's epilogue / DMA waits overlap the other's MFMAs) with one halo
+// buffer.  RR_CONV3R_WG=4 / 8 forces one kind (A/B)
 R3Pick r3_pick(const rr_igemm_desc *d) {
   const long long P = (long long)d->n * d->h * d->w;
   const int W = d->w;
   const bool square = d->h == W && (W == 8 || W == 16 || W == 32);
   const char *e = getenv("RR_CONV3R_WG");
-  const int nwv = e && atoi(e) == 8 ? 8 : 4;
+  const int nwv = e && (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : (d->c_out % 128 == 0 ? 8 : 4);
   R3Pick k{0, 0, 0, 0, 0};
   if (square) {
     if (nwv == 8) {

@@ -357,6 +357,8 @@ __global__ void ssim_chan_mean_kernel(int n, int C, const double *__restrict__ c
 
 }  // namespace
 
+int rr_copy_bytes(void *dst, const void *src, size_t bytes, hipStream_t st);   // misc.hip
+
 extern "C" size_t rr_resize_workspace(int n, int h, int w, int c, int oh, int ow) {
   RsPlan p;
   return rs_plan(n, h, w, c, oh, ow, &p) ? p.total : 0;
@@ -436,8 +438,7 @@ extern "C" int rr_cv_resize_linear_u8(int n, int h, int w, int c, int oh, int ow
   if (!in || !out) return RR_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   if (oh == h && ow == w) {                               // cv::resize: same size -> copy
-    const hipError_t e = hipMemcpyAsync(out, in, (size_t)n * h * w * c, hipMemcpyDeviceToDevice, st);
-    return e == hipSuccess ? RR_OK : RR_ELAUNCH;
+    return rr_copy_bytes(out, in, (size_t)n * h * w * c, st);   // (a kernel: graph-safe, misc.hip)
   }
   // hal::resize: scale = 1 / inv_scale, inv_scale = dst / src (double)
   const double sxs = 1.0 / ((double)ow / (double)w), sys = 1.0 / ((double)oh / (double)h);

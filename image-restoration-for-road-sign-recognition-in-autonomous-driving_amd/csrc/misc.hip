@@ -1937,9 +1937,72 @@ extern "C" int rr_scalar_accumulate(const float *x, double *acc, int64_t *count,
   return RR_OK;
 }
 
+// byte-range zero / copy as kernels (16-B stores over the 16-B aligned
+// body, bytes at the ends).  Not for zeroing inside a HIP-graph capture: a
+// zero node recorded from this library -- this kernel or a hipMemsetAsync --
+// reads back garbage from the graph's second replay on in torch's process
+// (tools/diag_memset2.py; torch's own fill node does not), so the captured
+// zeroing (engine.GradSink) uses torch's fill.
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+__global__ void zero_bytes_kernel(char *__restrict__ dst, long long head, long long nbody, long long bytes) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long k = i; k < nbody; k += stride)
+    reinterpret_cast<i32x4_t *>(dst + head)[k] = i32x4_t{0, 0, 0, 0};
+  const long long tail0 = head + nbody * 16;
+  for (long long k = i; k < head + (bytes - tail0); k += stride) dst[k < head ? k : tail0 + (k - head)] = 0;
+}
+__global__ void copy_bytes_kernel(char *__restrict__ dst, const char *__restrict__ src, long long head,
+                                  long long nbody, long long bytes) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long k = i; k < nbody; k += stride)
+    reinterpret_cast<i32x4_t *>(dst + head)[k] = reinterpret_cast<const i32x4_t *>(src + head)[k];
+  const long long tail0 = head + nbody * 16;
+  for (long long k = i; k < head + (bytes - tail0); k += stride) {
+    const long long b = k < head ? k : tail0 + (k - head);
+    dst[b] = src[b];
+  }
+}
+
+// head bytes before the 16-B aligned body (all bytes when src and dst
+// alignments differ), body 16-B chunks, blocks
+static void bytes_plan(uintptr_t d, uintptr_t s, bool copy, size_t bytes, long long &head,
+                       long long &nbody, unsigned &blocks) {
+  if (!copy || ((d ^ s) & 15) == 0) {
+    head = (long long)((16 - (d & 15)) & 15);
+    if (head > (long long)bytes) head = (long long)bytes;
+    nbody = ((long long)bytes - head) / 16;
+  } else {
+    head = (long long)bytes;
+    nbody = 0;
+  }
+  const long long work = nbody > head ? nbody : head;
+  long long b = (work + 255) / 256;
+  blocks = (unsigned)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
+}
+
 extern "C" int rr_zero(void *p, size_t bytes, rr_stream stream) {
   if (!p) return RR_EINVAL;
-  if (hipMemsetAsync(p, 0, bytes, (hipStream_t)stream) != hipSuccess) return RR_ELAUNCH;
+  if (!bytes) return RR_OK;
+  long long head, nbody;
+  unsigned blocks;
+  bytes_plan((uintptr_t)p, 0, false, bytes, head, nbody, blocks);
+  hipLaunchKernelGGL(zero_bytes_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (char *)p, head,
+                     nbody, (long long)bytes);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+int rr_copy_bytes(void *dst, const void *src, size_t bytes, hipStream_t st) {
+  if (!dst || !src) return RR_EINVAL;
+  if (!bytes) return RR_OK;
+  long long head, nbody;
+  unsigned blocks;
+  bytes_plan((uintptr_t)dst, (uintptr_t)src, true, bytes, head, nbody, blocks);
+  hipLaunchKernelGGL(copy_bytes_kernel, dim3(blocks), dim3(256), 0, st, (char *)dst, (const char *)src,
+                     head, nbody, (long long)bytes);
+  RR_CHECK_LAUNCH();
   return RR_OK;
 }
 

@@ -197,7 +197,10 @@ class GradSink:
             off += p.numel()
         nz = sum(p.numel() for p in zp)
         if nz:
-            ops.zero_(self.flat[:nz])
+            # torch's fill, not ops.zero_: a zero node recorded from the
+            # library returns garbage from a graph's second replay on
+            # (tools/diag_memset2.py)
+            self.flat[:nz].zero_()
         self.zero_count = nz
         self.hook = hook
 
@@ -535,10 +538,13 @@ def resblock_backward(blk, S, g_out, sink, pool=None):
     split = c_in1 if c_in2 else 0
     if has_sc:
         wgrad(RR_CONV1X1, ds, x1, x2, n, h, w, cout, dw=sink[sc0.weight])
-        if _SPLIT_DGRAD and split == 64 and cin == 128 and cout == 64:
+        if _SPLIT_DGRAD and split == 64 and cin == 128 and cout == 64 and \
+                _streams_half(dt1.dtype, n, h, w):
             # dec1 (64 + 64 -> 64): each half of the concat grad is a 64 -> 64
             # dgrad over a contiguous slice of the packed weights, the shape
-            # the row-streaming kernel serves
+            # the row-streaming kernel serves (only there: a slice of the
+            # [c_in][9][c_out] rows is not a pack the tap-reuse conv can
+            # read -- its weight tiles sit behind the whole pack)
             half = 64 * 9 * cout
             gx1, _, _ = ops.igemm(RR_CONV3X3, dt1, None, n, h, w, S.pk1[1][:half], 64)
             gx2, _, _ = ops.igemm(RR_CONV3X3, dt1, None, n, h, w, S.pk1[1][half:], 64)
@@ -644,6 +650,13 @@ _FUSED_POOL = os.environ.get("RR_FUSED_POOL", "1") != "0"
 _FUSED_POOL_BWD = os.environ.get("RR_FUSED_POOL_BWD", "1") != "0"
 # A/B switch: dec1's concat dgrad as two 64 -> 64 row-streaming launches
 _SPLIT_DGRAD = os.environ.get("RR_SPLIT_DGRAD", "1") != "0"
+
+
+def _streams_half(dtype, n, h, w):
+    """the 64 -> 64 dgrad of one concat half at n x h x w runs on the
+    row-streaming kernel (which reads the [c_in][9][c_out] rows only)"""
+    d = ops.IgemmDesc(ops.rr_dtype(dtype), RR_CONV3X3, n, h, w, 64, 0, 64, 0, 0, 0, 0, 0, 0, 0)
+    return ops.igemm_kernel_name(d).startswith("stream3")
 # A/B switch: the BN-shortcut tail's ReLU mask recomputed from t2 and the
 # shortcut's pre-BN output (read anyway) instead of read from the block output
 _RECOMPUTE_MASK = os.environ.get("RR_BN_RECOMPUTE_MASK", "1") != "0"

@@ -150,12 +150,12 @@ def test_kernel_selection_for_the_benched_layers():
     want = {  # (h, c_in1, c_in2, c_out): (fwd, wgrad)
         (64, 64, 0, 64): ("stream3_kernel<64>", "swgrad_kernel<64>"),
         (64, 64, 64, 64): ("stream3_kernel<64>", "swgrad_kernel<64>"),   # two passes
-        (32, 64, 0, 128): ("conv3r_kernel<32,128>", "swgrad_kernel<32>"),
+        (32, 64, 0, 128): ("conv3r_kernel<32,128,w8>", "swgrad_kernel<32>"),
         (32, 128, 64, 64): ("conv3r_kernel<32,64>", "swgrad_kernel<32>"),
-        (16, 256, 0, 256): ("conv3r_kernel<16,128>", "wgrad3_halo_kernel<16>"),
-        (16, 256, 128, 128): ("conv3r_kernel<16,128>", "wgrad3_halo_kernel<16>"),
-        (8, 512, 0, 512): ("conv3r_kernel<8,128>", "wgrad3_halo_kernel<8>"),
-        (8, 512, 0, 256): ("conv3r_kernel<8,128,32>", "wgrad3_halo_kernel<8>"),
+        (16, 256, 0, 256): ("conv3r_kernel<16,256,w8>", "wgrad3_halo_kernel<16>"),
+        (16, 256, 128, 128): ("conv3r_kernel<16,128,w8>", "wgrad3_halo_kernel<16>"),
+        (8, 512, 0, 512): ("conv3r_kernel<8,256,w8>", "wgrad3_halo_kernel<8>"),
+        (8, 512, 0, 256): ("conv3r_kernel<8,128,32,w8>", "wgrad3_halo_kernel<8>"),
     }
     for (h, c1, c2, co), (f, wg) in want.items():
         d = IgemmDesc(RR_BF16, RR_CONV3X3, 512, h, h, c1, c2, co, 0, 0, 0, 1, 0, 1, 0)
@@ -163,6 +163,27 @@ def test_kernel_selection_for_the_benched_layers():
         assert ops.wgrad_kernel_name(WgradDesc(RR_BF16, RR_CONV3X3, 512, h, h, c1, c2, co, 0)) == wg
         if f.startswith("conv3r"):     # one BN-statistics partial row per 128 pixels
             assert rr_stat_blocks(d) == 512 * h * h // 128
+
+
+def test_kernel_selection_at_the_reference_geometry():
+    """host-only: the 3x3 convs of the reference's 224x224 pipeline and its
+    112 / 56 / 28 / 14 maps (14:202-205, 17:66, 18:28-32) take the
+    row-segment tiles of the tap-reuse conv (32-column segments above W = 16,
+    16-column at 14x14), one statistics row per wave row of a tile"""
+    from roadrestore import ops
+    from roadrestore._lib import RR_BF16, RR_CONV3X3, IgemmDesc
+    want = {  # (h, c_in1, c_in2, c_out): (kernel, rows per image)
+        (224, 64, 0, 64): ("conv3r_kernel<s2,64>", 7 * 14 * 4),
+        (224, 64, 64, 64): ("conv3r_kernel<s2,64>", 7 * 14 * 4),
+        (112, 64, 0, 128): ("conv3r_kernel<s2,128>", 4 * 14 * 2),
+        (56, 128, 0, 256): ("conv3r_kernel<s2,128>", 2 * 7 * 2),
+        (28, 256, 0, 512): ("conv3r_kernel<s2,128>", 1 * 4 * 2),
+        (14, 512, 0, 512): ("conv3r_kernel<s1,128>", 1 * 2 * 1),
+    }
+    for (h, c1, c2, co), (f, rows) in want.items():
+        d = IgemmDesc(RR_BF16, RR_CONV3X3, 16, h, h, c1, c2, co, 0, 0, 0, 1, 0, 1, 0)
+        assert ops.igemm_kernel_name(d) == f, (h, ops.igemm_kernel_name(d))
+        assert rr_stat_blocks(d) == 16 * rows, (h, rr_stat_blocks(d))
 
 
 def _s1name(mode, n, h, w, c1, c2, co, split=0, act=0, acc=0, bias=0, mask=0, stats=0, nchw_=0):

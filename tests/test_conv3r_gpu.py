@@ -41,7 +41,8 @@ def _desc(n, w, c1, c2, co, split=0, act=0, acc=0, bias=0, mask=0, stats=0, h=No
                      bias, mask, stats, 0)
 
 
-# (n, w, c1, c2, c_out, kernel) -- default 4-wave workgroups (2 per CU)
+# (n, w, c1, c2, c_out, kernel) -- 4-wave workgroups (2 per CU; RR_CONV3R_WG=4,
+# the default where c_out % 128 != 0)
 SHAPES = [
     (4, 32, 64, 0, 128, "conv3r_kernel<32,128>"),     # res2.c1 / VGG conv2_1
     (2, 32, 128, 0, 128, "conv3r_kernel<32,128>"),    # res2.c2 / conv2_2 (fwd + dgrad)
@@ -54,7 +55,8 @@ SHAPES = [
     (8, 8, 256, 0, 512, "conv3r_kernel<8,128,32>"),   # small batch: 128 x 32 tiles
     (8, 8, 128, 0, 128, "conv3r_kernel<8,128,32>"),
 ]
-# the 8-wave, one-per-CU variant (RR_CONV3R_WG=8)
+# the 8-wave, one-per-CU variant (RR_CONV3R_WG=8, the default where
+# c_out % 128 == 0)
 SHAPES_W8 = [
     (4, 32, 64, 0, 128, "conv3r_kernel<32,128,w8>"),
     (4, 32, 128, 64, 64, "conv3r_kernel<32,64,32,w8>"),
@@ -73,6 +75,7 @@ def wg(request, monkeypatch):
 
 @pytest.mark.parametrize("shape", SHAPES + [s + ("w8",) for s in SHAPES_W8])
 def test_conv3r_selected(dev, shape, monkeypatch):
+    monkeypatch.setenv("RR_CONV3R_WG", "4")
     if len(shape) == 7:
         monkeypatch.setenv("RR_CONV3R_WG", "8")
         shape = shape[:6]

@@ -136,10 +136,10 @@ def test_opcheck_every_rr_op(dev):
     from roadrestore import layers as L
     f32 = L.dtype_code(torch.float32)
     xc = torch.rand(2, 64, 8, 8, device=dev)
-    w3 = torch.randn(32, 64, 3, 3, device=dev) * 0.05
-    b3 = torch.randn(32, device=dev)
+    w3 = torch.randn(64, 64, 3, 3, device=dev) * 0.05      # (64-multiple channels: layers.py)
+    b3 = torch.randn(64, device=dev)
     _opcheck(o.conv2d.default, (xc, w3, b3, 1, f32))
-    _opcheck(o.conv2d_backward.default, (torch.rand(2, 32, 8, 8, device=dev), xc, w3, 1, f32))
+    _opcheck(o.conv2d_backward.default, (torch.rand(2, 64, 8, 8, device=dev), xc, w3, 1, f32))
     wt = torch.randn(64, 64, 2, 2, device=dev) * 0.05
     bt = torch.randn(64, device=dev)
     _opcheck(o.conv_transpose2d.default, (xc, wt, bt, f32))

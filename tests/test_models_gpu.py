@@ -533,6 +533,13 @@ def test_hip_graph_step_follows_cosine_lr_schedule(dev):
         for (na, pa), (nb, pb) in zip(ma.named_parameters(), mb.named_parameters()):
             d = (pa - pb).abs().max().item()
             assert d <= 1e-5 * max(1.0, pa.abs().max().item()), (epoch, na, d)
+    # the exactly-zero gradients (conv biases before a train-mode BN) stay
+    # exactly zero through the replays (the graph re-zeroes that section of
+    # the flat gradient every replay)
+    zero = {id(z) for z in rr.engine.resunet_zero_grad_params(mb)}
+    for nb, pb in mb.named_parameters():
+        if id(pb) in zero:
+            assert pb.grad is not None and torch.count_nonzero(pb.grad).item() == 0, nb
     # the schedule really moved lr (cosine, 3 epochs of T_max = 25)
     assert abs(float(oa.param_groups[0]["lr"]) - 2e-4 * (1 + math.cos(math.pi * 3 / 25)) / 2) < 1e-9
 
