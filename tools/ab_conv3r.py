@@ -21,9 +21,20 @@ B = int(os.environ.get("B", 512))
 LAYERS = [("res2.c1", 32, 64, 0, 128), ("res2.c2", 32, 128, 0, 128), ("dec2.c1", 32, 128, 64, 64),
           ("res3.c1", 16, 128, 0, 256), ("res3.c2", 16, 256, 0, 256), ("dec3.c1", 16, 256, 128, 128),
           ("bott.c1", 8, 256, 0, 512), ("bott.512", 8, 512, 0, 512)]
+# SET=224: the cfg5 geometry (row-segment tiles), B = 64 by default
+LAYERS_224 = [("enc.224", 224, 64, 0, 64), ("dec1.224", 224, 64, 64, 64), ("e2.112", 112, 64, 0, 128),
+              ("r2.112", 112, 128, 0, 128), ("e3.56", 56, 128, 0, 256), ("r3.56", 56, 256, 0, 256),
+              ("b.28", 28, 512, 0, 512), ("v5.14", 14, 512, 0, 512)]
+if os.environ.get("SET") == "224":
+    LAYERS = LAYERS_224
+    B = int(os.environ.get("B", 64))
+if os.environ.get("ONLY"):
+    LAYERS = [l for l in LAYERS if l[0] in os.environ["ONLY"].split(",")]
+REPS = int(os.environ.get("REPS", 10))
 
 
-def timeit(fn, reps=10):
+def timeit(fn, reps=None):
+    reps = reps or REPS
     for _ in range(2):
         fn()
     ts = []
