@@ -411,7 +411,18 @@ def main():
     kernels = None
     if probe is not None:
         agg = probe.summary()
-        sym, (cnt, fl, ms, by) = max(agg.items(), key=lambda kv: kv[1][2])
+        # the dominant kernel = the template (family) with the most time: the
+        # probe names some families per variant (conv3r_kernel<W,BC,...>)
+        fams = {}
+        for k, v in agg.items():
+            f = fams.setdefault(k.split("<")[0], [0, 0.0, 0.0, 0.0])
+            for i in range(4):
+                f[i] += v[i]
+        sym, (cnt, fl, ms, by) = max(fams.items(), key=lambda kv: kv[1][2])
+        variants = {k: {"launches": v[0], "avg_launch_ms": round(v[2] / v[0], 4),
+                        "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 1)}
+                    for k, v in sorted(agg.items(), key=lambda kv: -kv[1][2])
+                    if k.split("<")[0] == sym}
         tflops = fl / (ms * 1e-3) / 1e12
         gbs = by / (ms * 1e-3) / 1e9
         pk = PEAK["bf16" if dt == torch.bfloat16 else "f32"]
@@ -429,6 +440,7 @@ def main():
                                 "WRITE_SIZE in separate --pmc passes of this bench "
                                 f"({os.path.relpath(PMC_TRAFFIC, REPO)})" if traffic else None,
                 "traffic_variants": traffic_per or None,
+                "probe_variants": variants,
                 "launches": cnt, "avg_launch_ms": round(ms / cnt, 4),
                 "flop_per_launch": fl / cnt, "algorithmic_bytes_per_launch": by / cnt,
                 "mfma_tflops": round(tflops, 2), "mfma_frac": round(tflops / pk, 4),

@@ -402,7 +402,8 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
       }
       __syncthreads();
       const float al = a.balpha[0];
-      float g0[NM / 2][8], g1[NM / 2][8], sa = 0.f;
+      float g0[NM / 2][8], g1[NM / 2][8];
+      double sa = 0.0;                                 // (fp64: igemm_epi.h store_staged_bnbwd)
 #pragma unroll
       for (int pp = 0; pp < NM / 2; ++pp)
 #pragma unroll
@@ -427,7 +428,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
               const float u = t[j] * cst[2 * BC + cl + j] + cst[3 * BC + cl + j];   // BN out
-              sa += u > 0.f ? 0.f : g[j] * u;
+              sa += u > 0.f ? 0.0 : (double)(g[j] * u);
               gm[j] = u > 0.f ? g[j] : al * g[j];
               g0[pp][j] += gm[j];
               g1[pp][j] += gm[j] * ((t[j] - cst[cl + j]) * cst[BC + cl + j]);
@@ -465,12 +466,12 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
       for (int off = 1; off < 64; off <<= 1) sa += __shfl_xor(sa, off, 64);
       float *ap = a.bapart + (long long)srow * (a.cout / 64) + (c0 + cb) / 64;
       if constexpr (NW == 64) {
-        if (lane == 0) *ap = sa;
+        if (lane == 0) *ap = (float)sa;
       } else {
-        float *red = cst + 4 * BC;
+        double *red = reinterpret_cast<double *>(cst + 4 * BC);
         if (lane == 0) red[wv] = sa;
         __syncthreads();
-        if (lane == 0 && (wc & 1) == 0) *ap = sa + red[wv + 1];
+        if (lane == 0 && (wc & 1) == 0) *ap = (float)(sa + red[wv + 1]);
       }
       return;
     }

@@ -52,7 +52,11 @@ __device__ __forceinline__ void store_staged_bnbwd(const IgemmArgs &a, float *st
     as[j] = a.baff_s[c + j]; ab[j] = a.baff_b[c + j];
   }
   const float al = a.balpha[0];
-  float s0[8], s1[8], sa = 0.f;
+  // the PReLU alpha partial in fp64: a sum of g * u over every pixel and
+  // channel of the tile with heavy cancellation (the 36x52 bottleneck's alpha
+  // grad sat at ~8x the fp32 CPU reference's error with fp32 partials)
+  float s0[8], s1[8];
+  double sa = 0.0;
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s0[j] = 0.f; s1[j] = 0.f; }
 #pragma unroll 2
@@ -71,7 +75,7 @@ __device__ __forceinline__ void store_staged_bnbwd(const IgemmArgs &a, float *st
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float u = t[j] * as[j] + ab[j];            // BN output (PReLU input)
-      sa += u > 0.f ? 0.f : g[j] * u;
+      sa += u > 0.f ? 0.0 : (double)(g[j] * u);
       gm[j] = u > 0.f ? g[j] : al * g[j];
       s0[j] += gm[j];
       s1[j] += gm[j] * ((t[j] - ms[j]) * iv[j]);
@@ -90,7 +94,7 @@ __device__ __forceinline__ void store_staged_bnbwd(const IgemmArgs &a, float *st
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) sa += __shfl_xor(sa, o, 64);
   __syncthreads();                             // stg reads done before red is written
-  float *red = stg + BP * SROW;                // [NW][BC][2] + [NW]
+  float *red = stg + BP * SROW;                // [NW][BC][2] floats + [NW] doubles
   const int lane = tid & 63, wv = tid >> 6;
   if (lane < CPR) {
 #pragma unroll
@@ -99,7 +103,8 @@ __device__ __forceinline__ void store_staged_bnbwd(const IgemmArgs &a, float *st
       red[(wv * BC + cc + j) * 2 + 1] = s1[j];
     }
   }
-  if (lane == 0) red[NW * BC * 2 + wv] = sa;
+  double *redd = reinterpret_cast<double *>(red + NW * BC * 2);   // (8-B aligned)
+  if (lane == 0) redd[wv] = sa;
   __syncthreads();
   for (int cl = tid; cl < BC; cl += NT) {
     float x = 0.f, y = 0.f;
@@ -112,14 +117,14 @@ __device__ __forceinline__ void store_staged_bnbwd(const IgemmArgs &a, float *st
     pp[0] = x; pp[1] = y; pp[2] = 0.f;
   }
   if (tid == 0) {
-    float x = 0.f;
+    double x = 0.0;
 #pragma unroll
-    for (int q = 0; q < NW; ++q) x += red[NW * BC * 2 + q];
+    for (int q = 0; q < NW; ++q) x += redd[q];
     // layout [npblk][cout / 64] (independent of BC): this tile's sum in its
     // first 64-channel slot, zeros in the rest
     float *ap = a.bapart + (long long)pblk * (a.cout / 64) + c0 / 64;
 #pragma unroll
-    for (int k = 0; k < BC / 64; ++k) ap[k] = k == 0 ? x : 0.f;
+    for (int k = 0; k < BC / 64; ++k) ap[k] = k == 0 ? (float)x : 0.f;
   }
 }
 

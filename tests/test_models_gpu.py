@@ -79,6 +79,8 @@ def _check_grads(model, z, g32, g64, strict=4.0, flip_cap=5e-2):
         # ill-conditioned tensors (the fp32 reference itself >= 1% off fp64:
         # a cancelling scalar sum such as a PReLU alpha grad over a 4x6
         # bottleneck at batch 2) are bounded relative to that error
+        if k.endswith("conv_block.2.weight"):      # the PReLU alpha grads (cancelling sums)
+            print(f"alpha grad {k}: ours {e_ours:.3e} vs fp32 reference {e_ref:.3e} (rel-L2 to fp64)")
         assert e_ours <= max(flip_cap, 8 * e_ref), (k, e_ours, e_ref)
         if e_ours > strict * e_ref + 1e-6:
             loose.append((e_ours, e_ref, k))
