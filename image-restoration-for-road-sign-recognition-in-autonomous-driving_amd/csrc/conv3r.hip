@@ -539,9 +539,21 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
             va += load4<bf16_t>(dst);
             vb += load4<bf16_t>(dst + 4);
           }
-          if (a.act == RR_ACT_RELU) {
+          if (a.res) {                                   // (rr_igemm_ex: y1's layout, no split)
+            const bf16_t *rp = reinterpret_cast<const bf16_t *>(a.res) + p * ld1 + c;
+            va += load4<bf16_t>(rp);
+            vb += load4<bf16_t>(rp + 4);
+          }
+          if ((a.act & 3) == RR_ACT_RELU) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) { va[j] = fmaxf(va[j], 0.f); vb[j] = fmaxf(vb[j], 0.f); }
+          } else if ((a.act & 3) == RR_ACT_PRELU) {
+            const float al = a.alpha[0];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              va[j] = va[j] > 0.f ? va[j] : al * va[j];
+              vb[j] = vb[j] > 0.f ? vb[j] : al * vb[j];
+            }
           }
           if (a.has_mask) {
             const bf16_t *mp = reinterpret_cast<const bf16_t *>(a.mask) + p * ld1 + c;

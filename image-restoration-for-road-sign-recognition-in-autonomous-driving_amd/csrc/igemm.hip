@@ -1235,6 +1235,8 @@ static int fill_args(const rr_igemm_desc *d, const void *x1, const void *x2, con
   a.ncblk = 1;
   a.bt = nullptr; a.bmean = a.binv = a.baff_s = a.baff_b = a.balpha = nullptr;
   a.bpart = a.bapart = nullptr;
+  a.alpha = nullptr;
+  a.res = nullptr;
   return RR_OK;
 }
 
@@ -1243,6 +1245,7 @@ static int fill_args(const rr_igemm_desc *d, const void *x1, const void *x2, con
 // benched schedule with it).  Static strings, never NULL.
 extern "C" const char *rr_igemm_kernel_name(const rr_igemm_desc *d, int bnbwd) {
   if (!d) return "invalid";
+  if (d->act > RR_ACT_RELU) return !bnbwd && conv3r_bc(d) ? conv3r_name(d) : "unsupported";
   if (stream3_blocks(d, bnbwd)) return d->w == 64 ? "stream3_kernel<64>" : "stream3_kernel<32>";
   S1Plan pl;
   if (!bnbwd && stream1_plan(d, &pl)) return stream1_name(pl);
@@ -1278,6 +1281,7 @@ extern "C" const char *rr_igemm_kernel_name(const rr_igemm_desc *d, int bnbwd) {
 extern "C" int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
                         const void *w, const float *bias, void *y1, void *y2,
                         const void *mask, float *stats_partial, rr_stream stream) {
+  if (d && (d->act < 0 || d->act > RR_ACT_RELU)) return RR_EINVAL;   // (PReLU / residual: rr_igemm_ex)
   IgemmArgs a;
   const int rc = fill_args(d, x1, x2, w, bias, y1, y2, mask, stats_partial, a);
   if (rc) return rc;
@@ -1301,6 +1305,25 @@ extern "C" int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
   if (conv3r_bc(d)) return conv3r_launch(d, a, st);
   if (d->dtype == RR_BF16) return dispatch<bf16_t>(d, a, st);
   return dispatch<float>(d, a, st);
+}
+
+extern "C" int rr_igemm_ex(const rr_igemm_desc *d, const void *x1, const void *x2, const void *w,
+                           const float *bias, const float *alpha, const void *res, void *y1,
+                           const void *mask, float *stats_partial, rr_stream stream) {
+  if (!d || d->act < 0 || d->act > (RR_ACT_PRELU | RR_ACT_RES) || (d->act & 3) == 3) return RR_EINVAL;
+  if ((d->act & 3) == RR_ACT_PRELU && !alpha) return RR_EINVAL;
+  if ((d->act & RR_ACT_RES) && (!res || d->out_split || d->accumulate || d->out_nchw)) return RR_EINVAL;
+  if (d->act > RR_ACT_RELU && !conv3r_bc(d)) return RR_EUNSUPPORTED;
+  IgemmArgs a;
+  const int rc = fill_args(d, x1, x2, w, bias, y1, nullptr, mask, stats_partial, a);
+  if (rc) return rc;
+  if (d->act <= RR_ACT_RELU) {
+    rr_igemm_desc d2 = *d;
+    return rr_igemm(&d2, x1, x2, w, bias, y1, nullptr, mask, stats_partial, stream);
+  }
+  a.alpha = alpha;
+  a.res = (const char *)res;
+  return conv3r_launch(d, a, (hipStream_t)stream);
 }
 
 static int bnbwd_rows(const rr_igemm_desc *d) { return rr_igemm_stat_blocks(d); }

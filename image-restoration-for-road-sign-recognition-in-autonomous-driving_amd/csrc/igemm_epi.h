@@ -28,6 +28,10 @@ struct IgemmArgs {
   float *bpart, *bapart;                       // [npblk][cout][3], [npblk][cout/64]
   int dbg;            // diagnostics (RR_IGEMM_DBG): bit0 skip epilogue, bit1 K loop x2
   int xcd;            // XCD-aware tile order (RR_XCD_MAP=0 disables)
+  // rr_igemm_ex (conv3r register epilogue): PReLU alpha (act & 3 ==
+  // RR_ACT_PRELU), residual added before the activation (act & RR_ACT_RES)
+  const float *alpha;
+  const char *res;
 };
 
 namespace {
@@ -213,7 +217,7 @@ __device__ __forceinline__ void store_staged(const IgemmArgs &a, float *stg, int
       v0 += load4<T>(dst);
       v1 += load4<T>(dst + 4);
     }
-    if (a.act == RR_ACT_RELU) {
+    if ((a.act & 3) == RR_ACT_RELU) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) { v0[k] = fmaxf(v0[k], 0.f); v1[k] = fmaxf(v1[k], 0.f); }
     }

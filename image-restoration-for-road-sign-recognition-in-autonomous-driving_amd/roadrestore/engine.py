@@ -384,11 +384,22 @@ def resblock_forward_eval_folded(blk, x1, x2, n, h, w, wc, dt, pool=False):
     cb = blk.conv_block
     c1, bn1, pr, c2, bn2 = cb[0], cb[1], cb[2], cb[3], cb[4]
     cout = c1.weight.shape[0]
+    c_in1, c_in2 = x1.shape[-1], (x2.shape[-1] if x2 is not None else 0)
     pk1, b1 = wc.conv_bn_folded(c1, bn1, dt)
-    t1, _, _ = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, pk1, cout, bias=b1)
     one, zero = _unit_affine(cout, x1.device)
-    a1 = ops.affine_act(t1, one, zero, alpha=pr.weight)
+    if _ex_fusable(x1.dtype, n, h, w, c_in1, c_in2, cout, ops.RR_ACT_PRELU):
+        # PReLU in conv1's epilogue (rr_igemm_ex): no separate activation pass
+        a1, _, _ = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, pk1, cout, bias=b1, alpha=pr.weight)
+    else:
+        t1, _, _ = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, pk1, cout, bias=b1)
+        a1 = ops.affine_act(t1, one, zero, alpha=pr.weight)
     pk2, b2 = wc.conv_bn_folded(c2, bn2, dt)
+    if not block_has_shortcut(blk) and x2 is None and \
+            _ex_fusable(a1.dtype, n, h, w, cout, 0, cout, RELU | ops.RR_ACT_RES):
+        # identity shortcut: relu(conv2'(a1) + x) in conv2's epilogue
+        out, _, _ = ops.igemm(RR_CONV3X3, a1, None, n, h, w, pk2, cout, bias=b2, res=x1, act=RELU)
+        S = Bag(x1=x1, x2=x2, n=n, h=h, w=w)
+        return (out, S, ops.maxpool2_fwd(out)) if pool else (out, S)
     t2, _, _ = ops.igemm(RR_CONV3X3, a1, None, n, h, w, pk2, cout, bias=b2)
     if block_has_shortcut(blk):
         pks, bs = wc.conv_bn_folded(blk.shortcut[0], blk.shortcut[1], dt)
@@ -402,6 +413,20 @@ def resblock_forward_eval_folded(blk, x1, x2, n, h, w, wc, dt, pool=False):
     if pool:
         return out, S, ops.maxpool2_fwd(out)
     return out, S
+
+
+def _ex_fusable(dtype, n, h, w, c1, c2, cout, act):
+    """rr_igemm_ex takes the epilogue ``act`` on this conv with the kernel the
+    plain conv would run anyway (the tap-reuse conv; on the 64x64 maps the
+    row-streaming kernel keeps the layer and the activation stays a pass)."""
+    if dtype != torch.bfloat16:
+        return False
+    rd = ops.rr_dtype(dtype)
+    fused = ops.igemm_kernel_name(ops.IgemmDesc(rd, RR_CONV3X3, n, h, w, c1, c2, cout, 0, act,
+                                                0, 1, 0, 0, 0))
+    plain = ops.igemm_kernel_name(ops.IgemmDesc(rd, RR_CONV3X3, n, h, w, c1, c2, cout, 0, 0,
+                                                0, 1, 0, 0, 0))
+    return fused.startswith("conv3r") and fused == plain
 
 
 def resblock_forward(blk, x1, x2, n, h, w, wc, dt, training, need_bwd, pool=False):

@@ -12,8 +12,8 @@ import ctypes as C
 
 import torch
 
-from ._lib import (RR_BF16, RR_F32, RR_CONV1X1, RR_CONV3X3, RR_CONVT_DOWN, RR_CONVT_UP,
-                   RR_DISTORT_KMAX, BnBwdDesc, DistortParam, IgemmDesc, PackJob, WgradDesc, lib)
+from ._lib import (RR_ACT_PRELU, RR_ACT_RES, RR_BF16, RR_F32, RR_CONV1X1, RR_CONV3X3,
+                   RR_CONVT_DOWN, RR_CONVT_UP, RR_DISTORT_KMAX, BnBwdDesc, DistortParam, IgemmDesc, PackJob, WgradDesc, lib)
 
 __all__ = [
     "rr_dtype", "stream", "pack_conv", "pack_convT", "bias_tile4", "igemm", "wgrad",
@@ -162,8 +162,9 @@ def bias_tile4(b: torch.Tensor):
 # implicit GEMM
 
 def igemm(mode, x1, x2, n, h, w, wpack, cout, bias=None, act=0, out=None, out2=None,
-          split=0, accumulate=False, mask=None, stats=False, out_nchw=False):
-    """Run rr_igemm.  Returns (y1, y2, stats_partial_or_None).
+          split=0, accumulate=False, mask=None, stats=False, out_nchw=False, alpha=None, res=None):
+    """Run rr_igemm (rr_igemm_ex with ``alpha`` -- act RR_ACT_PRELU -- or
+    ``res``, added before the activation).  Returns (y1, y2, stats_partial_or_None).
 
     mode RR_CONV3X3 / RR_CONV1X1: y [n, h, w, cout]
     mode RR_CONVT_UP: GEMM columns 4*cout_t, y [n, 2h, 2w, cout/4]
@@ -173,6 +174,11 @@ def igemm(mode, x1, x2, n, h, w, wpack, cout, bias=None, act=0, out=None, out2=N
     dt = x1.dtype
     c1 = x1.shape[-1]
     c2 = x2.shape[-1] if x2 is not None else 0
+    ex = alpha is not None or res is not None
+    if alpha is not None:
+        act = RR_ACT_PRELU
+    if res is not None:
+        act |= RR_ACT_RES
     d = IgemmDesc(rr_dtype(dt), mode, n, h, w, c1, c2, cout, split, act, int(accumulate),
                   int(bias is not None), int(mask is not None), int(stats), int(out_nchw))
     dev = x1.device
@@ -192,8 +198,13 @@ def igemm(mode, x1, x2, n, h, w, wpack, cout, bias=None, act=0, out=None, out2=N
         blocks = lib().rr_igemm_stat_blocks(C.byref(d))
         st = torch.empty((blocks, cout, 2), dtype=torch.float32, device=dev)
     def launch():
-        lib().check(lib().rr_igemm(C.byref(d), _p(x1), _p(x2), _p(wpack), _p(bias), _p(out),
-                                   _p(out2), _p(mask), _p(st), stream()), "rr_igemm")
+        if ex:
+            lib().check(lib().rr_igemm_ex(C.byref(d), _p(x1), _p(x2), _p(wpack), _p(bias),
+                                          _p(alpha), _p(res), _p(out), _p(mask), _p(st), stream()),
+                        "rr_igemm_ex")
+        else:
+            lib().check(lib().rr_igemm(C.byref(d), _p(x1), _p(x2), _p(wpack), _p(bias), _p(out),
+                                       _p(out2), _p(mask), _p(st), stream()), "rr_igemm")
     taps = 9 if mode == RR_CONV3X3 else (4 if mode == RR_CONVT_DOWN else 1)
     _launch(lambda: igemm_kernel_name(d), 2.0 * n * h * w * cout * taps * (c1 + c2), launch,
             f"fwd m{mode} {n}x{h}x{w} c{c1}+{c2}->{cout}")

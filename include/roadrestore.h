@@ -50,7 +50,9 @@ enum rr_igemm_mode {
   RR_CONVT_DOWN = 3 /* ConvTranspose2d(k2,s2) dgrad: gather 2x2 -> GEMM     */
 };
 
-enum rr_act { RR_ACT_NONE = 0, RR_ACT_RELU = 1 };
+enum rr_act { RR_ACT_NONE = 0, RR_ACT_RELU = 1, RR_ACT_PRELU = 2 };
+/* act flag (rr_igemm_ex): res[p, c] (y's layout) added before the activation */
+#define RR_ACT_RES 4
 
 /*
  * Implicit-GEMM convolution: y[p, c] = sum_k W[c, k] * X[p, k] (+ epilogue).
@@ -82,6 +84,18 @@ typedef struct {
 int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
              const void *w, const float *bias, void *y1, void *y2,
              const void *mask, float *stats_partial, rr_stream stream);
+/* rr_igemm with the inference epilogues of a residual block fused (eval mode,
+ * BatchNorm folded into the conv, 17:84-86; ResidualBlock 14:96-115):
+ *   act & 3 == RR_ACT_PRELU: y = PReLU_alpha(conv + bias), alpha[0] the
+ *     single nn.PReLU() weight (conv_block[2]);
+ *   act & RR_ACT_RES: res[p, c] (y1's layout) added before the activation --
+ *     the identity shortcut's relu(conv2(a1) + x).
+ * bf16 3x3 convs the tap-reuse kernel takes (rr_igemm_kernel_name reports
+ * "conv3r_kernel<...>" for the descriptor); no split / accumulate / NCHW
+ * output with these flags.  Other descriptors: RR_EUNSUPPORTED. */
+int rr_igemm_ex(const rr_igemm_desc *d, const void *x1, const void *x2, const void *w,
+                const float *bias, const float *alpha, const void *res, void *y1,
+                const void *mask, float *stats_partial, rr_stream stream);
 /* number of row blocks the partial stats buffer holds: [blocks][c_out][2] */
 int rr_igemm_stat_blocks(const rr_igemm_desc *d);
 /* The kernel rr_igemm (bnbwd = 0) or rr_igemm_bnbwd (bnbwd = 1) launches for

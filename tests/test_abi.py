@@ -186,6 +186,22 @@ def test_kernel_selection_at_the_reference_geometry():
         assert rr_stat_blocks(d) == 16 * rows, (h, rr_stat_blocks(d))
 
 
+def test_igemm_ex_kernel_selection():
+    """host-only: rr_igemm_ex's fused PReLU / residual epilogues run on the
+    tap-reuse conv only; other descriptors report "unsupported" (the engine
+    then keeps the activation pass)"""
+    from roadrestore import ops
+    from roadrestore._lib import RR_ACT_PRELU, RR_ACT_RES, RR_BF16, RR_CONV3X3, RR_F32, IgemmDesc
+
+    def name(dt, h, c, act, bnbwd=False):
+        return ops.igemm_kernel_name(IgemmDesc(dt, RR_CONV3X3, 4, h, h, c, 0, c, 0, act, 0, 1, 0, 0, 0),
+                                     bnbwd=bnbwd)
+    assert name(RR_BF16, 224, 64, RR_ACT_PRELU) == "conv3r_kernel<s2,64>"
+    assert name(RR_BF16, 16, 256, 1 | RR_ACT_RES).startswith("conv3r_kernel<16,256")
+    assert name(RR_F32, 224, 64, RR_ACT_PRELU) == "unsupported"
+    assert name(RR_BF16, 224, 64, RR_ACT_PRELU, bnbwd=True) == "unsupported"
+
+
 def _s1name(mode, n, h, w, c1, c2, co, split=0, act=0, acc=0, bias=0, mask=0, stats=0, nchw_=0):
     from roadrestore import ops
     from roadrestore._lib import RR_BF16, IgemmDesc

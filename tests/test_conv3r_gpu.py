@@ -380,3 +380,49 @@ def test_conv3r_seg_deterministic(dev, monkeypatch):
     a = rr.ops.igemm(RR_CONV3X3, x, None, n, h, w, wf, co, stats=True)
     b = rr.ops.igemm(RR_CONV3X3, x, None, n, h, w, wf, co, stats=True)
     assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2])
+
+
+@pytest.mark.parametrize("shape", [(2, 224, 224, 64, 0, 64), (2, 56, 56, 128, 0, 256), (4, 16, 16, 256, 0, 256),
+                                   (3, 36, 52, 64, 64, 128), (2, 32, 32, 128, 0, 128)])
+def test_conv3r_ex_prelu_and_residual(dev, shape, monkeypatch):
+    """rr_igemm_ex: the eval-mode residual block's epilogues (BN folded into
+    the conv, 17:84-86) -- PReLU after conv1 (14:101-103) and the identity
+    shortcut's relu(conv2 + x) (14:110-115) -- vs fp32 torch on bf16-exact
+    inputs, and vs the unfused conv + activation pass."""
+    import roadrestore as rr
+    from roadrestore import ops
+    from roadrestore._lib import RR_ACT_PRELU, RR_ACT_RES, RR_CONV3X3
+    monkeypatch.setenv("RR_CONV3R", "1")
+    n, h, w, c1, c2, co = shape
+    cin = c1 + c2
+    x = rnd(n, cin, h, w, seed=61).bfloat16().float()
+    wt = (rnd(co, cin, 3, 3, seed=62) / (3 * cin ** 0.5)).bfloat16().float()
+    b = rnd(co, seed=63) * 0.3
+    r = rnd(n, co, h, w, seed=64).bfloat16().float()
+    alpha = torch.tensor([0.17], device=dev)
+    pre = F.conv2d(x, wt, b, padding=1)
+    wf, _ = ops.pack_conv(wt.to(dev), BF)
+    x1 = nhwc(x[:, :c1], dev)
+    x2 = nhwc(x[:, c1:], dev) if c2 else None
+    assert ops.igemm_kernel_name(_desc(n, w, c1, c2, co, act=RR_ACT_PRELU, bias=1, h=h)).startswith("conv3r")
+    y, _, _ = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf, co, bias=b.to(dev), alpha=alpha)
+    ref = torch.where(pre > 0, pre, 0.17 * pre)
+    assert rel(nchw(y), ref) < 4e-3
+    t, _, _ = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf, co, bias=b.to(dev))
+    one, zero = torch.ones(co, device=dev), torch.zeros(co, device=dev)
+    y0 = ops.affine_act(t, one, zero, alpha=alpha)
+    assert rel(nchw(y), nchw(y0)) < 2e-3
+    # residual + ReLU
+    y, _, _ = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf, co, bias=b.to(dev), res=nhwc(r, dev), act=1)
+    assert rel(nchw(y), F.relu(pre + r)) < 4e-3
+    # residual + PReLU (both flags)
+    y, _, _ = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf, co, bias=b.to(dev), res=nhwc(r, dev),
+                        alpha=alpha)
+    s = pre + r
+    assert rel(nchw(y), torch.where(s > 0, s, 0.17 * s)) < 4e-3
+    torch.cuda.synchronize()
+    # the plain entry point refuses the fused activations
+    from roadrestore._lib import lib
+    import ctypes as C
+    d = _desc(n, w, c1, c2, co, act=RR_ACT_PRELU | RR_ACT_RES, h=h)
+    assert lib().rr_igemm(C.byref(d), None, None, None, None, None, None, None, None, None) != 0
