@@ -639,6 +639,13 @@ R3Pick r3_pick(const rr_igemm_desc *d) {
   }
   const char *se = getenv("RR_CONV3R_SEG");          // A/B: force 1 / 2 column blocks per segment
   const int sg = se && (atoi(se) == 1 || atoi(se) == 2) ? atoi(se) : (W > 16 ? 2 : 1);
+  // RR_CONV3R_SEGWG=8 (A/B): one 8-wave workgroup per CU with a
+  // double-buffered halo (the next chunk loads during this one's stages)
+  const char *sw = getenv("RR_CONV3R_SEGWG");
+  if (sw && atoi(sw) == 8) {
+    if (sg == 2) return d->c_out % 128 == 0 ? R3Pick{128, 64, 8, 2, 2} : R3Pick{64, 32, 8, 2, 2};
+    return d->c_out % 128 == 0 ? R3Pick{128, 32, 8, 2, 1} : R3Pick{64, 32, 8, 1, 1};
+  }
   if (sg == 2) return d->c_out % 128 == 0 ? R3Pick{128, 64, 4, 1, 2} : R3Pick{64, 64, 4, 1, 2};
   return d->c_out % 128 == 0 ? R3Pick{128, 32, 4, 1, 1} : R3Pick{64, 32, 4, 1, 1};
 }
@@ -700,10 +707,18 @@ int conv3r_launch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   if (!conv3r_bc(d)) return RR_EUNSUPPORTED;
   const R3Pick k = r3_pick(d);
   if (k.sg == 2) {
+    if (k.nwv == 8) {
+      if (k.bc == 128) return conv3r_go<128, 64, 8, 2, 2>(d, a, st);
+      return conv3r_go<64, 32, 8, 2, 2>(d, a, st);
+    }
     if (k.bc == 128) return conv3r_go<128, 64, 4, 1, 2>(d, a, st);
     return conv3r_go<64, 64, 4, 1, 2>(d, a, st);
   }
   if (k.sg == 1) {
+    if (k.nwv == 8) {
+      if (k.bc == 128) return conv3r_go<128, 32, 8, 2, 1>(d, a, st);
+      return conv3r_go<64, 32, 8, 1, 1>(d, a, st);
+    }
     if (k.bc == 128) return conv3r_go<128, 32, 4, 1, 1>(d, a, st);
     return conv3r_go<64, 32, 4, 1, 1>(d, a, st);
   }
@@ -722,12 +737,13 @@ const char *conv3r_name(const rr_igemm_desc *d) {
   if (!conv3r_bc(d)) return "invalid";
   const R3Pick k = r3_pick(d);
   static char names[3][4][2][40];
-  static char segnames[2][2][40];
+  static char segnames[2][2][2][40];
   char *n;
   if (k.sg) {
-    // conv3r_kernel<s2,BC> (32-column segments), <s1,BC> (16-column)
-    n = segnames[k.sg - 1][k.bc == 128];
-    if (!n[0]) snprintf(n, 40, "conv3r_kernel<s%d,%d>", k.sg, k.bc);
+    // conv3r_kernel<s2,BC> (32-column segments), <s1,BC> (16-column); ",w8":
+    // 8-wave workgroups
+    n = segnames[k.sg - 1][k.bc == 128][k.nwv == 8];
+    if (!n[0]) snprintf(n, 40, "conv3r_kernel<s%d,%d%s>", k.sg, k.bc, k.nwv == 8 ? ",w8" : "");
     return n;
   }
   const int wi = d->w == 8 ? 0 : d->w == 16 ? 1 : 2;
