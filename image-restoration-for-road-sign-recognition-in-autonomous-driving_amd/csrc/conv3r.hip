@@ -639,10 +639,15 @@ R3Pick r3_pick(const rr_igemm_desc *d) {
   }
   const char *se = getenv("RR_CONV3R_SEG");          // A/B: force 1 / 2 column blocks per segment
   const int sg = se && (atoi(se) == 1 || atoi(se) == 2) ? atoi(se) : (W > 16 ? 2 : 1);
-  // RR_CONV3R_SEGWG=8 (A/B): one 8-wave workgroup per CU with a
-  // double-buffered halo (the next chunk loads during this one's stages)
+  // one 8-wave workgroup per CU with a double-buffered halo (the next
+  // chunk loads during this one's stages) on the 128+-channel maps of
+  // W <= 28 (the 28x28 / 14x14 layers: 9-12 % faster), 2 x 4-wave elsewhere
+  // (the 224 / 112 / 56 layers: even or 5-10 % slower,
+  // profiles/r3v_ab224_segwg.jsonl); RR_CONV3R_SEGWG=4 / 8 forces one (A/B)
   const char *sw = getenv("RR_CONV3R_SEGWG");
-  if (sw && atoi(sw) == 8) {
+  const int segwg = sw && (atoi(sw) == 4 || atoi(sw) == 8) ? atoi(sw)
+                                                           : (d->c_out % 128 == 0 && W <= 28 ? 8 : 4);
+  if (segwg == 8) {
     if (sg == 2) return d->c_out % 128 == 0 ? R3Pick{128, 64, 8, 2, 2} : R3Pick{64, 32, 8, 2, 2};
     return d->c_out % 128 == 0 ? R3Pick{128, 32, 8, 2, 1} : R3Pick{64, 32, 8, 1, 1};
   }

@@ -13,6 +13,7 @@ struct S1Args {
   const char *mask;          // relu-backward mask (y1 layout) or null
   float *stats;              // [G][c_out][2] pre-bias partial sums or null
   int mode, P, h, w, hw, lw, lhw;
+  FastDiv fd_hw, fd_w;       // coarse pixel -> (image, row, column) for any h, w (convT up / down)
   int c1, c2, cout, cout_t, split, K, G, flags;
   int ksrc[16], kch[16], ktap[16];   // per 32-deep k fragment: source, channel, fine-grid tap offset
 };

@@ -94,8 +94,8 @@ __global__ __launch_bounds__(256, 2) void stream1_kernel(S1Args a) {
 
   // fine-grid pixel (2y, 2x) of coarse pixel p (convT up / down)
   auto fine_of = [&](int p) __attribute__((always_inline)) {
-    const int n = p >> a.lhw, rem = p & ((1 << a.lhw) - 1);
-    const int y = rem >> a.lw, x = rem & ((1 << a.lw) - 1);
+    const int n = (int)fdiv((uint32_t)p, a.fd_hw), rem = p - n * a.hw;
+    const int y = (int)fdiv((uint32_t)rem, a.fd_w), x = rem - y * a.w;
     return (long long)(n * 2 * a.h + 2 * y) * 2 * a.w + 2 * x;
   };
   // the lane's first column of widened pair q (see the epilogue)
@@ -369,7 +369,6 @@ int stream1_plan(const rr_igemm_desc *d, S1Plan *pl) {
   if (mode != RR_CONV1X1 && d->want_stats) return 0;
   if (mode != RR_CONV1X1 && mode != RR_CONVT_DOWN && d->has_mask) return 0;
   if (mode == RR_CONVT_UP && (d->c_out % 4 || (d->c_out / 4) % 8)) return 0;
-  if (mode != RR_CONV1X1 && (ilog2(d->w) < 0 || ilog2(d->h * d->w) < 0)) return 0;
   if (d->out_split && d->out_split % 32) return 0;
   if (mode == RR_CONVT_UP && (d->c_out / 4) % 32) return 0;
   if (d->accumulate && d->has_mask) return 0;
@@ -396,6 +395,8 @@ int stream1_launch(const rr_igemm_desc *d, const S1Plan &pl, S1Args a, hipStream
   a.hw = d->h * d->w;
   a.lw = ilog2(d->w) < 0 ? 0 : ilog2(d->w);
   a.lhw = ilog2(d->h * d->w) < 0 ? 0 : ilog2(d->h * d->w);
+  a.fd_hw = make_fastdiv((uint32_t)(d->h * d->w));
+  a.fd_w = make_fastdiv((uint32_t)d->w);
   a.c1 = d->c_in1; a.c2 = d->c_in2;
   a.cout = d->c_out;
   a.cout_t = d->mode == RR_CONVT_UP ? d->c_out / 4 : d->c_out;

@@ -177,8 +177,8 @@ def test_kernel_selection_at_the_reference_geometry():
         (224, 64, 64, 64): ("conv3r_kernel<s2,64>", 7 * 14 * 4),
         (112, 64, 0, 128): ("conv3r_kernel<s2,128>", 4 * 14 * 2),
         (56, 128, 0, 256): ("conv3r_kernel<s2,128>", 2 * 7 * 2),
-        (28, 256, 0, 512): ("conv3r_kernel<s2,128>", 1 * 4 * 2),
-        (14, 512, 0, 512): ("conv3r_kernel<s1,128>", 1 * 2 * 1),
+        (28, 256, 0, 512): ("conv3r_kernel<s2,128,w8>", 1 * 2 * 4),
+        (14, 512, 0, 512): ("conv3r_kernel<s1,128,w8>", 1 * 1 * 2),
     }
     for (h, c1, c2, co), (f, rows) in want.items():
         d = IgemmDesc(RR_BF16, RR_CONV3X3, 16, h, h, c1, c2, co, 0, 0, 0, 1, 0, 1, 0)

@@ -231,8 +231,8 @@ SHAPES_SEG = [
     (2, 224, 224, 64, 0, 64, "conv3r_kernel<s2,64>"),      # enc1.c2 / VGG conv1_2 at 224
     (2, 112, 112, 64, 0, 128, "conv3r_kernel<s2,128>"),    # enc2.c1 / conv2_1 (4th segment half out)
     (2, 56, 56, 128, 0, 256, "conv3r_kernel<s2,128>"),     # enc3.c1 / conv3_1
-    (2, 28, 28, 256, 0, 512, "conv3r_kernel<s2,128>"),     # bottleneck / conv4_1 (partial band)
-    (2, 14, 14, 512, 0, 512, "conv3r_kernel<s1,128>"),     # VGG conv5_x
+    (2, 28, 28, 256, 0, 512, "conv3r_kernel<s2,128,w8>"),  # bottleneck / conv4_1 (partial band)
+    (2, 14, 14, 512, 0, 512, "conv3r_kernel<s1,128,w8>"),  # VGG conv5_x (8-wave, W <= 28)
     (4, 14, 14, 64, 0, 64, "conv3r_kernel<s1,64>"),
     (3, 36, 52, 64, 64, 128, "conv3r_kernel<s2,128>"),     # odd sizes, concat input
     (2, 60, 60, 64, 0, 64, "conv3r_kernel<s2,64>"),        # partial bands of 16 rows
@@ -243,10 +243,17 @@ SHAPES_SEG = [
 def _seg_rows(n, h, w, co, name):
     sg = int(name.split("<s")[1][0])
     bc = int(name.split(",")[1].rstrip(">"))
-    nw = 64 if sg == 2 else 32
-    wp = 4 // (bc // nw)
+    w8 = ",w8" in name                          # RR_CONV3R_SEGWG=8: 8-wave workgroups
+    nw = 64 if (sg == 2 and (bc == 128 or not w8)) else 32
+    wp = (8 if w8 else 4) // (bc // nw)
     tr = wp * (8 // sg)
     return n * -(-w // (16 * sg)) * -(-h // tr) * wp
+
+
+def _seg_name_ok(got, name):
+    # RR_CONV3R_SEGWG=4 / 8 in the environment switch the workgroup kind
+    base = name.replace(",w8", "")
+    return got in (base, base[:-1] + ",w8>")
 
 
 @pytest.mark.parametrize("shape", SHAPES_SEG)
@@ -255,7 +262,8 @@ def test_conv3r_seg_fwd_bias_stats_relu(dev, shape, monkeypatch):
     from roadrestore._lib import RR_CONV3X3
     n, h, w, c1, c2, co, name = shape
     monkeypatch.setenv("RR_CONV3R", "1")
-    assert rr.ops.igemm_kernel_name(_desc(n, w, c1, c2, co, bias=1, stats=1, h=h)) == name
+    name_got = rr.ops.igemm_kernel_name(_desc(n, w, c1, c2, co, bias=1, stats=1, h=h))
+    assert _seg_name_ok(name_got, name), name_got
     cin = c1 + c2
     x = rnd(n, cin, h, w, seed=1).bfloat16().float()
     wt = (rnd(co, cin, 3, 3, seed=2) / (3 * cin ** 0.5)).bfloat16().float()
@@ -272,7 +280,7 @@ def test_conv3r_seg_fwd_bias_stats_relu(dev, shape, monkeypatch):
         torch.cuda.synchronize()
         outs[tag] = (nchw(y), st.double().sum(0).cpu(), nchw(yr), st.shape[0])
     y, s, yr, rows = outs["1"]
-    assert rows == _seg_rows(n, h, w, co, name)
+    assert rows == _seg_rows(n, h, w, co, name_got)
     ref = pre + b[None, :, None, None]
     assert rel(y, ref) < 4e-3
     assert rel(yr, F.relu(ref)) < 4e-3

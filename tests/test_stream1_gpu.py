@@ -148,7 +148,12 @@ def test_stream1_final_conv_nchw(dev, small_ok, shape):
     assert (y.cpu() - ref).abs().max().item() < 1e-4 * max(1.0, ref.abs().max().item())
 
 
-@pytest.mark.parametrize("shape", SHAPES)
+# the reference's 224-pipeline maps (14:202-205: 28 / 56 / 112 / 224) are not
+# powers of two: image / row / column of a coarse pixel by invariant division
+SHAPES_NP2 = [(8, 14, 14), (3, 28, 28), (2, 28, 56)]
+
+
+@pytest.mark.parametrize("shape", SHAPES + SHAPES_NP2)
 @pytest.mark.parametrize("cin,cout", [(64, 64), (128, 64), (256, 128)])
 def test_stream1_convT(dev, small_ok, shape, cin, cout, monkeypatch):
     """ConvTranspose2d(cin, cout, 2, stride=2) fwd (scatter by GEMM column)
