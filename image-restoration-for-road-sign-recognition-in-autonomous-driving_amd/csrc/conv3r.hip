@@ -521,50 +521,92 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     for (int m = 0; m < NM; ++m) bv[m] = *reinterpret_cast<const f32x4 *>(lbias + cb + m * 16 + fq * 4);
     const int ld1 = a.split > 0 ? a.split : a.cout;
     const int ld2 = a.cout - a.split;
+    // rr_igemm_ex RR_ACT_POOL: the 2x2 max-pool of the activated output
+    // (MaxPool2d(2, 2) after an encoder block / a VGG conv+ReLU, floor
+    // sizes) to a.ypool [n][h/2][w/2][c_out]; RR_ACT_NOFULL: only that.
+    // Rows are finished in pairs (o, o + 1: a wave's first row is even), the
+    // column pair is lane frow ^ 1 (same 8 channels after the swap)
+    const bool pool = (a.act & RR_ACT_POOL) != 0, full = (a.act & RR_ACT_NOFULL) == 0;
+    const int ph = a.h >> 1, pw = a.w >> 1;
 #pragma unroll
-    for (int o = 0; o < R; ++o)
+    for (int o2 = 0; o2 < R; o2 += 2)
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        const long long p = pix_at(o, s);
 #pragma unroll
         for (int pp = 0; pp < NM / 2; ++pp) {
-          f32x4 va = acc[o][s][2 * pp] + bv[2 * pp], vb = acc[o][s][2 * pp + 1] + bv[2 * pp + 1];
-          swap_pair(va, vb);
-          if (G::SEGM && p < 0) continue;
-          const int c = c0 + cb + 32 * pp + coff;
-          const bool second = a.split > 0 && c >= a.split;      // uniform per pair (split % 32 == 0)
-          bf16_t *dst = second ? reinterpret_cast<bf16_t *>(a.y2) + p * ld2 + (c - a.split)
-                               : reinterpret_cast<bf16_t *>(a.y1) + p * ld1 + c;
-          if (a.accumulate) {
-            va += load4<bf16_t>(dst);
-            vb += load4<bf16_t>(dst + 4);
-          }
-          if (a.res) {                                   // (rr_igemm_ex: y1's layout, no split)
-            const bf16_t *rp = reinterpret_cast<const bf16_t *>(a.res) + p * ld1 + c;
-            va += load4<bf16_t>(rp);
-            vb += load4<bf16_t>(rp + 4);
-          }
-          if ((a.act & 3) == RR_ACT_RELU) {
+          f32x4 fin[2][2];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) { va[j] = fmaxf(va[j], 0.f); vb[j] = fmaxf(vb[j], 0.f); }
-          } else if ((a.act & 3) == RR_ACT_PRELU) {
-            const float al = a.alpha[0];
+          for (int t = 0; t < 2; ++t) {
+            const int o = o2 + t;
+            const long long p = pix_at(o, s);
+            f32x4 va = acc[o][s][2 * pp] + bv[2 * pp], vb = acc[o][s][2 * pp + 1] + bv[2 * pp + 1];
+            swap_pair(va, vb);
+            fin[t][0] = va;
+            fin[t][1] = vb;
+            if (G::SEGM && p < 0) continue;
+            const int c = c0 + cb + 32 * pp + coff;
+            const bool second = a.split > 0 && c >= a.split;      // uniform per pair (split % 32 == 0)
+            bf16_t *dst = second ? reinterpret_cast<bf16_t *>(a.y2) + p * ld2 + (c - a.split)
+                                 : reinterpret_cast<bf16_t *>(a.y1) + p * ld1 + c;
+            if (a.accumulate) {
+              va += load4<bf16_t>(dst);
+              vb += load4<bf16_t>(dst + 4);
+            }
+            if (a.res) {                                   // (rr_igemm_ex: y1's layout, no split)
+              const bf16_t *rp = reinterpret_cast<const bf16_t *>(a.res) + p * ld1 + c;
+              va += load4<bf16_t>(rp);
+              vb += load4<bf16_t>(rp + 4);
+            }
+            if ((a.act & 3) == RR_ACT_RELU) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) { va[j] = fmaxf(va[j], 0.f); vb[j] = fmaxf(vb[j], 0.f); }
+            } else if ((a.act & 3) == RR_ACT_PRELU) {
+              const float al = a.alpha[0];
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                va[j] = va[j] > 0.f ? va[j] : al * va[j];
+                vb[j] = vb[j] > 0.f ? vb[j] : al * vb[j];
+              }
+            }
+            if (a.has_mask) {
+              const bf16_t *mp = reinterpret_cast<const bf16_t *>(a.mask) + p * ld1 + c;
+              const f32x4 ma = load4<bf16_t>(mp), mb = load4<bf16_t>(mp + 4);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                va[j] = ma[j] > 0.f ? va[j] : 0.f;
+                vb[j] = mb[j] > 0.f ? vb[j] : 0.f;
+              }
+            }
+            fin[t][0] = va;
+            fin[t][1] = vb;
+            if (full) store8<bf16_t>(dst, va, vb);
+          }
+          if (pool) {
+            // vertical max, then the column pair (every lane shuffles)
+            f32x4 m0, m1;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              va[j] = va[j] > 0.f ? va[j] : al * va[j];
-              vb[j] = vb[j] > 0.f ? vb[j] : al * vb[j];
+              m0[j] = fmaxf(fin[0][0][j], fin[1][0][j]);
+              m1[j] = fmaxf(fin[0][1][j], fin[1][1][j]);
             }
-          }
-          if (a.has_mask) {
-            const bf16_t *mp = reinterpret_cast<const bf16_t *>(a.mask) + p * ld1 + c;
-            const f32x4 ma = load4<bf16_t>(mp), mb = load4<bf16_t>(mp + 4);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              va[j] = ma[j] > 0.f ? va[j] : 0.f;
-              vb[j] = mb[j] > 0.f ? vb[j] : 0.f;
+              m0[j] = fmaxf(m0[j], __shfl_xor(m0[j], 1, 64));
+              m1[j] = fmaxf(m1[j], __shfl_xor(m1[j], 1, 64));
+            }
+            const long long p = pix_at(o2, s);            // the window's top-left pixel
+            if ((frow & 1) == 0 && (!G::SEGM || p >= 0)) {
+              const int n = (int)(p / ((long long)a.h * a.w));
+              const int rem = (int)(p - (long long)n * a.h * a.w);
+              const int y = rem / a.w, x = rem - (rem / a.w) * a.w;
+              if (y + 1 < a.h && x + 1 < a.w) {             // (floor: a last odd row / column drops)
+                const int c = c0 + cb + 32 * pp + coff;
+                bf16_t *q = reinterpret_cast<bf16_t *>(a.ypool) +
+                            (((long long)n * ph + (y >> 1)) * pw + (x >> 1)) * a.cout + c;
+                store8<bf16_t>(q, m0, m1);
+              }
             }
           }
-          store8<bf16_t>(dst, va, vb);
         }
       }
     return;

@@ -1237,6 +1237,7 @@ static int fill_args(const rr_igemm_desc *d, const void *x1, const void *x2, con
   a.bpart = a.bapart = nullptr;
   a.alpha = nullptr;
   a.res = nullptr;
+  a.ypool = nullptr;
   return RR_OK;
 }
 
@@ -1309,13 +1310,19 @@ extern "C" int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
 
 extern "C" int rr_igemm_ex(const rr_igemm_desc *d, const void *x1, const void *x2, const void *w,
                            const float *bias, const float *alpha, const void *res, void *y1,
-                           const void *mask, float *stats_partial, rr_stream stream) {
-  if (!d || d->act < 0 || d->act > (RR_ACT_PRELU | RR_ACT_RES) || (d->act & 3) == 3) return RR_EINVAL;
+                           void *y_pool, const void *mask, float *stats_partial, rr_stream stream) {
+  const int all = RR_ACT_RELU | RR_ACT_PRELU | RR_ACT_RES | RR_ACT_POOL | RR_ACT_NOFULL;
+  if (!d || d->act < 0 || (d->act & ~all) || (d->act & 3) == 3) return RR_EINVAL;
   if ((d->act & 3) == RR_ACT_PRELU && !alpha) return RR_EINVAL;
   if ((d->act & RR_ACT_RES) && (!res || d->out_split || d->accumulate || d->out_nchw)) return RR_EINVAL;
+  if ((d->act & RR_ACT_POOL) && (!y_pool || d->out_split || d->h < 2 || d->w < 2)) return RR_EINVAL;
+  if ((d->act & RR_ACT_NOFULL) && (!(d->act & RR_ACT_POOL) || d->accumulate || d->want_stats))
+    return RR_EINVAL;
   if (d->act > RR_ACT_RELU && !conv3r_bc(d)) return RR_EUNSUPPORTED;
+  // (y1 unused with RR_ACT_NOFULL: fill_args wants a pointer)
+  void *y1a = (d->act & RR_ACT_NOFULL) ? y_pool : y1;
   IgemmArgs a;
-  const int rc = fill_args(d, x1, x2, w, bias, y1, nullptr, mask, stats_partial, a);
+  const int rc = fill_args(d, x1, x2, w, bias, y1a, nullptr, mask, stats_partial, a);
   if (rc) return rc;
   if (d->act <= RR_ACT_RELU) {
     rr_igemm_desc d2 = *d;
@@ -1323,6 +1330,7 @@ extern "C" int rr_igemm_ex(const rr_igemm_desc *d, const void *x1, const void *x
   }
   a.alpha = alpha;
   a.res = (const char *)res;
+  a.ypool = (char *)y_pool;
   return conv3r_launch(d, a, (hipStream_t)stream);
 }
 

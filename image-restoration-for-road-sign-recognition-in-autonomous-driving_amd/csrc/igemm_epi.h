@@ -32,6 +32,7 @@ struct IgemmArgs {
   // RR_ACT_PRELU), residual added before the activation (act & RR_ACT_RES)
   const float *alpha;
   const char *res;
+  char *ypool;        // act & RR_ACT_POOL: [n][h/2][w/2][c_out] 2x2 max-pool of the output
 };
 
 namespace {

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("RR_LIB_PATH") or os.path.join(_HERE, "libroadrestore.
 
 RR_F32, RR_BF16 = 0, 1
 RR_CONV3X3, RR_CONV1X1, RR_CONVT_UP, RR_CONVT_DOWN = 0, 1, 2, 3
-RR_ACT_NONE, RR_ACT_RELU, RR_ACT_PRELU, RR_ACT_RES = 0, 1, 2, 4
+RR_ACT_NONE, RR_ACT_RELU, RR_ACT_PRELU, RR_ACT_RES, RR_ACT_POOL, RR_ACT_NOFULL = 0, 1, 2, 4, 8, 16
 
 _STATUS = {0: "ok", -1: "EINVAL", -2: "EUNSUPPORTED", -3: "ELAUNCH", -4: "EWORKSPACE"}
 RR_EUNSUPPORTED = -2
@@ -71,7 +71,7 @@ S_ = C.c_size_t
 # name -> (restype, argtypes)
 _SIGS = {
     "rr_igemm": (I_, [C.POINTER(IgemmDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_]),
-    "rr_igemm_ex": (I_, [C.POINTER(IgemmDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_, P_]),
+    "rr_igemm_ex": (I_, [C.POINTER(IgemmDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_, P_, P_]),
     "rr_igemm_stat_blocks": (I_, [C.POINTER(IgemmDesc)]),
     "rr_igemm_kernel_name": (C.c_char_p, [C.POINTER(IgemmDesc), I_]),
     "rr_wgrad_kernel_name": (C.c_char_p, [C.POINTER(WgradDesc)]),

@@ -394,12 +394,23 @@ def resblock_forward_eval_folded(blk, x1, x2, n, h, w, wc, dt, pool=False):
         t1, _, _ = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, pk1, cout, bias=b1)
         a1 = ops.affine_act(t1, one, zero, alpha=pr.weight)
     pk2, b2 = wc.conv_bn_folded(c2, bn2, dt)
+    S = Bag(x1=x1, x2=x2, n=n, h=h, w=w)
+    pl = ops.RR_ACT_POOL if pool else 0
     if not block_has_shortcut(blk) and x2 is None and \
-            _ex_fusable(a1.dtype, n, h, w, cout, 0, cout, RELU | ops.RR_ACT_RES):
-        # identity shortcut: relu(conv2'(a1) + x) in conv2's epilogue
-        out, _, _ = ops.igemm(RR_CONV3X3, a1, None, n, h, w, pk2, cout, bias=b2, res=x1, act=RELU)
-        S = Bag(x1=x1, x2=x2, n=n, h=h, w=w)
-        return (out, S, ops.maxpool2_fwd(out)) if pool else (out, S)
+            _ex_fusable(a1.dtype, n, h, w, cout, 0, cout, RELU | ops.RR_ACT_RES | pl):
+        # identity shortcut: relu(conv2'(a1) + x) in conv2's epilogue (+ the
+        # encoder's MaxPool2d: no index, nothing runs backward)
+        out, pooled, _ = ops.igemm(RR_CONV3X3, a1, None, n, h, w, pk2, cout, bias=b2, res=x1,
+                                   act=RELU, pool=pool)
+        return (out, S, (pooled, None)) if pool else (out, S)
+    if block_has_shortcut(blk) and pool and _ex_fusable(a1.dtype, n, h, w, cout, 0, cout, RELU | pl):
+        # the shortcut first, then conv2 accumulates onto it with the ReLU and
+        # the max-pool in its epilogue (relu(sc'(x) + conv2'(a1)))
+        pks, bs = wc.conv_bn_folded(blk.shortcut[0], blk.shortcut[1], dt)
+        out, _, _ = ops.igemm(RR_CONV1X1, x1, x2, n, h, w, pks, cout, bias=bs)
+        _, pooled, _ = ops.igemm(RR_CONV3X3, a1, None, n, h, w, pk2, cout, bias=b2, out=out,
+                                 accumulate=True, act=RELU, pool=True)
+        return out, S, (pooled, None)
     t2, _, _ = ops.igemm(RR_CONV3X3, a1, None, n, h, w, pk2, cout, bias=b2)
     if block_has_shortcut(blk):
         pks, bs = wc.conv_bn_folded(blk.shortcut[0], blk.shortcut[1], dt)
@@ -409,7 +420,6 @@ def resblock_forward_eval_folded(blk, x1, x2, n, h, w, wc, dt, pool=False):
         if x2 is not None:
             raise RuntimeError("identity shortcut with a concatenated input")
         out = ops.affine_act(t2, one, zero, res=x1, relu=True)
-    S = Bag(x1=x1, x2=x2, n=n, h=h, w=w)
     if pool:
         return out, S, ops.maxpool2_fwd(out)
     return out, S
@@ -781,9 +791,28 @@ def vgg_features_forward(features, x, wc, dt, upto=None, need_bwd=False):
     S = Bag(n=n, H=H, W=W, acts=[], layers=layers)
     h, w = H, W
     cur = None
+    skip_pool = False
     for li, (kind, mod) in enumerate(layers):
+        if skip_pool:                    # (its max-pool ran in the conv's epilogue)
+            skip_pool = False
+            h, w = h // 2, w // 2
+            continue
         if kind in ("conv", "conv_relu"):
             act = RELU if kind == "conv_relu" else 0
+            nxt_pool = li + 1 < len(layers) and layers[li + 1][0] == "pool"
+            if cur is not None and not need_bwd and nxt_pool and \
+                    _ex_fusable(cur.dtype, n, h, w, cur.shape[-1], 0, mod.weight.shape[0],
+                                act | ops.RR_ACT_POOL | ops.RR_ACT_NOFULL):
+                # no backward (the judge, the perceptual target): conv + ReLU +
+                # MaxPool2d in one pass, the full-size map never written
+                pk = wc.conv(mod.weight, dt, dgrad=False)
+                _, y, _ = ops.igemm(RR_CONV3X3, cur, None, n, h, w, pk[0], mod.weight.shape[0],
+                                    bias=mod.bias, act=act, pool_only=True)
+                S.acts.append((kind, mod, cur, pk, h, w, None))
+                S.acts.append(("pool", layers[li + 1][1], None, None, h, w, None))
+                cur = y
+                skip_pool = True
+                continue
             if cur is None:
                 y, _ = ops.first_conv_fwd(x, mod.weight, mod.bias, dt,
                                           wc.conv_in(mod.weight, mod.bias, dt), act=act)

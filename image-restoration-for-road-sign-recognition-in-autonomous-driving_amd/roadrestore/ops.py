@@ -12,7 +12,7 @@ import ctypes as C
 
 import torch
 
-from ._lib import (RR_ACT_PRELU, RR_ACT_RES, RR_BF16, RR_F32, RR_CONV1X1, RR_CONV3X3,
+from ._lib import (RR_ACT_NOFULL, RR_ACT_POOL, RR_ACT_PRELU, RR_ACT_RES, RR_BF16, RR_F32, RR_CONV1X1, RR_CONV3X3,
                    RR_CONVT_DOWN, RR_CONVT_UP, RR_DISTORT_KMAX, BnBwdDesc, DistortParam, IgemmDesc, PackJob, WgradDesc, lib)
 
 __all__ = [
@@ -162,9 +162,13 @@ def bias_tile4(b: torch.Tensor):
 # implicit GEMM
 
 def igemm(mode, x1, x2, n, h, w, wpack, cout, bias=None, act=0, out=None, out2=None,
-          split=0, accumulate=False, mask=None, stats=False, out_nchw=False, alpha=None, res=None):
-    """Run rr_igemm (rr_igemm_ex with ``alpha`` -- act RR_ACT_PRELU -- or
-    ``res``, added before the activation).  Returns (y1, y2, stats_partial_or_None).
+          split=0, accumulate=False, mask=None, stats=False, out_nchw=False, alpha=None, res=None,
+          pool=False, pool_only=False):
+    """Run rr_igemm (rr_igemm_ex with ``alpha`` -- act RR_ACT_PRELU --,
+    ``res`` added before the activation, or ``pool`` / ``pool_only``: the
+    2x2 max-pool of the result).  Returns (y1, y2, stats_partial_or_None);
+    with ``pool`` y2 is the pooled [n, h/2, w/2, cout] tensor (y1 None with
+    ``pool_only``).
 
     mode RR_CONV3X3 / RR_CONV1X1: y [n, h, w, cout]
     mode RR_CONVT_UP: GEMM columns 4*cout_t, y [n, 2h, 2w, cout/4]
@@ -174,15 +178,24 @@ def igemm(mode, x1, x2, n, h, w, wpack, cout, bias=None, act=0, out=None, out2=N
     dt = x1.dtype
     c1 = x1.shape[-1]
     c2 = x2.shape[-1] if x2 is not None else 0
-    ex = alpha is not None or res is not None
+    pool = pool or pool_only
+    ex = alpha is not None or res is not None or pool
     if alpha is not None:
         act = RR_ACT_PRELU
     if res is not None:
         act |= RR_ACT_RES
+    if pool:
+        act |= RR_ACT_POOL | (RR_ACT_NOFULL if pool_only else 0)
     d = IgemmDesc(rr_dtype(dt), mode, n, h, w, c1, c2, cout, split, act, int(accumulate),
                   int(bias is not None), int(mask is not None), int(stats), int(out_nchw))
     dev = x1.device
-    if out is None:
+    if pool:
+        if split or out2 is not None:
+            raise ValueError("pool: no split output")
+        out2 = torch.empty((n, h // 2, w // 2, cout), dtype=dt, device=dev)
+    if out is None and pool_only:
+        pass
+    elif out is None:
         if out_nchw:
             out = torch.empty((n, cout, h, w), dtype=torch.float32, device=dev)
         elif mode == RR_CONVT_UP:
@@ -200,8 +213,8 @@ def igemm(mode, x1, x2, n, h, w, wpack, cout, bias=None, act=0, out=None, out2=N
     def launch():
         if ex:
             lib().check(lib().rr_igemm_ex(C.byref(d), _p(x1), _p(x2), _p(wpack), _p(bias),
-                                          _p(alpha), _p(res), _p(out), _p(mask), _p(st), stream()),
-                        "rr_igemm_ex")
+                                          _p(alpha), _p(res), _p(out), _p(out2) if pool else None,
+                                          _p(mask), _p(st), stream()), "rr_igemm_ex")
         else:
             lib().check(lib().rr_igemm(C.byref(d), _p(x1), _p(x2), _p(wpack), _p(bias), _p(out),
                                        _p(out2), _p(mask), _p(st), stream()), "rr_igemm")

@@ -51,8 +51,13 @@ enum rr_igemm_mode {
 };
 
 enum rr_act { RR_ACT_NONE = 0, RR_ACT_RELU = 1, RR_ACT_PRELU = 2 };
-/* act flag (rr_igemm_ex): res[p, c] (y's layout) added before the activation */
+/* act flags (rr_igemm_ex): res[p, c] (y's layout) added before the
+ * activation; the 2x2 max-pool of the final output also written to y_pool
+ * [n][h/2][w/2][c_out] (nn.MaxPool2d(2) after it, floor sizes); NOFULL: only
+ * the pooled output (y1 not written) */
 #define RR_ACT_RES 4
+#define RR_ACT_POOL 8
+#define RR_ACT_NOFULL 16
 
 /*
  * Implicit-GEMM convolution: y[p, c] = sum_k W[c, k] * X[p, k] (+ epilogue).
@@ -89,13 +94,15 @@ int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
  *   act & 3 == RR_ACT_PRELU: y = PReLU_alpha(conv + bias), alpha[0] the
  *     single nn.PReLU() weight (conv_block[2]);
  *   act & RR_ACT_RES: res[p, c] (y1's layout) added before the activation --
- *     the identity shortcut's relu(conv2(a1) + x).
+ *     the identity shortcut's relu(conv2(a1) + x);
+ *   act & RR_ACT_POOL (+ RR_ACT_NOFULL): the encoder's / VGG's 2x2 max-pool
+ *     of the result (14:127-131, torchvision vgg16 features) to y_pool.
  * bf16 3x3 convs the tap-reuse kernel takes (rr_igemm_kernel_name reports
  * "conv3r_kernel<...>" for the descriptor); no split / accumulate / NCHW
  * output with these flags.  Other descriptors: RR_EUNSUPPORTED. */
 int rr_igemm_ex(const rr_igemm_desc *d, const void *x1, const void *x2, const void *w,
                 const float *bias, const float *alpha, const void *res, void *y1,
-                const void *mask, float *stats_partial, rr_stream stream);
+                void *y_pool, const void *mask, float *stats_partial, rr_stream stream);
 /* number of row blocks the partial stats buffer holds: [blocks][c_out][2] */
 int rr_igemm_stat_blocks(const rr_igemm_desc *d);
 /* The kernel rr_igemm (bnbwd = 0) or rr_igemm_bnbwd (bnbwd = 1) launches for

@@ -434,3 +434,37 @@ def test_conv3r_ex_prelu_and_residual(dev, shape, monkeypatch):
     import ctypes as C
     d = _desc(n, w, c1, c2, co, act=RR_ACT_PRELU | RR_ACT_RES, h=h)
     assert lib().rr_igemm(C.byref(d), None, None, None, None, None, None, None, None, None) != 0
+
+
+@pytest.mark.parametrize("shape", [(2, 224, 224, 64, 0, 64), (2, 56, 56, 128, 0, 256), (3, 28, 28, 256, 0, 512),
+                                   (2, 14, 14, 512, 0, 512), (4, 16, 16, 256, 0, 256), (8, 8, 8, 256, 0, 512),
+                                   (2, 32, 32, 128, 0, 128), (3, 36, 52, 64, 64, 128), (2, 30, 22, 128, 0, 128)])
+def test_conv3r_ex_pool(dev, shape, monkeypatch):
+    """rr_igemm_ex RR_ACT_POOL: conv + bias + ReLU (+ residual) with the 2x2
+    max-pool (MaxPool2d(2), floor sizes; the encoder's 14:127-131 and the VGG
+    judge's pools) written from the epilogue, with and without the full-size
+    output, vs fp32 torch on bf16-exact inputs"""
+    from roadrestore import ops
+    from roadrestore._lib import RR_CONV3X3
+    monkeypatch.setenv("RR_CONV3R", "1")
+    n, h, w, c1, c2, co = shape
+    cin = c1 + c2
+    x = rnd(n, cin, h, w, seed=71).bfloat16().float()
+    wt = (rnd(co, cin, 3, 3, seed=72) / (3 * cin ** 0.5)).bfloat16().float()
+    b = rnd(co, seed=73) * 0.3
+    r = rnd(n, co, h, w, seed=74).bfloat16().float()
+    pre = F.conv2d(x, wt, b, padding=1)
+    wf, _ = ops.pack_conv(wt.to(dev), BF)
+    x1 = nhwc(x[:, :c1], dev)
+    x2 = nhwc(x[:, c1:], dev) if c2 else None
+    y, yp, _ = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf, co, bias=b.to(dev), act=1, pool=True)
+    ref = F.relu(pre)
+    assert rel(nchw(y), ref) < 4e-3
+    # the pool of the rounded output equals the rounded pool (rounding is monotone)
+    assert torch.equal(nchw(yp), F.max_pool2d(nchw(y), 2))
+    y0, yp0, _ = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf, co, bias=b.to(dev), act=1, pool_only=True)
+    assert y0 is None and torch.equal(yp0, yp)
+    y, yp, _ = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf, co, bias=b.to(dev), act=1, res=nhwc(r, dev),
+                         pool=True)
+    assert rel(nchw(y), F.relu(pre + r)) < 4e-3
+    assert torch.equal(nchw(yp), F.max_pool2d(nchw(y), 2))
