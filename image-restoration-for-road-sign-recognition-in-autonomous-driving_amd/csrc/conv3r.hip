@@ -265,6 +265,11 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   // DMA in the K loop, bit3 no MFMAs, bit0 no epilogue, bit4 no weight DMA,
   // bit5 no halo DMA
   const bool dbg_nodma = (a.dbg & 4) != 0, dbg_nomfma = (a.dbg & 8) != 0;
+  // every row's MFMA cluster at wave priority 1 (cdna_hip_programming.md
+  // T5): +3.3-3.5 % on both layer sets (profiles/r3aa_ab*.jsonl; the static
+  // form -- the younger half of the workgroup at priority 1 for the whole
+  // loop -- +1 % / -3 %).  RR_IGEMM_DBG bit7 turns it off (A/B)
+  const bool prio_mfma = (a.dbg & 128) == 0;
   for (int st = 0; st < nst; ++st) {
     const int ch = st / 3, dx = st - ch * 3;       // uniform
     // operands of the next stage (weights) and of the next chunk (halo)
@@ -323,6 +328,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
           if (zhi) hi = i32x4{0, 0, 0, 0};
         }
       }
+      if (prio_mfma) __builtin_amdgcn_s_setprio(1);
       if (!dbg_nomfma) {
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy) {
@@ -337,6 +343,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
                   acc[o][s][m], 0, 0, 0);
         }
       }
+      if (prio_mfma) __builtin_amdgcn_s_setprio(0);
       // the DMA for the next stage / chunk goes out behind the first rows'
       // MFMAs (issued right after the barrier, every wave of a SIMD would
       // sit in ~60-cycle issue slots before its first MFMA); the weights
