@@ -282,6 +282,7 @@ struct Halo3Args {
   int split_stages;        // stages per split
   int nablk, nbblk;
   int xcd;                 // XCD-aware workgroup order (RR_XCD_MAP)
+  int prio;                // wave priority 1 around the MFMA clusters (RR_MFMA_PRIO=0: off)
 };
 
 template <int W>
@@ -408,11 +409,13 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
           fb[j] = tr_frag(sB + (hr0 + toff) * RS + col * 2 + pp * 8,
                           sB + (hr1 + toff) * RS + col * 2 + pp * 8);
         }
+        if (a.prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
             acc[i][j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j][t], 0, 0, 0);
+        if (a.prio) __builtin_amdgcn_s_setprio(0);
       }
     }
     if (s + 1 < nst) swrite(buf ^ 1);
@@ -703,6 +706,10 @@ extern "C" int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
     ha.stages = hp.stages; ha.split_stages = hp.split_stages;
     ha.nablk = ha.CA / 64; ha.nbblk = ha.CB / 64;
     ha.xcd = a.xcd;
+    {
+      const char *pe = getenv("RR_MFMA_PRIO");
+      ha.prio = !(pe && atoi(pe) == 0);
+    }
     const dim3 grid((unsigned)(ha.nablk * ha.nbblk * hp.nsplit)), block(256);
     switch (d->w) {
       case 64: hipLaunchKernelGGL(wgrad3_halo_kernel<64>, grid, block, 0, st, ha); break;
