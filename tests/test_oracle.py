@@ -78,7 +78,10 @@ def test_vgg16_oracle_logits(H):
     assert torch.equal(x, torch.from_numpy(z["x"]))
     with torch.no_grad():
         lg = R.vgg16_forward(sd, x)
-    assert torch.equal(lg, torch.from_numpy(z["logits"]))
+    # fp32 conv accumulation order depends on the host CPU's oneDNN kernels: the golden logits
+    # (generated from the imported reference on one host) reproduce bit-for-bit there and to
+    # ~1e-6 relative on another (AVX512 EPYC: max |diff| 1.9e-5 on logits of magnitude ~14)
+    torch.testing.assert_close(lg, torch.from_numpy(z["logits"]), rtol=1e-5, atol=1e-4)
     assert np.array_equal(R.top1(lg).numpy(), z["pred"])
 
 
