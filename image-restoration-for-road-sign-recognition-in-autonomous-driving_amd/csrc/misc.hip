@@ -55,74 +55,109 @@ __global__ void pack_conv_kernel(int co_n, int ci_n, int k, const float *__restr
   }
 }
 
-// all conv packs of a network in one launch.  A work item is one (co, ci)
-// pair of one job: its k*k taps are read together (one contiguous 4k^2-byte
-// run) and written to the k*k tap rows of the pack.  Two phases over the
-// pairs: the fwd pack [co][tap][ci] with ci fastest across lanes and the dgrad
-// pack [ci][flipped tap][co] with co fastest, so every store instruction
-// writes consecutive elements (the one-element-per-thread form wrote 2-byte
-// scattered stores to both packs: 104 -> 72 us for the ResUNet's 12.4 M
-// weights, tools/bench_pack.py; two pairs per item measured slower, 164 us).
-// Pair offsets per job come from an LDS scan of c_out * c_in; a thread finds
-// its job by binary search.
+// all conv packs of a network in one launch.  A work item is one output
+// channel x 8 consecutive input channels of one job (phase 0, the fwd pack
+// [co][tap][ci] and its conv3r tiles) or one input channel x 8 consecutive
+// output channels (phase 1, the dgrad pack [ci][flipped tap][co] and its
+// tiles): the item's 8 x k*k fp32 weights are read once and every tap is
+// written as one run of 8 consecutive pack elements -- a 16-B store in bf16
+// to the row pack and to the tile pack alike (the tile's innermost 8 elements
+// are 8 consecutive channels of one row).  Lanes walk the 8-channel groups
+// fastest, so a wave's row stores are contiguous.  (The (co, ci)-pair items
+// before wrote 2-byte stores: 98 us and 423 MB of HBM traffic per launch for
+// the 12.4 M ResUNet weights with their tiles, profiles/r3r_pmc_traffic.json,
+// against ~150 MB algorithmic.)  Channel counts that are not a multiple of 8
+// leave a partial last group, written element by element.  Item offsets per
+// job come from LDS scans; a thread finds its job by binary search.
 constexpr int PACKB_MAX = 256;
+template <typename T, int KK>
+__device__ __forceinline__ void pack_group(const rr_pack_job &jb, int phase, long long q, bool tiled) {
+  constexpr int k = KK == 9 ? 3 : 1;
+  const long long tot = (long long)jb.c_out * jb.c_in * KK;
+  const int cg = phase == 0 ? jb.c_in : jb.c_out;     // the grouped (contiguous in the pack) channel
+  const int ng = (cg + 7) >> 3;
+  const int g0 = (int)(q % ng) * 8, r = (int)(q / ng);
+  const int n = cg - g0 < 8 ? cg - g0 : 8;
+  float v[8][KK];
+  if (phase == 0) {
+    // w[r][g0 + e][tp]: n * KK contiguous floats
+    const float *src = jb.w + ((long long)r * jb.c_in + g0) * KK;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int tp = 0; tp < KK; ++tp) v[e][tp] = src[(e < n ? e : 0) * KK + tp];
+  } else {
+    // w[g0 + e][r][tp]: n runs of KK floats, c_in * KK apart
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float *src = jb.w + ((long long)(g0 + (e < n ? e : 0)) * jb.c_in + r) * KK;
+#pragma unroll
+      for (int tp = 0; tp < KK; ++tp) v[e][tp] = src[tp];
+    }
+  }
+  T *rows = (T *)(phase == 0 ? jb.w_fwd : jb.w_dgrad);
+#pragma unroll
+  for (int tp = 0; tp < KK; ++tp) {
+    const int ky = tp / k, kx = tp - ky * k;
+    // phase 0: row (r = co, tap tp); phase 1: row (r = ci, flipped tap)
+    const int tr = phase == 0 ? tp : (k - 1 - ky) * k + (k - 1 - kx);
+    const long long ro = ((long long)r * KK + tr) * cg + g0;
+    const long long to = tiled ? (phase == 0 ? r3_tile_off(jb.c_out, r, g0, ky, kx)
+                                             : r3_tile_off(jb.c_in, r, g0, 2 - ky, 2 - kx))
+                               : 0;
+    if (n == 8 && (cg & 7) == 0) {                   // 16-B aligned runs
+      store8<T>(rows + ro, f32x4{v[0][tp], v[1][tp], v[2][tp], v[3][tp]},
+                f32x4{v[4][tp], v[5][tp], v[6][tp], v[7][tp]});
+      if (tiled)
+        store8<T>(rows + tot + to, f32x4{v[0][tp], v[1][tp], v[2][tp], v[3][tp]},
+                  f32x4{v[4][tp], v[5][tp], v[6][tp], v[7][tp]});
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (e < n) Elt<T>::store(rows, ro + e, v[e][tp]);
+    }
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void pack_conv_batch_kernel(int count, const rr_pack_job *__restrict__ jobs,
                                                               long long total) {
-  __shared__ long long pb[PACKB_MAX + 1];
+  __shared__ long long pb[2][PACKB_MAX + 1];
   (void)total;
   const int t = threadIdx.x;
-  pb[t + 1] = t < count ? (long long)jobs[t].c_out * jobs[t].c_in : 0;
-  if (t == 0) pb[0] = 0;
+  if (t < count) {
+    const rr_pack_job &j = jobs[t];
+    pb[0][t + 1] = j.w_fwd ? (long long)j.c_out * ((j.c_in + 7) >> 3) : 0;
+    pb[1][t + 1] = j.w_dgrad ? (long long)j.c_in * ((j.c_out + 7) >> 3) : 0;
+  } else {
+    pb[0][t + 1] = 0;
+    pb[1][t + 1] = 0;
+  }
+  if (t == 0) { pb[0][0] = 0; pb[1][0] = 0; }
   __syncthreads();
-  for (int o = 1; o < PACKB_MAX; o <<= 1) {            // inclusive scan of pb[1..256]
-    const long long v = t >= o ? pb[t + 1 - o] : 0;
+  for (int o = 1; o < PACKB_MAX; o <<= 1) {            // inclusive scans of pb[*][1..256]
+    const long long v0 = t >= o ? pb[0][t + 1 - o] : 0, v1 = t >= o ? pb[1][t + 1 - o] : 0;
     __syncthreads();
-    pb[t + 1] += v;
+    pb[0][t + 1] += v0;
+    pb[1][t + 1] += v1;
     __syncthreads();
   }
-  const long long pairs = pb[count];
-  for (long long w = blockIdx.x * (long long)blockDim.x + t; w < 2 * pairs;
+  const long long n0 = pb[0][count], n1 = pb[1][count];
+  for (long long w = blockIdx.x * (long long)blockDim.x + t; w < n0 + n1;
        w += (long long)gridDim.x * blockDim.x) {
-    const int phase = w >= pairs;
-    const long long e = phase ? w - pairs : w;
-    int lo = 0, hi = count - 1;                         // last j with pb[j] <= e
+    const int phase = w >= n0;
+    const long long e = phase ? w - n0 : w;
+    const long long *p = pb[phase];
+    int lo = 0, hi = count - 1;                         // last j with p[j] <= e
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (pb[mid] <= e) lo = mid; else hi = mid - 1;
+      if (p[mid] <= e) lo = mid; else hi = mid - 1;
     }
     const rr_pack_job jb = jobs[lo];
-    const long long q = e - pb[lo];
-    const int k = jb.k, kk = k * k;
-    const long long tot = (long long)jb.c_out * jb.c_in * kk;
-    const bool tiled = sizeof(T) == 2 && r3_tiled(k, jb.c_out, jb.c_in);
-    if (phase == 0) {
-      if (!jb.w_fwd) continue;
-      const int ci = (int)(q % jb.c_in), co = (int)(q / jb.c_in);
-      const float *src = jb.w + ((long long)co * jb.c_in + ci) * kk;
-      T *dst = (T *)jb.w_fwd + (long long)co * kk * jb.c_in + ci;
-      for (int tp = 0; tp < kk; ++tp) Elt<T>::store(dst, (long long)tp * jb.c_in, src[tp]);
-      if (tiled) {
-        T *tl = (T *)jb.w_fwd + tot;
-        for (int tp = 0; tp < kk; ++tp)
-          Elt<T>::store(tl, r3_tile_off(jb.c_out, co, ci, tp / 3, tp % 3), src[tp]);
-      }
-    } else {
-      if (!jb.w_dgrad) continue;
-      const int co = (int)(q % jb.c_out), ci = (int)(q / jb.c_out);
-      const float *src = jb.w + ((long long)co * jb.c_in + ci) * kk;
-      T *dst = (T *)jb.w_dgrad + (long long)ci * kk * jb.c_out + co;
-      for (int tp = 0; tp < kk; ++tp) {
-        const int ky = tp / k, kx = tp - ky * k;
-        const int tf = (k - 1 - ky) * k + (k - 1 - kx);
-        Elt<T>::store(dst, (long long)tf * jb.c_out, src[tp]);
-      }
-      if (tiled) {
-        T *tl = (T *)jb.w_dgrad + tot;
-        for (int tp = 0; tp < kk; ++tp)
-          Elt<T>::store(tl, r3_tile_off(jb.c_in, ci, co, 2 - tp / 3, 2 - tp % 3), src[tp]);
-      }
-    }
+    const long long q = e - p[lo];
+    const bool tiled = sizeof(T) == 2 && r3_tiled(jb.k, jb.c_out, jb.c_in);
+    if (jb.k == 3) pack_group<T, 9>(jb, phase, q, tiled);
+    else pack_group<T, 1>(jb, phase, q, false);
   }
 }
 
@@ -1334,7 +1369,9 @@ extern "C" int rr_pack_conv_batch(int dtype, int count, const rr_pack_job *jobs,
                                   rr_stream stream) {
   if (!jobs || count <= 0 || count > PACKB_MAX || total <= 0) return RR_EINVAL;
   const char *e = getenv("RR_PACK_GRID");
-  dim3 g(rr_grid_cap((total + 255) / 256, e ? atoi(e) : 8192)), b(256);
+  // ~total / 36 items (8 channels x 9 taps each, two phases); the 1x1 jobs
+  // have 9x more per element, so size for ~total / 16 and grid-stride the rest
+  dim3 g(rr_grid_cap((total / 16 + 255) / 256, e ? atoi(e) : 8192)), b(256);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == RR_BF16)
     hipLaunchKernelGGL(pack_conv_batch_kernel<bf16_t>, g, b, 0, st, count, jobs, total);

@@ -285,8 +285,16 @@ struct Halo3Args {
   int prio;                // wave priority 1 around the MFMA clusters (RR_MFMA_PRIO=0: off)
 };
 
-template <int W>
+// MA: 16-row MFMA blocks of dy channels per wave (the wave tile is 16 MA dy
+// channels x 64 / MA x channels).  MA = 4: each wave owns all 64 dy channels
+// of the tile and 16 x channels, so per 32-pixel step it reads 4 A fragments
+// (reused over the 9 taps) and 9 B fragments -- 13 transposed fragment reads
+// per 36 MFMAs instead of the 2 x 2 tile's 20 (MA = 2): the LDS read port, at
+// ~2x the MFMA time on the 2 x 2 tile, was what bound this kernel
+template <int W, int MA>
 __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
+  constexpr int MB = 4 / MA;                   // 16-column x blocks per wave
+  constexpr int WA = 4 / MA;                   // waves along the dy channels
   constexpr int R = 64 / W;                    // image rows per stage
   constexpr int HW2 = W + 2;
   constexpr int HROWS = (R + 2) * HW2;         // halo pixel rows
@@ -303,7 +311,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wa = wv & 1, wb = wv >> 1;
+  const int wa = wv % WA, wb = wv / WA;
   int bid = xcd_order(blockIdx.x, a.xcd);
   const int ablk = bid % a.nablk; bid /= a.nablk;
   const int bblk = bid % a.nbblk; bid /= a.nbblk;
@@ -366,11 +374,11 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
     }
   };
 
-  f32x4 acc[2][2][9];
+  f32x4 acc[MA][MB][9];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MA; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < MB; ++j)
 #pragma unroll
       for (int t = 0; t < 9; ++t) acc[i][j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -390,10 +398,10 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int k0 = kk * 32 + 8 * g + q, k1 = k0 + 4;      // this lane's address rows
-      bf16x8 fa[2];
+      bf16x8 fa[MA];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int col = wa * 32 + i * 16;
+      for (int i = 0; i < MA; ++i) {
+        const int col = wa * 16 * MA + i * 16;
         fa[i] = tr_frag(sA + k0 * RS + col * 2 + pp * 8, sA + k1 * RS + col * 2 + pp * 8);
       }
       // halo rows of the pixels k0 / k1 at tap (0, 0)
@@ -402,18 +410,18 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int toff = (t / 3) * HW2 + (t % 3);
-        bf16x8 fb[2];
+        bf16x8 fb[MB];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int col = wb * 32 + j * 16;
+        for (int j = 0; j < MB; ++j) {
+          const int col = wb * 16 * MB + j * 16;
           fb[j] = tr_frag(sB + (hr0 + toff) * RS + col * 2 + pp * 8,
                           sB + (hr1 + toff) * RS + col * 2 + pp * 8);
         }
         if (a.prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < MA; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < MB; ++j)
             acc[i][j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j][t], 0, 0, 0);
         if (a.prio) __builtin_amdgcn_s_setprio(0);
       }
@@ -424,15 +432,15 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
 
   // partial[split][a][tap][b]
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MA; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int b = b0 + wb * 32 + j * 16 + gi;
+    for (int j = 0; j < MB; ++j) {
+      const int b = b0 + wb * 16 * MB + j * 16 + gi;
 #pragma unroll
       for (int t = 0; t < 9; ++t)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int ar = a0 + wa * 32 + i * 16 + g * 4 + e;
+          const int ar = a0 + wa * 16 * MA + i * 16 + g * 4 + e;
           a.partial[(((long long)split * a.CA + ar) * 9 + t) * a.CB + b] = acc[i][j][t][e];
         }
     }
@@ -711,11 +719,25 @@ extern "C" int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
       ha.prio = !(pe && atoi(pe) == 0);
     }
     const dim3 grid((unsigned)(ha.nablk * ha.nbblk * hp.nsplit)), block(256);
-    switch (d->w) {
-      case 64: hipLaunchKernelGGL(wgrad3_halo_kernel<64>, grid, block, 0, st, ha); break;
-      case 32: hipLaunchKernelGGL(wgrad3_halo_kernel<32>, grid, block, 0, st, ha); break;
-      case 16: hipLaunchKernelGGL(wgrad3_halo_kernel<16>, grid, block, 0, st, ha); break;
-      default: hipLaunchKernelGGL(wgrad3_halo_kernel<8>, grid, block, 0, st, ha); break;
+    // RR_WGRAD_HALO_MA=2: the 2 x 2 wave tiles (A/B)
+    static const int ma = [] {
+      const char *e = getenv("RR_WGRAD_HALO_MA");
+      return e && atoi(e) == 2 ? 2 : 4;
+    }();
+    if (ma == 4) {
+      switch (d->w) {
+        case 64: hipLaunchKernelGGL((wgrad3_halo_kernel<64, 4>), grid, block, 0, st, ha); break;
+        case 32: hipLaunchKernelGGL((wgrad3_halo_kernel<32, 4>), grid, block, 0, st, ha); break;
+        case 16: hipLaunchKernelGGL((wgrad3_halo_kernel<16, 4>), grid, block, 0, st, ha); break;
+        default: hipLaunchKernelGGL((wgrad3_halo_kernel<8, 4>), grid, block, 0, st, ha); break;
+      }
+    } else {
+      switch (d->w) {
+        case 64: hipLaunchKernelGGL((wgrad3_halo_kernel<64, 2>), grid, block, 0, st, ha); break;
+        case 32: hipLaunchKernelGGL((wgrad3_halo_kernel<32, 2>), grid, block, 0, st, ha); break;
+        case 16: hipLaunchKernelGGL((wgrad3_halo_kernel<16, 2>), grid, block, 0, st, ha); break;
+        default: hipLaunchKernelGGL((wgrad3_halo_kernel<8, 2>), grid, block, 0, st, ha); break;
+      }
     }
     RR_CHECK_LAUNCH();
     launch_reduce((const float *)ws, dw, ha.CA, ha.CB, 9, hp.nsplit, d->accumulate, st);

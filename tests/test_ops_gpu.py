@@ -523,7 +523,8 @@ def test_pack_conv_batch_equals_single_packs(dev, dt):
     per weight, bitwise, including 1x1 and fwd-only entries"""
     from roadrestore import ops
     shapes = [(64, 3, 3, True), (64, 64, 3, True), (128, 64, 1, True), (3, 64, 1, False),
-              (512, 256, 3, True), (7, 5, 3, False)]
+              (512, 256, 3, True), (7, 5, 3, False), (16, 12, 3, True), (128, 384, 3, True),
+              (20, 24, 1, True)]
     ws = [rnd(co, ci, k, k, seed=i).to(dev) for i, (co, ci, k, _) in enumerate(shapes)]
     pb = ops.PackBatch([(w, dt, dg) for w, (_, _, _, dg) in zip(ws, shapes)])
     outs = pb.run()
