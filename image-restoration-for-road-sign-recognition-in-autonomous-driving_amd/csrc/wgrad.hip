@@ -291,7 +291,9 @@ struct Halo3Args {
 // (reused over the 9 taps) and 9 B fragments -- 13 transposed fragment reads
 // per 36 MFMAs instead of the 2 x 2 tile's 20 (MA = 2): the LDS read port, at
 // ~2x the MFMA time on the 2 x 2 tile, was what bound this kernel
-template <int W, int MA>
+// PF: stages of global prefetch in flight (2: two register sets, a stage's
+// loads issued two compute phases before their LDS write)
+template <int W, int MA, int PF>
 __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
   constexpr int MB = 4 / MA;                   // 16-column x blocks per wave
   constexpr int WA = 4 / MA;                   // waves along the dy channels
@@ -326,8 +328,8 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
   const int hw = a.h * a.w;
 
   typedef uint4 V;
-  V ra[LA], rb[LB];
-  auto gload = [&](int st) {
+  V ra[LA], rb[LB], ra2[PF == 2 ? LA : 1], rb2[PF == 2 ? LB : 1];
+  auto gload_to = [&](int st, V *ra, V *rb) __attribute__((always_inline)) {
     const int p0 = st * 64;                    // first pixel of the stage
     const int nn = p0 / hw;
     const int h0 = (p0 - nn * hw) >> a.lw;
@@ -353,7 +355,8 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
       rb[i] = v;
     }
   };
-  auto swrite = [&](int buf) {
+  auto gload = [&](int st) __attribute__((always_inline)) { gload_to(st, ra, rb); };
+  auto swrite_from = [&](int buf, const V *ra, const V *rb) __attribute__((always_inline)) {
     char *sA = smem + buf * STAGE;
     char *sB = sA + A_BYTES;
 #pragma unroll
@@ -373,6 +376,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
       }
     }
   };
+  auto swrite = [&](int buf) __attribute__((always_inline)) { swrite_from(buf, ra, rb); };
 
   f32x4 acc[MA][MB][9];
 #pragma unroll
@@ -385,14 +389,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
   const int g = lane >> 4, gi = lane & 15;
   const int q = gi >> 2, pp = gi & 3;
   const int nst = send - sbeg;
-  if (nst > 0) {
-    gload(sbeg);
-    swrite(0);
-    __syncthreads();
-  }
-  for (int s = 0; s < nst; ++s) {
-    const int buf = s & 1;
-    if (s + 1 < nst) gload(sbeg + s + 1);
+  auto compute = [&](int buf) __attribute__((always_inline)) {
     const char *sA = smem + buf * STAGE;
     const char *sB = sA + A_BYTES;
 #pragma unroll
@@ -426,8 +423,41 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
         if (a.prio) __builtin_amdgcn_s_setprio(0);
       }
     }
-    if (s + 1 < nst) swrite(buf ^ 1);
+  };
+  if constexpr (PF == 1) {
+    if (nst > 0) {
+      gload(sbeg);
+      swrite(0);
+      __syncthreads();
+    }
+    for (int s = 0; s < nst; ++s) {
+      const int buf = s & 1;
+      if (s + 1 < nst) gload(sbeg + s + 1);
+      compute(buf);
+      if (s + 1 < nst) swrite(buf ^ 1);
+      __syncthreads();
+    }
+  } else {
+    // register set (ra2, rb2) holds the odd stages, (ra, rb) the even ones
+    if (nst > 0) {
+      gload(sbeg);
+      swrite(0);
+    }
+    if (nst > 1) gload_to(sbeg + 1, ra2, rb2);
+    if (nst > 2) gload_to(sbeg + 2, ra, rb);
     __syncthreads();
+    // stage s computes from LDS buffer s & 1 while the registers hold stages
+    // s + 1 (written to the other buffer after the MFMAs) and s + 2 (in flight)
+    auto body = [&](int s, V *xa, V *xb) __attribute__((always_inline)) {
+      compute(s & 1);
+      if (s + 1 < nst) swrite_from((s & 1) ^ 1, xa, xb);
+      if (s + 3 < nst) gload_to(sbeg + s + 3, xa, xb);
+      __syncthreads();
+    };
+    for (int s = 0; s < nst; s += 2) {
+      body(s, ra2, rb2);
+      if (s + 1 < nst) body(s + 1, ra, rb);
+    }
   }
 
   // partial[split][a][tap][b]
@@ -720,23 +750,31 @@ extern "C" int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
     }
     const dim3 grid((unsigned)(ha.nablk * ha.nbblk * hp.nsplit)), block(256);
     // RR_WGRAD_HALO_MA=2: the 2 x 2 wave tiles (A/B)
-    static const int ma = [] {
-      const char *e = getenv("RR_WGRAD_HALO_MA");
-      return e && atoi(e) == 2 ? 2 : 4;
-    }();
-    if (ma == 4) {
+    const char *mae = getenv("RR_WGRAD_HALO_MA");
+    const int ma = mae && atoi(mae) == 2 ? 2 : 4;
+    // RR_WGRAD_HALO_PF=1: one stage of global prefetch (A/B)
+    const char *pfe = getenv("RR_WGRAD_HALO_PF");
+    const int pf = pfe && atoi(pfe) == 1 ? 1 : 2;
+    if (ma == 4 && pf == 2) {
       switch (d->w) {
-        case 64: hipLaunchKernelGGL((wgrad3_halo_kernel<64, 4>), grid, block, 0, st, ha); break;
-        case 32: hipLaunchKernelGGL((wgrad3_halo_kernel<32, 4>), grid, block, 0, st, ha); break;
-        case 16: hipLaunchKernelGGL((wgrad3_halo_kernel<16, 4>), grid, block, 0, st, ha); break;
-        default: hipLaunchKernelGGL((wgrad3_halo_kernel<8, 4>), grid, block, 0, st, ha); break;
+        case 64: hipLaunchKernelGGL((wgrad3_halo_kernel<64, 4, 2>), grid, block, 0, st, ha); break;
+        case 32: hipLaunchKernelGGL((wgrad3_halo_kernel<32, 4, 2>), grid, block, 0, st, ha); break;
+        case 16: hipLaunchKernelGGL((wgrad3_halo_kernel<16, 4, 2>), grid, block, 0, st, ha); break;
+        default: hipLaunchKernelGGL((wgrad3_halo_kernel<8, 4, 2>), grid, block, 0, st, ha); break;
+      }
+    } else if (ma == 4) {
+      switch (d->w) {
+        case 64: hipLaunchKernelGGL((wgrad3_halo_kernel<64, 4, 1>), grid, block, 0, st, ha); break;
+        case 32: hipLaunchKernelGGL((wgrad3_halo_kernel<32, 4, 1>), grid, block, 0, st, ha); break;
+        case 16: hipLaunchKernelGGL((wgrad3_halo_kernel<16, 4, 1>), grid, block, 0, st, ha); break;
+        default: hipLaunchKernelGGL((wgrad3_halo_kernel<8, 4, 1>), grid, block, 0, st, ha); break;
       }
     } else {
       switch (d->w) {
-        case 64: hipLaunchKernelGGL((wgrad3_halo_kernel<64, 2>), grid, block, 0, st, ha); break;
-        case 32: hipLaunchKernelGGL((wgrad3_halo_kernel<32, 2>), grid, block, 0, st, ha); break;
-        case 16: hipLaunchKernelGGL((wgrad3_halo_kernel<16, 2>), grid, block, 0, st, ha); break;
-        default: hipLaunchKernelGGL((wgrad3_halo_kernel<8, 2>), grid, block, 0, st, ha); break;
+        case 64: hipLaunchKernelGGL((wgrad3_halo_kernel<64, 2, 1>), grid, block, 0, st, ha); break;
+        case 32: hipLaunchKernelGGL((wgrad3_halo_kernel<32, 2, 1>), grid, block, 0, st, ha); break;
+        case 16: hipLaunchKernelGGL((wgrad3_halo_kernel<16, 2, 1>), grid, block, 0, st, ha); break;
+        default: hipLaunchKernelGGL((wgrad3_halo_kernel<8, 2, 1>), grid, block, 0, st, ha); break;
       }
     }
     RR_CHECK_LAUNCH();

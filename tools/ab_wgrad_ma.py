@@ -1,5 +1,6 @@
-"""A/B of the halo wgrad wave tiles (RR_WGRAD_HALO_MA = 2: 2 x 2 tiles of
-16x16 MFMA blocks per wave, 4: all 64 dy channels x 16 x channels per wave)
+"""A/B of the halo wgrad variants: wave tiles (RR_WGRAD_HALO_MA = 2: 2 x 2
+tiles of 16x16 MFMA blocks per wave, 4: all 64 dy channels x 16 x channels
+per wave) and global prefetch depth (RR_WGRAD_HALO_PF = 1 / 2 stages)
 at the cfg3 W <= 16 weight-grad shapes, B = 512: per-layer median time in
 alternating rounds, TFLOP/s, and whether the two results are bitwise equal
 (same pixel order per output element, same split-K partials)."""
@@ -31,18 +32,21 @@ def timeit(fn, reps=10):
     return v[len(v) // 2]
 
 
-tot = {"2": [0.0, 0.0], "4": [0.0, 0.0]}
+CFG = {"ma2": {"RR_WGRAD_HALO_MA": "2", "RR_WGRAD_HALO_PF": "1"},
+       "ma4": {"RR_WGRAD_HALO_MA": "4", "RR_WGRAD_HALO_PF": "1"},
+       "ma4pf2": {"RR_WGRAD_HALO_MA": "4", "RR_WGRAD_HALO_PF": "2"}}
+tot = {k: [0.0, 0.0] for k in CFG}
 for name, H, c1, c2, co in LAYERS:
     g = torch.Generator(device=dev).manual_seed(7)
     x1 = torch.randn(B, H, H, c1, device=dev, generator=g).bfloat16()
     x2 = torch.randn(B, H, H, c2, device=dev, generator=g).bfloat16() if c2 else None
     dy = torch.randn(B, H, H, co, device=dev, generator=g).bfloat16()
     fl = 2.0 * B * H * H * co * (c1 + c2) * 9
-    res = {"2": [], "4": []}
+    res = {k: [] for k in CFG}
     outs = {}
     for rnd in range(3):
-        for tag in ("2", "4"):
-            os.environ["RR_WGRAD_HALO_MA"] = tag
+        for tag, env in CFG.items():
+            os.environ.update(env)
             dw = torch.empty(co, c1 + c2, 3, 3, device=dev)
             res[tag].append(timeit(lambda: ops.wgrad(RR_CONV3X3, dy, x1, x2, B, H, H, co, dw=dw)))
             outs[tag] = dw.clone()
@@ -50,9 +54,10 @@ for name, H, c1, c2, co in LAYERS:
     for k in t:
         tot[k][0] += fl
         tot[k][1] += t[k]
-    print(json.dumps(dict(layer=name, ma2_ms=round(t["2"], 4), ma4_ms=round(t["4"], 4),
-                          ma2_tf=round(fl / t["2"] / 1e9, 1), ma4_tf=round(fl / t["4"] / 1e9, 1),
-                          bitwise_equal=bool(torch.equal(outs["2"], outs["4"])))), flush=True)
-os.environ.pop("RR_WGRAD_HALO_MA")
+    print(json.dumps(dict(layer=name, **{f"{k}_ms": round(t[k], 4) for k in CFG},
+                          **{f"{k}_tf": round(fl / t[k] / 1e9, 1) for k in CFG},
+                          bitwise_equal=all(torch.equal(outs["ma2"], outs[k]) for k in CFG))), flush=True)
+for k in ("RR_WGRAD_HALO_MA", "RR_WGRAD_HALO_PF"):
+    os.environ.pop(k)
 print(json.dumps({"total_ms": {k: round(v[1], 4) for k, v in tot.items()},
                   "tflops": {k: round(v[0] / v[1] / 1e9, 1) for k, v in tot.items()}}))
