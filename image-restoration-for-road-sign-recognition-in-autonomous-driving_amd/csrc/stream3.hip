@@ -595,12 +595,12 @@ int s3_concat_flags(const rr_igemm_desc *d) {
   }
 }
 
-template <int W, int MP, int F>
+template <int W, int MP, int F, int STG = -1>
 void launch1(const S3Args &a, int P, hipStream_t st) {
   // the late-epilogue stagger measured faster only for 256-pixel steps
   // without the BN-statistics registers (it keeps acc live across the loop
   // back-edge: the stats variants spill with it)
-  constexpr int STAG = (MP == 4 && !(F & F_STATS)) ? 1 : 0;
+  constexpr int STAG = STG >= 0 ? STG : ((MP == 4 && !(F & F_STATS)) ? 1 : 0);
   hipLaunchKernelGGL((stream3_kernel<W, MP, F, STAG>), dim3(S3_WG), dim3(512), 0, st, a, P / (64 * MP));
 }
 
@@ -609,8 +609,30 @@ int launch_w(const S3Args &a, int f, int P, hipStream_t st) {
   switch (f) {
     case 0: launch1<W, 4, 0>(a, P, st); break;
     case F_BIAS: launch1<W, 4, F_BIAS>(a, P, st); break;
-    case F_STATS: launch1<W, 4, F_STATS>(a, P, st); break;
-    case F_BIAS | F_STATS: launch1<W, 4, F_BIAS | F_STATS>(a, P, st); break;
+    case F_STATS:
+    case F_BIAS | F_STATS: {
+      // the BN-statistics forward in 128-pixel steps: with 256-pixel steps
+      // (mode 0) the statistics registers pushed the kernel past 256 VGPRs
+      // (10 spilled at W = 64, 26 at W = 32: scratch traffic in the step
+      // loop, 224 us vs 139 us for the non-statistics 64x64 forward); 128-pixel
+      // steps fit in 220 (graph step +1.3 %, profiles/r3am_ab_s3_stats.txt).
+      // RR_S3_STATS_MODE (A/B): 0 = 256-pixel steps, no stagger; 1 = 256 +
+      // stagger; 2 = 128-pixel steps + stagger; 3 (default) = 128-pixel steps
+      const char *e = getenv("RR_S3_STATS_MODE");
+      const int m = e ? atoi(e) : 3;
+      if (f == F_STATS) {
+        if (m == 1) launch1<W, 4, F_STATS, 1>(a, P, st);
+        else if (m == 2) launch1<W, 2, F_STATS, 1>(a, P, st);
+        else if (m == 3) launch1<W, 2, F_STATS, 0>(a, P, st);
+        else launch1<W, 4, F_STATS>(a, P, st);
+      } else {
+        if (m == 1) launch1<W, 4, F_BIAS | F_STATS, 1>(a, P, st);
+        else if (m == 2) launch1<W, 2, F_BIAS | F_STATS, 1>(a, P, st);
+        else if (m == 3) launch1<W, 2, F_BIAS | F_STATS, 0>(a, P, st);
+        else launch1<W, 4, F_BIAS | F_STATS>(a, P, st);
+      }
+      break;
+    }
     case F_RELU: launch1<W, 4, F_RELU>(a, P, st); break;
     case F_BIAS | F_RELU: launch1<W, 4, F_BIAS | F_RELU>(a, P, st); break;
     case F_ACC: launch1<W, 2, F_ACC>(a, P, st); break;
