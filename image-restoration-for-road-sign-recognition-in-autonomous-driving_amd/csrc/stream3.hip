@@ -606,6 +606,23 @@ void launch1(const S3Args &a, int P, hipStream_t st) {
 
 template <int W>
 int launch_w(const S3Args &a, int f, int P, hipStream_t st) {
+  // the dgrad (no epilogue) and the bias + ReLU forward in 128-pixel steps
+  // too: in the graph-captured step they beat the staggered 256-pixel form
+  // by 0.8 % (profiles/r3an_ab_s3_mp4.txt; the stagger had been measured
+  // faster on eager launches).  RR_S3_MP4_MODE (A/B): 0 = 256-pixel steps +
+  // stagger; 2 = 128-pixel steps + stagger; 3 (default) = 128-pixel steps
+  const char *em = getenv("RR_S3_MP4_MODE");
+  const int m4 = em ? atoi(em) : 3;
+  if (m4 == 2 || m4 == 3) {
+    switch (f) {
+      case 0: m4 == 2 ? launch1<W, 2, 0, 1>(a, P, st) : launch1<W, 2, 0, 0>(a, P, st); RR_CHECK_LAUNCH(); return RR_OK;
+      case F_BIAS | F_RELU:
+        m4 == 2 ? launch1<W, 2, F_BIAS | F_RELU, 1>(a, P, st) : launch1<W, 2, F_BIAS | F_RELU, 0>(a, P, st);
+        RR_CHECK_LAUNCH();
+        return RR_OK;
+      default: break;
+    }
+  }
   switch (f) {
     case 0: launch1<W, 4, 0>(a, P, st); break;
     case F_BIAS: launch1<W, 4, F_BIAS>(a, P, st); break;
