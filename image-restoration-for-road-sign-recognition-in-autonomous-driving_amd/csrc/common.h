@@ -97,6 +97,29 @@ template <> __device__ __forceinline__ void store8<bf16_t>(bf16_t *p, f32x4 a, f
   *reinterpret_cast<u16x8 *>(p) = r;
 }
 
+// ---- reductions over the 16 lanes of a DPP row (lanes 16r .. 16r + 15) ----
+// VALU data-parallel-primitive moves instead of __shfl_xor, which hipcc
+// lowers to ds_bpermute_b32 (an LDS-pipe instruction with LDS latency: 368 of
+// them in one conv3r epilogue).  The pairing follows the xor tree over lane
+// offsets 1, 2, 4, 8: xor 1 and xor 2 are quad permutes; the last two steps
+// pair each lane with one in the other quad of its 8 (row_half_mirror: 7 - i)
+// and in the other half of the row (row_mirror: 15 - i).  After the first two
+// steps every lane of a quad holds the quad's value, so the mirrors add the
+// same operands as xor 4 / xor 8 would: the result is bitwise the xor tree's.
+template <int CTRL> __device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<DPP_XOR1>(v);
+  v += dpp_f<DPP_XOR2>(v);
+  v += dpp_f<DPP_HALF_MIRROR>(v);
+  v += dpp_f<DPP_MIRROR>(v);
+  return v;
+}
+// max with the neighbouring lane (lane ^ 1)
+__device__ __forceinline__ float max_xor1(float v) { return fmaxf(v, dpp_f<DPP_XOR1>(v)); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -444,17 +444,15 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
                            f32x4{gm[4], gm[5], gm[6], gm[7]});
           }
         }
-      // over the 16 pixel lanes (fixed xor tree), then one partial row per
+      // over the 16 pixel lanes (row16_sum: the fixed xor-tree order), then one partial row per
       // wave row: [srow][cout][3] = (sum gm, sum gm * xhat, 0)
 #pragma unroll
-      for (int off = 1; off < 16; off <<= 1)
+      for (int pp = 0; pp < NM / 2; ++pp)
 #pragma unroll
-        for (int pp = 0; pp < NM / 2; ++pp)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            g0[pp][j] += __shfl_xor(g0[pp][j], off, 64);
-            g1[pp][j] += __shfl_xor(g1[pp][j], off, 64);
-          }
+        for (int j = 0; j < 8; ++j) {
+          g0[pp][j] = row16_sum(g0[pp][j]);
+          g1[pp][j] = row16_sum(g1[pp][j]);
+        }
       if (frow == 0) {
 #pragma unroll
         for (int pp = 0; pp < NM / 2; ++pp) {
@@ -489,7 +487,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     if (a.stats) {
       // per-channel partial sums of the pre-bias accumulator over the wave's
       // 128 pixels: over (o, s) in registers, then over the 16 pixel lanes
-      // (fixed xor tree), one partial row per 128 pixels
+      // (row16_sum: the fixed xor-tree order), one partial row per 128 pixels
       f32x4 s1[NM], s2[NM];
 #pragma unroll
       for (int m = 0; m < NM; ++m) { s1[m] = f32x4{0.f, 0.f, 0.f, 0.f}; s2[m] = s1[m]; }
@@ -506,14 +504,12 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
           }
         }
 #pragma unroll
-      for (int off = 1; off < 16; off <<= 1)
+      for (int m = 0; m < NM; ++m)
 #pragma unroll
-        for (int m = 0; m < NM; ++m)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            s1[m][j] += __shfl_xor(s1[m][j], off, 64);
-            s2[m][j] += __shfl_xor(s2[m][j], off, 64);
-          }
+        for (int j = 0; j < 4; ++j) {
+          s1[m][j] = row16_sum(s1[m][j]);
+          s2[m][j] = row16_sum(s2[m][j]);
+        }
       if (frow == 0) {
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
@@ -598,8 +594,8 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              m0[j] = fmaxf(m0[j], __shfl_xor(m0[j], 1, 64));
-              m1[j] = fmaxf(m1[j], __shfl_xor(m1[j], 1, 64));
+              m0[j] = max_xor1(m0[j]);
+              m1[j] = max_xor1(m1[j]);
             }
             const long long p = pix_at(o2, s);            // the window's top-left pixel
             if ((frow & 1) == 0 && (!G::SEGM || p >= 0)) {

@@ -339,13 +339,8 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs a) {
     for (int mi = 0; mi < MC; ++mi)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float x = s1[mi][i], y = s2[mi][i];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          x += __shfl_xor(x, o, 64);
-          y += __shfl_xor(y, o, 64);
-        }
-        s1[mi][i] = x; s2[mi][i] = y;
+        s1[mi][i] = row16_sum(s1[mi][i]);
+        s2[mi][i] = row16_sum(s2[mi][i]);
       }
     float *red = reinterpret_cast<float *>(smem);   // [WP][BC][2]
     // (the K loop ended with a barrier; smem is free)

@@ -271,10 +271,9 @@ __global__ __launch_bounds__(256, 2) void stream1_kernel(S1Args a) {
     for (int mi = 0; mi < MC; ++mi)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          r0[mi][j] += __shfl_xor(r0[mi][j], o, 64);
-          r1[mi][j] += __shfl_xor(r1[mi][j], o, 64);
+        {
+          r0[mi][j] = row16_sum(r0[mi][j]);
+          r1[mi][j] = row16_sum(r1[mi][j]);
         }
     if (frow == 0) {
 #pragma unroll

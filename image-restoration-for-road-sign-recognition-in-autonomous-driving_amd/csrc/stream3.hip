@@ -516,10 +516,9 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     for (int mi = 0; mi < MC; ++mi)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          r0[mi][j] += __shfl_xor(r0[mi][j], o, 64);
-          r1[mi][j] += __shfl_xor(r1[mi][j], o, 64);
+        {
+          r0[mi][j] = row16_sum(r0[mi][j]);
+          r1[mi][j] = row16_sum(r1[mi][j]);
         }
     float *red = reinterpret_cast<float *>(smem);   // [4 wp][64][2] + [8 waves]
     if (frow == 0) {

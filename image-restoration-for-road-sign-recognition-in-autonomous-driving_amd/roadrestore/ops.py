@@ -220,7 +220,7 @@ def igemm(mode, x1, x2, n, h, w, wpack, cout, bias=None, act=0, out=None, out2=N
                                        _p(out2), _p(mask), _p(st), stream()), "rr_igemm")
     taps = 9 if mode == RR_CONV3X3 else (4 if mode == RR_CONVT_DOWN else 1)
     _launch(lambda: igemm_kernel_name(d), 2.0 * n * h * w * cout * taps * (c1 + c2), launch,
-            f"fwd m{mode} {n}x{h}x{w} c{c1}+{c2}->{cout}")
+            f"fwd m{mode} {n}x{h}x{w} c{c1}+{c2}->{cout}" + (f" ex{act}" if ex else ""))
     return out, out2, st
 
 

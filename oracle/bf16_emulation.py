@@ -134,7 +134,7 @@ def resunet_forward(p, x, training):
 def vgg16_features_forward(p, x, upto=16, prefix="slice"):
     first = True
     for idx, kind, _, _ in R.vgg16_feature_layers():
-        if idx >= upto:
+        if upto is not None and idx >= upto:
             break
         if kind == "conv":
             name = f"{prefix}.{idx}"
@@ -154,3 +154,59 @@ def unified_loss(out, clean, perc_params):
     fx = vgg16_features_forward(perc_params, out)
     fy = vgg16_features_forward(perc_params, clean)
     return R.l1_loss(out, clean) + 0.1 * torch.mean((fx - fy) ** 2)
+
+
+# ---------------------------------------------------------------------------
+# inference (cfg5, 17:84-86 and 18:46-47): eval-mode BN folded into the conv
+# before it, as roadrestore.engine.resblock_forward_eval_folded runs it
+
+def _fold(p, conv, bn):
+    """W' = s.W, b' = s.b + t with s = gamma / sqrt(var + eps), t = beta - mean.s
+    (rr_fold_conv_bn); the packed W' is stored bf16, b' stays fp32."""
+    s = p[bn + ".weight"] / torch.sqrt(p[bn + ".running_var"] + R.BN_EPS)
+    t = p[bn + ".bias"] - p[bn + ".running_mean"] * s
+    return qw(p[conv + ".weight"] * s.view(-1, 1, 1, 1)), p[conv + ".bias"] * s + t
+
+
+def residual_block_forward_folded(p, prefix, x, has_shortcut, pooled_after=False):
+    cb = prefix + ".conv_block"
+    w1, b1 = _fold(p, cb + ".0", cb + ".1")
+    a1 = q(F.prelu(F.conv2d(x, w1, b1, padding=1), p[cb + ".2.weight"]))
+    w2, b2 = _fold(p, cb + ".3", cb + ".4")
+    c2 = F.conv2d(a1, w2, b2, padding=1)
+    if not has_shortcut:
+        return q(F.relu(c2 + x))                      # identity: one epilogue
+    ws, bs = _fold(p, prefix + ".shortcut.0", prefix + ".shortcut.1")
+    s = q(F.conv2d(x, ws, bs))                        # the 1x1 output, stored
+    if pooled_after:
+        return q(F.relu(c2 + s))                      # conv2 accumulates onto it
+    return q(F.relu(q(c2) + F.conv2d(x, ws, bs)))     # the 1x1 accumulates onto t2
+
+
+def resunet_forward_eval_folded(p, x):
+    e1 = q(F.prelu(_first_conv(p, "enc1.0", x), p["enc1.1.weight"]))
+    r1 = residual_block_forward_folded(p, "res1", e1, R._RB["res1"], True)
+    r2 = residual_block_forward_folded(p, "res2", R._maxpool(r1), R._RB["res2"], True)
+    r3 = residual_block_forward_folded(p, "res3", R._maxpool(r2), R._RB["res3"], True)
+    b = R._maxpool(r3)
+    for i in range(3):
+        n = f"bottleneck.{i}"
+        b = residual_block_forward_folded(p, n, b, R._RB[n])
+    d3 = torch.cat((R._align(_convT(p, "up3", b), r3), r3), dim=1)
+    d3 = residual_block_forward_folded(p, "dec3", d3, R._RB["dec3"])
+    d2 = torch.cat((R._align(_convT(p, "up2", d3), r2), r2), dim=1)
+    d2 = residual_block_forward_folded(p, "dec2", d2, R._RB["dec2"])
+    d1 = torch.cat((R._align(_convT(p, "up1", d2), r1), r1), dim=1)
+    d1 = residual_block_forward_folded(p, "dec1", d1, R._RB["dec1"])
+    return _conv(p, "final", d1, 0)
+
+
+def vgg16_forward(p, x):
+    """The bf16 judge (engine.vgg_classifier_forward): conv + ReLU outputs,
+    the 7x7 average pool and each Linear output stored bf16 (the logits too),
+    bf16 weights, fp32 biases."""
+    f = vgg16_features_forward(p, x, upto=None, prefix="features")
+    f = q(torch.flatten(F.adaptive_avg_pool2d(f, (7, 7)), 1))
+    f = q(F.relu(F.linear(f, qw(p["classifier.0.weight"]), p["classifier.0.bias"])))
+    f = q(F.relu(F.linear(f, qw(p["classifier.3.weight"]), p["classifier.3.bias"])))
+    return q(F.linear(f, qw(p["classifier.6.weight"]), p["classifier.6.bias"]))
