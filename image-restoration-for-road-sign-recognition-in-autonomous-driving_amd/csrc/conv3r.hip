@@ -52,7 +52,7 @@
 
 namespace {
 
-template <int W, int BC, int NW, int NWV, int HB, int SG> struct R3 {
+template <int W, int BC, int NW, int NWV, int HB, int SG, int NWB> struct R3 {
   // SG > 0: row-segment tiles of any H x W (W ignored): TR rows x 16 SG
   // columns of one image; out-of-image rows / columns are zero in the halo
   // and masked in the epilogue
@@ -82,14 +82,16 @@ template <int W, int BC, int NW, int NWV, int HB, int SG> struct R3 {
   static constexpr int NWG = (WBLK + NWV - 1) / NWV;   // weight DMA pieces per wave per stage
   static constexpr int SROW = BC + 4;
   static constexpr int STG = 128 * SROW * 4 + (NWV * BC * 2 + NWV) * 4 + 256;
-  // [weights x2][halo x HB][guard block]: the shifted edge reads stay inside
-  // (row-segment tiles read inside their side blocks: no guard)
-  static constexpr int KBYTES = 2 * WBYTES + HB * HBYTES + (SEGM ? 0 : 1024);
+  // [weights x NWB][halo x HB][guard block]: the shifted edge reads stay
+  // inside (row-segment tiles read inside their side blocks: no guard)
+  static constexpr int KBYTES = NWB * WBYTES + HB * HBYTES + (SEGM ? 0 : 1024);
   static constexpr int BIAS = KBYTES;               // [BC] fp32 bias for the register epilogue
   static constexpr int LDS = KBYTES + BC * 4 > STG || SEGM ? KBYTES + BC * 4 : STG;
-  static_assert(LDS <= 160 * 1024 && (NWV != 4 || 2 * LDS <= 160 * 1024), "LDS");
+  // one 8-wave workgroup or two 4-wave workgroups per CU
+  static constexpr bool FITS = LDS <= 160 * 1024 && (NWV != 4 || 2 * LDS <= 160 * 1024);
   static_assert(WC * WP == NWV && NM * 16 == NW, "wave grid");
   static_assert(HB == 1 || HB == 2, "halo buffers");
+  static_assert(NWB == 2 || NWB == 3, "weight ring");
   static_assert(!SEGM || (SG == 1 || SG == 2), "segment width");
   static_assert(SEGM || PAIR || TR % W == 0 || W % TR == 0, "tile rows");
   static_assert(2 * WBYTES >= 1024, "the edge read of the first halo block stays in LDS");
@@ -97,13 +99,41 @@ template <int W, int BC, int NW, int NWV, int HB, int SG> struct R3 {
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
+#ifdef RR_CONV3R_STAMPS
+// diagnostic build only (tools/conv3r_stamps.py): per-wave sums of the K
+// loop's segments, read with rr_conv3r_stamps; never in the shipped library
+__device__ unsigned long long rr_c3_stamps[1 << 18];
+#define C3_STAMP(t)                                                              \
+  do {                                                                          \
+    __builtin_amdgcn_sched_barrier(0);                                          \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");   \
+    __builtin_amdgcn_sched_barrier(0);                                          \
+  } while (0)
+// the vmcnt wait and the barrier stamped apart
+template <int N> __device__ __forceinline__ void vm_barrier_st(unsigned long long &tw, unsigned long long &tb) {
+  unsigned long long t0, t1, t2;
+  C3_STAMP(t0);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  C3_STAMP(t1);
+  asm volatile("s_barrier" ::: "memory");
+  C3_STAMP(t2);
+  tw += t1 - t0;
+  tb += t2 - t1;
+}
+#define VM_BARRIER(N) vm_barrier_st<N>(st_vm, st_bar)
+#else
+#define C3_STAMP(t) do {} while (0)
+#define VM_BARRIER(N) vm_barrier<N>()
+#endif
+
 template <int N> __device__ __forceinline__ void vm_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-template <int W, int BC, int NW, int NWV, int HB, int SG>
+template <int W, int BC, int NW, int NWV, int HB, int SG, int NWB>
 __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) {
-  using G = R3<W, BC, NW, NWV, HB, SG>;
+  using G = R3<W, BC, NW, NWV, HB, SG, NWB>;
+  static_assert(G::FITS, "LDS");
   constexpr int NS = G::NS, R = G::R, NM = G::NM, WC = G::WC, RS = G::RS;
   constexpr int HW = W * W;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
@@ -138,7 +168,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   }
 
   const uint32_t sbase = (uint32_t)(uintptr_t)smem;
-  const uint32_t wbase = sbase, hbase = sbase + 2 * G::WBYTES;
+  const uint32_t wbase = sbase, hbase = sbase + NWB * G::WBYTES;
 
   // ---- per-lane DMA sources ----
   // halo block b = (segment k, halo row hr, column block s): pixel index of
@@ -187,7 +217,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   const char *wtile = a.wt + (long long)a.cout * a.K * 2;
   auto issue_w = [&](int st) __attribute__((always_inline)) {
     const int ch = st / 3, dx = st - ch * 3;
-    char *dst = smem + (st & 1) * G::WBYTES;
+    char *dst = smem + (NWB == 3 ? st % 3 : st & 1) * G::WBYTES;
 #pragma unroll
     for (int i = 0; i < G::NWG; ++i) {
       // tile (chunk ch, column dx, row dy, block mb): 3 contiguous runs per stage
@@ -202,7 +232,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     const long long cs = first ? a.c1 : a.c2;
     const long long cl = first ? ci0 : ci0 - a.c1;
     const long long zoff = (long long)((uintptr_t)rr_zero_page - (uintptr_t)base) + fq * 16;
-    char *dst = smem + 2 * G::WBYTES + (HB == 2 ? (ch & 1) * G::HBYTES : 0);
+    char *dst = smem + NWB * G::WBYTES + (HB == 2 ? (ch & 1) * G::HBYTES : 0);
 #pragma unroll
     for (int i = 0; i < G::NHG; ++i) {
       const long long off = hpix[i] >= 0 ? ((long long)hpix[i] * cs + cl) * 2 + fq * 16 : zoff;
@@ -256,10 +286,18 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   __builtin_amdgcn_s_waitcnt(0x0F70);               // vmcnt(0) (gfx9 encoding)
 
   const int kc = a.cin / 32, nst = 3 * kc;
-  // prologue: chunk 0's halo, stage 0's weights
+  [[maybe_unused]] unsigned long long st_vm = 0, st_bar = 0, st_row0 = 0, st_loop0 = 0, st_loop1 = 0, st_t = 0;
+  C3_STAMP(st_loop0);
+  // prologue: chunk 0's halo, stage 0's weights (and with a 3-deep ring
+  // stage 1's, left in flight)
   issue_h(0);
   issue_w(0);
-  vm_barrier<0>();
+  if (NWB == 3 && nst > 1) {
+    issue_w(1);
+    vm_barrier<G::NWG>();
+  } else {
+    vm_barrier<0>();
+  }
 
   // diagnostics (RR_IGEMM_DBG, timing only -- results are wrong): bit2 no
   // DMA in the K loop, bit3 no MFMAs, bit0 no epilogue, bit4 no weight DMA,
@@ -270,93 +308,272 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   // form -- the younger half of the workgroup at priority 1 for the whole
   // loop -- +1 % / -3 %).  RR_IGEMM_DBG bit7 turns it off (A/B)
   const bool prio_mfma = (a.dbg & 128) == 0;
-  for (int st = 0; st < nst; ++st) {
-    const int ch = st / 3, dx = st - ch * 3;       // uniform
-    // operands of the next stage (weights) and of the next chunk (halo)
-    const bool next_h = HB == 2 && dx == 0 && ch + 1 < kc && !dbg_nodma && !(a.dbg & 32);
-    const bool next_w = st + 1 < nst && !dbg_nodma && !(a.dbg & 16);
-    if (HB == 1 && dx == 0 && ch > 0) {
-      // one halo buffer: every wave is past the previous chunk's last read
-      // (the barrier that ended the last stage); load this chunk's halo
-      if (!dbg_nodma && !(a.dbg & 32)) issue_h(ch);
-      vm_barrier<0>();
-    }
-
-    const uint32_t aa = a_lane + (st & 1) * G::WBYTES;
-    const uint32_t ba = b_wave + (HB == 2 ? (ch & 1) * G::HBYTES : 0) +
-                        (dx == 0 ? loff[0] : (dx == 1 ? loff[1] : loff[2]));
-    const bool zlo = dx == 0 && zl[0];               // left padding column (block s = 0)
-    const bool zhi = dx == 2 && zl[2];               // right padding column (block NS - 1)
-    i32x4 af[3][NM];
-#pragma unroll
-    for (int dy = 0; dy < 3; ++dy)
+  if constexpr (NWB == 3) {
+    // ---- stage-pipelined K loop (3-deep weight ring) ----
+    // The A fragments of stage st + 1 are read in the last two halo rows of
+    // stage st, where the taps whose registers they replace are finished
+    // (row R uses dy = 1, 2; row R + 1 only dy = 2), and the next stage's B
+    // row 0 behind them: no wave starts a stage waiting on 12 + NS fragment
+    // reads.  A mid-stage barrier (before row R) publishes the next stage's
+    // weights (issued a whole stage earlier) and, before a chunk change, the
+    // next chunk's halo.  LDS reads in issue order across a stage boundary:
+    //   row R: [af0'] [B(R+1)]   row R+1: [af1'] [B0']   tail: [af2']
+    //   row 0': [B1'] (waits for af0', B0')   row 1': [B2'] ...
+    i32x4 af[3][NM], bf[2][NS];
+    auto b_addr = [&](int s_) __attribute__((always_inline)) -> uint32_t {
+      const int c_ = s_ / 3, d_ = s_ - c_ * 3;
+      return b_wave + (HB == 2 ? (c_ & 1) * G::HBYTES : 0) +
+             (d_ == 0 ? loff[0] : (d_ == 1 ? loff[1] : loff[2]));
+    };
+    auto read_a = [&](int s_, int dy) __attribute__((always_inline)) {
+      const uint32_t aa = a_lane + (s_ % 3) * G::WBYTES;
 #pragma unroll
       for (int m = 0; m < NM; ++m)
         asm volatile("ds_read_b128 %0, %1 offset:%2"
                      : "=v"(af[dy][m]) : "v"(aa), "i"((dy * (BC / 16) + m) * 1024));
-    i32x4 bf[2][NS];
+    };
+    read_a(0, 0);
+    read_a(0, 1);
+    read_a(0, 2);
+    {
+      const uint32_t b0 = b_addr(0);
 #pragma unroll
-    for (int s = 0; s < NS; ++s)
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bf[0][s]) : "v"(ba), "i"(s * 1024));
-#pragma unroll
-    for (int ri = 0; ri < R + 2; ++ri) {
-      if (ri + 1 < R + 2) {
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-          asm volatile("ds_read_b128 %0, %1 offset:%2"
-                       : "=v"(bf[(ri + 1) & 1][s]) : "v"(ba), "i"(((ri + 1) * RS + s) * 1024));
-        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
-      } else {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      }
-#pragma unroll
-      for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(bf[ri & 1][s]));
-      if (ri == 0) {
-#pragma unroll
-        for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-          for (int m = 0; m < NM; ++m) asm volatile("" : "+v"(af[dy][m]));
-      }
-      // the padding columns: zero the shifted edge reads
-      if constexpr (!G::SEGM) {
-        i32x4 &lo = bf[ri & 1][0];
-        i32x4 &hi = bf[ri & 1][NS - 1];
-        if (G::PAIR) {
-          if (zlo || zhi) lo = i32x4{0, 0, 0, 0};
-        } else {
-          if (zlo) lo = i32x4{0, 0, 0, 0};
-          if (zhi) hi = i32x4{0, 0, 0, 0};
-        }
-      }
-      if (prio_mfma) __builtin_amdgcn_s_setprio(1);
-      if (!dbg_nomfma) {
-#pragma unroll
-        for (int dy = 0; dy < 3; ++dy) {
-          const int o = ri - dy;
-          if (o < 0 || o >= R) continue;
-#pragma unroll
-          for (int s = 0; s < NS; ++s)
-#pragma unroll
-            for (int m = 0; m < NM; ++m)
-              acc[o][s][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                  __builtin_bit_cast(bf16x8, af[dy][m]), __builtin_bit_cast(bf16x8, bf[ri & 1][s]),
-                  acc[o][s][m], 0, 0, 0);
-        }
-      }
-      if (prio_mfma) __builtin_amdgcn_s_setprio(0);
-      // the DMA for the next stage / chunk goes out behind the first rows'
-      // MFMAs (issued right after the barrier, every wave of a SIMD would
-      // sit in ~60-cycle issue slots before its first MFMA); the weights
-      // first, the halo (waited for one stage later) last
-      if (ri == 0 && next_w) issue_w(st + 1);
-      if (ri == 1 && next_h) issue_h(ch + 1);
+      for (int s_ = 0; s_ < NS; ++s_)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bf[0][s_]) : "v"(b0), "i"(s_ * 1024));
     }
-    // the next stage's weights must have landed; a next chunk's halo (issued
-    // after them) may stay in flight for one more stage
-    if (next_h) vm_barrier<G::NHG>();
-    else vm_barrier<0>();
+    static_assert((R & 1) == 0, "the next stage's B row 0 lands in bf[0]");
+    bool prev_h = false;                             // the previous stage issued a halo
+    for (int st = 0; st < nst; ++st) {
+      const int ch = st / 3, dx = st - ch * 3;       // uniform
+      C3_STAMP(st_t);
+      const bool has_next = st + 1 < nst;
+      // HB == 1: the next chunk's halo can only be loaded once every wave is
+      // past this chunk's last row, so its row 0 is not prefetched
+      const bool pre_b = has_next && !(HB == 1 && dx == 2);
+      const bool next_w = st + 2 < nst && !dbg_nodma && !(a.dbg & 16);
+      const bool next_h = HB == 2 && dx == 0 && ch + 1 < kc && !dbg_nodma && !(a.dbg & 32);
+      bool row0_fresh = st == 0;                     // B row 0 read right before row 0
+      if (HB == 1 && dx == 0 && ch > 0) {
+        // one halo buffer: wait until every wave is past the previous chunk's
+        // last row, load this chunk's halo, then read its B row 0
+        asm volatile("s_barrier" ::: "memory");
+        if (!dbg_nodma && !(a.dbg & 32)) issue_h(ch);
+        VM_BARRIER(0);
+        const uint32_t b0 = b_addr(st);
+#pragma unroll
+        for (int s_ = 0; s_ < NS; ++s_)
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bf[0][s_]) : "v"(b0), "i"(s_ * 1024));
+        row0_fresh = true;
+      }
+      const uint32_t ba = b_addr(st);
+      const uint32_t ban = b_addr(has_next ? st + 1 : st);
+      const bool zlo = dx == 0 && zl[0];             // left padding column (block s = 0)
+      const bool zhi = dx == 2 && zl[2];             // right padding column (block NS - 1)
+#pragma unroll
+      for (int ri = 0; ri < R + 2; ++ri) {
+        if (ri == R && has_next) {
+          // publish the next stage's weights (issued at row 0 of the previous
+          // stage) and a next chunk's halo (issued two stages ago); in flight
+          // may stay what was issued after them: this stage's weights and, at
+          // dx = 1, the halo the previous stage issued
+          if (next_w && dx == 1 && prev_h) VM_BARRIER(G::NWG + G::NHG);
+          else if (next_w) VM_BARRIER(G::NWG);
+          else if (dx == 1 && prev_h) VM_BARRIER(G::NHG);
+          else VM_BARRIER(0);
+          read_a(st + 1, 0);
+        }
+        if (ri + 1 < R + 2) {
+#pragma unroll
+          for (int s_ = 0; s_ < NS; ++s_)
+            asm volatile("ds_read_b128 %0, %1 offset:%2"
+                         : "=v"(bf[(ri + 1) & 1][s_]) : "v"(ba), "i"(((ri + 1) * RS + s_) * 1024));
+        }
+        if (ri == R + 1 && has_next) {
+          read_a(st + 1, 1);
+          if (pre_b) {
+#pragma unroll
+            for (int s_ = 0; s_ < NS; ++s_)
+              asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bf[0][s_]) : "v"(ban), "i"(s_ * 1024));
+          }
+        }
+        // wait for this row's B fragments (and the taps first used here)
+        if (ri == 0) {
+          if (row0_fresh) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
+          else asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NM + NS) : "memory");
+        } else if (ri < R) {
+          asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
+        } else if (ri == R) {
+          if (has_next) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NM + NS) : "memory");
+          else asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
+        } else {
+          if (has_next && pre_b) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NM + NS) : "memory");
+          else if (has_next) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NM) : "memory");
+          else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+#pragma unroll
+        for (int s_ = 0; s_ < NS; ++s_) asm volatile("" : "+v"(bf[ri & 1][s_]));
+#ifdef RR_CONV3R_STAMPS
+        if (ri == 0) {
+          unsigned long long t1;
+          C3_STAMP(t1);
+          st_row0 += t1 - st_t;
+        }
+#endif
+        if (ri < 3) {
+#pragma unroll
+          for (int m = 0; m < NM; ++m) asm volatile("" : "+v"(af[ri][m]));
+        }
+        if constexpr (!G::SEGM) {
+          i32x4 &lo = bf[ri & 1][0];
+          i32x4 &hi = bf[ri & 1][NS - 1];
+          if (G::PAIR) {
+            if (zlo || zhi) lo = i32x4{0, 0, 0, 0};
+          } else {
+            if (zlo) lo = i32x4{0, 0, 0, 0};
+            if (zhi) hi = i32x4{0, 0, 0, 0};
+          }
+        }
+        if (prio_mfma) __builtin_amdgcn_s_setprio(1);
+        if (!dbg_nomfma) {
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy) {
+            const int o = ri - dy;
+            if (o < 0 || o >= R) continue;
+#pragma unroll
+            for (int s_ = 0; s_ < NS; ++s_)
+#pragma unroll
+              for (int m = 0; m < NM; ++m)
+                acc[o][s_][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                    __builtin_bit_cast(bf16x8, af[dy][m]), __builtin_bit_cast(bf16x8, bf[ri & 1][s_]),
+                    acc[o][s_][m], 0, 0, 0);
+          }
+        }
+        if (prio_mfma) __builtin_amdgcn_s_setprio(0);
+        // DMA: the weights two stages ahead behind row 0's MFMAs (their
+        // buffer's last reads were before the previous stage's barrier); a
+        // next chunk's halo behind row R's (after this stage's barrier: the
+        // buffer's last reads, two stages back, are then finished everywhere)
+        if (ri == 0 && next_w) issue_w(st + 2);
+        if (ri == R && next_h) issue_h(ch + 1);
+      }
+      if (has_next) read_a(st + 1, 2);
+      prev_h = next_h;
+    }
+  } else {
+    for (int st = 0; st < nst; ++st) {
+      const int ch = st / 3, dx = st - ch * 3;       // uniform
+      C3_STAMP(st_t);
+      // operands of the next stage (weights) and of the next chunk (halo)
+      const bool next_h = HB == 2 && dx == 0 && ch + 1 < kc && !dbg_nodma && !(a.dbg & 32);
+      // the ring's next free buffer: stage st + 1 (2 buffers) or st + 2 (3)
+      const bool next_w = st + NWB - 1 < nst && !dbg_nodma && !(a.dbg & 16);
+      if (HB == 1 && dx == 0 && ch > 0) {
+        // one halo buffer: every wave is past the previous chunk's last read
+        // (the barrier that ended the last stage); load this chunk's halo
+        if (!dbg_nodma && !(a.dbg & 32)) issue_h(ch);
+        VM_BARRIER(0);
+      }
+
+      const uint32_t aa = a_lane + (NWB == 3 ? dx : st & 1) * G::WBYTES;   // (st % 3 = dx)
+      const uint32_t ba = b_wave + (HB == 2 ? (ch & 1) * G::HBYTES : 0) +
+                          (dx == 0 ? loff[0] : (dx == 1 ? loff[1] : loff[2]));
+      const bool zlo = dx == 0 && zl[0];               // left padding column (block s = 0)
+      const bool zhi = dx == 2 && zl[2];               // right padding column (block NS - 1)
+      i32x4 af[3][NM];
+  #pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+  #pragma unroll
+        for (int m = 0; m < NM; ++m)
+          asm volatile("ds_read_b128 %0, %1 offset:%2"
+                       : "=v"(af[dy][m]) : "v"(aa), "i"((dy * (BC / 16) + m) * 1024));
+      i32x4 bf[2][NS];
+  #pragma unroll
+      for (int s = 0; s < NS; ++s)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bf[0][s]) : "v"(ba), "i"(s * 1024));
+  #pragma unroll
+      for (int ri = 0; ri < R + 2; ++ri) {
+        if (ri + 1 < R + 2) {
+  #pragma unroll
+          for (int s = 0; s < NS; ++s)
+            asm volatile("ds_read_b128 %0, %1 offset:%2"
+                         : "=v"(bf[(ri + 1) & 1][s]) : "v"(ba), "i"(((ri + 1) * RS + s) * 1024));
+          asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+  #pragma unroll
+        for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(bf[ri & 1][s]));
+#ifdef RR_CONV3R_STAMPS
+        if (ri == 0) {
+          unsigned long long t1;
+          C3_STAMP(t1);
+          st_row0 += t1 - st_t;
+        }
+#endif
+        if (ri == 0) {
+  #pragma unroll
+          for (int dy = 0; dy < 3; ++dy)
+  #pragma unroll
+            for (int m = 0; m < NM; ++m) asm volatile("" : "+v"(af[dy][m]));
+        }
+        // the padding columns: zero the shifted edge reads
+        if constexpr (!G::SEGM) {
+          i32x4 &lo = bf[ri & 1][0];
+          i32x4 &hi = bf[ri & 1][NS - 1];
+          if (G::PAIR) {
+            if (zlo || zhi) lo = i32x4{0, 0, 0, 0};
+          } else {
+            if (zlo) lo = i32x4{0, 0, 0, 0};
+            if (zhi) hi = i32x4{0, 0, 0, 0};
+          }
+        }
+        if (prio_mfma) __builtin_amdgcn_s_setprio(1);
+        if (!dbg_nomfma) {
+  #pragma unroll
+          for (int dy = 0; dy < 3; ++dy) {
+            const int o = ri - dy;
+            if (o < 0 || o >= R) continue;
+  #pragma unroll
+            for (int s = 0; s < NS; ++s)
+  #pragma unroll
+              for (int m = 0; m < NM; ++m)
+                acc[o][s][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                    __builtin_bit_cast(bf16x8, af[dy][m]), __builtin_bit_cast(bf16x8, bf[ri & 1][s]),
+                    acc[o][s][m], 0, 0, 0);
+          }
+        }
+        if (prio_mfma) __builtin_amdgcn_s_setprio(0);
+        // the DMA for the next stage / chunk goes out behind the first rows'
+        // MFMAs (issued right after the barrier, every wave of a SIMD would
+        // sit in ~60-cycle issue slots before its first MFMA); the weights
+        // first, the halo (waited for one stage later) last
+        if (ri == 0 && next_w) issue_w(st + NWB - 1);
+        if (ri == 1 && next_h) issue_h(ch + 1);
+      }
+      // the next stage's weights must have landed; a next chunk's halo (issued
+      // after them) may stay in flight for one more stage, and with a 3-deep
+      // ring so may the weights issued this stage (vmcnt retires in issue
+      // order: everything issued before this stage is then complete)
+      if constexpr (NWB == 3) {
+        if (next_w && next_h) VM_BARRIER(G::NWG + G::NHG);
+        else if (next_w) VM_BARRIER(G::NWG);
+        else if (next_h) VM_BARRIER(G::NHG);
+        else VM_BARRIER(0);
+      } else {
+        if (next_h) VM_BARRIER(G::NHG);
+        else VM_BARRIER(0);
+      }
+    }
   }
 
+#ifdef RR_CONV3R_STAMPS
+  C3_STAMP(st_loop1);
+  if (lane == 0 && blockIdx.x < (1 << 18) / (8 * NWV)) {
+    unsigned long long *o = rr_c3_stamps + ((long long)blockIdx.x * NWV + wv) * 8;
+    o[0] = st_loop1 - st_loop0; o[1] = st_row0; o[2] = st_vm; o[3] = st_bar;
+    o[4] = (unsigned long long)nst; o[5] = 1;
+  }
+#endif
   if (a.dbg & 1) {
     float t = 0.f;
 #pragma unroll
@@ -662,8 +879,13 @@ R3Pick r3_pick(const rr_igemm_desc *d) {
   const int nwv = e && (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : (d->c_out % 128 == 0 ? 8 : 4);
   R3Pick k{0, 0, 0, 0, 0};
   if (square) {
+    // RR_CONV3R_BC256=0: the 256-channel column blocks (2-deep weight ring:
+    // a 3-deep one does not fit beside their halo) take 128-channel blocks
+    // with the 3-deep ring instead (A/B)
+    const char *e256 = getenv("RR_CONV3R_BC256");
+    const bool bc256 = !(e256 && atoi(e256) == 0);
     if (nwv == 8) {
-      if (d->c_out % 256 == 0) {
+      if (d->c_out % 256 == 0 && bc256) {
         if (W != 8 || (P / 256) * (d->c_out / 256) >= 256 || P % 256) k = {256, 64, 8, 2, 0};
         else k = {128, 32, 8, 2, 0};
       } else if (d->c_out % 128 == 0) {
@@ -734,6 +956,23 @@ int conv3r_stat_blocks(const rr_igemm_desc *d) {
   return (int)(r3_ptiles(d, k) * (k.nwv / (k.bc / k.nw)));   // one row per wave row of a tile
 }
 
+// the weight ring: 2 buffers and one barrier per stage by default;
+// RR_CONV3R_RING=3 (A/B): 3 buffers and the stage-pipelined K loop wherever
+// the LDS holds them (measured no faster: profiles/r4e_conv3r*.jsonl)
+static bool r3_ring2_forced() {
+  const char *e = getenv("RR_CONV3R_RING");
+  return !(e && atoi(e) == 3);
+}
+template <int W, int BC, int NW, int NWV, int HB, int SG>
+static void conv3r_go_w(const dim3 &grid, const dim3 &block, IgemmArgs &a, hipStream_t st) {
+  if constexpr (R3<W, BC, NW, NWV, HB, SG, 3>::FITS) {
+    if (!r3_ring2_forced()) {
+      hipLaunchKernelGGL((conv3r_kernel<W, BC, NW, NWV, HB, SG, 3>), grid, block, 0, st, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((conv3r_kernel<W, BC, NW, NWV, HB, SG, 2>), grid, block, 0, st, a);
+}
 template <int BC, int NW, int NWV, int HB, int SG>
 static int conv3r_go(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   a.ncblk = a.cout / BC;
@@ -741,12 +980,12 @@ static int conv3r_go(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   if (nblk <= 0 || nblk > 0x7fffffffLL) return RR_EUNSUPPORTED;
   const dim3 grid((unsigned)nblk), block(64 * NWV);
   if constexpr (SG > 0) {
-    hipLaunchKernelGGL((conv3r_kernel<0, BC, NW, NWV, HB, SG>), grid, block, 0, st, a);
+    conv3r_go_w<0, BC, NW, NWV, HB, SG>(grid, block, a, st);
   } else {
     switch (d->w) {
-      case 32: hipLaunchKernelGGL((conv3r_kernel<32, BC, NW, NWV, HB, 0>), grid, block, 0, st, a); break;
-      case 16: hipLaunchKernelGGL((conv3r_kernel<16, BC, NW, NWV, HB, 0>), grid, block, 0, st, a); break;
-      default: hipLaunchKernelGGL((conv3r_kernel<8, BC, NW, NWV, HB, 0>), grid, block, 0, st, a); break;
+      case 32: conv3r_go_w<32, BC, NW, NWV, HB, 0>(grid, block, a, st); break;
+      case 16: conv3r_go_w<16, BC, NW, NWV, HB, 0>(grid, block, a, st); break;
+      default: conv3r_go_w<8, BC, NW, NWV, HB, 0>(grid, block, a, st); break;
     }
   }
   RR_CHECK_LAUNCH();
@@ -807,3 +1046,15 @@ const char *conv3r_name(const rr_igemm_desc *d) {
   }
   return n;
 }
+
+#ifdef RR_CONV3R_STAMPS
+extern "C" int rr_conv3r_stamps(unsigned long long *host, int n, int clear) {
+  if (n > (1 << 18)) n = 1 << 18;
+  if (host && hipMemcpyFromSymbol(host, HIP_SYMBOL(rr_c3_stamps), (size_t)n * 8) != hipSuccess) return -3;
+  if (clear) {
+    static unsigned long long z[1 << 18];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rr_c3_stamps), z, sizeof(z)) != hipSuccess) return -3;
+  }
+  return 0;
+}
+#endif

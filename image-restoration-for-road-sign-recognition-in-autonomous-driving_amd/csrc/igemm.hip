@@ -1241,7 +1241,11 @@ static int fill_args(const rr_igemm_desc *d, const void *x1, const void *x2, con
 // benched schedule with it).  Static strings, never NULL.
 extern "C" const char *rr_igemm_kernel_name(const rr_igemm_desc *d, int bnbwd) {
   if (!d) return "invalid";
-  if (d->act > RR_ACT_RELU) return !bnbwd && conv3r_bc(d) ? conv3r_name(d) : "unsupported";
+  if (d->act > RR_ACT_RELU) {
+    // (the pool epilogue needs a 2x2 window: rr_igemm_ex refuses such maps)
+    if ((d->act & RR_ACT_POOL) && (d->h < 2 || d->w < 2)) return "unsupported";
+    return !bnbwd && conv3r_bc(d) ? conv3r_name(d) : "unsupported";
+  }
   if (stream3_blocks(d, bnbwd)) return d->w == 64 ? "stream3_kernel<64>" : "stream3_kernel<32>";
   S1Plan pl;
   if (!bnbwd && stream1_plan(d, &pl)) return stream1_name(pl);

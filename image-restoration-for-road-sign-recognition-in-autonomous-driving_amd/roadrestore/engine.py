@@ -343,10 +343,8 @@ def _bn_affine(bn, st, bias, count, training, out=None, need_bwd=False):
     """-> (scale, shift, mean, invstd).  Eval mode: the running statistics;
     mean / invstd only when a backward follows (eval-mode BN backward)."""
     if training:
-        if bn.momentum is None:
-            raise NotImplementedError("BatchNorm2d(momentum=None) is not supported")
         return ops.bn_finalize(st, count, bias, bn.weight, bn.bias, bn.running_mean,
-                               bn.running_var, bn.momentum, bn.eps, bn.num_batches_tracked,
+                               bn.running_var, _momentum(bn), bn.eps, bn.num_batches_tracked,
                                out=out)
     s, b = ops.bn_eval_affine(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, out=out)
     if not need_bwd:
@@ -359,9 +357,16 @@ def _bn_affine(bn, st, bias, count, training, out=None, need_bwd=False):
 _PAIR_FINALIZE = os.environ.get("RR_BN_PAIR_FINALIZE", "1") != "0"
 
 
+def _momentum(bn):
+    """BatchNorm2d(momentum=None) (cumulative moving average): -1, the
+    finalize then reads the factor 1 / num_batches_tracked on the device (no
+    host sync; as layers.batch_norm)"""
+    return -1.0 if bn.momentum is None else bn.momentum
+
+
 def _fin_args(bn, st, bias, count, out):
     return dict(st=st, count=count, bias=bias, gamma=bn.weight, beta=bn.bias,
-                running_mean=bn.running_mean, running_var=bn.running_var, momentum=bn.momentum,
+                running_mean=bn.running_mean, running_var=bn.running_var, momentum=_momentum(bn),
                 eps=bn.eps, num_batches_tracked=bn.num_batches_tracked, out=out)
 
 
@@ -431,6 +436,8 @@ def _ex_fusable(dtype, n, h, w, c1, c2, cout, act):
     row-streaming kernel keeps the layer and the activation stays a pass)."""
     if dtype != torch.bfloat16:
         return False
+    if act & ops.RR_ACT_POOL and (h < 2 or w < 2):
+        return False                       # (no 2x2 window: the unfused max-pool path)
     rd = ops.rr_dtype(dtype)
     fused = ops.igemm_kernel_name(ops.IgemmDesc(rd, RR_CONV3X3, n, h, w, c1, c2, cout, 0, act,
                                                 0, 1, 0, 0, 0))
@@ -469,7 +476,7 @@ def resblock_forward(blk, x1, x2, n, h, w, wc, dt, training, need_bwd, pool=Fals
         s, _, sts = ops.igemm(RR_CONV1X1, x1, x2, n, h, w, pks[0], cout, bias=sc0.bias,
                               stats=training)
         outs = (pair[0][1], pair[1][1]) if pair else None
-        if training and _PAIR_FINALIZE and bn2.momentum is not None and sc1.momentum is not None:
+        if training and _PAIR_FINALIZE:
             # both statistics are ready: the two finalizes as one launch
             (s2, sh2, m2, i2), (ss, shs, ms, is_) = ops.bn_finalize_pair(
                 _fin_args(bn2, st2, c2.bias, P, out2), _fin_args(sc1, sts, sc0.bias, P, outs))
@@ -762,6 +769,14 @@ def resunet_backward(m, S, g_out, sink):
 # ---------------------------------------------------------------------------
 # VGG16 features (torchvision cfg D) -- perceptual slice and classifier trunk
 
+def _pool_2x2(mod):
+    """MaxPool2d(2) / MaxPool2d(2, 2): the window the conv epilogue pools"""
+    def two(v):
+        return v == 2 or v == (2, 2)
+    return (two(mod.kernel_size) and two(mod.stride if mod.stride is not None else mod.kernel_size)
+            and mod.padding in (0, (0, 0)) and mod.dilation in (1, (1, 1)) and not mod.ceil_mode)
+
+
 def vgg_layers(features, upto=None):
     """[(kind, module)] of features[:upto]; ReLU after each conv is fused."""
     mods = list(features)
@@ -799,7 +814,8 @@ def vgg_features_forward(features, x, wc, dt, upto=None, need_bwd=False):
             continue
         if kind in ("conv", "conv_relu"):
             act = RELU if kind == "conv_relu" else 0
-            nxt_pool = li + 1 < len(layers) and layers[li + 1][0] == "pool"
+            nxt_pool = li + 1 < len(layers) and layers[li + 1][0] == "pool" and \
+                _pool_2x2(layers[li + 1][1])
             if cur is not None and not need_bwd and nxt_pool and \
                     _ex_fusable(cur.dtype, n, h, w, cur.shape[-1], 0, mod.weight.shape[0],
                                 act | ops.RR_ACT_POOL | ops.RR_ACT_NOFULL):

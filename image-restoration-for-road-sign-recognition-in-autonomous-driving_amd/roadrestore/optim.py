@@ -11,12 +11,19 @@ one launch per parameter.  The learning-rate schedule is host arithmetic:
 torch.optim.lr_scheduler.CosineAnnealingLR works unchanged (14:223, 248).
 
 ``capturable=True`` (HIP-graph replay of the whole step): the step count AND
-the learning rate live on the device.  Each group's ``lr`` becomes a
-1-element fp32 device tensor; torch's LR schedulers update a tensor lr in
-place (``fill_``), which the captured ``rr_adamw_dev`` launch reads on every
-replay, so ``scheduler.step()`` between replays takes effect.
+the learning rate live on the device.  Each group's ``lr`` becomes ONE
+persistent 1-element fp32 device tensor; torch's LR schedulers update a tensor
+lr in place (``fill_``), which the captured ``rr_adamw_dev`` launch reads on
+every replay, so ``scheduler.step()`` between replays takes effect.  Only
+in-place updates reach a replay: a plain ``group["lr"] = x`` (warm-up code)
+swaps the tensor out of the group, and the graph keeps reading the old one.
+The next eager ``step()`` (or capture) copies such a value back into the
+persistent tensor, with a warning once a graph has been captured.
+``state_dict()`` reports lr as a Python float.
 """
 from __future__ import annotations
+
+import warnings
 
 import torch
 
@@ -83,28 +90,47 @@ class _FusedAdamBase(torch.optim.Optimizer):
         # bias correction and follows the LR schedule
         self.capturable = capturable
         if capturable:
-            for group in self.param_groups:
-                self._lr_to_device(group)
+            for gi, group in enumerate(self.param_groups):
+                self._lr_to_device(gi, group, warn=False)
 
-    @staticmethod
-    def _lr_to_device(group):
-        """group["lr"] as a 1-element fp32 tensor on the parameters' device
-        (once the parameters are on a GPU); returns it or None"""
-        lr = group["lr"]
+    def _lr_to_device(self, gi, group, warn=True):
+        """The group's persistent 1-element fp32 lr tensor on the parameters'
+        device (once they are on a GPU), holding group["lr"]'s value; put back
+        into the group if it was replaced.  Returns it or None."""
         dev = next((p.device for p in group["params"] if p.is_cuda), None)
         if dev is None:
             return None
-        if not (isinstance(lr, torch.Tensor) and lr.is_cuda and lr.dtype == torch.float32
-                and lr.numel() == 1 and lr.device == dev):
-            lr = torch.full((1,), float(lr), dtype=torch.float32, device=dev)
-            group["lr"] = lr
-        return lr
+        gstate = self._gstate.setdefault(gi, {})
+        lr_t = gstate.get("lr_dev")
+        lr = group["lr"]
+        if lr_t is None or lr_t.device != dev:
+            lr_t = torch.empty(1, dtype=torch.float32, device=dev)
+            lr_t.fill_(float(lr))
+            gstate["lr_dev"] = lr_t
+        elif lr is not lr_t:
+            if warn and gstate.get("captured"):
+                warnings.warn("param_groups[%d]['lr'] was replaced after a HIP-graph capture: "
+                              "graph replays keep reading the persistent lr tensor; update it "
+                              "in place (group['lr'].fill_(x)) between replays" % gi)
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("param_groups[%d]['lr'] was replaced; it cannot be copied to "
+                                   "the device during a capture" % gi)
+            lr_t.fill_(float(lr))
+        group["lr"] = lr_t
+        return lr_t
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
         if self.capturable:
-            for group in self.param_groups:
-                self._lr_to_device(group)
+            for gi, group in enumerate(self.param_groups):
+                self._lr_to_device(gi, group, warn=False)
+
+    def state_dict(self):
+        sd = super().state_dict()
+        for g in sd["param_groups"]:
+            if isinstance(g.get("lr"), torch.Tensor):
+                g["lr"] = float(g["lr"].item())
+        return sd
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -119,7 +145,8 @@ class _FusedAdamBase(torch.optim.Optimizer):
             if any(not p.is_cuda for p in ps):
                 raise RuntimeError("fused Adam/AdamW runs on the GPU only")
             b1, b2 = group["betas"]
-            gstate = self._gstate.setdefault(self.param_groups.index(group), {})
+            gi = self.param_groups.index(group)
+            gstate = self._gstate.setdefault(gi, {})
             gstate["step"] = gstate.get("step", 0) + 1
             step = gstate["step"]
             pspan = _span([p.data for p in ps])
@@ -145,7 +172,9 @@ class _FusedAdamBase(torch.optim.Optimizer):
                     if "step_dev" not in gstate:
                         gstate["step_dev"] = torch.full((1,), step - 1, dtype=torch.int64,
                                                         device=ps[0].device)
-                    lr_dev = self._lr_to_device(group)
+                    lr_dev = self._lr_to_device(gi, group)
+                    if torch.cuda.is_current_stream_capturing():
+                        gstate["captured"] = True
                     lib().check(lib().rr_adamw_dev(
                         total, pspan[0][0], gspan[0][0], gstate["m"].data_ptr(),
                         gstate["v"].data_ptr(), lr_dev.data_ptr(), float(b1), float(b2),

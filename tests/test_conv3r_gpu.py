@@ -438,7 +438,8 @@ def test_conv3r_ex_prelu_and_residual(dev, shape, monkeypatch):
 
 @pytest.mark.parametrize("shape", [(2, 224, 224, 64, 0, 64), (2, 56, 56, 128, 0, 256), (3, 28, 28, 256, 0, 512),
                                    (2, 14, 14, 512, 0, 512), (4, 16, 16, 256, 0, 256), (8, 8, 8, 256, 0, 512),
-                                   (2, 32, 32, 128, 0, 128), (3, 36, 52, 64, 64, 128), (2, 30, 22, 128, 0, 128)])
+                                   (2, 32, 32, 128, 0, 128), (3, 36, 52, 64, 64, 128), (2, 30, 22, 128, 0, 128),
+                                   (2, 15, 17, 64, 0, 128), (3, 29, 13, 128, 0, 64)])
 def test_conv3r_ex_pool(dev, shape, monkeypatch):
     """rr_igemm_ex RR_ACT_POOL: conv + bias + ReLU (+ residual) with the 2x2
     max-pool (MaxPool2d(2), floor sizes; the encoder's 14:127-131 and the VGG
@@ -466,5 +467,13 @@ def test_conv3r_ex_pool(dev, shape, monkeypatch):
     assert y0 is None and torch.equal(yp0, yp)
     y, yp, _ = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf, co, bias=b.to(dev), act=1, res=nhwc(r, dev),
                          pool=True)
+    assert rel(nchw(y), F.relu(pre + r)) < 4e-3
+    assert torch.equal(nchw(yp), F.max_pool2d(nchw(y), 2))
+    # accumulate + ReLU + pool (the eval BN-shortcut block: conv2 adds onto the
+    # 1x1 shortcut's output, engine.resblock_forward_eval_folded)
+    base = nhwc(r, dev)
+    y, yp, _ = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf, co, bias=b.to(dev), out=base,
+                         accumulate=True, act=1, pool=True)
+    assert y.data_ptr() == base.data_ptr()
     assert rel(nchw(y), F.relu(pre + r)) < 4e-3
     assert torch.equal(nchw(yp), F.max_pool2d(nchw(y), 2))

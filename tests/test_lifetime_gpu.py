@@ -172,3 +172,47 @@ def test_opcheck_every_rr_op(dev):
     u8 = o.to_uint8_hwc(x, False)
     _opcheck(o.psnr_u8.default, (u8, o.to_uint8_hwc(y, False)))
     _opcheck(o.argmax_rows.default, (torch.rand(7, 43, device=dev),))
+
+
+@pytest.mark.parametrize("nbytes", [16 * 1024, 4 * 1024 + 6, 3 << 20])
+def test_library_zero_in_hip_graph_replays(dev, nbytes):
+    """ops.zero_ (rr_zero, a library kernel) recorded in a HIP
+    graph, alone and between torch / library nodes, zeroes its buffer on
+    every replay (4 replays, the buffer refilled with garbage between them),
+    and so does RunningLoss.reset() captured with an add."""
+    import roadrestore as rr
+    from roadrestore import ops
+    n = nbytes
+    for mode in ("alone", "between"):
+        buf = torch.empty(n, dtype=torch.uint8, device=dev)
+        other = torch.ones(1024, device=dev)
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(dev)
+        with torch.cuda.graph(g):
+            if mode == "between":
+                other.mul_(2.0)
+            ops.zero_(buf)
+            if mode == "between":
+                ops.zero_(other[:7])
+                other.add_(1.0)
+        for r in range(4):
+            buf.fill_(0xA5)
+            other.fill_(3.0)
+            g.replay()
+            torch.cuda.synchronize(dev)
+            assert int(buf.count_nonzero()) == 0, (mode, r)
+            if mode == "between":
+                assert torch.all(other[:7] == 1.0) and torch.all(other[7:] == 7.0), (mode, r)
+    run = rr.RunningLoss(dev)
+    loss = torch.full((1,), 0.5, device=dev)
+    g = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize(dev)
+    with torch.cuda.graph(g):
+        run.reset()
+        run.add(loss)
+        run.add(loss)
+    for r in range(4):
+        run.acc.fill_(123.0)
+        run.count.fill_(9)
+        g.replay()
+        assert run.steps() == 2 and run.total() == 1.0, r

@@ -546,6 +546,56 @@ def test_hip_graph_step_follows_cosine_lr_schedule(dev):
     assert abs(float(oa.param_groups[0]["lr"]) - 2e-4 * (1 + math.cos(math.pi * 3 / 25)) / 2) < 1e-9
 
 
+def test_capturable_lr_is_one_persistent_tensor(dev):
+    """a capturable optimizer keeps ONE lr tensor per group.  A
+    plain ``group["lr"] = x`` (warm-up code) is copied back into it by the next
+    eager step (with a warning once a graph was captured, since replays in
+    between kept the old value); an in-place fill_ reaches replays;
+    state_dict() reports a float."""
+    import warnings
+    import roadrestore as rr
+    from roadrestore.optim import flatten_parameters
+    torch.manual_seed(3)
+    m = torch.nn.Linear(8, 8).to(dev)
+    flatten_parameters(m, list(m.parameters()))
+    gflat = torch.zeros(72, device=dev)              # grads tiling one span too (zero_grad
+    m.weight.grad = gflat[:64].view(8, 8)             # and backward accumulate in place)
+    m.bias.grad = gflat[64:]
+    opt = rr.AdamW(m.parameters(), lr=1e-3, capturable=True)
+    lr_t = opt.param_groups[0]["lr"]
+    assert isinstance(lr_t, torch.Tensor) and lr_t.is_cuda
+    x = torch.randn(4, 8, device=dev)
+
+    def step():
+        opt.zero_grad(set_to_none=False)
+        m(x).square().sum().backward()
+        opt.step()
+    step()
+    opt.param_groups[0]["lr"] = 5e-4                  # replaced before any capture: no warning
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        step()
+    assert opt.param_groups[0]["lr"] is lr_t and abs(lr_t.item() - 5e-4) < 1e-12
+    assert opt.state_dict()["param_groups"][0]["lr"] == pytest.approx(5e-4)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step()
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    p0 = m.weight.detach().clone()
+    lr_t.fill_(0.0)                                  # in place: the replay sees lr 0
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(m.weight.detach(), p0)
+    opt.param_groups[0]["lr"] = 2e-4                 # replaced after the capture
+    with pytest.warns(UserWarning, match="replaced after a HIP-graph capture"):
+        step()
+    assert opt.param_groups[0]["lr"] is lr_t and abs(lr_t.item() - 2e-4) < 1e-12
+
+
 def test_hip_graph_dp_step_with_rccl_matches_eager(dev):
     """The N > 1 bench step (DataParallel bucket all-reduces on the comm
     stream, launched from the backward's ready hooks) captured in a HIP graph:
@@ -822,3 +872,39 @@ def test_resunet_eval_mode_backward(dev):
     for k, v in m.state_dict().items():
         if "running" in k or "num_batches" in k:
             assert torch.equal(v.cpu(), sd[k].to(v.dtype)), k
+
+
+def test_resunet_bn_momentum_none_cumulative_average(dev):
+    """BatchNorm2d(momentum=None) inside the fused ResUNet engine
+    (cumulative moving average, factor 1 / num_batches_tracked read on the
+    device).  After two train forwards every running statistic is the mean of
+    the two batch statistics, which momentum=1.0 forwards give one at a time."""
+    import roadrestore as rr
+    torch.manual_seed(21)
+    a = rr.ResUNet().to(dev)
+    b = rr.ResUNet().to(dev)
+    b.load_state_dict(a.state_dict())
+    for mod in a.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.momentum = None
+    for mod in b.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.momentum = 1.0
+    a.train()
+    b.train()
+    x1 = torch.rand(2, 3, 32, 32, device=dev)
+    x2 = torch.rand(2, 3, 32, 32, device=dev)
+    names = [k for k in a.state_dict() if k.endswith("running_mean") or k.endswith("running_var")]
+    with torch.no_grad():
+        a(x1)
+        a(x2)
+        b(x1)
+        s1 = {k: b.state_dict()[k].clone() for k in names}
+        b(x2)
+        s2 = {k: b.state_dict()[k].clone() for k in names}
+    sa = a.state_dict()
+    for k in names:
+        exp = (s1[k] + s2[k]) / 2
+        err = (sa[k] - exp).abs().max().item()
+        assert err <= 1e-5 * max(1.0, exp.abs().max().item()), (k, err)
+    assert all(int(sa[k]) == 2 for k in sa if k.endswith("num_batches_tracked"))

@@ -4,7 +4,8 @@ every value of an environment switch given on the command line, e.g.
 
     python tools/ab_conv3r.py RR_CONV3R=1,0 RR_IGEMM_DBG=0,1,4,8
 
-(each NAME=v1,v2,... is swept; the first switch varies fastest)."""
+(each NAME=v1,v2,... is swept; the first switch varies fastest; the values
+alternate per layer, ROUNDS times, and each is reported as its median)."""
 import itertools
 import json
 import os
@@ -58,21 +59,31 @@ for name, H, c1, c2, co in LAYERS:
     bias = torch.randn(co, device=dev)
     data[name] = (H, c1, c2, co, x1, x2, dy, wf, wd, bias)
 combos = list(itertools.product(*[[(k, v) for v in vals] for k, vals in sweeps])) or [()]
+# the switch values alternate per layer, ROUNDS times (a box drifts by several
+# per cent over a sweep: sequential sweeps are not an A/B); median per value
+ROUNDS = int(os.environ.get("ROUNDS", 3))
 tot = {}
-for combo in combos:
-    for k, v in combo:
-        os.environ[k] = v
-    tag = " ".join(f"{k}={v}" for k, v in combo)
-    for name, (H, c1, c2, co, x1, x2, dy, wf, wd, bias) in data.items():
-        fl = 2.0 * B * H * H * co * (c1 + c2) * 9
-        d = ops.IgemmDesc(ops.RR_BF16, RR_CONV3X3, B, H, H, c1, c2, co, 0, 0, 0, 1, 0, 1, 0)
-        tf = timeit(lambda: ops.igemm(RR_CONV3X3, x1, x2, B, H, H, wf, co, bias=bias, stats=True))
-        td = timeit(lambda: ops.igemm(RR_CONV3X3, dy, None, B, H, H, wd, c1 + c2,
-                                      split=c1 if c2 else 0))
+for name, (H, c1, c2, co, x1, x2, dy, wf, wd, bias) in data.items():
+    fl = 2.0 * B * H * H * co * (c1 + c2) * 9
+    d = ops.IgemmDesc(ops.RR_BF16, RR_CONV3X3, B, H, H, c1, c2, co, 0, 0, 0, 1, 0, 1, 0)
+    meas = {}
+    for _ in range(ROUNDS):
+        for combo in combos:
+            for k, v in combo:
+                os.environ[k] = v
+            tag = " ".join(f"{k}={v}" for k, v in combo)
+            tf = timeit(lambda: ops.igemm(RR_CONV3X3, x1, x2, B, H, H, wf, co, bias=bias, stats=True))
+            td = timeit(lambda: ops.igemm(RR_CONV3X3, dy, None, B, H, H, wd, c1 + c2,
+                                          split=c1 if c2 else 0))
+            m = meas.setdefault(tag, ([], [], ops.igemm_kernel_name(d)))
+            m[0].append(tf)
+            m[1].append(td)
+    for tag, (tfs, tds, kname) in meas.items():
+        tf, td = sorted(tfs)[len(tfs) // 2], sorted(tds)[len(tds) // 2]
         t = tot.setdefault(tag, [0.0, 0.0])
         t[0] += 2 * fl
         t[1] += tf + td
-        print(json.dumps({"cfg": tag, "layer": name, "kernel": ops.igemm_kernel_name(d),
+        print(json.dumps({"cfg": tag, "layer": name, "kernel": kname,
                           "fwd_ms": round(tf, 4), "dgrad_ms": round(td, 4),
                           "fwd_tf": round(fl / tf / 1e9, 1), "dgrad_tf": round(fl / td / 1e9, 1)}),
               flush=True)
