@@ -1233,6 +1233,7 @@ static int fill_args(const rr_igemm_desc *d, const void *x1, const void *x2, con
   a.alpha = nullptr;
   a.res = nullptr;
   a.ypool = nullptr;
+  a.ntile = 0;
   return RR_OK;
 }
 

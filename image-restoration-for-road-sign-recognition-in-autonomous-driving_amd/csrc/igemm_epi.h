@@ -33,6 +33,7 @@ struct IgemmArgs {
   const float *alpha;
   const char *res;
   char *ypool;        // act & RR_ACT_POOL: [n][h/2][w/2][c_out] 2x2 max-pool of the output
+  int ntile;          // conv3r: tiles of the launch (a persistent grid walks them)
 };
 
 namespace {

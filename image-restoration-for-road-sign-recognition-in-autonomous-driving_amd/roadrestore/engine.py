@@ -773,8 +773,11 @@ def _pool_2x2(mod):
     """MaxPool2d(2) / MaxPool2d(2, 2): the window the conv epilogue pools"""
     def two(v):
         return v == 2 or v == (2, 2)
-    return (two(mod.kernel_size) and two(mod.stride if mod.stride is not None else mod.kernel_size)
-            and mod.padding in (0, (0, 0)) and mod.dilation in (1, (1, 1)) and not mod.ceil_mode)
+    ks = getattr(mod, "kernel_size", None)
+    st = getattr(mod, "stride", None)
+    return (two(ks) and two(st if st is not None else ks)
+            and getattr(mod, "padding", 0) in (0, (0, 0))
+            and getattr(mod, "dilation", 1) in (1, (1, 1)) and not getattr(mod, "ceil_mode", False))
 
 
 def vgg_layers(features, upto=None):

@@ -14,10 +14,16 @@ tile counts and split-K choices are the ones bench.py times.
   statistics.  fp32: output MAE <= 1e-4 / max 1e-3 (the golden bounds), loss
   1e-5 relative, gradient rel-L2 median <= 1e-3 with every tensor within
   5e-2 (ReLU / max-pool decision flips between fp32 summation orders, DESIGN
-  §4), running statistics 1e-5.  bf16 (the benched path): the envelope
-  measured at B=64 (test_bf16_model_gpu.py): output <= 5e-2, loss 1e-2,
-  gradient median <= 0.5 with cosine median >= 0.9, running statistics 5e-2.
-  The bf16 step is also compared with the fp32 HIP step, as before.
+  §4), running statistics 1e-5.  bf16 (the benched path): the same step is
+  also run in fp64 (the 'true' values) and by the bf16-storage emulation
+  oracle (oracle/bf16_emulation.py: fp64 with every tensor the HIP path
+  stores rounded to bf16 at the same point -- the error of an ideal bf16
+  implementation), and the HIP bf16 step must be as accurate as that ideal at
+  B=512, with the B=64 bounds of test_bf16_model_gpu.py: output rel-L2 <=
+  1.25 x ideal + 1e-3, loss <= 2 x ideal + 1e-4, gradient rel-L2 median <=
+  1.25 x ideal + 1e-3 and 90th percentile <= 1.5 x ideal + 1e-3, cosine
+  median >= ideal - 0.01; running statistics 5e-2 against fp32.  The bf16
+  step is also compared with the fp32 HIP step, as before.
 """
 import os
 
@@ -48,6 +54,60 @@ def _resunet(dev, sd, dt):
     m.load_state_dict(sd)
     m.compute_dtype = dt
     return m
+
+
+def _oracle_step(sd, perc_sd, bad, clean, emulate):
+    """the unified step (14:235-242) on the CPU oracle in fp64, or the
+    bf16-storage emulation -> (out, loss, grads), on this process's 16-thread
+    CPU share"""
+    from oracle import bf16_emulation as E
+    from oracle import reference_cpu as R
+    M = E if emulate else R
+    nt = torch.get_num_threads()
+    torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
+    try:
+        p = {k: (v.detach().clone().double() if v.dtype.is_floating_point else v.clone())
+             for k, v in sd.items()}
+        for k, v in p.items():
+            if v.dtype.is_floating_point and "running" not in k:
+                v.requires_grad_(True)
+        pp = {k: v.detach().clone().double() for k, v in perc_sd.items()}
+        out = M.resunet_forward(p, bad.double(), True)
+        loss = M.unified_loss(out, clean.double(), pp)
+        loss.backward()
+        res = (out.detach(), loss.item(),
+               {k: v.grad.detach() for k, v in p.items() if v.requires_grad})
+    finally:
+        torch.set_num_threads(nt)
+    return res
+
+
+def _check_vs_ideal(out, loss, grads, ref64, emu, zero):
+    """the HIP bf16 step as accurate as the ideal bf16 (test_bf16_model_gpu.py
+    bounds), all against fp64"""
+    o64, l64, g64 = ref64
+    oe, le, ge = emu
+    ours, ideal = [], []
+    for k, t in g64.items():
+        if k in zero or t.norm().item() < 1e-9:
+            continue
+        t = t.double()
+        for rows, g in ((ours, grads[k].double()), (ideal, ge[k].double())):
+            rows.append((_rel(g, t), (g * t).sum().item() / max((g.norm() * t.norm()).item(), 1e-300), k))
+    r_o, r_i = np.array([x[0] for x in ours]), np.array([x[0] for x in ideal])
+    c_o, c_i = np.array([x[1] for x in ours]), np.array([x[1] for x in ideal])
+    e_out, e_out_i = _rel(out, o64), _rel(oe, o64)
+    e_loss, e_loss_i = abs(loss - l64) / abs(l64), abs(le - l64) / abs(l64)
+    print(f"B=512 vs fp64, HIP bf16 / ideal bf16: out rel-L2 {e_out:.3e} / {e_out_i:.3e}; loss rel "
+          f"{e_loss:.2e} / {e_loss_i:.2e}; grad rel-L2 median {np.median(r_o):.3e} / "
+          f"{np.median(r_i):.3e}, p90 {np.percentile(r_o, 90):.3e} / {np.percentile(r_i, 90):.3e}; "
+          f"cos median {np.median(c_o):.5f} / {np.median(c_i):.5f} ({len(r_o)} tensors)")
+    print("  worst (HIP):", [(round(e, 3), k) for e, _, k in sorted(ours, reverse=True)[:5]])
+    assert e_out <= 1.25 * e_out_i + 1e-3, (e_out, e_out_i)
+    assert e_loss <= 2.0 * e_loss_i + 1e-4, (e_loss, e_loss_i)
+    assert np.median(r_o) <= 1.25 * np.median(r_i) + 1e-3, (np.median(r_o), np.median(r_i))
+    assert np.percentile(r_o, 90) <= 1.5 * np.percentile(r_i, 90) + 1e-3
+    assert np.median(c_o) >= np.median(c_i) - 0.01, (np.median(c_o), np.median(c_i))
 
 
 def test_eval_forward_full_batch_per_image_oracle(dev):
@@ -116,6 +176,9 @@ def test_train_step_full_batch_bf16_vs_fp32(dev):
     rg = {k: v.grad.detach() for k, v in p.items() if v.requires_grad}
     rb = {k: v.detach() for k, v in p.items() if not v.requires_grad}
     del out_r, loss_r, p
+    # fp64 and the ideal-bf16 emulation of the same step (the bf16 bounds)
+    ref64 = _oracle_step(sd, perc_sd, bad, clean, emulate=False)
+    emu = _oracle_step(sd, perc_sd, bad, clean, emulate=True)
     # conv biases feeding a train-mode BN: exactly-zero gradients (the HIP
     # step writes 0; the fp32 oracle's are summation noise)
     mz = rr.ResUNet()
@@ -149,8 +212,7 @@ def test_train_step_full_batch_bf16_vs_fp32(dev):
             assert np.median(r) <= 1e-3 and r.max() <= 5e-2, sorted(rows, reverse=True)[:4]
             assert e_run <= 1e-5
         else:
-            assert _rel(o, ro) <= 5e-2 and e_l <= 1e-2
-            assert np.median(r) <= 0.5 and np.median(c) >= 0.9
+            _check_vs_ideal(o, lo, g, ref64, emu, zero)
             assert e_run <= 5e-2
     o32, l32, g32, b32 = res[torch.float32]
     o16, l16, g16, b16 = res[torch.bfloat16]
