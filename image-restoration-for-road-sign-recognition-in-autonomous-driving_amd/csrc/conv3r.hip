@@ -85,8 +85,7 @@ template <int W, int BC, int NW, int NWV, int HB, int SG> struct R3 {
   static constexpr int KBYTES = 2 * WBYTES + HB * HBYTES + (SEGM ? 0 : 1024);
   static constexpr int LDS = KBYTES;
   // one 8-wave workgroup or two 4-wave workgroups per CU
-  // (NW = 128: one 4-wave workgroup per CU, one wave per SIMD, 512 registers)
-  static constexpr bool FITS = LDS <= 160 * 1024 && (NWV != 4 || NW == 128 || 2 * LDS <= 160 * 1024);
+  static constexpr bool FITS = LDS <= 160 * 1024 && (NWV != 4 || 2 * LDS <= 160 * 1024);
   static_assert(WC * WP == NWV && NM * 16 == NW, "wave grid");
   static_assert(HB == 1 || HB == 2, "halo buffers");
   static_assert(!SEGM || (SG == 1 || SG == 2), "segment width");
@@ -129,15 +128,9 @@ template <int N> __device__ __forceinline__ void vm_barrier() {
 }
 
 template <int W, int BC, int NW, int NWV, int HB, int SG>
-__global__ __launch_bounds__(64 * NWV, NW == 128 ? 1 : 8 / NWV) void conv3r_kernel(IgemmArgs a) {
+__global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) {
   using G = R3<W, BC, NW, NWV, HB, SG>;
   static_assert(G::FITS, "LDS");
-  // NW = 128: 128 x 128 wave tiles at one wave per SIMD, the stage-pipelined
-  // K loop (register double-buffered A fragments, one barrier per stage)
-  constexpr bool PIPE = NW == 128;
-  static_assert(!PIPE || (HB == 2 && !G::SEGM && NWV == 4), "pipelined geometry");
-  static_assert(!PIPE || G::HBYTES >= 16 * BC + 8 * NWV, "BN-backward constants fit a halo buffer");
-  static_assert(!PIPE || G::R * G::NS * G::NM / 2 <= 63, "vmcnt");
   constexpr int NS = G::NS, R = G::R, NM = G::NM, WC = G::WC, RS = G::RS;
   constexpr int HW = W * W;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
@@ -302,33 +295,6 @@ __global__ __launch_bounds__(64 * NWV, NW == 128 ? 1 : 8 / NWV) void conv3r_kern
   issue_w(0, 0, c0);
   vm_barrier<0>();
   int wpar = 0, hpar = 0;                            // buffers of the current stage / chunk
-  // PIPE state: the two A-fragment sets, the B rows, whether the previous
-  // stage issued a halo, whether the last epilogue issued >= EPI_OPS
-  // vector-memory ops (its unconditional stores)
-  [[maybe_unused]] i32x4 af[3][NM], bf[2][NS];
-  [[maybe_unused]] bool prev_h = false;
-  [[maybe_unused]] int epi_ops = 0;
-  constexpr int EPI_OPS = R * NS * NM / 2;
-  if constexpr (PIPE) {
-    // stage 1's weights (needed at stage 0's barrier); stage 0's A
-    // fragments and B row 0 in the order the loop's waits assume (dy = 0,
-    // 1, B0, dy = 2)
-    if (nst > 1 && !dbg_nodma && !(a.dbg & 16)) issue_w(1, 1, c0);
-#pragma unroll
-    for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-      for (int m = 0; m < NM; ++m)
-        asm volatile("ds_read_b128 %0, %1 offset:%2"
-                     : "=v"(af[dy][m]) : "v"(a_lane), "i"((dy * (BC / 16) + m) * 1024));
-    const uint32_t b0 = b_wave + loff[0];
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bf[0][s]) : "v"(b0), "i"(s * 1024));
-#pragma unroll
-    for (int m = 0; m < NM; ++m)
-      asm volatile("ds_read_b128 %0, %1 offset:%2"
-                   : "=v"(af[2][m]) : "v"(a_lane), "i"((2 * (BC / 16) + m) * 1024));
-  }
   for (;;) {
     const int tnext = tile + (xmap ? nslot : (int)gridDim.x);
     const bool has_nt = persist && tnext < (xmap ? xend : a.ntile);   // uniform
@@ -343,221 +309,105 @@ __global__ __launch_bounds__(64 * NWV, NW == 128 ? 1 : 8 / NWV) void conv3r_kern
 #pragma unroll
         for (int m = 0; m < NM; ++m) acc[o][s][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    if constexpr (PIPE) {
-      // ==== 1-wave-per-SIMD pipelined K loop (NW = 128: 128 x 128 wave
-      // tiles, 512 registers per wave) ====
-      // One barrier per stage, before row R: it publishes stage st + 1's
-      // weights (issued right after the previous stage's barrier) and,
-      // before a chunk change, the next chunk's halo; the weights two stages
-      // ahead go into this stage's buffer right after it (its readers --
-      // this stage's A fragments, loaded during the previous stage -- are
-      // done everywhere).  The A fragments of stage st + 1 replace this
-      // stage's as its taps finish: dy = 0 (last used in row R - 1) in row
-      // R, dy = 1 in row R + 1, dy = 2 after it, with the next B row 0.
-      // LDS reads in issue order:
-      //   row R: [af0'][B(R+1)]   row R+1: [af1'][B0']   tail: [af2']
-      //   row 0': [B1'] (waits for af0', B0')   row 1': [B2'] ...
-      auto read_a = [&](uint32_t aa, int dy) __attribute__((always_inline)) {
+    for (int st = 0; st < nst; ++st) {
+      const int ch = st / 3, dx = st - ch * 3;       // uniform
+      C3_STAMP(st_t);
+      const bool last = st + 1 == nst;
+      // operands of the next stage (weights: this tile's next stage or the
+      // next tile's stage 0) and of the next chunk (halo: this tile's next
+      // chunk or the next tile's chunk 0)
+      const bool next_h = HB == 2 && dx == 0 && (ch + 1 < kc || has_nt) && !dbg_nodma && !(a.dbg & 32);
+      const bool next_w = (!last || has_nt) && !dbg_nodma && !(a.dbg & 16);
+      if (HB == 1 && dx == 0 && ch > 0) {
+        // one halo buffer: every wave is past the previous chunk's last read
+        // (the barrier that ended the last stage); load this chunk's halo
+        if (!dbg_nodma && !(a.dbg & 32)) issue_h(T, ch, 0);
+        VM_BARRIER(0);
+      }
+
+      const uint32_t aa = a_lane + wpar * G::WBYTES;
+      const uint32_t ba = b_wave + (HB == 2 ? hpar * G::HBYTES : 0) +
+                          (dx == 0 ? loff[0] : (dx == 1 ? loff[1] : loff[2]));
+      const bool zlo = dx == 0 && zl[0];             // left padding column (block s = 0)
+      const bool zhi = dx == 2 && zl[2];             // right padding column (block NS - 1)
+      i32x4 af[3][NM];
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
         for (int m = 0; m < NM; ++m)
           asm volatile("ds_read_b128 %0, %1 offset:%2"
                        : "=v"(af[dy][m]) : "v"(aa), "i"((dy * (BC / 16) + m) * 1024));
-      };
-      for (int st = 0; st < nst; ++st) {
-        const int ch = st / 3, dx = st - ch * 3;     // uniform
-        const bool last = st + 1 == nst;
-        const bool has_next = !last || has_nt;
-        const bool w2_here = st + 2 < nst;
-        const bool next_w = (w2_here || has_nt) && !dbg_nodma && !(a.dbg & 16);
-        const bool next_h = dx == 0 && (ch + 1 < kc || has_nt) && !dbg_nodma && !(a.dbg & 32);
-        const uint32_t ba = b_wave + hpar * G::HBYTES + (dx == 0 ? loff[0] : (dx == 1 ? loff[1] : loff[2]));
-        const uint32_t ban = dx < 2 ? b_wave + hpar * G::HBYTES + (dx == 0 ? loff[1] : loff[2])
-                                    : b_wave + (hpar ^ 1) * G::HBYTES + loff[0];
-        const uint32_t aan = a_lane + (wpar ^ 1) * G::WBYTES;
-        const bool zlo = dx == 0 && zl[0];
-        const bool zhi = dx == 2 && zl[2];
+      i32x4 bf[2][NS];
 #pragma unroll
-        for (int ri = 0; ri < R + 2; ++ri) {
-          if (ri == R && has_next) {
-            // in flight may stay what was issued after stage st + 1's
-            // weights: the halo the previous stage issued (dx = 1) or, at a
-            // tile's first stage, the previous tile's epilogue (epi_ops: a
-            // lower bound of its stores)
-            if (st == 0 && epi_ops > 0) vm_barrier<EPI_OPS>();
-            else if (dx == 1 && prev_h) vm_barrier<G::NHG>();
-            else vm_barrier<0>();
-            if (next_w) {
-              if (w2_here) issue_w(st + 2, wpar, c0);
-              else issue_w(st + 2 - nst, wpar, c0n);
-            }
-            if (next_h) {
-              if (ch + 1 < kc) issue_h(T, ch + 1, hpar ^ 1);
-              else issue_h(TN, 0, hpar ^ 1);
-            }
-            read_a(aan, 0);
-          }
-          if (ri + 1 < R + 2) {
+      for (int s = 0; s < NS; ++s)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bf[0][s]) : "v"(ba), "i"(s * 1024));
 #pragma unroll
-            for (int s = 0; s < NS; ++s)
-              asm volatile("ds_read_b128 %0, %1 offset:%2"
-                           : "=v"(bf[(ri + 1) & 1][s]) : "v"(ba), "i"(((ri + 1) * RS + s) * 1024));
-          } else if (has_next) {
-            read_a(aan, 1);
+      for (int ri = 0; ri < R + 2; ++ri) {
+        if (ri + 1 < R + 2) {
 #pragma unroll
-            for (int s = 0; s < NS; ++s)
-              asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bf[0][s]) : "v"(ban), "i"(s * 1024));
-          }
-          if (ri == 0) {
-            asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NM + NS) : "memory");
-          } else if (ri < R) {
-            asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
-          } else if (ri == R) {
-            if (has_next) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NM + NS) : "memory");
-            else asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
-          } else {
-            if (has_next) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NM + NS) : "memory");
-            else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          }
-#pragma unroll
-          for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(bf[ri & 1][s]));
-          if (ri < 3) {
-#pragma unroll
-            for (int m = 0; m < NM; ++m) asm volatile("" : "+v"(af[ri][m]));
-          }
-          {
-            i32x4 &lo = bf[ri & 1][0];
-            i32x4 &hi = bf[ri & 1][NS - 1];
-            if (G::PAIR) {
-              if (zlo || zhi) lo = i32x4{0, 0, 0, 0};
-            } else {
-              if (zlo) lo = i32x4{0, 0, 0, 0};
-              if (zhi) hi = i32x4{0, 0, 0, 0};
-            }
-          }
-          if (prio_mfma) __builtin_amdgcn_s_setprio(1);
-          if (!dbg_nomfma) {
-#pragma unroll
-            for (int dy = 0; dy < 3; ++dy) {
-              const int o = ri - dy;
-              if (o < 0 || o >= R) continue;
-#pragma unroll
-              for (int s = 0; s < NS; ++s)
-#pragma unroll
-                for (int m = 0; m < NM; ++m)
-                  acc[o][s][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                      __builtin_bit_cast(bf16x8, af[dy][m]), __builtin_bit_cast(bf16x8, bf[ri & 1][s]),
-                      acc[o][s][m], 0, 0, 0);
-            }
-          }
-          if (prio_mfma) __builtin_amdgcn_s_setprio(0);
-        }
-        if (has_next) read_a(aan, 2);
-        prev_h = next_h;
-        epi_ops = 0;
-        wpar ^= 1;
-        if (dx == 2) hpar ^= 1;
-      }
-    } else {
-      for (int st = 0; st < nst; ++st) {
-        const int ch = st / 3, dx = st - ch * 3;       // uniform
-        C3_STAMP(st_t);
-        const bool last = st + 1 == nst;
-        // operands of the next stage (weights: this tile's next stage or the
-        // next tile's stage 0) and of the next chunk (halo: this tile's next
-        // chunk or the next tile's chunk 0)
-        const bool next_h = HB == 2 && dx == 0 && (ch + 1 < kc || has_nt) && !dbg_nodma && !(a.dbg & 32);
-        const bool next_w = (!last || has_nt) && !dbg_nodma && !(a.dbg & 16);
-        if (HB == 1 && dx == 0 && ch > 0) {
-          // one halo buffer: every wave is past the previous chunk's last read
-          // (the barrier that ended the last stage); load this chunk's halo
-          if (!dbg_nodma && !(a.dbg & 32)) issue_h(T, ch, 0);
-          VM_BARRIER(0);
-        }
-
-        const uint32_t aa = a_lane + wpar * G::WBYTES;
-        const uint32_t ba = b_wave + (HB == 2 ? hpar * G::HBYTES : 0) +
-                            (dx == 0 ? loff[0] : (dx == 1 ? loff[1] : loff[2]));
-        const bool zlo = dx == 0 && zl[0];             // left padding column (block s = 0)
-        const bool zhi = dx == 2 && zl[2];             // right padding column (block NS - 1)
-        i32x4 af[3][NM];
-  #pragma unroll
-        for (int dy = 0; dy < 3; ++dy)
-  #pragma unroll
-          for (int m = 0; m < NM; ++m)
+          for (int s = 0; s < NS; ++s)
             asm volatile("ds_read_b128 %0, %1 offset:%2"
-                         : "=v"(af[dy][m]) : "v"(aa), "i"((dy * (BC / 16) + m) * 1024));
-        i32x4 bf[2][NS];
-  #pragma unroll
-        for (int s = 0; s < NS; ++s)
-          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bf[0][s]) : "v"(ba), "i"(s * 1024));
-  #pragma unroll
-        for (int ri = 0; ri < R + 2; ++ri) {
-          if (ri + 1 < R + 2) {
-  #pragma unroll
-            for (int s = 0; s < NS; ++s)
-              asm volatile("ds_read_b128 %0, %1 offset:%2"
-                           : "=v"(bf[(ri + 1) & 1][s]) : "v"(ba), "i"(((ri + 1) * RS + s) * 1024));
-            asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
+                         : "=v"(bf[(ri + 1) & 1][s]) : "v"(ba), "i"(((ri + 1) * RS + s) * 1024));
+          asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(bf[ri & 1][s]));
+        if (ri == 0) {
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int m = 0; m < NM; ++m) asm volatile("" : "+v"(af[dy][m]));
+#ifdef RR_CONV3R_STAMPS
+          unsigned long long t1;
+          C3_STAMP(t1);
+          st_row0 += t1 - st_t;
+#endif
+        }
+        // the padding columns: zero the shifted edge reads
+        if constexpr (!G::SEGM) {
+          i32x4 &lo = bf[ri & 1][0];
+          i32x4 &hi = bf[ri & 1][NS - 1];
+          if (G::PAIR) {
+            if (zlo || zhi) lo = i32x4{0, 0, 0, 0};
           } else {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          }
-  #pragma unroll
-          for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(bf[ri & 1][s]));
-          if (ri == 0) {
-  #pragma unroll
-            for (int dy = 0; dy < 3; ++dy)
-  #pragma unroll
-              for (int m = 0; m < NM; ++m) asm volatile("" : "+v"(af[dy][m]));
-  #ifdef RR_CONV3R_STAMPS
-            unsigned long long t1;
-            C3_STAMP(t1);
-            st_row0 += t1 - st_t;
-  #endif
-          }
-          // the padding columns: zero the shifted edge reads
-          if constexpr (!G::SEGM) {
-            i32x4 &lo = bf[ri & 1][0];
-            i32x4 &hi = bf[ri & 1][NS - 1];
-            if (G::PAIR) {
-              if (zlo || zhi) lo = i32x4{0, 0, 0, 0};
-            } else {
-              if (zlo) lo = i32x4{0, 0, 0, 0};
-              if (zhi) hi = i32x4{0, 0, 0, 0};
-            }
-          }
-          if (prio_mfma) __builtin_amdgcn_s_setprio(1);
-          if (!dbg_nomfma) {
-  #pragma unroll
-            for (int dy = 0; dy < 3; ++dy) {
-              const int o = ri - dy;
-              if (o < 0 || o >= R) continue;
-  #pragma unroll
-              for (int s = 0; s < NS; ++s)
-  #pragma unroll
-                for (int m = 0; m < NM; ++m)
-                  acc[o][s][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                      __builtin_bit_cast(bf16x8, af[dy][m]), __builtin_bit_cast(bf16x8, bf[ri & 1][s]),
-                      acc[o][s][m], 0, 0, 0);
-            }
-          }
-          if (prio_mfma) __builtin_amdgcn_s_setprio(0);
-          // the DMA for the next stage / chunk goes out behind the first rows'
-          // MFMAs (issued right after the barrier, every wave of a SIMD would
-          // sit in ~60-cycle issue slots before its first MFMA); the weights
-          // first, the halo (waited for one stage later) last
-          if (ri == 0 && next_w) issue_w(last ? 0 : st + 1, wpar ^ 1, last ? c0n : c0);
-          if (ri == 1 && next_h) {
-            if (ch + 1 < kc) issue_h(T, ch + 1, hpar ^ 1);
-            else issue_h(TN, 0, hpar ^ 1);
+            if (zlo) lo = i32x4{0, 0, 0, 0};
+            if (zhi) hi = i32x4{0, 0, 0, 0};
           }
         }
-        // the next stage's weights must have landed; a next chunk's halo (issued
-        // after them) may stay in flight for one more stage
-        if (next_h) VM_BARRIER(G::NHG);
-        else VM_BARRIER(0);
-        wpar ^= 1;
-        if (HB == 2 && dx == 2) hpar ^= 1;
+        if (prio_mfma) __builtin_amdgcn_s_setprio(1);
+        if (!dbg_nomfma) {
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy) {
+            const int o = ri - dy;
+            if (o < 0 || o >= R) continue;
+#pragma unroll
+            for (int s = 0; s < NS; ++s)
+#pragma unroll
+              for (int m = 0; m < NM; ++m)
+                acc[o][s][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                    __builtin_bit_cast(bf16x8, af[dy][m]), __builtin_bit_cast(bf16x8, bf[ri & 1][s]),
+                    acc[o][s][m], 0, 0, 0);
+          }
+        }
+        if (prio_mfma) __builtin_amdgcn_s_setprio(0);
+        // the DMA for the next stage / chunk goes out behind the first rows'
+        // MFMAs (issued right after the barrier, every wave of a SIMD would
+        // sit in ~60-cycle issue slots before its first MFMA); the weights
+        // first, the halo (waited for one stage later) last
+        if (ri == 0 && next_w) issue_w(last ? 0 : st + 1, wpar ^ 1, last ? c0n : c0);
+        if (ri == 1 && next_h) {
+          if (ch + 1 < kc) issue_h(T, ch + 1, hpar ^ 1);
+          else issue_h(TN, 0, hpar ^ 1);
+        }
       }
+      // the next stage's weights must have landed; a next chunk's halo (issued
+      // after them) may stay in flight for one more stage
+      if (next_h) VM_BARRIER(G::NHG);
+      else VM_BARRIER(0);
+      wpar ^= 1;
+      if (HB == 2 && dx == 2) hpar ^= 1;
     }
 
 #ifdef RR_CONV3R_STAMPS
@@ -622,14 +472,8 @@ __global__ __launch_bounds__(64 * NWV, NW == 128 ? 1 : 8 / NWV) void conv3r_kern
       // channels of one pixel per block pair.  The channel constants go to
       // the weight buffer the next stage does not use (free since the K
       // loop's last barrier; the next tile's stage 0 barrier-guards it) ----
-      // (PIPE: the next tile's first two weight stages are in LDS / in
-      // flight; the halo buffer the finished tile's last chunk used is free)
-      float *cst = reinterpret_cast<float *>(
-          PIPE ? smem + 2 * G::WBYTES + (hpar ^ 1) * G::HBYTES : smem + (wpar ^ 1) * G::WBYTES);   // [4][BC]
+      float *cst = reinterpret_cast<float *>(smem + (wpar ^ 1) * G::WBYTES);   // [4][BC]
       double *red = reinterpret_cast<double *>(cst + 4 * BC);                 // [NWV]
-      // (PIPE: no barrier ended the K loop -- slower waves may still read
-      // the last chunk's halo there)
-      if constexpr (PIPE) asm volatile("s_barrier" ::: "memory");
       for (int i = tid; i < BC; i += G::NT) {
         cst[i] = A.bmean[c0 + i]; cst[BC + i] = A.binv[c0 + i];
         cst[2 * BC + i] = A.baff_s[c0 + i]; cst[3 * BC + i] = A.baff_b[c0 + i];
@@ -839,15 +683,11 @@ __global__ __launch_bounds__(64 * NWV, NW == 128 ? 1 : 8 / NWV) void conv3r_kern
           }
         }
     }
-    // (a lower bound of the vector-memory ops the epilogue issued after the
-    // next tile's first weights: its unconditional stores)
-    epi_ops = !(a.dbg & 1) && (a.bpart || (a.act & RR_ACT_NOFULL) == 0) ? 1 : 0;
     if (!has_nt) break;
     tile = tnext;
     T = TN;
     c0 = c0n;
-    // (PIPE: the next stage's barrier guards cst before any DMA is issued)
-    if (a.bpart && !PIPE) asm volatile("s_barrier" ::: "memory");   // every wave is done with cst
+    if (a.bpart) asm volatile("s_barrier" ::: "memory");   // every wave is done with cst
     if (HB == 1) {
       // one halo buffer: the next tile's chunk 0 loads now
       if (!dbg_nodma && !(a.dbg & 32)) issue_h(T, 0, 0);
@@ -879,13 +719,6 @@ R3Pick r3_pick(const rr_igemm_desc *d) {
   const char *e = getenv("RR_CONV3R_WG");
   const int nwv = e && (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : (d->c_out % 128 == 0 ? 8 : 4);
   R3Pick k{0, 0, 0, 0, 0};
-  // RR_CONV3R_W1=1: 128 x 128 wave tiles at one wave per SIMD with the
-  // stage-pipelined K loop (128- / 256-channel column blocks; c_in % 64 = 0)
-  const char *ew1 = getenv("RR_CONV3R_W1");
-  if (square && ew1 && atoi(ew1) == 1 && d->c_out % 128 == 0 && (d->c_in1 + d->c_in2) % 64 == 0) {
-    k = {d->c_out % 256 == 0 && W != 32 ? 256 : 128, 128, 4, 2, 0};
-    if (P % r3_tpx(k) == 0) return k;
-  }
   if (square) {
     // RR_CONV3R_BC256=0: the 256-channel column blocks take 128-channel
     // blocks (A/B); RR_CONV3R_NW32=1: 128-channel blocks of 128 x 32 wave
@@ -989,7 +822,8 @@ static long long r3_grid(long long ntile, int nw, int nwv, int hb) {
   const char *e = getenv("RR_CONV3R_PERSIST");
   const int ev = e ? atoi(e) : 1;
   if (ev == 0 || hb != 2) return ntile;
-  const long long slots = ev >= 2 ? ev : (long long)cu_count() * (nw == 128 ? 1 : 8 / nwv);
+  (void)nw;
+  const long long slots = ev >= 2 ? ev : (long long)cu_count() * (8 / nwv);
   return slots > 0 && ntile > slots ? slots : ntile;
 }
 
@@ -1032,10 +866,6 @@ int conv3r_launch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
     if (k.bc == 128) return conv3r_go<128, 32, 4, 1, 1>(d, a, st);
     return conv3r_go<64, 32, 4, 1, 1>(d, a, st);
   }
-  if (k.nw == 128) {
-    if (k.bc == 256) return conv3r_go<256, 128, 4, 2, 0>(d, a, st);
-    return conv3r_go<128, 128, 4, 2, 0>(d, a, st);
-  }
   if (k.nwv == 8) {
     if (k.bc == 256) return conv3r_go<256, 64, 8, 2, 0>(d, a, st);
     if (k.bc == 128 && k.nw == 64) return conv3r_go<128, 64, 8, 2, 0>(d, a, st);
@@ -1061,13 +891,6 @@ const char *conv3r_name(const rr_igemm_desc *d) {
     return n;
   }
   const int wi = d->w == 8 ? 0 : d->w == 16 ? 1 : 2;
-  if (k.nw == 128) {
-    // conv3r_kernel<W,BC,w1>: 128 x 128 wave tiles, one wave per SIMD
-    static char names1[3][2][40];
-    n = names1[wi][k.bc == 256];
-    if (!n[0]) snprintf(n, 40, "conv3r_kernel<%d,%d,w1>", d->w, k.bc);
-    return n;
-  }
   const int bi = k.bc == 64 ? 0 : k.bc == 256 ? 3 : (k.nw == 64 ? 1 : 2);
   const int vi = k.nwv == 8;
   n = names[wi][bi][vi];

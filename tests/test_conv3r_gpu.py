@@ -483,8 +483,6 @@ def test_conv3r_ex_pool(dev, shape, monkeypatch):
 # the next tile's first weights and halo loaded behind the current tile's
 # last stages): bitwise equal to one tile per workgroup in every epilogue
 PERSIST_SHAPES = [(6, 32, 64, 0, 128, "8"), (4, 32, 128, 64, 64, "8"), (8, 16, 128, 0, 256, "8"),
-                  (6, 32, 64, 0, 128, "w1"), (8, 16, 128, 0, 256, "w1"), (8, 16, 256, 128, 128, "w1"),
-                  (64, 8, 256, 0, 512, "w1"), (64, 8, 128, 0, 128, "w1"),
                   (8, 16, 256, 128, 128, "8"), (64, 8, 256, 0, 512, "8"), (64, 8, 128, 0, 256, "8"),
                   (3, 60, 52, 128, 0, 128, "8"), (2, 28, 28, 256, 0, 512, "8"), (2, 56, 56, 64, 64, 64, "8")]
 
@@ -501,9 +499,6 @@ def test_conv3r_persistent_bitwise(dev, shape, slots, monkeypatch):
     else:
         n, w, c1, c2, co, wgs = shape
         h = w
-    if wgs == "w1":                                  # 128 x 128 wave tiles, one wave per SIMD
-        monkeypatch.setenv("RR_CONV3R_W1", "1")
-        wgs = "8"
     monkeypatch.setenv("RR_CONV3R_WG", wgs)
     monkeypatch.setenv("RR_CONV3R_SEGWG", wgs)       # (8 waves: the double-buffered halo)
     cin = c1 + c2
@@ -550,37 +545,3 @@ def test_conv3r_persistent_bitwise(dev, shape, slots, monkeypatch):
     for i, (g, r) in enumerate(zip(got, ref)):
         assert torch.equal(g, r), (i, (g.float() - r.float()).abs().max().item())
 
-
-@pytest.mark.parametrize("shape", [(2, 32, 128, 0, 128), (4, 32, 64, 64, 128), (8, 16, 256, 0, 256),
-                                   (8, 16, 256, 128, 128), (64, 8, 512, 0, 512), (32, 8, 128, 0, 256)])
-def test_conv3r_w1_vs_torch(dev, shape, monkeypatch):
-    """128 x 128 wave tiles at one wave per SIMD (RR_CONV3R_W1=1, the
-    stage-pipelined K loop): fwd + BN statistics and dgrad vs fp32 torch on
-    bf16-exact inputs, and the kernel choice"""
-    import roadrestore as rr
-    from roadrestore._lib import RR_CONV3X3
-    ops = rr.ops
-    monkeypatch.setenv("RR_CONV3R", "1")
-    monkeypatch.setenv("RR_CONV3R_W1", "1")
-    n, w, c1, c2, co = shape
-    cin = c1 + c2
-    assert ops.igemm_kernel_name(_desc(n, w, c1, c2, co, bias=1, stats=1)).endswith(",w1>")
-    x = rnd(n, cin, w, w, seed=81).bfloat16().float()
-    wt = (rnd(co, cin, 3, 3, seed=82) / (3 * cin ** 0.5)).bfloat16().float()
-    b = rnd(co, seed=83)
-    pre = F.conv2d(x, wt, None, padding=1)
-    wf, wd = ops.pack_conv(wt.to(dev), BF)
-    x1 = nhwc(x[:, :c1], dev)
-    x2 = nhwc(x[:, c1:], dev) if c2 else None
-    y, _, st = ops.igemm(RR_CONV3X3, x1, x2, n, w, w, wf, co, bias=b.to(dev), stats=True)
-    torch.cuda.synchronize()
-    assert rel(nchw(y), pre + b[None, :, None, None]) < 4e-3
-    s = st.double().sum(0).cpu()
-    assert rel(s[:, 0], pre.double().sum((0, 2, 3))) < 1e-5
-    assert rel(s[:, 1], (pre.double() ** 2).sum((0, 2, 3))) < 1e-5
-    gy = rnd(n, co, w, w, seed=84).bfloat16().float()
-    ref = torch.nn.grad.conv2d_input(x.shape, wt, gy, padding=1)
-    if cin % 128 == 0 and w in (8, 16, 32):
-        g1, g2, _ = ops.igemm(RR_CONV3X3, nhwc(gy, dev), None, n, w, w, wd, cin, split=c1 if c2 else 0)
-        got = nchw(g1) if not c2 else torch.cat([nchw(g1), nchw(g2)], 1)
-        assert rel(got, ref) < 4e-3

@@ -575,7 +575,7 @@ def test_capturable_lr_is_one_persistent_tensor(dev):
     with warnings.catch_warnings():
         warnings.simplefilter("error")
         step()
-    assert opt.param_groups[0]["lr"] is lr_t and abs(lr_t.item() - 5e-4) < 1e-12
+    assert opt.param_groups[0]["lr"] is lr_t and abs(lr_t.item() - 5e-4) < 1e-9
     assert opt.state_dict()["param_groups"][0]["lr"] == pytest.approx(5e-4)
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
@@ -593,7 +593,7 @@ def test_capturable_lr_is_one_persistent_tensor(dev):
     opt.param_groups[0]["lr"] = 2e-4                 # replaced after the capture
     with pytest.warns(UserWarning, match="replaced after a HIP-graph capture"):
         step()
-    assert opt.param_groups[0]["lr"] is lr_t and abs(lr_t.item() - 2e-4) < 1e-12
+    assert opt.param_groups[0]["lr"] is lr_t and abs(lr_t.item() - 2e-4) < 1e-9
 
 
 def test_hip_graph_dp_step_with_rccl_matches_eager(dev):
@@ -884,12 +884,16 @@ def test_resunet_bn_momentum_none_cumulative_average(dev):
     a = rr.ResUNet().to(dev)
     b = rr.ResUNet().to(dev)
     b.load_state_dict(a.state_dict())
+    from roadrestore.nn import BatchNorm2d
+    na = 0
     for mod in a.modules():
-        if isinstance(mod, torch.nn.BatchNorm2d):
+        if isinstance(mod, BatchNorm2d):
             mod.momentum = None
+            na += 1
     for mod in b.modules():
-        if isinstance(mod, torch.nn.BatchNorm2d):
+        if isinstance(mod, BatchNorm2d):
             mod.momentum = 1.0
+    assert na >= 20
     a.train()
     b.train()
     x1 = torch.rand(2, 3, 32, 32, device=dev)
