@@ -148,13 +148,15 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   // range (its slots b / 8 interleaved), so the column blocks of a pixel
   // tile run at the same time on one XCD and share its L2 (the halo)
   const bool persist = (int)gridDim.x < a.ntile;
-  const bool xmap = a.xcd && gridDim.x % 8 == 0;
   const int nslot = (int)gridDim.x / 8, xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  // persistent: XCD x walks tiles [x * xper, (x + 1) * xper) with its slots
+  // interleaved (a grid of whole XCD slot sets); one tile per workgroup: the
+  // first nslot * 8 tiles in the same order, the rest in place
+  const bool xmap = a.xcd && (persist ? gridDim.x % 8 == 0 : (int)blockIdx.x < nslot * 8);
   const int xper = persist ? (a.ntile + 7) / 8 : nslot;   // tiles per XCD
   const int xend = min(a.ntile, (xcd + 1) * xper);
   int tile = xmap ? xcd * xper + slot : (int)blockIdx.x;
-  // (the non-persistent grid is exactly a.ntile workgroups: every tile once;
-  // a persistent XCD's last slots can be idle)
+  // (a persistent XCD's last slots can be idle)
   if (tile >= (xmap ? xend : a.ntile)) return;
 
   // pixel tile -> first pixel, image, first tile row / column

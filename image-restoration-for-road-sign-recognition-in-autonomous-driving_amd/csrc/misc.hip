@@ -1975,11 +1975,11 @@ extern "C" int rr_scalar_accumulate(const float *x, double *acc, int64_t *count,
 }
 
 // byte-range zero / copy as kernels (16-B stores over the 16-B aligned
-// body, bytes at the ends).  Not for zeroing inside a HIP-graph capture: a
-// zero node recorded from this library -- this kernel or a hipMemsetAsync --
-// reads back garbage from the graph's second replay on in torch's process
-// (tools/diag_memset2.py; torch's own fill node does not), so the captured
-// zeroing (engine.GradSink) uses torch's fill.
+// body, bytes at the ends).  Capturable: recorded in a HIP graph (alone and
+// between torch / library nodes) it zeroes on every replay
+// (tests/test_lifetime_gpu.py::test_library_zero_in_hip_graph_replays,
+// tools/diag_memset*.py; a round-3 observation of garbage after a second
+// replay does not reproduce, profiles/r4i_diag_memset2.log).
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 __global__ void zero_bytes_kernel(char *__restrict__ dst, long long head, long long nbody, long long bytes) {
   const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;

@@ -676,9 +676,12 @@ int stream3_blocks(const rr_igemm_desc *d, int bnbwd) {
   if (d->w != 64 && d->w != 32) return 0;
   if (d->c_in2 == 64) {
     // concat input (dec1: 64 + 64 -> 64): two passes, the second accumulating
-    // (RR_STREAM3_CONCAT=0: the tiled halo kernel)
+    // onto the first's bf16 half -- only with RR_STREAM3_CONCAT=1 (A/B).  By
+    // default the tap-reuse conv takes the layer in one pass with the whole
+    // K = 1152 sum in fp32: the same graph-step time (profiles/
+    // r4j_abstep_concat_splitdgrad.txt) without the extra bf16 rounding
     const char *ec = getenv("RR_STREAM3_CONCAT");
-    if ((ec && !atoi(ec)) || bnbwd || s3_concat_flags(d) < 0) return 0;
+    if (!(ec && atoi(ec)) || bnbwd || s3_concat_flags(d) < 0) return 0;
   } else if (d->c_in2 != 0 || s3_flags(d, bnbwd != 0) < 0) {
     return 0;
   }

@@ -197,9 +197,9 @@ class GradSink:
             off += p.numel()
         nz = sum(p.numel() for p in zp)
         if nz:
-            # torch's fill, not ops.zero_: a zero node recorded from the
-            # library returns garbage from a graph's second replay on
-            # (tools/diag_memset2.py)
+            # (torch's fill; the library zero is replay-safe too: round 3 saw
+            # garbage after a second replay, which tools/diag_memset*.py no
+            # longer reproduce -- test_library_zero_in_hip_graph_replays)
             self.flat[:nz].zero_()
         self.zero_count = nz
         self.hook = hook
