@@ -80,25 +80,30 @@ template <int W, int BC, int NW, int NWV, int HB, int SG> struct R3 {
   static constexpr int WBYTES = WBLK * 1024;
   static constexpr int NHG = (HBLK + NWV - 1) / NWV;   // halo DMA pieces per wave per chunk
   static constexpr int NWG = (WBLK + NWV - 1) / NWV;   // weight DMA pieces per wave per stage
+  static constexpr int SROW = BC + 4;
+  static constexpr int STG = 128 * SROW * 4 + (NWV * BC * 2 + NWV) * 4 + 256;
   // [weights x2][halo x HB][guard block]: the shifted edge reads stay inside
   // (row-segment tiles read inside their side blocks: no guard)
   static constexpr int KBYTES = 2 * WBYTES + HB * HBYTES + (SEGM ? 0 : 1024);
-  static constexpr int LDS = KBYTES;
-  // one 8-wave workgroup or two 4-wave workgroups per CU
-  static constexpr bool FITS = LDS <= 160 * 1024 && (NWV != 4 || 2 * LDS <= 160 * 1024);
+  static constexpr int BIAS = KBYTES;               // [BC] fp32 bias for the register epilogue
+  static constexpr int LDS = KBYTES + BC * 4 > STG || SEGM ? KBYTES + BC * 4 : STG;
+  static_assert(LDS <= 160 * 1024 && (NWV != 4 || 2 * LDS <= 160 * 1024), "LDS");
   static_assert(WC * WP == NWV && NM * 16 == NW, "wave grid");
   static_assert(HB == 1 || HB == 2, "halo buffers");
   static_assert(!SEGM || (SG == 1 || SG == 2), "segment width");
   static_assert(SEGM || PAIR || TR % W == 0 || W % TR == 0, "tile rows");
   static_assert(2 * WBYTES >= 1024, "the edge read of the first halo block stays in LDS");
-  static_assert(WBYTES >= 16 * BC + 8 * NWV, "BN-backward constants fit a weight buffer");
 };
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
+template <int N> __device__ __forceinline__ void vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
 #ifdef RR_CONV3R_STAMPS
-// diagnostic build only (tools/conv3r_stamps.py): per-wave sums of the K
-// loop's segments, read with rr_conv3r_stamps; never in the shipped library
+// diagnostic build only (make stamps; tools/conv3r_stamps.py): per-wave sums
+// of the K loop's segments, read with rr_conv3r_stamps; never shipped
 __device__ unsigned long long rr_c3_stamps[1 << 18];
 #define C3_STAMP(t)                                                              \
   do {                                                                          \
@@ -106,7 +111,6 @@ __device__ unsigned long long rr_c3_stamps[1 << 18];
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");   \
     __builtin_amdgcn_sched_barrier(0);                                          \
   } while (0)
-// the vmcnt wait and the barrier stamped apart
 template <int N> __device__ __forceinline__ void vm_barrier_st(unsigned long long &tw, unsigned long long &tb) {
   unsigned long long t0, t1, t2;
   C3_STAMP(t0);
@@ -123,14 +127,9 @@ template <int N> __device__ __forceinline__ void vm_barrier_st(unsigned long lon
 #define VM_BARRIER(N) vm_barrier<N>()
 #endif
 
-template <int N> __device__ __forceinline__ void vm_barrier() {
-  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
-}
-
 template <int W, int BC, int NW, int NWV, int HB, int SG>
 __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) {
   using G = R3<W, BC, NW, NWV, HB, SG>;
-  static_assert(G::FITS, "LDS");
   constexpr int NS = G::NS, R = G::R, NM = G::NM, WC = G::WC, RS = G::RS;
   constexpr int HW = W * W;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
@@ -140,55 +139,41 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   const int wc = wv % WC, wp = wv / WC;
   const int frow = lane & 15, fq = lane >> 4;
 
-  // Tiles (tile = pixel tile * ncblk + column block): one per workgroup
-  // (grid = a.ntile), or a persistent grid (gridDim.x < a.ntile) walking
-  // several: the next tile's first weights and halo load behind the current
-  // tile's last stages, and its stage 0 runs while the epilogue's stores
-  // drain.  XCD-aware order either way: XCD b % 8 walks a contiguous tile
-  // range (its slots b / 8 interleaved), so the column blocks of a pixel
-  // tile run at the same time on one XCD and share its L2 (the halo)
-  const bool persist = (int)gridDim.x < a.ntile;
-  const int nslot = (int)gridDim.x / 8, xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-  // persistent: XCD x walks tiles [x * xper, (x + 1) * xper) with its slots
-  // interleaved (a grid of whole XCD slot sets); one tile per workgroup: the
-  // first nslot * 8 tiles in the same order, the rest in place
-  const bool xmap = a.xcd && (persist ? gridDim.x % 8 == 0 : (int)blockIdx.x < nslot * 8);
-  const int xper = persist ? (a.ntile + 7) / 8 : nslot;   // tiles per XCD
-  const int xend = min(a.ntile, (xcd + 1) * xper);
-  int tile = xmap ? xcd * xper + slot : (int)blockIdx.x;
-  // (a persistent XCD's last slots can be idle)
-  if (tile >= (xmap ? xend : a.ntile)) return;
-
-  // pixel tile -> first pixel, image, first tile row / column
-  struct TileG { int pblk, p0, n0, ys, xs; };
-  auto tgeo = [&](int t) __attribute__((always_inline)) -> TileG {
-    TileG g;
-    g.pblk = t / a.ncblk;
-    g.p0 = g.pblk * G::TPX;
-    g.xs = 0;
-    if constexpr (G::SEGM) {
-      // pixel tile = (image, row band, column segment), segments fastest
-      const int nseg = (a.w + 16 * NS - 1) / (16 * NS), nband = (a.h + G::TR - 1) / G::TR;
-      const int seg = g.pblk % nseg, t2 = g.pblk / nseg;
-      const int band = t2 % nband;
-      g.n0 = t2 / nband;
-      g.ys = band * G::TR;
-      g.xs = seg * 16 * NS;
-    } else {
-      g.n0 = g.p0 / HW;
-      g.ys = G::PAIR || G::TR >= W ? 0 : (g.p0 - g.n0 * HW) / W;   // (one segment)
-    }
-    return g;
-  };
+  // XCD-aware tile order (as igemm3_halo_kernel): XCD b % 8 walks a
+  // contiguous tile range, so column blocks of a pixel tile share its L2
+  int tile = blockIdx.x;
+  if (a.xcd) {
+    const int per = (int)gridDim.x / 8;
+    if ((int)blockIdx.x < per * 8) tile = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
+  }
+  const int cblk = tile % a.ncblk, pblk = tile / a.ncblk;
+  const int c0 = cblk * BC;
+  const int p0 = pblk * G::TPX;
+  int n0, ys, xs = 0;                                // image, first tile row / column
+  if constexpr (G::SEGM) {
+    // pixel tile = (image, row band, column segment), segments fastest
+    const int nseg = (a.w + 16 * NS - 1) / (16 * NS), nband = (a.h + G::TR - 1) / G::TR;
+    const int seg = pblk % nseg, t2 = pblk / nseg;
+    const int band = t2 % nband;
+    n0 = t2 / nband;
+    ys = band * G::TR;
+    xs = seg * 16 * NS;
+  } else {
+    n0 = p0 / HW;
+    ys = G::PAIR || G::TR >= W ? 0 : (p0 - n0 * HW) / W;   // (one segment)
+  }
 
   const uint32_t sbase = (uint32_t)(uintptr_t)smem;
   const uint32_t wbase = sbase, hbase = sbase + 2 * G::WBYTES;
 
-  // ---- DMA issue (per-lane sources computed on the fly: no per-piece
-  // registers live across the K loop) ----
-  // halo block b = (segment k, halo row hr, column block s) of tile T: the
-  // pixel of this lane's 16 B (-1: zero padding)
-  auto halo_pix = [&](const TileG &T, int b) __attribute__((always_inline)) -> int {
+  // ---- per-lane DMA sources ----
+  // halo block b = (segment k, halo row hr, column block s): pixel index of
+  // this lane's 16 B (-1: zero padding row)
+  int hpix[G::NHG], hdst[G::NHG];
+#pragma unroll
+  for (int i = 0; i < G::NHG; ++i) {
+    int b = wv + NWV * i;
+    if (b >= G::HBLK) b -= NWV;                     // a duplicate of this wave's previous block
     const int k = b / ((G::HS + 2) * RS);
     const int rem = b - k * ((G::HS + 2) * RS);
     const int hr = rem / RS, s = rem - (rem / RS) * RS;
@@ -198,51 +183,56 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
       // hr - 1); s >= 1: columns 16 (s - 1) .. of row hr (one segment: the
       // trailing side block is row HS + 2)
       const int hr_ = b / RS, s_ = b - hr_ * RS;
-      int y = T.ys + hr_ - 1, x = -1;
-      if (s_ > 0) x = T.xs + 16 * (s_ - 1) + frow;
-      else if (frow == 15) x = T.xs - 1;
-      else if (frow == 0) { x = T.xs + 16 * NS; --y; }
-      if (x >= 0 && x < a.w && y >= 0 && y < a.h) pix = (T.n0 * a.h + y) * a.w + x;
+      int y = ys + hr_ - 1, x = -1;
+      if (s_ > 0) x = xs + 16 * (s_ - 1) + frow;
+      else if (frow == 15) x = xs - 1;
+      else if (frow == 0) { x = xs + 16 * NS; --y; }
+      if (x >= 0 && x < a.w && y >= 0 && y < a.h) pix = (n0 * a.h + y) * a.w + x;
     } else if constexpr (G::PAIR) {
       const int y = hr - 1;
-      if (y >= 0 && y < W) pix = ((T.n0 + 2 * k + (frow >> 3)) * W + y) * W + (frow & 7);
+      if (y >= 0 && y < W) pix = ((n0 + 2 * k + (frow >> 3)) * W + y) * W + (frow & 7);
     } else {
-      const int y = T.ys + hr - 1;
-      if (y >= 0 && y < W) pix = ((T.n0 + k) * W + y) * W + 16 * s + frow;
+      const int y = ys + hr - 1;
+      if (y >= 0 && y < W) pix = ((n0 + k) * W + y) * W + 16 * s + frow;
     }
-    return pix;
-  };
-  // the weight tiles follow the [c_out][9][c_in] pack (rr_pack_conv): tile
-  // (chunk ch, column dx, row dy, block mb), 3 contiguous runs per stage
-  const char *wpack = a.wt + (long long)a.cout * a.K * 2 + lane * 16;
-  auto issue_w = [&](int st, int buf, int c0) __attribute__((always_inline)) {
-    const char *wtile = wpack + (long long)(c0 / 16) * 1024;
+    hpix[i] = pix;
+    hdst[i] = b * 1024;
+  }
+  // weight block wb = (tap row dy, 16-channel block m): this lane's row
+  int wrow[G::NWG], wdst[G::NWG], wdy[G::NWG];
+#pragma unroll
+  for (int i = 0; i < G::NWG; ++i) {
+    int b = wv + NWV * i;
+    if (b >= G::WBLK) b -= NWV;
+    const int dy = b / (BC / 16), m = b - dy * (BC / 16);
+    wrow[i] = (c0 / 16 + m) * 1024 + lane * 16;      // block mb of the tiles, this lane's 16 B
+    wdst[i] = b * 1024;
+    wdy[i] = dy;
+  }
+  // the weight tiles follow the [c_out][9][c_in] pack (rr_pack_conv)
+  const char *wtile = a.wt + (long long)a.cout * a.K * 2;
+  auto issue_w = [&](int st) __attribute__((always_inline)) {
     const int ch = st / 3, dx = st - ch * 3;
-    char *dst = smem + buf * G::WBYTES;
+    char *dst = smem + (st & 1) * G::WBYTES;
 #pragma unroll
     for (int i = 0; i < G::NWG; ++i) {
-      int b = wv + NWV * i;
-      if (b >= G::WBLK) b -= NWV;                   // a duplicate of this wave's previous block
-      const int dy = b / (BC / 16), m = b - dy * (BC / 16);
-      const long long off = ((((long long)ch * 3 + dx) * 3 + dy) * (a.cout / 16) + m) * 1024;
-      __builtin_amdgcn_global_load_lds((const void *)(wtile + off), LDS_PTR(dst + b * 1024), 16, 0, 0);
+      // tile (chunk ch, column dx, row dy, block mb): 3 contiguous runs per stage
+      const long long off = (((long long)ch * 3 + dx) * 3 + wdy[i]) * (a.cout / 16) * 1024 + wrow[i];
+      __builtin_amdgcn_global_load_lds((const void *)(wtile + off), LDS_PTR(dst + wdst[i]), 16, 0, 0);
     }
   };
-  auto issue_h = [&](const TileG &T, int ch, int buf) __attribute__((always_inline)) {
+  auto issue_h = [&](int ch) __attribute__((always_inline)) {
     const int ci0 = ch * 32;
     const bool first = ci0 < a.c1;                  // uniform
     const char *base = first ? a.x1 : a.x2;
     const long long cs = first ? a.c1 : a.c2;
     const long long cl = first ? ci0 : ci0 - a.c1;
     const long long zoff = (long long)((uintptr_t)rr_zero_page - (uintptr_t)base) + fq * 16;
-    char *dst = smem + 2 * G::WBYTES + buf * G::HBYTES;
+    char *dst = smem + 2 * G::WBYTES + (HB == 2 ? (ch & 1) * G::HBYTES : 0);
 #pragma unroll
     for (int i = 0; i < G::NHG; ++i) {
-      int b = wv + NWV * i;
-      if (b >= G::HBLK) b -= NWV;
-      const int pix = halo_pix(T, b);
-      const long long off = pix >= 0 ? ((long long)pix * cs + cl) * 2 + fq * 16 : zoff;
-      __builtin_amdgcn_global_load_lds((const void *)(base + off), LDS_PTR(dst + b * 1024), 16, 0, 0);
+      const long long off = hpix[i] >= 0 ? ((long long)hpix[i] * cs + cl) * 2 + fq * 16 : zoff;
+      __builtin_amdgcn_global_load_lds((const void *)(base + off), LDS_PTR(dst + hdst[i]), 16, 0, 0);
     }
   };
 
@@ -277,9 +267,28 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   }
   const uint32_t b_wave = hbase + (hrow0 * RS + (G::SEGM ? 1 : 0)) * 1024;
 
+  f32x4 acc[R][NS][NM];
+#pragma unroll
+  for (int o = 0; o < R; ++o)
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int m = 0; m < NM; ++m) acc[o][s][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // the bias of the column block for the register epilogue, read before any
+  // DMA is in flight (the compiler's wait for a plain load would drain them)
+  float *lbias = reinterpret_cast<float *>(smem + G::BIAS);
+  if (!a.bpart && tid < BC) lbias[tid] = a.bias ? a.bias[c0 + tid] : 0.f;
+  __builtin_amdgcn_s_waitcnt(0x0F70);               // vmcnt(0) (gfx9 encoding)
+
   const int kc = a.cin / 32, nst = 3 * kc;
   [[maybe_unused]] unsigned long long st_vm = 0, st_bar = 0, st_row0 = 0, st_loop0 = 0, st_loop1 = 0, st_t = 0;
   C3_STAMP(st_loop0);
+  // prologue: chunk 0's halo, stage 0's weights
+  issue_h(0);
+  issue_w(0);
+  vm_barrier<0>();
+
   // diagnostics (RR_IGEMM_DBG, timing only -- results are wrong): bit2 no
   // DMA in the K loop, bit3 no MFMAs, bit0 no epilogue, bit4 no weight DMA,
   // bit5 no halo DMA
@@ -289,199 +298,159 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   // form -- the younger half of the workgroup at priority 1 for the whole
   // loop -- +1 % / -3 %).  RR_IGEMM_DBG bit7 turns it off (A/B)
   const bool prio_mfma = (a.dbg & 128) == 0;
+  for (int st = 0; st < nst; ++st) {
+    const int ch = st / 3, dx = st - ch * 3;       // uniform
+    C3_STAMP(st_t);
+    // operands of the next stage (weights) and of the next chunk (halo)
+    const bool next_h = HB == 2 && dx == 0 && ch + 1 < kc && !dbg_nodma && !(a.dbg & 32);
+    const bool next_w = st + 1 < nst && !dbg_nodma && !(a.dbg & 16);
+    if (HB == 1 && dx == 0 && ch > 0) {
+      // one halo buffer: every wave is past the previous chunk's last read
+      // (the barrier that ended the last stage); load this chunk's halo
+      if (!dbg_nodma && !(a.dbg & 32)) issue_h(ch);
+      VM_BARRIER(0);
+    }
 
-  TileG T = tgeo(tile);
-  int c0 = (tile % a.ncblk) * BC;
-  // prologue: the first tile's chunk-0 halo and stage-0 weights
-  issue_h(T, 0, 0);
-  issue_w(0, 0, c0);
-  vm_barrier<0>();
-  int wpar = 0, hpar = 0;                            // buffers of the current stage / chunk
-  for (;;) {
-    const int tnext = tile + (xmap ? nslot : (int)gridDim.x);
-    const bool has_nt = persist && tnext < (xmap ? xend : a.ntile);   // uniform
-    const TileG TN = tgeo(has_nt ? tnext : tile);
-    const int c0n = ((has_nt ? tnext : tile) % a.ncblk) * BC;
+    const uint32_t aa = a_lane + (st & 1) * G::WBYTES;
+    const uint32_t ba = b_wave + (HB == 2 ? (ch & 1) * G::HBYTES : 0) +
+                        (dx == 0 ? loff[0] : (dx == 1 ? loff[1] : loff[2]));
+    const bool zlo = dx == 0 && zl[0];               // left padding column (block s = 0)
+    const bool zhi = dx == 2 && zl[2];               // right padding column (block NS - 1)
+    i32x4 af[3][NM];
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int m = 0; m < NM; ++m)
+        asm volatile("ds_read_b128 %0, %1 offset:%2"
+                     : "=v"(af[dy][m]) : "v"(aa), "i"((dy * (BC / 16) + m) * 1024));
+    i32x4 bf[2][NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bf[0][s]) : "v"(ba), "i"(s * 1024));
+#pragma unroll
+    for (int ri = 0; ri < R + 2; ++ri) {
+      if (ri + 1 < R + 2) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+          asm volatile("ds_read_b128 %0, %1 offset:%2"
+                       : "=v"(bf[(ri + 1) & 1][s]) : "v"(ba), "i"(((ri + 1) * RS + s) * 1024));
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+#pragma unroll
+      for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(bf[ri & 1][s]));
+      if (ri == 0) {
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int m = 0; m < NM; ++m) asm volatile("" : "+v"(af[dy][m]));
+#ifdef RR_CONV3R_STAMPS
+        unsigned long long t1;
+        C3_STAMP(t1);
+        st_row0 += t1 - st_t;
+#endif
+      }
+      // the padding columns: zero the shifted edge reads
+      if constexpr (!G::SEGM) {
+        i32x4 &lo = bf[ri & 1][0];
+        i32x4 &hi = bf[ri & 1][NS - 1];
+        if (G::PAIR) {
+          if (zlo || zhi) lo = i32x4{0, 0, 0, 0};
+        } else {
+          if (zlo) lo = i32x4{0, 0, 0, 0};
+          if (zhi) hi = i32x4{0, 0, 0, 0};
+        }
+      }
+      if (prio_mfma) __builtin_amdgcn_s_setprio(1);
+      if (!dbg_nomfma) {
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) {
+          const int o = ri - dy;
+          if (o < 0 || o >= R) continue;
+#pragma unroll
+          for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int m = 0; m < NM; ++m)
+              acc[o][s][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  __builtin_bit_cast(bf16x8, af[dy][m]), __builtin_bit_cast(bf16x8, bf[ri & 1][s]),
+                  acc[o][s][m], 0, 0, 0);
+        }
+      }
+      if (prio_mfma) __builtin_amdgcn_s_setprio(0);
+      // the DMA for the next stage / chunk goes out behind the first rows'
+      // MFMAs (issued right after the barrier, every wave of a SIMD would
+      // sit in ~60-cycle issue slots before its first MFMA); the weights
+      // first, the halo (waited for one stage later) last
+      if (ri == 0 && next_w) issue_w(st + 1);
+      if (ri == 1 && next_h) issue_h(ch + 1);
+    }
+    // the next stage's weights must have landed; a next chunk's halo (issued
+    // after them) may stay in flight for one more stage
+    if (next_h) VM_BARRIER(G::NHG);
+    else VM_BARRIER(0);
+  }
+#ifdef RR_CONV3R_STAMPS
+  C3_STAMP(st_loop1);
+  if (lane == 0 && blockIdx.x < (1 << 18) / (8 * NWV)) {
+    unsigned long long *o = rr_c3_stamps + ((long long)blockIdx.x * NWV + wv) * 8;
+    o[0] = st_loop1 - st_loop0; o[1] = st_row0; o[2] = st_vm; o[3] = st_bar;
+    o[4] = (unsigned long long)nst; o[5] = 1;
+  }
+#endif
 
-    f32x4 acc[R][NS][NM];
+  if (a.dbg & 1) {
+    float t = 0.f;
 #pragma unroll
     for (int o = 0; o < R; ++o)
 #pragma unroll
       for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int m = 0; m < NM; ++m) acc[o][s][m] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    for (int st = 0; st < nst; ++st) {
-      const int ch = st / 3, dx = st - ch * 3;       // uniform
-      C3_STAMP(st_t);
-      const bool last = st + 1 == nst;
-      // operands of the next stage (weights: this tile's next stage or the
-      // next tile's stage 0) and of the next chunk (halo: this tile's next
-      // chunk or the next tile's chunk 0)
-      const bool next_h = HB == 2 && dx == 0 && (ch + 1 < kc || has_nt) && !dbg_nodma && !(a.dbg & 32);
-      const bool next_w = (!last || has_nt) && !dbg_nodma && !(a.dbg & 16);
-      if (HB == 1 && dx == 0 && ch > 0) {
-        // one halo buffer: every wave is past the previous chunk's last read
-        // (the barrier that ended the last stage); load this chunk's halo
-        if (!dbg_nodma && !(a.dbg & 32)) issue_h(T, ch, 0);
-        VM_BARRIER(0);
-      }
-
-      const uint32_t aa = a_lane + wpar * G::WBYTES;
-      const uint32_t ba = b_wave + (HB == 2 ? hpar * G::HBYTES : 0) +
-                          (dx == 0 ? loff[0] : (dx == 1 ? loff[1] : loff[2]));
-      const bool zlo = dx == 0 && zl[0];             // left padding column (block s = 0)
-      const bool zhi = dx == 2 && zl[2];             // right padding column (block NS - 1)
-      i32x4 af[3][NM];
-#pragma unroll
-      for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-        for (int m = 0; m < NM; ++m)
-          asm volatile("ds_read_b128 %0, %1 offset:%2"
-                       : "=v"(af[dy][m]) : "v"(aa), "i"((dy * (BC / 16) + m) * 1024));
-      i32x4 bf[2][NS];
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bf[0][s]) : "v"(ba), "i"(s * 1024));
-#pragma unroll
-      for (int ri = 0; ri < R + 2; ++ri) {
-        if (ri + 1 < R + 2) {
-#pragma unroll
-          for (int s = 0; s < NS; ++s)
-            asm volatile("ds_read_b128 %0, %1 offset:%2"
-                         : "=v"(bf[(ri + 1) & 1][s]) : "v"(ba), "i"(((ri + 1) * RS + s) * 1024));
-          asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
-        } else {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
-#pragma unroll
-        for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(bf[ri & 1][s]));
-        if (ri == 0) {
-#pragma unroll
-          for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-            for (int m = 0; m < NM; ++m) asm volatile("" : "+v"(af[dy][m]));
-#ifdef RR_CONV3R_STAMPS
-          unsigned long long t1;
-          C3_STAMP(t1);
-          st_row0 += t1 - st_t;
-#endif
-        }
-        // the padding columns: zero the shifted edge reads
-        if constexpr (!G::SEGM) {
-          i32x4 &lo = bf[ri & 1][0];
-          i32x4 &hi = bf[ri & 1][NS - 1];
-          if (G::PAIR) {
-            if (zlo || zhi) lo = i32x4{0, 0, 0, 0};
-          } else {
-            if (zlo) lo = i32x4{0, 0, 0, 0};
-            if (zhi) hi = i32x4{0, 0, 0, 0};
-          }
-        }
-        if (prio_mfma) __builtin_amdgcn_s_setprio(1);
-        if (!dbg_nomfma) {
-#pragma unroll
-          for (int dy = 0; dy < 3; ++dy) {
-            const int o = ri - dy;
-            if (o < 0 || o >= R) continue;
-#pragma unroll
-            for (int s = 0; s < NS; ++s)
-#pragma unroll
-              for (int m = 0; m < NM; ++m)
-                acc[o][s][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                    __builtin_bit_cast(bf16x8, af[dy][m]), __builtin_bit_cast(bf16x8, bf[ri & 1][s]),
-                    acc[o][s][m], 0, 0, 0);
-          }
-        }
-        if (prio_mfma) __builtin_amdgcn_s_setprio(0);
-        // the DMA for the next stage / chunk goes out behind the first rows'
-        // MFMAs (issued right after the barrier, every wave of a SIMD would
-        // sit in ~60-cycle issue slots before its first MFMA); the weights
-        // first, the halo (waited for one stage later) last
-        if (ri == 0 && next_w) issue_w(last ? 0 : st + 1, wpar ^ 1, last ? c0n : c0);
-        if (ri == 1 && next_h) {
-          if (ch + 1 < kc) issue_h(T, ch + 1, hpar ^ 1);
-          else issue_h(TN, 0, hpar ^ 1);
-        }
-      }
-      // the next stage's weights must have landed; a next chunk's halo (issued
-      // after them) may stay in flight for one more stage
-      if (next_h) VM_BARRIER(G::NHG);
-      else VM_BARRIER(0);
-      wpar ^= 1;
-      if (HB == 2 && dx == 2) hpar ^= 1;
+        for (int m = 0; m < NM; ++m) t += acc[o][s][m][0];
+    if (t == 1234.5f) a.y1[tid] = 1;                  // keep the accumulators live
+    return;
+  }
+  const int cb = wc * NW;                           // the wave's first column in the block
+  const int srow = pblk * G::WP + wp;               // the wave's statistics / partial row
+  // output pixel of accumulator tile (o, s) for this lane; -1: outside the
+  // image (row-segment tiles)
+  auto pix_at = [&](int o, int s) __attribute__((always_inline)) -> long long {
+    if constexpr (G::SEGM) {
+      const int y = ys + wp * R + o, x = xs + 16 * s + frow;
+      return y < a.h && x < a.w ? ((long long)n0 * a.h + y) * a.w + x : -1LL;
+    } else {
+      return (long long)p0 + wp * 128 +
+             (G::PAIR ? (frow >> 3) * 64 + o * 8 + (frow & 7) : o * W + 16 * s + frow);
     }
-
-#ifdef RR_CONV3R_STAMPS
-    C3_STAMP(st_loop1);
-    if (lane == 0 && blockIdx.x < (1 << 18) / (8 * NWV) && !persist) {
-      unsigned long long *o = rr_c3_stamps + ((long long)blockIdx.x * NWV + wv) * 8;
-      o[0] = st_loop1 - st_loop0; o[1] = st_row0; o[2] = st_vm; o[3] = st_bar;
-      o[4] = (unsigned long long)nst; o[5] = 1;
+  };
+  // 16-B stores: per pair of 16-channel blocks (2p, 2p + 1) one
+  // v_permlane16_swap per dword (odd rows of the first <-> even rows of the
+  // second) leaves lane (row fq, pixel frow) with 8 consecutive channels at
+  // 32 p + {0, 16, 8, 24}[fq]: 4 lanes write a pixel's 64 B (8-B stores of
+  // 32-B pieces were store-issue bound)
+  const int coff = (fq & 1) * 16 + (fq >> 1) * 8;
+  auto swap_pair = [&](f32x4 &va, f32x4 &vb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const auto t = __builtin_amdgcn_permlane16_swap(__float_as_uint(va[j]), __float_as_uint(vb[j]),
+                                                      false, false);
+      va[j] = __uint_as_float(t[0]);
+      vb[j] = __uint_as_float(t[1]);
     }
-#endif
-
-    // the epilogue reads its arguments through a pointer made opaque per
-    // tile, so the compiler reloads them here (scalar loads) instead of
-    // keeping ~40 SGPRs of them live across the K loop
-    const __attribute__((address_space(4))) IgemmArgs *kap =
-        (const __attribute__((address_space(4))) IgemmArgs *)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(kap));
-    const __attribute__((address_space(4))) IgemmArgs &A = *kap;
-    // ==== epilogue of tile T (registers only: the LDS holds the next
-    // tile's first operands; a BN-backward epilogue keeps its channel
-    // constants in the weight buffer the next tile does not use yet) ====
-    const int cb = wc * NW;                          // the wave's first column in the block
-    const int srow = T.pblk * G::WP + wp;            // the wave's statistics / partial row
-    // output pixel of accumulator tile (o, s) for this lane; -1: outside the
-    // image (row-segment tiles)
-    auto pix_at = [&](int o, int s) __attribute__((always_inline)) -> long long {
-      if constexpr (G::SEGM) {
-        const int y = T.ys + wp * R + o, x = T.xs + 16 * s + frow;
-        return y < A.h && x < A.w ? ((long long)T.n0 * A.h + y) * A.w + x : -1LL;
-      } else {
-        return (long long)T.p0 + wp * 128 +
-               (G::PAIR ? (frow >> 3) * 64 + o * 8 + (frow & 7) : o * W + 16 * s + frow);
-      }
-    };
-    // 16-B stores: per pair of 16-channel blocks (2p, 2p + 1) one
-    // v_permlane16_swap per dword (odd rows of the first <-> even rows of the
-    // second) leaves lane (row fq, pixel frow) with 8 consecutive channels at
-    // 32 p + {0, 16, 8, 24}[fq]: 4 lanes write a pixel's 64 B (8-B stores of
-    // 32-B pieces were store-issue bound)
-    const int coff = (fq & 1) * 16 + (fq >> 1) * 8;
-    auto swap_pair = [&](f32x4 &va, f32x4 &vb) __attribute__((always_inline)) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const auto t = __builtin_amdgcn_permlane16_swap(__float_as_uint(va[j]), __float_as_uint(vb[j]),
-                                                        false, false);
-        va[j] = __uint_as_float(t[0]);
-        vb[j] = __uint_as_float(t[1]);
-      }
-    };
-    if (A.dbg & 1) {
-      float t = 0.f;
-#pragma unroll
-      for (int o = 0; o < R; ++o)
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-#pragma unroll
-          for (int m = 0; m < NM; ++m) t += acc[o][s][m][0];
-      if (t == 1234.5f) A.y1[tid] = 1;                // keep the accumulators live
-    } else if (A.bpart) {
+  };
+  if constexpr (G::SEGM) {
+    if (a.bpart) {
       // ---- fused BN -> PReLU backward (rr_igemm_bnbwd; IgemmArgs::bpart)
       // in registers: the accumulator is dL/d(PReLU out); per lane 8
-      // channels of one pixel per block pair.  The channel constants go to
-      // the weight buffer the next stage does not use (free since the K
-      // loop's last barrier; the next tile's stage 0 barrier-guards it) ----
-      float *cst = reinterpret_cast<float *>(smem + (wpar ^ 1) * G::WBYTES);   // [4][BC]
-      double *red = reinterpret_cast<double *>(cst + 4 * BC);                 // [NWV]
+      // channels of one pixel per block pair.  The K loop's last barrier
+      // freed the LDS: the channel constants go there ----
+      float *cst = reinterpret_cast<float *>(smem);   // [4][BC] mean, invstd, aff_s, aff_b
       for (int i = tid; i < BC; i += G::NT) {
-        cst[i] = A.bmean[c0 + i]; cst[BC + i] = A.binv[c0 + i];
-        cst[2 * BC + i] = A.baff_s[c0 + i]; cst[3 * BC + i] = A.baff_b[c0 + i];
+        cst[i] = a.bmean[c0 + i]; cst[BC + i] = a.binv[c0 + i];
+        cst[2 * BC + i] = a.baff_s[c0 + i]; cst[3 * BC + i] = a.baff_b[c0 + i];
       }
-      __syncthreads();                                // (nothing in flight: the last stage drained)
-      const float al = A.balpha[0];
+      __syncthreads();
+      const float al = a.balpha[0];
       float g0[NM / 2][8], g1[NM / 2][8];
       double sa = 0.0;                                 // (fp64: igemm_epi.h store_staged_bnbwd)
 #pragma unroll
@@ -499,9 +468,9 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
             swap_pair(va, vb);
             if (p < 0) continue;
             const int cl = cb + 32 * pp + coff;          // column in the block
-            const long long e = p * A.cout + c0 + cl;
-            const f32x4 t0 = load4<bf16_t>(reinterpret_cast<const bf16_t *>(A.bt) + e);
-            const f32x4 t1 = load4<bf16_t>(reinterpret_cast<const bf16_t *>(A.bt) + e + 4);
+            const long long e = p * a.cout + c0 + cl;
+            const f32x4 t0 = load4<bf16_t>(reinterpret_cast<const bf16_t *>(a.bt) + e);
+            const f32x4 t1 = load4<bf16_t>(reinterpret_cast<const bf16_t *>(a.bt) + e + 4);
             const float g[8] = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
             const float t[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
             float gm[8];
@@ -513,7 +482,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
               g0[pp][j] += gm[j];
               g1[pp][j] += gm[j] * ((t[j] - cst[cl + j]) * cst[BC + cl + j]);
             }
-            store8<bf16_t>(reinterpret_cast<bf16_t *>(A.y1) + e, f32x4{gm[0], gm[1], gm[2], gm[3]},
+            store8<bf16_t>(reinterpret_cast<bf16_t *>(a.y1) + e, f32x4{gm[0], gm[1], gm[2], gm[3]},
                            f32x4{gm[4], gm[5], gm[6], gm[7]});
           }
         }
@@ -529,7 +498,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
       if (frow == 0) {
 #pragma unroll
         for (int pp = 0; pp < NM / 2; ++pp) {
-          f32x4 *bp = reinterpret_cast<f32x4 *>(A.bpart + ((long long)srow * A.cout + c0 + cb + 32 * pp + coff) * 3);
+          f32x4 *bp = reinterpret_cast<f32x4 *>(a.bpart + ((long long)srow * a.cout + c0 + cb + 32 * pp + coff) * 3);
           bp[0] = f32x4{g0[pp][0], g1[pp][0], 0.f, g0[pp][1]};
           bp[1] = f32x4{g1[pp][1], 0.f, g0[pp][2], g1[pp][2]};
           bp[2] = f32x4{0.f, g0[pp][3], g1[pp][3], 0.f};
@@ -542,158 +511,171 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
       // channels (a 32-channel wave adds its partner's through LDS)
 #pragma unroll
       for (int off = 1; off < 64; off <<= 1) sa += __shfl_xor(sa, off, 64);
-      float *ap = A.bapart + (long long)srow * (A.cout / 64) + (c0 + cb) / 64;
+      float *ap = a.bapart + (long long)srow * (a.cout / 64) + (c0 + cb) / 64;
       if constexpr (NW == 64) {
         if (lane == 0) *ap = (float)sa;
       } else {
+        double *red = reinterpret_cast<double *>(cst + 4 * BC);
         if (lane == 0) red[wv] = sa;
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // (stores may stay in flight)
+        __syncthreads();
         if (lane == 0 && (wc & 1) == 0) *ap = (float)(sa + red[wv + 1]);
       }
-    } else {
-      // ---- register epilogue: lane = 4 NHWC channels of one pixel per
-      // accumulator tile ----
-      if (A.stats) {
-        // per-channel partial sums of the pre-bias accumulator over the wave's
-        // 128 pixels: over (o, s) in registers, then over the 16 pixel lanes
-        // (row16_sum: the fixed xor-tree order), one partial row per 128 pixels
-        f32x4 s1[NM], s2[NM];
+      return;
+    }
+  }
+  if (G::SEGM || !a.bpart) {
+    // ---- register epilogue: lane = 4 NHWC channels of one pixel per
+    // accumulator tile ----
+    if (a.stats) {
+      // per-channel partial sums of the pre-bias accumulator over the wave's
+      // 128 pixels: over (o, s) in registers, then over the 16 pixel lanes
+      // (row16_sum: the fixed xor-tree order), one partial row per 128 pixels
+      f32x4 s1[NM], s2[NM];
 #pragma unroll
-        for (int m = 0; m < NM; ++m) { s1[m] = f32x4{0.f, 0.f, 0.f, 0.f}; s2[m] = s1[m]; }
+      for (int m = 0; m < NM; ++m) { s1[m] = f32x4{0.f, 0.f, 0.f, 0.f}; s2[m] = s1[m]; }
+#pragma unroll
+      for (int o = 0; o < R; ++o)
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          const bool ok = !G::SEGM || pix_at(o, s) >= 0;
+#pragma unroll
+          for (int m = 0; m < NM; ++m) {
+            const f32x4 v = ok ? acc[o][s][m] : f32x4{0.f, 0.f, 0.f, 0.f};
+            s1[m] += v;
+            s2[m] += v * v;
+          }
+        }
+#pragma unroll
+      for (int m = 0; m < NM; ++m)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s1[m][j] = row16_sum(s1[m][j]);
+          s2[m][j] = row16_sum(s2[m][j]);
+        }
+      if (frow == 0) {
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+          float *sp = a.stats + ((long long)srow * a.cout + c0 + cb + m * 16 + fq * 4) * 2;
+          *reinterpret_cast<f32x4 *>(sp) = f32x4{s1[m][0], s2[m][0], s1[m][1], s2[m][1]};
+          *reinterpret_cast<f32x4 *>(sp + 4) = f32x4{s1[m][2], s2[m][2], s1[m][3], s2[m][3]};
+        }
+      }
+    }
+    f32x4 bv[NM];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) bv[m] = *reinterpret_cast<const f32x4 *>(lbias + cb + m * 16 + fq * 4);
+    const int ld1 = a.split > 0 ? a.split : a.cout;
+    const int ld2 = a.cout - a.split;
+    // rr_igemm_ex RR_ACT_POOL: the 2x2 max-pool of the activated output
+    // (MaxPool2d(2, 2) after an encoder block / a VGG conv+ReLU, floor
+    // sizes) to a.ypool [n][h/2][w/2][c_out]; RR_ACT_NOFULL: only that.
+    // Rows are finished in pairs (o, o + 1: a wave's first row is even), the
+    // column pair is lane frow ^ 1 (same 8 channels after the swap)
+    const bool pool = (a.act & RR_ACT_POOL) != 0, full = (a.act & RR_ACT_NOFULL) == 0;
+    const int ph = a.h >> 1, pw = a.w >> 1;
+#pragma unroll
+    for (int o2 = 0; o2 < R; o2 += 2)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+#pragma unroll
+        for (int pp = 0; pp < NM / 2; ++pp) {
+          f32x4 fin[2][2];
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            const int o = o2 + t;
+            const long long p = pix_at(o, s);
+            f32x4 va = acc[o][s][2 * pp] + bv[2 * pp], vb = acc[o][s][2 * pp + 1] + bv[2 * pp + 1];
+            swap_pair(va, vb);
+            fin[t][0] = va;
+            fin[t][1] = vb;
+            if (G::SEGM && p < 0) continue;
+            const int c = c0 + cb + 32 * pp + coff;
+            const bool second = a.split > 0 && c >= a.split;      // uniform per pair (split % 32 == 0)
+            bf16_t *dst = second ? reinterpret_cast<bf16_t *>(a.y2) + p * ld2 + (c - a.split)
+                                 : reinterpret_cast<bf16_t *>(a.y1) + p * ld1 + c;
+            if (a.accumulate) {
+              va += load4<bf16_t>(dst);
+              vb += load4<bf16_t>(dst + 4);
+            }
+            if (a.res) {                                   // (rr_igemm_ex: y1's layout, no split)
+              const bf16_t *rp = reinterpret_cast<const bf16_t *>(a.res) + p * ld1 + c;
+              va += load4<bf16_t>(rp);
+              vb += load4<bf16_t>(rp + 4);
+            }
+            if ((a.act & 3) == RR_ACT_RELU) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) { va[j] = fmaxf(va[j], 0.f); vb[j] = fmaxf(vb[j], 0.f); }
+            } else if ((a.act & 3) == RR_ACT_PRELU) {
+              const float al = a.alpha[0];
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                va[j] = va[j] > 0.f ? va[j] : al * va[j];
+                vb[j] = vb[j] > 0.f ? vb[j] : al * vb[j];
+              }
+            }
+            if (a.has_mask) {
+              const bf16_t *mp = reinterpret_cast<const bf16_t *>(a.mask) + p * ld1 + c;
+              const f32x4 ma = load4<bf16_t>(mp), mb = load4<bf16_t>(mp + 4);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                va[j] = ma[j] > 0.f ? va[j] : 0.f;
+                vb[j] = mb[j] > 0.f ? vb[j] : 0.f;
+              }
+            }
+            fin[t][0] = va;
+            fin[t][1] = vb;
+            if (full) store8<bf16_t>(dst, va, vb);
+          }
+          if (pool) {
+            // vertical max, then the column pair (every lane shuffles)
+            f32x4 m0, m1;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              m0[j] = fmaxf(fin[0][0][j], fin[1][0][j]);
+              m1[j] = fmaxf(fin[0][1][j], fin[1][1][j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              m0[j] = max_xor1(m0[j]);
+              m1[j] = max_xor1(m1[j]);
+            }
+            const long long p = pix_at(o2, s);            // the window's top-left pixel
+            if ((frow & 1) == 0 && (!G::SEGM || p >= 0)) {
+              const int n = (int)(p / ((long long)a.h * a.w));
+              const int rem = (int)(p - (long long)n * a.h * a.w);
+              const int y = rem / a.w, x = rem - (rem / a.w) * a.w;
+              if (y + 1 < a.h && x + 1 < a.w) {             // (floor: a last odd row / column drops)
+                const int c = c0 + cb + 32 * pp + coff;
+                bf16_t *q = reinterpret_cast<bf16_t *>(a.ypool) +
+                            (((long long)n * ph + (y >> 1)) * pw + (x >> 1)) * a.cout + c;
+                store8<bf16_t>(q, m0, m1);
+              }
+            }
+          }
+        }
+      }
+    return;
+  }
+  if constexpr (!G::SEGM) {
+    // ---- BN-backward epilogue: one 128-pixel group (= one wave row of the
+    // grid) at a time as fp32 [128][BC] in LDS, then the staged store ----
+    float *stg = reinterpret_cast<float *>(smem);
+    for (int g = 0; g < G::WP; ++g) {
+      if (wp == g) {
 #pragma unroll
         for (int o = 0; o < R; ++o)
 #pragma unroll
-          for (int s = 0; s < NS; ++s) {
-            const bool ok = !G::SEGM || pix_at(o, s) >= 0;
+          for (int s = 0; s < NS; ++s)
 #pragma unroll
             for (int m = 0; m < NM; ++m) {
-              const f32x4 v = ok ? acc[o][s][m] : f32x4{0.f, 0.f, 0.f, 0.f};
-              s1[m] += v;
-              s2[m] += v * v;
+              const int r = G::PAIR ? (frow >> 3) * 64 + o * 8 + (frow & 7) : o * W + 16 * s + frow;
+              const int col = wc * NW + m * 16 + fq * 4;
+              *reinterpret_cast<f32x4 *>(stg + r * G::SROW + col) = acc[o][s][m];
             }
-          }
-#pragma unroll
-        for (int m = 0; m < NM; ++m)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            s1[m][j] = row16_sum(s1[m][j]);
-            s2[m][j] = row16_sum(s2[m][j]);
-          }
-        if (frow == 0) {
-#pragma unroll
-          for (int m = 0; m < NM; ++m) {
-            float *sp = A.stats + ((long long)srow * A.cout + c0 + cb + m * 16 + fq * 4) * 2;
-            *reinterpret_cast<f32x4 *>(sp) = f32x4{s1[m][0], s2[m][0], s1[m][1], s2[m][1]};
-            *reinterpret_cast<f32x4 *>(sp + 4) = f32x4{s1[m][2], s2[m][2], s1[m][3], s2[m][3]};
-          }
-        }
       }
-      // the bias (nothing in flight here: the K loop's last stage drained)
-      f32x4 bv[NM];
-#pragma unroll
-      for (int m = 0; m < NM; ++m)
-        bv[m] = A.bias ? *reinterpret_cast<const f32x4 *>(A.bias + c0 + cb + m * 16 + fq * 4)
-                       : f32x4{0.f, 0.f, 0.f, 0.f};
-      const int ld1 = A.split > 0 ? A.split : A.cout;
-      const int ld2 = A.cout - A.split;
-      // rr_igemm_ex RR_ACT_POOL: the 2x2 max-pool of the activated output
-      // (MaxPool2d(2, 2) after an encoder block / a VGG conv+ReLU, floor
-      // sizes) to A.ypool [n][h/2][w/2][c_out]; RR_ACT_NOFULL: only that.
-      // Rows are finished in pairs (o, o + 1: a wave's first row is even), the
-      // column pair is lane frow ^ 1 (same 8 channels after the swap)
-      const bool pool = (A.act & RR_ACT_POOL) != 0, full = (A.act & RR_ACT_NOFULL) == 0;
-      const int ph = A.h >> 1, pw = A.w >> 1;
-#pragma unroll
-      for (int o2 = 0; o2 < R; o2 += 2)
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-#pragma unroll
-          for (int pp = 0; pp < NM / 2; ++pp) {
-            f32x4 fin[2][2];
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-              const int o = o2 + t;
-              const long long p = pix_at(o, s);
-              f32x4 va = acc[o][s][2 * pp] + bv[2 * pp], vb = acc[o][s][2 * pp + 1] + bv[2 * pp + 1];
-              swap_pair(va, vb);
-              fin[t][0] = va;
-              fin[t][1] = vb;
-              if (G::SEGM && p < 0) continue;
-              const int c = c0 + cb + 32 * pp + coff;
-              const bool second = A.split > 0 && c >= A.split;      // uniform per pair (split % 32 == 0)
-              bf16_t *dst = second ? reinterpret_cast<bf16_t *>(A.y2) + p * ld2 + (c - A.split)
-                                   : reinterpret_cast<bf16_t *>(A.y1) + p * ld1 + c;
-              if (A.accumulate) {
-                va += load4<bf16_t>(dst);
-                vb += load4<bf16_t>(dst + 4);
-              }
-              if (A.res) {                                   // (rr_igemm_ex: y1's layout, no split)
-                const bf16_t *rp = reinterpret_cast<const bf16_t *>(A.res) + p * ld1 + c;
-                va += load4<bf16_t>(rp);
-                vb += load4<bf16_t>(rp + 4);
-              }
-              if ((A.act & 3) == RR_ACT_RELU) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) { va[j] = fmaxf(va[j], 0.f); vb[j] = fmaxf(vb[j], 0.f); }
-              } else if ((A.act & 3) == RR_ACT_PRELU) {
-                const float al = A.alpha[0];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                  va[j] = va[j] > 0.f ? va[j] : al * va[j];
-                  vb[j] = vb[j] > 0.f ? vb[j] : al * vb[j];
-                }
-              }
-              if (A.has_mask) {
-                const bf16_t *mp = reinterpret_cast<const bf16_t *>(A.mask) + p * ld1 + c;
-                const f32x4 ma = load4<bf16_t>(mp), mb = load4<bf16_t>(mp + 4);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                  va[j] = ma[j] > 0.f ? va[j] : 0.f;
-                  vb[j] = mb[j] > 0.f ? vb[j] : 0.f;
-                }
-              }
-              fin[t][0] = va;
-              fin[t][1] = vb;
-              if (full) store8<bf16_t>(dst, va, vb);
-            }
-            if (pool) {
-              // vertical max, then the column pair (every lane shuffles)
-              f32x4 m0, m1;
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                m0[j] = fmaxf(fin[0][0][j], fin[1][0][j]);
-                m1[j] = fmaxf(fin[0][1][j], fin[1][1][j]);
-              }
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                m0[j] = max_xor1(m0[j]);
-                m1[j] = max_xor1(m1[j]);
-              }
-              const long long p = pix_at(o2, s);            // the window's top-left pixel
-              if ((frow & 1) == 0 && (!G::SEGM || p >= 0)) {
-                const int n = (int)(p / ((long long)A.h * A.w));
-                const int rem = (int)(p - (long long)n * A.h * A.w);
-                const int y = rem / A.w, x = rem - (rem / A.w) * A.w;
-                if (y + 1 < A.h && x + 1 < A.w) {             // (floor: a last odd row / column drops)
-                  const int c = c0 + cb + 32 * pp + coff;
-                  bf16_t *q = reinterpret_cast<bf16_t *>(A.ypool) +
-                              (((long long)n * ph + (y >> 1)) * pw + (x >> 1)) * A.cout + c;
-                  store8<bf16_t>(q, m0, m1);
-                }
-              }
-            }
-          }
-        }
-    }
-    if (!has_nt) break;
-    tile = tnext;
-    T = TN;
-    c0 = c0n;
-    if (a.bpart) asm volatile("s_barrier" ::: "memory");   // every wave is done with cst
-    if (HB == 1) {
-      // one halo buffer: the next tile's chunk 0 loads now
-      if (!dbg_nodma && !(a.dbg & 32)) issue_h(T, 0, 0);
-      VM_BARRIER(0);
+      __syncthreads();
+      store_staged<bf16_t, BC, 128, G::NT, RR_CONV3X3>(a, stg, c0, p0 + g * 128, p0 / 128 + g, tid);
+      __syncthreads();
     }
   }
 }
@@ -722,18 +704,8 @@ R3Pick r3_pick(const rr_igemm_desc *d) {
   const int nwv = e && (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : (d->c_out % 128 == 0 ? 8 : 4);
   R3Pick k{0, 0, 0, 0, 0};
   if (square) {
-    // RR_CONV3R_BC256=0: the 256-channel column blocks take 128-channel
-    // blocks (A/B); RR_CONV3R_NW32=1: 128-channel blocks of 128 x 32 wave
-    // tiles on the 16x16 / 8x8 maps (half-size pixel tiles: twice the tiles
-    // for the persistent grid to walk; A/B)
-    const char *e256 = getenv("RR_CONV3R_BC256");
-    const char *e32 = getenv("RR_CONV3R_NW32");
-    const bool nw32 = e32 && atoi(e32) == 1 && W <= 16 && d->c_out % 128 == 0;
-    const bool bc256 = !(e256 && atoi(e256) == 0) && !nw32;
-    if (nwv == 8 && nw32) {
-      k = {128, 32, 8, 2, 0};
-    } else if (nwv == 8) {
-      if (d->c_out % 256 == 0 && bc256) {
+    if (nwv == 8) {
+      if (d->c_out % 256 == 0) {
         if (W != 8 || (P / 256) * (d->c_out / 256) >= 256 || P % 256) k = {256, 64, 8, 2, 0};
         else k = {128, 32, 8, 2, 0};
       } else if (d->c_out % 128 == 0) {
@@ -804,38 +776,12 @@ int conv3r_stat_blocks(const rr_igemm_desc *d) {
   return (int)(r3_ptiles(d, k) * (k.nwv / (k.bc / k.nw)));   // one row per wave row of a tile
 }
 
-// Persistent grid (RR_CONV3R_PERSIST, default on): where the halo is double
-// buffered (the next tile's chunk 0 can load behind the current tile's last
-// chunk) and there are more tiles than workgroup slots, the grid is the
-// slots (one 8-wave or two 4-wave workgroups per CU).
-// RR_CONV3R_PERSIST=0: one tile per workgroup; =N >= 2: N slots (tests: many
-// uneven tiles per workgroup on small inputs)
-static int cu_count() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    hipDeviceProp_t pr;
-    n = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&pr, dev) == hipSuccess &&
-         pr.multiProcessorCount > 0) ? pr.multiProcessorCount : 256;
-  }
-  return n;
-}
-static long long r3_grid(long long ntile, int nw, int nwv, int hb) {
-  const char *e = getenv("RR_CONV3R_PERSIST");
-  const int ev = e ? atoi(e) : 1;
-  if (ev == 0 || hb != 2) return ntile;
-  (void)nw;
-  const long long slots = ev >= 2 ? ev : (long long)cu_count() * (8 / nwv);
-  return slots > 0 && ntile > slots ? slots : ntile;
-}
-
 template <int BC, int NW, int NWV, int HB, int SG>
 static int conv3r_go(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   a.ncblk = a.cout / BC;
   const long long nblk = r3_ptiles(d, R3Pick{BC, NW, NWV, HB, SG}) * a.ncblk;
   if (nblk <= 0 || nblk > 0x7fffffffLL) return RR_EUNSUPPORTED;
-  a.ntile = (int)nblk;
-  const dim3 grid((unsigned)r3_grid(nblk, NW, NWV, HB)), block(64 * NWV);
+  const dim3 grid((unsigned)nblk), block(64 * NWV);
   if constexpr (SG > 0) {
     hipLaunchKernelGGL((conv3r_kernel<0, BC, NW, NWV, HB, SG>), grid, block, 0, st, a);
   } else {

@@ -478,70 +478,3 @@ def test_conv3r_ex_pool(dev, shape, monkeypatch):
     assert rel(nchw(y), F.relu(pre + r)) < 4e-3
     assert torch.equal(nchw(yp), F.max_pool2d(nchw(y), 2))
 
-
-# persistent grid (RR_CONV3R_PERSIST=N: N workgroup slots walking the tiles,
-# the next tile's first weights and halo loaded behind the current tile's
-# last stages): bitwise equal to one tile per workgroup in every epilogue
-PERSIST_SHAPES = [(6, 32, 64, 0, 128, "8"), (4, 32, 128, 64, 64, "8"), (8, 16, 128, 0, 256, "8"),
-                  (8, 16, 256, 128, 128, "8"), (64, 8, 256, 0, 512, "8"), (64, 8, 128, 0, 256, "8"),
-                  (3, 60, 52, 128, 0, 128, "8"), (2, 28, 28, 256, 0, 512, "8"), (2, 56, 56, 64, 64, 64, "8")]
-
-
-@pytest.mark.parametrize("shape", PERSIST_SHAPES)
-@pytest.mark.parametrize("slots", ["3", "7"])
-def test_conv3r_persistent_bitwise(dev, shape, slots, monkeypatch):
-    import roadrestore as rr
-    from roadrestore._lib import RR_CONV3X3
-    ops = rr.ops
-    monkeypatch.setenv("RR_CONV3R", "1")
-    if len(shape) == 7:
-        n, h, w, c1, c2, co, wgs = shape
-    else:
-        n, w, c1, c2, co, wgs = shape
-        h = w
-    monkeypatch.setenv("RR_CONV3R_WG", wgs)
-    monkeypatch.setenv("RR_CONV3R_SEGWG", wgs)       # (8 waves: the double-buffered halo)
-    cin = c1 + c2
-    x = rnd(n, cin, h, w, seed=91)
-    x1 = nhwc(x[:, :c1], dev)
-    x2 = nhwc(x[:, c1:], dev) if c2 else None
-    wt = (rnd(co, cin, 3, 3, seed=92) / (3 * cin ** 0.5)).to(dev)
-    wf, wd = ops.pack_conv(wt, BF)
-    b = rnd(co, seed=93).to(dev)
-    base = nhwc(rnd(n, co, h, w, seed=94), dev)
-    msk = nhwc(rnd(n, co, h, w, seed=95), dev)
-    gy = nhwc(rnd(n, co, h, w, seed=96), dev)
-    t1 = nhwc(rnd(n, cin, h, w, seed=97) + 0.2, dev)
-    mean = t1.float().reshape(-1, cin).mean(0)
-    inv = 1.0 / torch.sqrt(t1.float().reshape(-1, cin).var(0, unbiased=False) + 1e-5)
-    s1 = (torch.rand(cin, generator=torch.Generator().manual_seed(98)) + 0.5).to(dev) * inv
-    sh1 = -mean * s1
-    alpha = torch.tensor([0.2], device=dev)
-    assert ops.igemm_kernel_name(_desc(n, w, c1, c2, co, bias=1, stats=1, h=h)).startswith("conv3r")
-
-    def run():
-        out = []
-        y, _, st = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf, co, bias=b, stats=True)
-        out += [y, st]
-        y = base.clone()
-        ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf, co, bias=b, out=y, accumulate=True, act=1,
-                  mask=msk)
-        out.append(y)
-        g1, g2, _ = ops.igemm(RR_CONV3X3, gy, None, n, h, w, wd, cin, split=c1 if c2 else 0)
-        out += [g1] + ([g2] if c2 else [])
-        if not c2:
-            gm, part, _, _ = ops.igemm_bnbwd(RR_CONV3X3, gy, n, h, w, wd, cin, t1, mean, inv, s1,
-                                             sh1, alpha)
-            out += [gm, part]
-            if h % 2 == 0 and w % 2 == 0:
-                y, yp, _ = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf, co, bias=b, act=1, pool=True)
-                out += [y, yp]
-        torch.cuda.synchronize()
-        return [t.clone() for t in out]
-    monkeypatch.setenv("RR_CONV3R_PERSIST", "0")
-    ref = run()
-    monkeypatch.setenv("RR_CONV3R_PERSIST", slots)
-    got = run()
-    for i, (g, r) in enumerate(zip(got, ref)):
-        assert torch.equal(g, r), (i, (g.float() - r.float()).abs().max().item())
-

@@ -8,7 +8,7 @@ RR_CONV3R_STAMPS) sums per wave the s_memtime segments of every stage:
   rest  everything else in the loop (MFMA issue, B-row reads, DMA issue)
 
 Read the SHARES, not the totals: every stamp drains the LDS reads in flight.
-Usage: python tools/conv3r_stamps.py [RR_CONV3R_RING=2,3 ...] (cfg3 layers, B=512)."""
+Usage: python tools/conv3r_stamps.py [NAME=v1,v2 ...] (env switches to sweep; cfg3 layers, B=512)."""
 import ctypes as C
 import itertools
 import json
