@@ -123,8 +123,14 @@ class KernelProbe:
 
 def _latest_pmc():
     import glob
-    c = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json")),
-               key=lambda f: (len(os.path.basename(f).split("_")[0]), os.path.basename(f)))
+    import re
+
+    def order(f):
+        # run tags are r<round><letters>: r4q is newer than r3aq (round first,
+        # then a, ..., z, aa, ...)
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(f))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+    c = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json")), key=order)
     return c[-1] if c else None
 
 

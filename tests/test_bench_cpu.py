@@ -51,3 +51,16 @@ def test_self_launch_maps_ranks(tmp_path):
         assert g["RANK"] == str(r) and g["LOCAL_RANK"] == str(r)
         assert g["WORLD_SIZE"] == "2" and g["MASTER_ADDR"] == "127.0.0.1"
         assert g["argv"] == ["--gpus", "2", "--steps", "3"]
+
+
+def test_roofline_traffic_reads_the_newest_pmc_summary():
+    """roofline.traffic comes from the newest committed PMC summary: run tags
+    order by round, then by letters (r4q after r3aq, r3aa after r3z)."""
+    import bench
+    base = os.path.basename(bench.PMC_TRAFFIC)
+    tags = sorted(f.split("_")[0] for f in os.listdir(os.path.join(REPO, "profiles"))
+                  if f.endswith("_pmc_traffic.json"))
+    rounds = [int("".join(ch for ch in t[1:] if ch.isdigit())) for t in tags]
+    assert int("".join(ch for ch in base.split("_")[0][1:] if ch.isdigit())) == max(rounds)
+    bytes_, per = bench.pmc_traffic("conv3r_kernel")
+    assert bytes_ and per and all(v["hbm_bytes_per_launch"] > 0 for v in per.values())
