@@ -93,6 +93,7 @@ template <int W, int BC, int NW, int NWV, int HB, int SG> struct R3 {
   static_assert(!SEGM || (SG == 1 || SG == 2), "segment width");
   static_assert(SEGM || PAIR || TR % W == 0 || W % TR == 0, "tile rows");
   static_assert(2 * WBYTES >= 1024, "the edge read of the first halo block stays in LDS");
+  static_assert(2 * NM + NS <= 15, "lgkmcnt of the row-0 wait");
 };
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -199,27 +200,26 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     hdst[i] = b * 1024;
   }
   // weight block wb = (tap row dy, 16-channel block m): this lane's row
-  int wrow[G::NWG], wdst[G::NWG], wdy[G::NWG];
+  int wrow[G::NWG], wdst[G::NWG];
 #pragma unroll
   for (int i = 0; i < G::NWG; ++i) {
     int b = wv + NWV * i;
     if (b >= G::WBLK) b -= NWV;
     const int dy = b / (BC / 16), m = b - dy * (BC / 16);
-    wrow[i] = (c0 / 16 + m) * 1024 + lane * 16;      // block mb of the tiles, this lane's 16 B
+    // (row dy of the stage's 3 runs, block mb of the tiles, this lane's 16 B)
+    wrow[i] = (dy * (a.cout / 16) + c0 / 16 + m) * 1024 + lane * 16;
     wdst[i] = b * 1024;
-    wdy[i] = dy;
   }
   // the weight tiles follow the [c_out][9][c_in] pack (rr_pack_conv)
   const char *wtile = a.wt + (long long)a.cout * a.K * 2;
   auto issue_w = [&](int st) __attribute__((always_inline)) {
     const int ch = st / 3, dx = st - ch * 3;
     char *dst = smem + (st & 1) * G::WBYTES;
+    // tiles (chunk ch, column dx, row dy, block mb): 3 contiguous runs per stage
+    const char *wst = wtile + (long long)((ch * 3 + dx) * 3) * (a.cout / 16) * 1024;
 #pragma unroll
-    for (int i = 0; i < G::NWG; ++i) {
-      // tile (chunk ch, column dx, row dy, block mb): 3 contiguous runs per stage
-      const long long off = (((long long)ch * 3 + dx) * 3 + wdy[i]) * (a.cout / 16) * 1024 + wrow[i];
-      __builtin_amdgcn_global_load_lds((const void *)(wtile + off), LDS_PTR(dst + wdst[i]), 16, 0, 0);
-    }
+    for (int i = 0; i < G::NWG; ++i)
+      __builtin_amdgcn_global_load_lds((const void *)(wst + wrow[i]), LDS_PTR(dst + wdst[i]), 16, 0, 0);
   };
   auto issue_h = [&](int ch) __attribute__((always_inline)) {
     const int ci0 = ch * 32;
@@ -290,14 +290,14 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   vm_barrier<0>();
 
   // diagnostics (RR_IGEMM_DBG, timing only -- results are wrong): bit2 no
-  // DMA in the K loop, bit3 no MFMAs, bit0 no epilogue, bit4 no weight DMA,
-  // bit5 no halo DMA
-  const bool dbg_nodma = (a.dbg & 4) != 0, dbg_nomfma = (a.dbg & 8) != 0;
+  // DMA in the K loop, bit0 no epilogue, bit4 no weight DMA, bit5 no halo
+  // DMA (per stage; nothing run-time-switched inside the row loop: each such
+  // switch is a scalar branch around every row's MFMA cluster)
+  const bool dbg_nodma = (a.dbg & 4) != 0;
   // every row's MFMA cluster at wave priority 1 (cdna_hip_programming.md
   // T5): +3.3-3.5 % on both layer sets (profiles/r3aa_ab*.jsonl; the static
   // form -- the younger half of the workgroup at priority 1 for the whole
-  // loop -- +1 % / -3 %).  RR_IGEMM_DBG bit7 turns it off (A/B)
-  const bool prio_mfma = (a.dbg & 128) == 0;
+  // loop -- +1 % / -3 %)
   for (int st = 0; st < nst; ++st) {
     const int ch = st / 3, dx = st - ch * 3;       // uniform
     C3_STAMP(st_t);
@@ -316,17 +316,24 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
                         (dx == 0 ? loff[0] : (dx == 1 ? loff[1] : loff[2]));
     const bool zlo = dx == 0 && zl[0];               // left padding column (block s = 0)
     const bool zhi = dx == 2 && zl[2];               // right padding column (block NS - 1)
+    // fragment reads in the order the rows need them: row 0 uses only the
+    // dy = 0 taps, so A(dy 0) and halo row 0 go first and row 0's MFMAs
+    // start after NM + NS reads; A(dy 1, 2) and halo row 1 land behind them
+    // (waited for at row 1)
     i32x4 af[3][NM];
-#pragma unroll
-    for (int dy = 0; dy < 3; ++dy)
+    i32x4 bf[2][NS];
+    auto read_a = [&](int dy) __attribute__((always_inline)) {
 #pragma unroll
       for (int m = 0; m < NM; ++m)
         asm volatile("ds_read_b128 %0, %1 offset:%2"
                      : "=v"(af[dy][m]) : "v"(aa), "i"((dy * (BC / 16) + m) * 1024));
-    i32x4 bf[2][NS];
+    };
+    read_a(0);
 #pragma unroll
     for (int s = 0; s < NS; ++s)
       asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bf[0][s]) : "v"(ba), "i"(s * 1024));
+    read_a(1);
+    read_a(2);
 #pragma unroll
     for (int ri = 0; ri < R + 2; ++ri) {
       if (ri + 1 < R + 2) {
@@ -334,7 +341,8 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
         for (int s = 0; s < NS; ++s)
           asm volatile("ds_read_b128 %0, %1 offset:%2"
                        : "=v"(bf[(ri + 1) & 1][s]) : "v"(ba), "i"(((ri + 1) * RS + s) * 1024));
-        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
+        if (ri == 0) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(2 * NM + NS) : "memory");
+        else asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
       } else {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
@@ -342,14 +350,18 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
       for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(bf[ri & 1][s]));
       if (ri == 0) {
 #pragma unroll
-        for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-          for (int m = 0; m < NM; ++m) asm volatile("" : "+v"(af[dy][m]));
+        for (int m = 0; m < NM; ++m) asm volatile("" : "+v"(af[0][m]));
 #ifdef RR_CONV3R_STAMPS
         unsigned long long t1;
         C3_STAMP(t1);
         st_row0 += t1 - st_t;
 #endif
+      }
+      if (ri == 1) {
+#pragma unroll
+        for (int dy = 1; dy < 3; ++dy)
+#pragma unroll
+          for (int m = 0; m < NM; ++m) asm volatile("" : "+v"(af[dy][m]));
       }
       // the padding columns: zero the shifted edge reads
       if constexpr (!G::SEGM) {
@@ -362,22 +374,20 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
           if (zhi) hi = i32x4{0, 0, 0, 0};
         }
       }
-      if (prio_mfma) __builtin_amdgcn_s_setprio(1);
-      if (!dbg_nomfma) {
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int dy = 0; dy < 3; ++dy) {
-          const int o = ri - dy;
-          if (o < 0 || o >= R) continue;
+      for (int dy = 0; dy < 3; ++dy) {
+        const int o = ri - dy;
+        if (o < 0 || o >= R) continue;
 #pragma unroll
-          for (int s = 0; s < NS; ++s)
+        for (int s = 0; s < NS; ++s)
 #pragma unroll
-            for (int m = 0; m < NM; ++m)
-              acc[o][s][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                  __builtin_bit_cast(bf16x8, af[dy][m]), __builtin_bit_cast(bf16x8, bf[ri & 1][s]),
-                  acc[o][s][m], 0, 0, 0);
-        }
+          for (int m = 0; m < NM; ++m)
+            acc[o][s][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8, af[dy][m]), __builtin_bit_cast(bf16x8, bf[ri & 1][s]),
+                acc[o][s][m], 0, 0, 0);
       }
-      if (prio_mfma) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_setprio(0);
       // the DMA for the next stage / chunk goes out behind the first rows'
       // MFMAs (issued right after the barrier, every wave of a SIMD would
       // sit in ~60-cycle issue slots before its first MFMA); the weights

@@ -16,7 +16,6 @@ struct S3Args {
   float *stats;              // [nwg][64][2] pre-bias partial sums or null
   int n, h;                  // w is the template width
   int act, accumulate;
-  int prio;                  // wave priority 1 around the MFMA clusters (RR_MFMA_PRIO=0: off)
   // BN -> PReLU backward epilogue (rr_igemm_bnbwd), bt != null selects it
   const char *bt;
   const float *bmean, *binv, *baff_s, *baff_b, *balpha;

@@ -332,7 +332,7 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
       }
 #pragma unroll
       for (int ni = 0; ni < MP; ++ni) asm volatile("" : "+v"(fb[q & 1][ni]));
-      if (a.prio) __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int mi = 0; mi < MC; ++mi)
 #pragma unroll
@@ -340,7 +340,7 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
               wr[mi][q >> 1][q & 1], __builtin_bit_cast(bf16x8, fb[q & 1][ni]),
               q == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[mi][ni], 0, 0, 0);
-      if (a.prio) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_setprio(0);
     }
   };
   // epilogue: lane = pixel (frow) x 4 channels of each 16 x 16 block
@@ -696,8 +696,6 @@ int stream3_blocks(const rr_igemm_desc *d, int bnbwd) {
 int stream3_launch(const rr_igemm_desc *d, const S3Args &a0, int bnbwd, hipStream_t st) {
   if (!stream3_blocks(d, bnbwd)) return RR_EUNSUPPORTED;
   S3Args a = a0;
-  const char *pe = getenv("RR_MFMA_PRIO");
-  a.prio = !(pe && atoi(pe) == 0);
   const int P = d->n * d->h * d->w;
   auto go = [&](const S3Args &x, int f) { return d->w == 64 ? launch_w<64>(x, f, P, st) : launch_w<32>(x, f, P, st); };
   if (d->c_in2 == 64) {

@@ -14,7 +14,6 @@ struct SWArgs {
   int n, h;                  // w is the template width
   int nwg_ps;                // workgroups per (dy slice, input slice) pair
   int nsteps;                // 128-pixel steps (n h w / 128)
-  int prio;                  // wave priority 1 around the MFMA pairs (RR_MFMA_PRIO=0: off)
   unsigned long long *ts;    // debug phase timestamps [nwg][4] or null
 };
 

@@ -270,14 +270,14 @@ __global__ __launch_bounds__(512, 2) void swgrad_kernel(SWArgs a) {
         }
         const bf16x8 fb = __builtin_bit_cast(
             bf16x8, __builtin_shufflevector(rb[gi % (PF + 1)][0], rb[gi % (PF + 1)][1], 0, 1, 2, 3, 4, 5, 6, 7));
-        if (a.prio) __builtin_amdgcn_s_setprio(1);
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
           const bf16x8 fa = __builtin_bit_cast(
               bf16x8, __builtin_shufflevector(ra[kk & 1][m][0], ra[kk & 1][m][1], 0, 1, 2, 3, 4, 5, 6, 7));
           acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[m][t], 0, 0, 0);
         }
-        if (a.prio) __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(0);
       }
     }
     advance(cp);
@@ -360,10 +360,6 @@ int swgrad_launch(const rr_wgrad_desc *d, const void *dy, const void *x1, const 
   if (ts && !tsb && hipMalloc(&tsb, SW_WG * 4 * 8) != hipSuccess) tsb = nullptr;
   a.ts = ts ? tsb : nullptr;
   const dim3 grid(a.nwg_ps * S), block(512);
-  {
-    const char *pe = getenv("RR_MFMA_PRIO");
-    a.prio = !(pe && atoi(pe) == 0);
-  }
   if (d->w == 64) hipLaunchKernelGGL(swgrad_kernel<64>, grid, block, 0, st, a);
   else hipLaunchKernelGGL(swgrad_kernel<32>, grid, block, 0, st, a);
   RR_CHECK_LAUNCH();

@@ -282,7 +282,6 @@ struct Halo3Args {
   int split_stages;        // stages per split
   int nablk, nbblk;
   int xcd;                 // XCD-aware workgroup order (RR_XCD_MAP)
-  int prio;                // wave priority 1 around the MFMA clusters (RR_MFMA_PRIO=0: off)
 };
 
 // MA: 16-row MFMA blocks of dy channels per wave (the wave tile is 16 MA dy
@@ -414,13 +413,13 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
           fb[j] = tr_frag(sB + (hr0 + toff) * RS + col * 2 + pp * 8,
                           sB + (hr1 + toff) * RS + col * 2 + pp * 8);
         }
-        if (a.prio) __builtin_amdgcn_s_setprio(1);
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < MA; ++i)
 #pragma unroll
           for (int j = 0; j < MB; ++j)
             acc[i][j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j][t], 0, 0, 0);
-        if (a.prio) __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(0);
       }
     }
   };
@@ -744,10 +743,6 @@ extern "C" int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
     ha.stages = hp.stages; ha.split_stages = hp.split_stages;
     ha.nablk = ha.CA / 64; ha.nbblk = ha.CB / 64;
     ha.xcd = a.xcd;
-    {
-      const char *pe = getenv("RR_MFMA_PRIO");
-      ha.prio = !(pe && atoi(pe) == 0);
-    }
     const dim3 grid((unsigned)(ha.nablk * ha.nbblk * hp.nsplit)), block(256);
     // RR_WGRAD_HALO_MA=2: the 2 x 2 wave tiles (A/B)
     const char *mae = getenv("RR_WGRAD_HALO_MA");

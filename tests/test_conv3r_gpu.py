@@ -478,3 +478,4 @@ def test_conv3r_ex_pool(dev, shape, monkeypatch):
     assert rel(nchw(y), F.relu(pre + r)) < 4e-3
     assert torch.equal(nchw(yp), F.max_pool2d(nchw(y), 2))
 
+

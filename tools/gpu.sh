@@ -18,6 +18,7 @@
 #   abstep:NAME=a,b  graph-step A/B of one switch, alternating, 3 rounds
 #                                                               -> <tag>_abstep.txt
 #   ablibs:PATH      graph-step A/B of this build vs another .so -> <tag>_ablibs.txt
+#   abconv:PATH      per-layer conv3r A/B of this build vs another .so -> <tag>_abconv.txt
 #   py:SCRIPT[;ARGS] python SCRIPT ARGS                         -> <tag>_py.log
 set -o pipefail
 TAG=$1; shift
@@ -80,6 +81,21 @@ run_step() {
       done
       unset RR_LIB_PATH
       cat ${O}_ablibs.txt ;;
+    abconv)
+      # per-layer conv3r A/B of this build vs another .so (cfg3 and the 224
+      # set), alternating processes, 3 rounds
+      for i in 1 2 3; do
+        for L in cur other; do
+          for S in cfg3 224; do
+            if [ $L = other ]; then export RR_LIB_PATH=$arg; else unset RR_LIB_PATH; fi
+            if [ $S = 224 ]; then export SET=224; else unset SET; fi
+            timeout -k 10 150 python -u tools/ab_conv3r.py > ${O}_abconv.log 2>&1 || return 1
+            echo "$L $S $(tail -1 ${O}_abconv.log)" >> ${O}_abconv.txt
+          done
+        done
+      done
+      unset RR_LIB_PATH SET
+      cat ${O}_abconv.txt ;;
     py)
       local script=${arg%%;*} rest=""
       [ "$script" != "$arg" ] && rest=${arg#*;}
