@@ -163,17 +163,22 @@ def test_wgrad(dev, dt, k):
     close(dw.cpu(), wt.grad, dt, scale=wt.grad.abs().max().item())
 
 
-@pytest.mark.parametrize("hw", [(8, 8), (16, 16), (12, 32), (2, 64)])
+@pytest.mark.parametrize("hw", [(8, 8), (16, 16), (12, 32), (2, 64), (1, 8, 8), (3, 8, 8), (1, 16, 16)])
 @pytest.mark.parametrize("halo", [True, False])
 def test_wgrad3_halo(dev, hw, halo, monkeypatch):
     """bf16 3x3 weight grad through the LDS-halo kernel (64-pixel stages of
     whole image rows, zero-padded halo) and through the per-tap kernel, with a
-    concat second source (dec*.c1 shape), vs fp32 torch."""
+    concat second source (dec*.c1 shape), vs fp32 torch.  (n, h, w) cases
+    give splits of 1-3 stages: the prefetching loop runs past a split's end
+    with clamped loads and LDS writes no stage reads."""
     import roadrestore as rr
     from roadrestore._lib import RR_CONV3X3
     monkeypatch.setenv("RR_WGRAD_NOHALO", "0" if halo else "1")
+    n = 5
+    if len(hw) == 3:
+        n, hw = hw[0], hw[1:]
     h, w = hw
-    n, c1, c2, cout = 5, 64, 128, 128
+    c1, c2, cout = 64, 128, 128
     x = rnd(n, c1 + c2, h, w, seed=30).bfloat16().float()
     g = rnd(n, cout, h, w, seed=31).bfloat16().float()
     wt = torch.zeros(cout, c1 + c2, 3, 3, requires_grad=True)
