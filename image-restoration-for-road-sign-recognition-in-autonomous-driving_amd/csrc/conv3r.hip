@@ -702,16 +702,18 @@ int r3_tpx(R3Pick k) { return (k.nwv / (k.bc / k.nw)) * 128; }
 // 14 maps, odd sizes, small batches) the row-segment tiles: 32-column
 // segments x 4 rows per wave above W = 16, 16 x 8 at W <= 16
 // workgroups of whole-row tiles: one 8-wave workgroup per CU with a
-// double-buffered halo where c_out % 128 == 0 (measured 5-12% faster on the
-// 128-512-channel layers, profiles/r3i_ab.jsonl), else 4-wave workgroups, 2
-// per CU (one's epilogue / DMA waits overlap the other's MFMAs) with one halo
-// buffer.  RR_CONV3R_WG=4 / 8 forces one kind (A/B)
+// double-buffered halo where c_out % 128 == 0 on the 16x16 / 8x8 maps
+// (5-12% faster there, profiles/r3i_ab.jsonl, r4z_conv3r_wg_ab.jsonl), else
+// 4-wave workgroups, 2 per CU (one's epilogue / DMA waits overlap the other's
+// MFMAs) with one halo buffer -- also at W = 32, where the 8-wave tiles were
+// 4-11 % slower once the row loop lost its run-time switches (r4z).
+// RR_CONV3R_WG=4 / 8 forces one kind (A/B)
 R3Pick r3_pick(const rr_igemm_desc *d) {
   const long long P = (long long)d->n * d->h * d->w;
   const int W = d->w;
   const bool square = d->h == W && (W == 8 || W == 16 || W == 32);
   const char *e = getenv("RR_CONV3R_WG");
-  const int nwv = e && (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : (d->c_out % 128 == 0 ? 8 : 4);
+  const int nwv = e && (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : (d->c_out % 128 == 0 && W != 32 ? 8 : 4);
   R3Pick k{0, 0, 0, 0, 0};
   if (square) {
     if (nwv == 8) {

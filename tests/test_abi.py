@@ -151,7 +151,7 @@ def test_kernel_selection_for_the_benched_layers():
     want = {  # (h, c_in1, c_in2, c_out): (fwd, wgrad)
         (64, 64, 0, 64): ("stream3_kernel<64>", "swgrad_kernel<64>"),
         (64, 64, 64, 64): ("conv3r_kernel<s2,64>", "swgrad_kernel<64>"),  # one pass, fp32 sum
-        (32, 64, 0, 128): ("conv3r_kernel<32,128,w8>", "swgrad_kernel<32>"),
+        (32, 64, 0, 128): ("conv3r_kernel<32,128>", "swgrad_kernel<32>"),
         (32, 128, 64, 64): ("conv3r_kernel<32,64>", "swgrad_kernel<32>"),
         (16, 256, 0, 256): ("conv3r_kernel<16,256,w8>", "wgrad3_halo_kernel<16>"),
         (16, 256, 128, 128): ("conv3r_kernel<16,128,w8>", "wgrad3_halo_kernel<16>"),
