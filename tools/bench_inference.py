@@ -11,7 +11,8 @@
 
 Synthetic data, random-init weights (no checkpoints ship with the reference).
 Batch 8192 processed in chunks (``--chunk``).  usage:
-  python tools/bench_inference.py [--images 8192] [--chunk 256] [--size 48]"""
+  python tools/bench_inference.py [--images 8192] [--chunk 1024] [--size 48]
+(chunk 256 / 512 / 1024 / 2048: 8,906 / 9,071 / 9,115 / 9,101 img/s bf16, profiles/r4zb_inference_chunks.txt)"""
 import argparse
 import json
 import os
@@ -30,7 +31,7 @@ from roadrestore import imgproc as T, ops  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--images", type=int, default=8192)
-    ap.add_argument("--chunk", type=int, default=256)
+    ap.add_argument("--chunk", type=int, default=1024)
     ap.add_argument("--size", type=int, default=48, help="source crop side (GTSRB ~30-250)")
     ap.add_argument("--res", type=int, default=224)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
