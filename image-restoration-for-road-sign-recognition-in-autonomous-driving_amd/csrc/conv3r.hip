@@ -294,10 +294,9 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   // DMA (per stage; nothing run-time-switched inside the row loop: each such
   // switch is a scalar branch around every row's MFMA cluster)
   const bool dbg_nodma = (a.dbg & 4) != 0;
-  // every row's MFMA cluster at wave priority 1 (cdna_hip_programming.md
-  // T5): +3.3-3.5 % on both layer sets (profiles/r3aa_ab*.jsonl; the static
-  // form -- the younger half of the workgroup at priority 1 for the whole
-  // loop -- +1 % / -3 %)
+  // (no wave priority around the MFMA clusters: +3.3 % when it was added
+  // next to the run-time switches, profiles/r3aa_ab*.jsonl; without them it
+  // measured -0.6 % at 224 and -0.2 % on the step, r4zd)
   for (int st = 0; st < nst; ++st) {
     const int ch = st / 3, dx = st - ch * 3;       // uniform
     C3_STAMP(st_t);
@@ -374,7 +373,6 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
           if (zhi) hi = i32x4{0, 0, 0, 0};
         }
       }
-      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int dy = 0; dy < 3; ++dy) {
         const int o = ri - dy;
@@ -387,7 +385,6 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
                 __builtin_bit_cast(bf16x8, af[dy][m]), __builtin_bit_cast(bf16x8, bf[ri & 1][s]),
                 acc[o][s][m], 0, 0, 0);
       }
-      __builtin_amdgcn_s_setprio(0);
       // the DMA for the next stage / chunk goes out behind the first rows'
       // MFMAs (issued right after the barrier, every wave of a SIMD would
       // sit in ~60-cycle issue slots before its first MFMA); the weights
