@@ -713,10 +713,17 @@ R3Pick r3_pick(const rr_igemm_desc *d) {
   const int nwv = e && (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : (d->c_out % 128 == 0 && W != 32 ? 8 : 4);
   R3Pick k{0, 0, 0, 0, 0};
   if (square) {
+    // 128-channel column blocks where c_out % 256 == 0 too: 2-3 % faster per
+    // layer than 256-channel ones at 16x16 / 8x8 once the row loop lost its
+    // run-time switches (profiles/r4zk_conv3r_bc_ab.jsonl); the small-batch
+    // 8x8 layers keep 128 x 32 wave tiles.  RR_CONV3R_BC256=1: the 256-channel
+    // blocks (A/B)
+    const char *b256 = getenv("RR_CONV3R_BC256");
     if (nwv == 8) {
-      if (d->c_out % 256 == 0) {
-        if (W != 8 || (P / 256) * (d->c_out / 256) >= 256 || P % 256) k = {256, 64, 8, 2, 0};
-        else k = {128, 32, 8, 2, 0};
+      if (d->c_out % 256 == 0 && W == 8 && (P / 256) * (d->c_out / 256) < 256 && P % 256 == 0) {
+        k = {128, 32, 8, 2, 0};
+      } else if (d->c_out % 256 == 0 && b256 && atoi(b256)) {
+        k = {256, 64, 8, 2, 0};
       } else if (d->c_out % 128 == 0) {
         k = {128, 64, 8, 2, 0};
       } else {

@@ -153,9 +153,9 @@ def test_kernel_selection_for_the_benched_layers():
         (64, 64, 64, 64): ("conv3r_kernel<s2,64>", "swgrad_kernel<64>"),  # one pass, fp32 sum
         (32, 64, 0, 128): ("conv3r_kernel<32,128>", "swgrad_kernel<32>"),
         (32, 128, 64, 64): ("conv3r_kernel<32,64>", "swgrad_kernel<32>"),
-        (16, 256, 0, 256): ("conv3r_kernel<16,256,w8>", "wgrad3_halo_kernel<16>"),
+        (16, 256, 0, 256): ("conv3r_kernel<16,128,w8>", "wgrad3_halo_kernel<16>"),
         (16, 256, 128, 128): ("conv3r_kernel<16,128,w8>", "wgrad3_halo_kernel<16>"),
-        (8, 512, 0, 512): ("conv3r_kernel<8,256,w8>", "wgrad3_halo_kernel<8>"),
+        (8, 512, 0, 512): ("conv3r_kernel<8,128,w8>", "wgrad3_halo_kernel<8>"),
         (8, 512, 0, 256): ("conv3r_kernel<8,128,32,w8>", "wgrad3_halo_kernel<8>"),
     }
     for (h, c1, c2, co), (f, wg) in want.items():
@@ -198,7 +198,7 @@ def test_igemm_ex_kernel_selection():
         return ops.igemm_kernel_name(IgemmDesc(dt, RR_CONV3X3, 4, h, h, c, 0, c, 0, act, 0, 1, 0, 0, 0),
                                      bnbwd=bnbwd)
     assert name(RR_BF16, 224, 64, RR_ACT_PRELU) == "conv3r_kernel<s2,64>"
-    assert name(RR_BF16, 16, 256, 1 | RR_ACT_RES).startswith("conv3r_kernel<16,256")
+    assert name(RR_BF16, 16, 256, 1 | RR_ACT_RES).startswith("conv3r_kernel<16,128")
     assert name(RR_F32, 224, 64, RR_ACT_PRELU) == "unsupported"
     assert name(RR_BF16, 224, 64, RR_ACT_PRELU, bnbwd=True) == "unsupported"
 

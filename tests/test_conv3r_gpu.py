@@ -60,9 +60,9 @@ SHAPES = [
 SHAPES_W8 = [
     (4, 32, 64, 0, 128, "conv3r_kernel<32,128,w8>"),
     (4, 32, 128, 64, 64, "conv3r_kernel<32,64,32,w8>"),
-    (2, 32, 128, 0, 256, "conv3r_kernel<32,256,w8>"),
-    (8, 16, 128, 0, 256, "conv3r_kernel<16,256,w8>"),
-    (512, 8, 512, 0, 512, "conv3r_kernel<8,256,w8>"),
+    (2, 32, 128, 0, 256, "conv3r_kernel<32,128,w8>"),
+    (8, 16, 128, 0, 256, "conv3r_kernel<16,128,w8>"),
+    (512, 8, 512, 0, 512, "conv3r_kernel<8,128,w8>"),
     (8, 8, 256, 0, 512, "conv3r_kernel<8,128,32,w8>"),
 ]
 
@@ -479,3 +479,34 @@ def test_conv3r_ex_pool(dev, shape, monkeypatch):
     assert torch.equal(nchw(yp), F.max_pool2d(nchw(y), 2))
 
 
+
+
+@pytest.mark.parametrize("shape", [(2, 32, 128, 0, 256), (8, 16, 128, 0, 256), (512, 8, 512, 0, 512)])
+def test_conv3r_bc256_variant(dev, shape, monkeypatch):
+    """RR_CONV3R_BC256=1 (A/B): the 256-channel column blocks of 8-wave
+    workgroups (the round-3 default where c_out % 256 == 0) against fp32
+    torch, and bitwise against the 128-channel default: every output sums the
+    same taps in the same stage / row order, only the tile shape differs."""
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    monkeypatch.setenv("RR_CONV3R", "1")
+    monkeypatch.setenv("RR_CONV3R_WG", "8")
+    n, w, c1, c2, co = shape
+    x = rnd(n, c1, w, w, seed=21).bfloat16().float()
+    wt = (rnd(co, c1, 3, 3, seed=22) / (3 * c1 ** 0.5)).bfloat16().float()
+    b = rnd(co, seed=23)
+    pre = F.conv2d(x, wt, None, padding=1)
+    wf, _ = rr.ops.pack_conv(wt.to(dev), BF)
+    x1 = nhwc(x, dev)
+    outs = {}
+    for tag in ("1", "0"):
+        monkeypatch.setenv("RR_CONV3R_BC256", tag)
+        name = rr.ops.igemm_kernel_name(_desc(n, w, c1, c2, co, bias=1, stats=1))
+        assert name.startswith("conv3r") and (",256" in name or "<%d,256" % w in name) == (tag == "1"), name
+        y, _, st = rr.ops.igemm(RR_CONV3X3, x1, None, n, w, w, wf, co, bias=b.to(dev), stats=True)
+        torch.cuda.synchronize()
+        outs[tag] = (nchw(y), st.double().sum(0).cpu())
+    ref = pre + b[None, :, None, None]
+    assert rel(outs["1"][0], ref) < 4e-3
+    assert torch.equal(outs["1"][0], outs["0"][0])
+    assert rel(outs["1"][1], outs["0"][1]) < 1e-12
