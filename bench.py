@@ -321,11 +321,15 @@ def main():
     # (the kernel probe turns it off: per-kernel durations are taken without
     # a concurrent kernel sharing the chip)
     prefetch = [w_perc != 0.0 and os.environ.get("RR_PERC_PREFETCH", "1") != "0"]
+    # where the side stream forks off the step (A/B): "now" = before the
+    # distortion, or a point of the ResUNet forward (engine.FORWARD_POINTS)
+    prefetch_at = os.environ.get("RR_PERC_PREFETCH_AT", "now")
+    prefetch_at = None if prefetch_at == "now" else prefetch_at
 
     def step():
         clean = to_tensor(clean_u8)
         if prefetch[0]:
-            clean = perc.prefetch_target(clean)
+            clean = perc.prefetch_target(clean, at=prefetch_at)
         bad = to_tensor(distort(clean_u8))
         opt.zero_grad(set_to_none=True)
         out = model(bad)

@@ -119,6 +119,21 @@ __device__ __forceinline__ float row16_sum(float v) {
 }
 // max with the neighbouring lane (lane ^ 1)
 __device__ __forceinline__ float max_xor1(float v) { return fmaxf(v, dpp_f<DPP_XOR1>(v)); }
+// the neighbouring lane's (lane ^ 1) value, any 32-bit pattern
+__device__ __forceinline__ uint32_t xor1_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_XOR1, 0xF, 0xF, false);
+}
+// MaxPool2d(2, 2) of one window in window order (0,0) (0,1) (1,0) (1,1):
+// the value and the index of its FIRST occurrence (nn.MaxPool2d's routing of
+// the backward), a NaN replacing a number (maxpool_fwd8_kernel's rule)
+__device__ __forceinline__ float pool4_first_max(float v0, float v1, float v2, float v3, uint32_t &id) {
+  float m = v0;
+  id = 0;
+  if (v1 > m || (v1 != v1 && m == m)) { m = v1; id = 1; }
+  if (v2 > m || (v2 != v2 && m == m)) { m = v2; id = 2; }
+  if (v3 > m || (v3 != v3 && m == m)) { m = v3; id = 3; }
+  return m;
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

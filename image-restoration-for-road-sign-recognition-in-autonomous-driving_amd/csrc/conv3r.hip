@@ -49,10 +49,21 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
+
+// the fused BN/PReLU-backward dgrad epilogue runs in registers on the
+// row-segment tiles and the 8-wave whole-row tiles (16x16 / 8x8: 1-4 %
+// faster than staging it through the LDS one 128-pixel group at a time,
+// profiles/r5d_ablayers_bnbwd.txt), staged on the 4-wave whole-row tiles
+// (32x32: the register form 12 % slower there).  RR_C3_BNREG (a separate
+// build, A/B): 1 = registers everywhere, 2 = staged on every whole-row tile
+#ifndef RR_C3_BNREG
+#define RR_C3_BNREG 0
+#endif
 
 namespace {
 
-template <int W, int BC, int NW, int NWV, int HB, int SG> struct R3 {
+template <int W, int BC, int NW, int NWV, int HB, int SG, int RW> struct R3 {
   // SG > 0: row-segment tiles of any H x W (W ignored): TR rows x 16 SG
   // columns of one image; out-of-image rows / columns are zero in the halo
   // and masked in the epilogue
@@ -83,8 +94,11 @@ template <int W, int BC, int NW, int NWV, int HB, int SG> struct R3 {
   static constexpr int SROW = BC + 4;
   static constexpr int STG = 128 * SROW * 4 + (NWV * BC * 2 + NWV) * 4 + 256;
   // [weights x2][halo x HB][guard block]: the shifted edge reads stay inside
-  // (row-segment tiles read inside their side blocks: no guard)
-  static constexpr int KBYTES = 2 * WBYTES + HB * HBYTES + (SEGM ? 0 : 1024);
+  // (row-segment tiles read inside their side blocks: no guard).  RW (the
+  // weights in registers, straight from the tiles in L2): [guard][halo x 2]
+  // [guard] -- the left-shifted read of the first block lands in the front one
+  static constexpr int HOFF = RW ? 1024 : 2 * WBYTES;            // halo base
+  static constexpr int KBYTES = RW ? 2048 + HB * HBYTES : 2 * WBYTES + HB * HBYTES + (SEGM ? 0 : 1024);
   static constexpr int BIAS = KBYTES;               // [BC] fp32 bias for the register epilogue
   static constexpr int LDS = KBYTES + BC * 4 > STG || SEGM ? KBYTES + BC * 4 : STG;
   static_assert(LDS <= 160 * 1024 && (NWV != 4 || 2 * LDS <= 160 * 1024), "LDS");
@@ -92,8 +106,10 @@ template <int W, int BC, int NW, int NWV, int HB, int SG> struct R3 {
   static_assert(HB == 1 || HB == 2, "halo buffers");
   static_assert(!SEGM || (SG == 1 || SG == 2), "segment width");
   static_assert(SEGM || PAIR || TR % W == 0 || W % TR == 0, "tile rows");
-  static_assert(2 * WBYTES >= 1024, "the edge read of the first halo block stays in LDS");
+  static_assert(RW || 2 * WBYTES >= 1024, "the edge read of the first halo block stays in LDS");
   static_assert(2 * NM + NS <= 15, "lgkmcnt of the row-0 wait");
+  static_assert(!RW || (HB == 2 && !SEGM && R % 2 == 0 && R >= 4 && 8 * NM <= 63),
+                "RW: double halo, whole rows, even R (the next stage's row 0 lands in slot 0), vmcnt range");
 };
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -128,9 +144,12 @@ template <int N> __device__ __forceinline__ void vm_barrier_st(unsigned long lon
 #define VM_BARRIER(N) vm_barrier<N>()
 #endif
 
-template <int W, int BC, int NW, int NWV, int HB, int SG>
+template <int N> using ic = std::integral_constant<int, N>;
+
+template <int W, int BC, int NW, int NWV, int HB, int SG, int RW>
 __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) {
-  using G = R3<W, BC, NW, NWV, HB, SG>;
+  using G = R3<W, BC, NW, NWV, HB, SG, RW>;
+  constexpr bool BNREG = G::SEGM || RR_C3_BNREG == 1 || (RR_C3_BNREG == 0 && NWV == 8);
   constexpr int NS = G::NS, R = G::R, NM = G::NM, WC = G::WC, RS = G::RS;
   constexpr int HW = W * W;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
@@ -165,7 +184,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   }
 
   const uint32_t sbase = (uint32_t)(uintptr_t)smem;
-  const uint32_t wbase = sbase, hbase = sbase + 2 * G::WBYTES;
+  const uint32_t wbase = sbase, hbase = sbase + G::HOFF;
 
   // ---- per-lane DMA sources ----
   // halo block b = (segment k, halo row hr, column block s): pixel index of
@@ -221,17 +240,19 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     for (int i = 0; i < G::NWG; ++i)
       __builtin_amdgcn_global_load_lds((const void *)(wst + wrow[i]), LDS_PTR(dst + wdst[i]), 16, 0, 0);
   };
-  auto issue_h = [&](int ch) __attribute__((always_inline)) {
+  // dummy (RW only): every piece reads the zero page (the chunk past the
+  // last keeps the DMA count of a stage uniform)
+  auto issue_h = [&](int ch, bool dummy = false) __attribute__((always_inline)) {
     const int ci0 = ch * 32;
     const bool first = ci0 < a.c1;                  // uniform
     const char *base = first ? a.x1 : a.x2;
     const long long cs = first ? a.c1 : a.c2;
     const long long cl = first ? ci0 : ci0 - a.c1;
     const long long zoff = (long long)((uintptr_t)rr_zero_page - (uintptr_t)base) + fq * 16;
-    char *dst = smem + 2 * G::WBYTES + (HB == 2 ? (ch & 1) * G::HBYTES : 0);
+    char *dst = smem + G::HOFF + (HB == 2 ? (ch & 1) * G::HBYTES : 0);
 #pragma unroll
     for (int i = 0; i < G::NHG; ++i) {
-      const long long off = hpix[i] >= 0 ? ((long long)hpix[i] * cs + cl) * 2 + fq * 16 : zoff;
+      const long long off = hpix[i] >= 0 && !dummy ? ((long long)hpix[i] * cs + cl) * 2 + fq * 16 : zoff;
       __builtin_amdgcn_global_load_lds((const void *)(base + off), LDS_PTR(dst + hdst[i]), 16, 0, 0);
     }
   };
@@ -284,6 +305,188 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   const int kc = a.cin / 32, nst = 3 * kc;
   [[maybe_unused]] unsigned long long st_vm = 0, st_bar = 0, st_row0 = 0, st_loop0 = 0, st_loop1 = 0, st_t = 0;
   C3_STAMP(st_loop0);
+  if constexpr (RW) {
+    // ---- RW K loop: every wave loads its own A fragments (its NM 1-KB
+    // weight tiles per tap row dy) from global memory (L2) into registers,
+    // one stage ahead, through a ring of 4 fragment sets: stage st (phase p =
+    // st % 4) holds tap dy in set (dy - p) & 3; the next stage's dy = 0 goes
+    // into the spare set at the stage start, its dy = 1 / 2 into the sets of
+    // this stage's dy = 0 / 1 once their last rows (R - 1 / R) are done.  The
+    // LDS holds only the halo, double-buffered, so the only barrier is at the
+    // end of a 32-channel chunk (3 stages): the weights no longer need one per
+    // stage.  Per accumulator the MFMA order is the LDS-weight loop's, so the
+    // results are bitwise equal to it.  The A loads are ordinary (compiler-
+    // visible) global loads: the compiler's waitcnt pass counts them with the
+    // halo DMA; the chunk-end wait for the halo is counted here (8 NM loads
+    // issued after it) ----
+    typedef __attribute__((address_space(1))) const i32x4 gi32x4;
+    const long long run = (long long)(a.cout / 16) * 1024;   // one (chunk, dx, dy) run of tiles
+    // uniform tile base (SGPRs) + the lane's 16 B (one 32-bit VGPR) + m KB
+    // (the instruction offset): global_load_dwordx4 v, v_lane, s_base offset:m*1024
+    const char *wu = wtile + (long long)(c0 / 16 + wc * NM) * 1024;
+    const uint32_t l16 = (uint32_t)lane * 16;
+    i32x4 ar[4][NM];
+    auto load_a = [&](auto SETc, int st, int dy) __attribute__((always_inline)) {
+      constexpr int SET = decltype(SETc)::value;
+      const char *p = wu + ((long long)st * 3 + dy) * run;
+#pragma unroll
+      for (int m = 0; m < NM; ++m) ar[SET][m] = *(gi32x4 *)(p + l16 + m * 1024);
+    };
+    i32x4 bf[2][NS];
+    // B fragments of halo row `row` (of the wave's rows) at lane address ba
+    auto read_row = [&](int slot, uint32_t ba, int row) __attribute__((always_inline)) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bf[slot][s]) : "v"(ba), "i"((row * RS + s) * 1024));
+    };
+    // the halo DMA with the piece geometry recomputed at issue (uniform but
+    // for the lane's pixel): no per-piece pixel registers live in the loop
+    const int lanepix = G::PAIR ? (frow >> 3) * HW + (frow & 7) : frow;
+    auto issue_h_rw = [&](int ch, bool dummy) __attribute__((always_inline)) {
+      const int ci0 = ch * 32;
+      const bool first = ci0 < a.c1;                // uniform
+      const char *base = first ? a.x1 : a.x2;
+      const long long cs = first ? a.c1 : a.c2;
+      const long long cl = first ? ci0 : ci0 - a.c1;
+      const long long zoff = (long long)((uintptr_t)rr_zero_page - (uintptr_t)base) + fq * 16;
+      char *dst = smem + G::HOFF + (ch & 1) * G::HBYTES;
+#pragma unroll
+      for (int i = 0; i < G::NHG; ++i) {
+        int b = wv + NWV * i;
+        if (b >= G::HBLK) b -= NWV;                 // a duplicate of this wave's previous block
+        const int k = b / ((G::HS + 2) * RS);
+        const int rem = b - k * ((G::HS + 2) * RS);
+        const int hr = rem / RS, s = rem - (rem / RS) * RS;
+        int y, pb;
+        if constexpr (G::PAIR) {
+          y = hr - 1;
+          pb = ((n0 + 2 * k) * W + y) * W;
+        } else {
+          y = ys + hr - 1;
+          pb = ((n0 + k) * W + y) * W + 16 * s;
+        }
+        const bool ok = y >= 0 && y < W && !dummy;  // uniform
+        const long long off = ok ? ((long long)(pb + lanepix) * cs + cl) * 2 + fq * 16 : zoff;
+        __builtin_amdgcn_global_load_lds((const void *)(base + off), LDS_PTR(dst + b * 1024), 16, 0, 0);
+      }
+    };
+    auto stage = [&](auto DXc, auto PHc, int ch) __attribute__((always_inline)) {
+      constexpr int DX = decltype(DXc)::value, PH = decltype(PHc)::value;
+      constexpr int SA[3] = {(4 - PH) & 3, (5 - PH) & 3, (6 - PH) & 3};   // set of tap row dy
+      constexpr int SP = (7 - PH) & 3;                                     // spare set
+      const int st = ch * 3 + DX;
+      const int stn = st + 1 < nst ? st + 1 : st;   // (the last stage's prefetch re-reads itself)
+      const uint32_t hb = b_wave + (uint32_t)(ch & 1) * G::HBYTES;
+      // the lane part of a read at tap column dx and whether it is a padding
+      // column (recomputed per stage: nothing extra stays live in the loop)
+      auto lanecol = [&](int dx, bool &z) __attribute__((always_inline)) -> uint32_t {
+        if constexpr (G::PAIR) {
+          const int x = (frow & 7) + dx - 1;
+          const int xc = x < 0 ? 0 : (x > 7 ? 7 : x);
+          z = x != xc;
+          return fq * 256 + ((frow >> 3) * 8 + xc) * 16;
+        } else {
+          const int x = frow + dx - 1;
+          z = x < 0 || x > 15;
+          return x < 0 ? fq * 256 + 240 - 1024 : (x > 15 ? fq * 256 + 1024 : fq * 256 + x * 16);
+        }
+      };
+      bool zcol;
+      const uint32_t ba = hb + lanecol(DX, zcol);
+      const bool zlo = DX == 0 && zcol;               // left padding column (block s = 0)
+      const bool zhi = DX == 2 && zcol;               // right padding column (block NS - 1)
+      if constexpr (DX == 0) read_row(0, ba, 0);      // (DX > 0: read by the previous stage)
+      __builtin_amdgcn_sched_barrier(0);
+      load_a(ic<SP>{}, stn, 0);                       // the next stage's dy = 0 taps
+      if constexpr (DX == 0) issue_h_rw(ch + 1, ch + 1 >= kc);   // the next chunk's halo
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ri = 0; ri < R + 2; ++ri) {
+        if (ri + 1 < R + 2) {
+          read_row((ri + 1) & 1, ba, ri + 1);
+          asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
+        } else if constexpr (DX < 2) {
+          // the next stage's row 0 (same chunk, next tap column) into slot 0
+          bool zn;
+          read_row(0, hb + lanecol(DX + 1, zn), 0);
+          asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(bf[ri & 1][s]));
+        {
+          i32x4 &lo = bf[ri & 1][0];
+          i32x4 &hi = bf[ri & 1][NS - 1];
+          if (G::PAIR) {
+            if (zlo || zhi) lo = i32x4{0, 0, 0, 0};
+          } else {
+            if (zlo) lo = i32x4{0, 0, 0, 0};
+            if (zhi) hi = i32x4{0, 0, 0, 0};
+          }
+        }
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) {
+          const int o = ri - dy;
+          if (o < 0 || o >= R) continue;
+#pragma unroll
+          for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int m = 0; m < NM; ++m)
+              acc[o][s][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  __builtin_bit_cast(bf16x8, ar[SA[dy]][m]), __builtin_bit_cast(bf16x8, bf[ri & 1][s]),
+                  acc[o][s][m], 0, 0, 0);
+        }
+        // tap rows dy = 0 / 1 are done after rows R - 1 / R: their sets take
+        // the next stage's dy = 1 / 2
+        if (ri == R - 1) {
+          __builtin_amdgcn_sched_barrier(0);
+          load_a(ic<SA[0]>{}, stn, 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (ri == R) {
+          __builtin_amdgcn_sched_barrier(0);
+          load_a(ic<SA[1]>{}, stn, 2);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if constexpr (DX == 2) {
+        // the next chunk's halo (issued at this chunk's first stage, 8 NM A
+        // loads ago) has landed for every wave, and every wave is done with
+        // this chunk's buffer (the one the chunk after next loads into)
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(8 * NM) : "memory");
+      }
+    };
+    // prologue: chunk 0's halo, stage 0's A fragments (phase 0: sets 0, 1, 2)
+    issue_h_rw(0, false);
+    __builtin_amdgcn_sched_barrier(0);
+    load_a(ic<0>{}, 0, 0);
+    load_a(ic<1>{}, 0, 1);
+    load_a(ic<2>{}, 0, 2);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(3 * NM) : "memory");
+    // chunk q of a 4-chunk group starts at stage phase (3 q) % 4
+    auto chunk = [&](auto PHc, int ch) __attribute__((always_inline)) {
+      constexpr int PH = decltype(PHc)::value;
+      stage(ic<0>{}, ic<PH>{}, ch);
+      stage(ic<1>{}, ic<(PH + 1) & 3>{}, ch);
+      stage(ic<2>{}, ic<(PH + 2) & 3>{}, ch);
+    };
+    int ch = 0;
+    for (; ch + 4 <= kc; ch += 4) {
+      chunk(ic<0>{}, ch);
+      chunk(ic<3>{}, ch + 1);
+      chunk(ic<2>{}, ch + 2);
+      chunk(ic<1>{}, ch + 3);
+    }
+    if (ch < kc) {                                    // kc % 4 == 2 (RW takes even kc)
+      chunk(ic<0>{}, ch);
+      chunk(ic<3>{}, ch + 1);
+    }
+    // the last prefetches (and the dummy halo) land before the epilogue
+    // stages through the LDS
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  } else {
   // prologue: chunk 0's halo, stage 0's weights
   issue_h(0);
   issue_w(0);
@@ -397,6 +600,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     if (next_h) VM_BARRIER(G::NHG);
     else VM_BARRIER(0);
   }
+  }   // (LDS-weight K loop)
 #ifdef RR_CONV3R_STAMPS
   C3_STAMP(st_loop1);
   if (lane == 0 && blockIdx.x < (1 << 18) / (8 * NWV)) {
@@ -430,6 +634,25 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
              (G::PAIR ? (frow >> 3) * 64 + o * 8 + (frow & 7) : o * W + 16 * s + frow);
     }
   };
+  // element address of accumulator tile (o, s) at a uniform channel cu plus
+  // the lane's channel cl in a [P][ld] bf16 tensor.  Whole-row tiles: the
+  // pixel is a uniform part + the lane's part, so the address is a uniform
+  // 64-bit base plus one 32-bit lane offset (the epilogue's 64-bit per-lane
+  // addresses spilled next to the accumulators); row-segment tiles: the
+  // pixel (out-of-image: pixel 0, never used)
+  const int lpix = G::PAIR ? (frow >> 3) * 64 + (frow & 7) : frow;
+  auto elem = [&](const void *base, int o, int s, int cu, int cl, int ld) __attribute__((always_inline))
+      -> const char * {
+    const char *b = reinterpret_cast<const char *>(base);
+    if constexpr (G::SEGM) {
+      long long p = pix_at(o, s);
+      if (p < 0) p = 0;
+      return b + (p * ld + cu + cl) * 2;
+    } else {
+      const long long up = (long long)p0 + wp * 128 + (G::PAIR ? o * 8 : o * W + 16 * s);
+      return b + (up * ld + cu) * 2 + (uint32_t)(lpix * ld + cl) * 2u;
+    }
+  };
   // 16-B stores: per pair of 16-channel blocks (2p, 2p + 1) one
   // v_permlane16_swap per dword (odd rows of the first <-> even rows of the
   // second) leaves lane (row fq, pixel frow) with 8 consecutive channels at
@@ -445,7 +668,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
       vb[j] = __uint_as_float(t[1]);
     }
   };
-  if constexpr (G::SEGM) {
+  if constexpr (BNREG) {
     if (a.bpart) {
       // ---- fused BN -> PReLU backward (rr_igemm_bnbwd; IgemmArgs::bpart)
       // in registers: the accumulator is dL/d(PReLU out); per lane 8
@@ -458,6 +681,21 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
       }
       __syncthreads();
       const float al = a.balpha[0];
+      // the wave tile's pre-BN inputs t first (every load in flight before
+      // the first store, as in the register epilogue below)
+      // (in two halves of the wave's rows, as the register epilogue's operand)
+      constexpr int RHB = R / 2;
+      uint4 tq[RHB * NS * (NM / 2)];
+      auto preload_t = [&](int oh) __attribute__((always_inline)) {
+#pragma unroll
+        for (int o = oh; o < oh + RHB; ++o)
+#pragma unroll
+          for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int pp = 0; pp < NM / 2; ++pp)
+              tq[((o - oh) * NS + s) * (NM / 2) + pp] =
+                  *reinterpret_cast<const uint4 *>(elem(a.bt, o, s, c0 + cb + 32 * pp, coff, a.cout));
+      };
       float g0[NM / 2][8], g1[NM / 2][8];
       double sa = 0.0;                                 // (fp64: igemm_epi.h store_staged_bnbwd)
 #pragma unroll
@@ -465,7 +703,8 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
 #pragma unroll
         for (int j = 0; j < 8; ++j) { g0[pp][j] = 0.f; g1[pp][j] = 0.f; }
 #pragma unroll
-      for (int o = 0; o < R; ++o)
+      for (int o = 0; o < R; ++o) {
+        if (o % RHB == 0) preload_t(o);
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
           const long long p = pix_at(o, s);
@@ -475,9 +714,11 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
             swap_pair(va, vb);
             if (p < 0) continue;
             const int cl = cb + 32 * pp + coff;          // column in the block
-            const long long e = p * a.cout + c0 + cl;
-            const f32x4 t0 = load4<bf16_t>(reinterpret_cast<const bf16_t *>(a.bt) + e);
-            const f32x4 t1 = load4<bf16_t>(reinterpret_cast<const bf16_t *>(a.bt) + e + 4);
+            const uint4 tr = tq[((o % RHB) * NS + s) * (NM / 2) + pp];
+            const f32x4 t0 = f32x4{__uint_as_float(tr.x << 16), __uint_as_float(tr.x & 0xffff0000u),
+                                   __uint_as_float(tr.y << 16), __uint_as_float(tr.y & 0xffff0000u)};
+            const f32x4 t1 = f32x4{__uint_as_float(tr.z << 16), __uint_as_float(tr.z & 0xffff0000u),
+                                   __uint_as_float(tr.w << 16), __uint_as_float(tr.w & 0xffff0000u)};
             const float g[8] = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
             const float t[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
             float gm[8];
@@ -489,10 +730,12 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
               g0[pp][j] += gm[j];
               g1[pp][j] += gm[j] * ((t[j] - cst[cl + j]) * cst[BC + cl + j]);
             }
-            store8<bf16_t>(reinterpret_cast<bf16_t *>(a.y1) + e, f32x4{gm[0], gm[1], gm[2], gm[3]},
-                           f32x4{gm[4], gm[5], gm[6], gm[7]});
+            store8<bf16_t>(reinterpret_cast<bf16_t *>(const_cast<char *>(elem(a.y1, o, s, c0 + cb + 32 * pp, coff,
+                                                                               a.cout))),
+                           f32x4{gm[0], gm[1], gm[2], gm[3]}, f32x4{gm[4], gm[5], gm[6], gm[7]});
           }
         }
+      }
       // over the 16 pixel lanes (row16_sum: the fixed xor-tree order), then one partial row per
       // wave row: [srow][cout][3] = (sum gm, sum gm * xhat, 0)
 #pragma unroll
@@ -530,7 +773,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
       return;
     }
   }
-  if (G::SEGM || !a.bpart) {
+  if (BNREG || !a.bpart) {
     // ---- register epilogue: lane = 4 NHWC channels of one pixel per
     // accumulator tile ----
     if (a.stats) {
@@ -580,8 +823,49 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     // column pair is lane frow ^ 1 (same 8 channels after the swap)
     const bool pool = (a.act & RR_ACT_POOL) != 0, full = (a.act & RR_ACT_NOFULL) == 0;
     const int ph = a.h >> 1, pw = a.w >> 1;
+    // one epilogue operand of the whole wave tile -- the accumulate input,
+    // else the residual, else the ReLU mask (uniform) -- is loaded before the
+    // first store: a store may alias a later load, so the compiler keeps them
+    // in program order, and loaded next to its use every 16-B group paid a
+    // memory latency of its own (the 32x32 dgrads ran 30-70 % over the plain
+    // conv).  A second operand (accumulate AND mask) still loads in place.
+    const int pre = a.accumulate ? 1 : (a.res ? 2 : (a.has_mask ? 3 : 0));
+    // operand / destination address of tile (o, s), block pair pp (the
+    // concat split is uniform per pair: split % 32 == 0)
+    auto op_ptr = [&](int kind, int o, int s, int pp) __attribute__((always_inline)) -> const char * {
+      const int cu = c0 + cb + 32 * pp;
+      if (kind == 1) {
+        const bool second = a.split > 0 && cu >= a.split;
+        return second ? elem(a.y2, o, s, cu - a.split, coff, ld2) : elem(a.y1, o, s, cu, coff, ld1);
+      }
+      return elem(kind == 2 ? a.res : a.mask, o, s, cu, coff, ld1);
+    };
+    // (in two halves of the wave's rows: the whole tile's operand, 64 VGPRs
+    // on the 128 x 64 tiles, spilled next to the accumulators)
+    constexpr int RH = R / 2;                         // rows per half (even: row pairs stay whole)
+    constexpr int NQ = RH * NS * (NM / 2);
+    uint4 opq[NQ];
+    auto preload = [&](int oh) __attribute__((always_inline)) {
+      if (!pre) return;
 #pragma unroll
-    for (int o2 = 0; o2 < R; o2 += 2)
+      for (int o = oh; o < oh + RH; ++o)
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+          for (int pp = 0; pp < NM / 2; ++pp)
+            opq[((o - oh) * NS + s) * (NM / 2) + pp] =
+                *reinterpret_cast<const uint4 *>(op_ptr(pre, o, s, pp));
+    };
+    static_assert(RH % 2 == 0, "halves of whole row pairs");
+    auto unpack8 = [](const uint4 r, f32x4 &lo, f32x4 &hi) __attribute__((always_inline)) {
+      lo = f32x4{__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u),
+                 __uint_as_float(r.y << 16), __uint_as_float(r.y & 0xffff0000u)};
+      hi = f32x4{__uint_as_float(r.z << 16), __uint_as_float(r.z & 0xffff0000u),
+                 __uint_as_float(r.w << 16), __uint_as_float(r.w & 0xffff0000u)};
+    };
+#pragma unroll
+    for (int o2 = 0; o2 < R; o2 += 2) {
+      if (o2 % RH == 0) preload(o2);
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
 #pragma unroll
@@ -596,18 +880,25 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
             fin[t][0] = va;
             fin[t][1] = vb;
             if (G::SEGM && p < 0) continue;
-            const int c = c0 + cb + 32 * pp + coff;
-            const bool second = a.split > 0 && c >= a.split;      // uniform per pair (split % 32 == 0)
-            bf16_t *dst = second ? reinterpret_cast<bf16_t *>(a.y2) + p * ld2 + (c - a.split)
-                                 : reinterpret_cast<bf16_t *>(a.y1) + p * ld1 + c;
+            bf16_t *dst = reinterpret_cast<bf16_t *>(const_cast<char *>(op_ptr(1, o, s, pp)));
+            const int q = ((o % RH) * NS + s) * (NM / 2) + pp;
             if (a.accumulate) {
-              va += load4<bf16_t>(dst);
-              vb += load4<bf16_t>(dst + 4);
+              f32x4 lo, hi;
+              unpack8(opq[q], lo, hi);                      // (pre == 1)
+              va += lo;
+              vb += hi;
             }
             if (a.res) {                                   // (rr_igemm_ex: y1's layout, no split)
-              const bf16_t *rp = reinterpret_cast<const bf16_t *>(a.res) + p * ld1 + c;
-              va += load4<bf16_t>(rp);
-              vb += load4<bf16_t>(rp + 4);
+              f32x4 lo, hi;
+              if (pre == 2) {
+                unpack8(opq[q], lo, hi);
+              } else {
+                const bf16_t *rp = reinterpret_cast<const bf16_t *>(op_ptr(2, o, s, pp));
+                lo = load4<bf16_t>(rp);
+                hi = load4<bf16_t>(rp + 4);
+              }
+              va += lo;
+              vb += hi;
             }
             if ((a.act & 3) == RR_ACT_RELU) {
 #pragma unroll
@@ -621,8 +912,14 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
               }
             }
             if (a.has_mask) {
-              const bf16_t *mp = reinterpret_cast<const bf16_t *>(a.mask) + p * ld1 + c;
-              const f32x4 ma = load4<bf16_t>(mp), mb = load4<bf16_t>(mp + 4);
+              f32x4 ma, mb;
+              if (pre == 3) {
+                unpack8(opq[q], ma, mb);
+              } else {
+                const bf16_t *mp = reinterpret_cast<const bf16_t *>(op_ptr(3, o, s, pp));
+                ma = load4<bf16_t>(mp);
+                mb = load4<bf16_t>(mp + 4);
+              }
 #pragma unroll
               for (int j = 0; j < 4; ++j) {
                 va[j] = ma[j] > 0.f ? va[j] : 0.f;
@@ -634,17 +931,21 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
             if (full) store8<bf16_t>(dst, va, vb);
           }
           if (pool) {
-            // vertical max, then the column pair (every lane shuffles)
+            // the window in window order -- (o2, x) own, (o2, x + 1) the xor-1
+            // lane's, (o2 + 1, x) own, (o2 + 1, x + 1) the neighbour's -- on the
+            // bf16-rounded values (the stored ones maxpool_fwd8 reads): the
+            // first max and its index (rr_igemm_pool's a.pidx)
             f32x4 m0, m1;
+            uint32_t id[8];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              m0[j] = fmaxf(fin[0][0][j], fin[1][0][j]);
-              m1[j] = fmaxf(fin[0][1][j], fin[1][1][j]);
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              m0[j] = max_xor1(m0[j]);
-              m1[j] = max_xor1(m1[j]);
+            for (int j = 0; j < 8; ++j) {
+              const float u0 = bf16_to_f32(f32_to_bf16(fin[0][j >> 2][j & 3]));
+              const float u1 = bf16_to_f32(f32_to_bf16(fin[1][j >> 2][j & 3]));
+              const float v0 = __uint_as_float(xor1_u32(__float_as_uint(u0)));
+              const float v1 = __uint_as_float(xor1_u32(__float_as_uint(u1)));
+              const float m = pool4_first_max(u0, v0, u1, v1, id[j]);
+              if (j < 4) m0[j] = m;
+              else m1[j - 4] = m;
             }
             const long long p = pix_at(o2, s);            // the window's top-left pixel
             if ((frow & 1) == 0 && (!G::SEGM || p >= 0)) {
@@ -653,17 +954,21 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
               const int y = rem / a.w, x = rem - (rem / a.w) * a.w;
               if (y + 1 < a.h && x + 1 < a.w) {             // (floor: a last odd row / column drops)
                 const int c = c0 + cb + 32 * pp + coff;
-                bf16_t *q = reinterpret_cast<bf16_t *>(a.ypool) +
-                            (((long long)n * ph + (y >> 1)) * pw + (x >> 1)) * a.cout + c;
-                store8<bf16_t>(q, m0, m1);
+                const long long q = (((long long)n * ph + (y >> 1)) * pw + (x >> 1)) * a.cout + c;
+                store8<bf16_t>(reinterpret_cast<bf16_t *>(a.ypool) + q, m0, m1);
+                if (a.pidx)
+                  *reinterpret_cast<uint2 *>(a.pidx + q) =
+                      make_uint2(id[0] | (id[1] << 8) | (id[2] << 16) | (id[3] << 24),
+                                 id[4] | (id[5] << 8) | (id[6] << 16) | (id[7] << 24));
               }
             }
           }
         }
       }
+    }
     return;
   }
-  if constexpr (!G::SEGM) {
+  if constexpr (!BNREG) {
     // ---- BN-backward epilogue: one 128-pixel group (= one wave row of the
     // grid) at a time as fp32 [128][BC] in LDS, then the staged store ----
     float *stg = reinterpret_cast<float *>(smem);
@@ -691,7 +996,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
 // except where that leaves fewer than 256 workgroups (one per CU): the
 // 8x8 256-channel layers (B = 512: 128 tiles) take 128 x 32 wave tiles.
 // sg > 0: row-segment tiles (any H x W)
-struct R3Pick { int bc, nw, nwv, hb, sg; };
+struct R3Pick { int bc, nw, nwv, hb, sg, rw; };
 int r3_tpx(R3Pick k) { return (k.nwv / (k.bc / k.nw)) * 128; }
 
 // square 8 / 16 / 32 maps whose pixel count fills whole tiles take the
@@ -704,41 +1009,64 @@ int r3_tpx(R3Pick k) { return (k.nwv / (k.bc / k.nw)) * 128; }
 // 4-wave workgroups, 2 per CU (one's epilogue / DMA waits overlap the other's
 // MFMAs) with one halo buffer -- also at W = 32, where the 8-wave tiles were
 // 4-11 % slower once the row loop lost its run-time switches (r4z).
-// RR_CONV3R_WG=4 / 8 forces one kind (A/B)
+// RR_CONV3R_WG=4 / 8 forces one kind (A/B).
+// RW (register weights, whole-row tiles with an even number of 32-channel
+// chunks): RR_CONV3R_RW=0 / 1 (A/B); RW tiles always double-buffer the halo
 R3Pick r3_pick(const rr_igemm_desc *d) {
   const long long P = (long long)d->n * d->h * d->w;
   const int W = d->w;
   const bool square = d->h == W && (W == 8 || W == 16 || W == 32);
   const char *e = getenv("RR_CONV3R_WG");
   const int nwv = e && (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : (d->c_out % 128 == 0 && W != 32 ? 8 : 4);
-  R3Pick k{0, 0, 0, 0, 0};
   if (square) {
+    // RR_CONV3R_RW: 0 = LDS weights, 1 = register weights, 32 = register
+    // weights with 128 x 32 wave tiles on the 32x32 maps only
+    const char *re = getenv("RR_CONV3R_RW");
+    const int rwm = re ? atoi(re) : 0;
+    const int rw = ((d->c_in1 + d->c_in2) % 64 == 0) && (rwm == 1 || (rwm == 32 && W == 32)) &&
+                   !(W == 8 && d->c_out % 128 != 0);
     // 128-channel column blocks where c_out % 256 == 0 too: 2-3 % faster per
     // layer than 256-channel ones at 16x16 / 8x8 once the row loop lost its
     // run-time switches (profiles/r4zk_conv3r_bc_ab.jsonl); the small-batch
     // 8x8 layers keep 128 x 32 wave tiles.  RR_CONV3R_BC256=1: the 256-channel
-    // blocks (A/B)
+    // blocks (A/B, LDS weights only)
     const char *b256 = getenv("RR_CONV3R_BC256");
+    const int h8 = 2, h4 = rw ? 2 : 1;
+    R3Pick c[3];
+    int nc = 0;
     if (nwv == 8) {
       if (d->c_out % 256 == 0 && W == 8 && (P / 256) * (d->c_out / 256) < 256 && P % 256 == 0) {
-        k = {128, 32, 8, 2, 0};
-      } else if (d->c_out % 256 == 0 && b256 && atoi(b256)) {
-        k = {256, 64, 8, 2, 0};
+        c[nc++] = {128, 32, 8, h8, 0, rw};
+      } else if (d->c_out % 256 == 0 && b256 && atoi(b256) && !rw) {
+        c[nc++] = {256, 64, 8, h8, 0, 0};
       } else if (d->c_out % 128 == 0) {
-        k = {128, 64, 8, 2, 0};
+        c[nc++] = {128, 64, 8, h8, 0, rw};
       } else {
-        k = {64, 32, 8, 2, 0};
+        c[nc++] = {64, 32, 8, h8, 0, rw};
       }
     } else if (d->c_out % 128 == 0) {
       // 128-channel column blocks of 128 x 64 wave tiles (256-pixel tiles);
       // below 512 workgroups (2 per CU) the 8x8 layers take 128 x 32 wave
       // tiles (128-pixel tiles)
-      if (W == 8 && (P / 256) * (d->c_out / 128) < 512 && P % 128 == 0) k = {128, 32, 4, 1, 0};
-      else k = {128, 64, 4, 1, 0};
+      if (W == 8 && (P / 256) * (d->c_out / 128) < 512 && P % 128 == 0) c[nc++] = {128, 32, 4, h4, 0, rw};
+      else c[nc++] = {128, 64, 4, h4, 0, rw};
     } else {
-      k = {64, 64, 4, 1, 0};
+      c[nc++] = {64, 64, 4, h4, 0, rw};
     }
-    if (P % r3_tpx(k) == 0) return k;
+    // batches whose pixels do not fill the first pick's tiles: smaller
+    // whole-row tiles before the row-segment ones (an odd batch of 16x16
+    // 256-channel maps stays on whole rows)
+    if (d->c_out % 128 == 0) {
+      c[nc++] = {128, 32, 8, h8, 0, rw};
+      c[nc++] = {128, 32, 4, h4, 0, rw};
+    } else {
+      c[nc++] = {64, 32, 4, h4, 0, rw};
+    }
+    // RR_CONV3R_NW=32 (A/B): 128 x 32 wave tiles for the first pick
+    const char *nwe = getenv("RR_CONV3R_NW");
+    if (((nwe && atoi(nwe) == 32) || (rw && rwm == 32)) && c[0].bc <= 128) c[0].nw = 32;
+    for (int i = 0; i < nc; ++i)
+      if (P % r3_tpx(c[i]) == 0) return c[i];
   }
   const char *se = getenv("RR_CONV3R_SEG");          // A/B: force 1 / 2 column blocks per segment
   const int sg = se && (atoi(se) == 1 || atoi(se) == 2) ? atoi(se) : (W > 16 ? 2 : 1);
@@ -751,11 +1079,11 @@ R3Pick r3_pick(const rr_igemm_desc *d) {
   const int segwg = sw && (atoi(sw) == 4 || atoi(sw) == 8) ? atoi(sw)
                                                            : (d->c_out % 128 == 0 && W <= 28 ? 8 : 4);
   if (segwg == 8) {
-    if (sg == 2) return d->c_out % 128 == 0 ? R3Pick{128, 64, 8, 2, 2} : R3Pick{64, 32, 8, 2, 2};
-    return d->c_out % 128 == 0 ? R3Pick{128, 32, 8, 2, 1} : R3Pick{64, 32, 8, 1, 1};
+    if (sg == 2) return d->c_out % 128 == 0 ? R3Pick{128, 64, 8, 2, 2, 0} : R3Pick{64, 32, 8, 2, 2, 0};
+    return d->c_out % 128 == 0 ? R3Pick{128, 32, 8, 2, 1, 0} : R3Pick{64, 32, 8, 1, 1, 0};
   }
-  if (sg == 2) return d->c_out % 128 == 0 ? R3Pick{128, 64, 4, 1, 2} : R3Pick{64, 64, 4, 1, 2};
-  return d->c_out % 128 == 0 ? R3Pick{128, 32, 4, 1, 1} : R3Pick{64, 32, 4, 1, 1};
+  if (sg == 2) return d->c_out % 128 == 0 ? R3Pick{128, 64, 4, 1, 2, 0} : R3Pick{64, 64, 4, 1, 2, 0};
+  return d->c_out % 128 == 0 ? R3Pick{128, 32, 4, 1, 1, 0} : R3Pick{64, 32, 4, 1, 1, 0};
 }
 // row-segment tiles: rows per tile, column segments and row bands per image
 int r3_tr(R3Pick k) { return (k.nwv / (k.bc / k.nw)) * (8 / k.sg); }
@@ -792,23 +1120,44 @@ int conv3r_stat_blocks(const rr_igemm_desc *d) {
   return (int)(r3_ptiles(d, k) * (k.nwv / (k.bc / k.nw)));   // one row per wave row of a tile
 }
 
-template <int BC, int NW, int NWV, int HB, int SG>
+template <int BC, int NW, int NWV, int HB, int SG, int RW>
 static int conv3r_go(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   a.ncblk = a.cout / BC;
-  const long long nblk = r3_ptiles(d, R3Pick{BC, NW, NWV, HB, SG}) * a.ncblk;
+  const long long nblk = r3_ptiles(d, R3Pick{BC, NW, NWV, HB, SG, RW}) * a.ncblk;
   if (nblk <= 0 || nblk > 0x7fffffffLL) return RR_EUNSUPPORTED;
   const dim3 grid((unsigned)nblk), block(64 * NWV);
   if constexpr (SG > 0) {
-    hipLaunchKernelGGL((conv3r_kernel<0, BC, NW, NWV, HB, SG>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((conv3r_kernel<0, BC, NW, NWV, HB, SG, 0>), grid, block, 0, st, a);
   } else {
     switch (d->w) {
-      case 32: hipLaunchKernelGGL((conv3r_kernel<32, BC, NW, NWV, HB, 0>), grid, block, 0, st, a); break;
-      case 16: hipLaunchKernelGGL((conv3r_kernel<16, BC, NW, NWV, HB, 0>), grid, block, 0, st, a); break;
-      default: hipLaunchKernelGGL((conv3r_kernel<8, BC, NW, NWV, HB, 0>), grid, block, 0, st, a); break;
+      case 32: hipLaunchKernelGGL((conv3r_kernel<32, BC, NW, NWV, HB, 0, RW>), grid, block, 0, st, a); break;
+      case 16: hipLaunchKernelGGL((conv3r_kernel<16, BC, NW, NWV, HB, 0, RW>), grid, block, 0, st, a); break;
+      default:
+        // (RW 4-wave 64 x 64 tiles of 8x8 pairs: 2 x 40 KB of halo, past two
+        // workgroups per CU; the picker does not take it)
+        if constexpr (RW && NWV == 4 && BC == 64 && NW == 64) return RR_EUNSUPPORTED;
+        else hipLaunchKernelGGL((conv3r_kernel<8, BC, NW, NWV, HB, 0, RW>), grid, block, 0, st, a);
+        break;
     }
   }
   RR_CHECK_LAUNCH();
   return RR_OK;
+}
+
+template <int RW>
+static int conv3r_go_rows(const R3Pick &k, const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
+  constexpr int H4 = RW ? 2 : 1;
+  if (k.nwv == 8) {
+    if constexpr (!RW)
+      if (k.bc == 256) return conv3r_go<256, 64, 8, 2, 0, 0>(d, a, st);
+    if (k.bc == 128 && k.nw == 64) return conv3r_go<128, 64, 8, 2, 0, RW>(d, a, st);
+    if (k.bc == 128) return conv3r_go<128, 32, 8, 2, 0, RW>(d, a, st);
+    return conv3r_go<64, 32, 8, 2, 0, RW>(d, a, st);
+  }
+  if (k.bc == 128 && k.nw == 64) return conv3r_go<128, 64, 4, H4, 0, RW>(d, a, st);
+  if (k.bc == 128) return conv3r_go<128, 32, 4, H4, 0, RW>(d, a, st);
+  if (k.nw == 64) return conv3r_go<64, 64, 4, H4, 0, RW>(d, a, st);
+  return conv3r_go<64, 32, 4, H4, 0, RW>(d, a, st);
 }
 
 int conv3r_launch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
@@ -816,35 +1165,27 @@ int conv3r_launch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   const R3Pick k = r3_pick(d);
   if (k.sg == 2) {
     if (k.nwv == 8) {
-      if (k.bc == 128) return conv3r_go<128, 64, 8, 2, 2>(d, a, st);
-      return conv3r_go<64, 32, 8, 2, 2>(d, a, st);
+      if (k.bc == 128) return conv3r_go<128, 64, 8, 2, 2, 0>(d, a, st);
+      return conv3r_go<64, 32, 8, 2, 2, 0>(d, a, st);
     }
-    if (k.bc == 128) return conv3r_go<128, 64, 4, 1, 2>(d, a, st);
-    return conv3r_go<64, 64, 4, 1, 2>(d, a, st);
+    if (k.bc == 128) return conv3r_go<128, 64, 4, 1, 2, 0>(d, a, st);
+    return conv3r_go<64, 64, 4, 1, 2, 0>(d, a, st);
   }
   if (k.sg == 1) {
     if (k.nwv == 8) {
-      if (k.bc == 128) return conv3r_go<128, 32, 8, 2, 1>(d, a, st);
-      return conv3r_go<64, 32, 8, 1, 1>(d, a, st);
+      if (k.bc == 128) return conv3r_go<128, 32, 8, 2, 1, 0>(d, a, st);
+      return conv3r_go<64, 32, 8, 1, 1, 0>(d, a, st);
     }
-    if (k.bc == 128) return conv3r_go<128, 32, 4, 1, 1>(d, a, st);
-    return conv3r_go<64, 32, 4, 1, 1>(d, a, st);
+    if (k.bc == 128) return conv3r_go<128, 32, 4, 1, 1, 0>(d, a, st);
+    return conv3r_go<64, 32, 4, 1, 1, 0>(d, a, st);
   }
-  if (k.nwv == 8) {
-    if (k.bc == 256) return conv3r_go<256, 64, 8, 2, 0>(d, a, st);
-    if (k.bc == 128 && k.nw == 64) return conv3r_go<128, 64, 8, 2, 0>(d, a, st);
-    if (k.bc == 128) return conv3r_go<128, 32, 8, 2, 0>(d, a, st);
-    return conv3r_go<64, 32, 8, 2, 0>(d, a, st);
-  }
-  if (k.bc == 128 && k.nw == 64) return conv3r_go<128, 64, 4, 1, 0>(d, a, st);
-  if (k.bc == 128) return conv3r_go<128, 32, 4, 1, 0>(d, a, st);
-  return conv3r_go<64, 64, 4, 1, 0>(d, a, st);
+  return k.rw ? conv3r_go_rows<1>(k, d, a, st) : conv3r_go_rows<0>(k, d, a, st);
 }
 
 const char *conv3r_name(const rr_igemm_desc *d) {
   if (!conv3r_bc(d)) return "invalid";
   const R3Pick k = r3_pick(d);
-  static char names[3][4][2][40];
+  static char names[3][5][2][2][40];
   static char segnames[2][2][2][40];
   char *n;
   if (k.sg) {
@@ -855,13 +1196,14 @@ const char *conv3r_name(const rr_igemm_desc *d) {
     return n;
   }
   const int wi = d->w == 8 ? 0 : d->w == 16 ? 1 : 2;
-  const int bi = k.bc == 64 ? 0 : k.bc == 256 ? 3 : (k.nw == 64 ? 1 : 2);
+  const int bi = k.bc == 64 ? (k.nw == 64 ? 0 : 4) : k.bc == 256 ? 3 : (k.nw == 64 ? 1 : 2);
   const int vi = k.nwv == 8;
-  n = names[wi][bi][vi];
+  n = names[wi][bi][vi][k.rw != 0];
   if (!n[0]) {
     // conv3r_kernel<W,BC> (128 x 64 wave tiles), <W,BC,32> (128 x 32); the
-    // 8-wave one-per-CU variant adds ",w8"
-    snprintf(n, 40, "conv3r_kernel<%d,%d%s%s>", d->w, k.bc, k.nw == 32 ? ",32" : "", vi ? ",w8" : "");
+    // 8-wave one-per-CU variant adds ",w8", the register-weight K loop ",rw"
+    snprintf(n, 40, "conv3r_kernel<%d,%d%s%s%s>", d->w, k.bc, k.nw == 32 ? ",32" : "", vi ? ",w8" : "",
+             k.rw ? ",rw" : "");
   }
   return n;
 }

@@ -1233,6 +1233,7 @@ static int fill_args(const rr_igemm_desc *d, const void *x1, const void *x2, con
   a.alpha = nullptr;
   a.res = nullptr;
   a.ypool = nullptr;
+  a.pidx = nullptr;
   a.ntile = 0;
   return RR_OK;
 }
@@ -1332,6 +1333,46 @@ extern "C" int rr_igemm_ex(const rr_igemm_desc *d, const void *x1, const void *x
   a.res = (const char *)res;
   a.ypool = (char *)y_pool;
   return conv3r_launch(d, a, (hipStream_t)stream);
+}
+
+// conv (+ bias) + ReLU + MaxPool2d(2, 2) with the window index, the full-size
+// output never written (the perceptual VGG slice's conv1_2 / conv2_2 + pool,
+// 14:189-196, and every no-backward pool of it): the row-streaming kernel
+// where it takes the layer, else the tap-reuse conv's register epilogue
+extern "C" int rr_igemm_pool(const rr_igemm_desc *d, const void *x1, const void *x2, const void *w,
+                             const float *bias, void *y_pool, uint8_t *pool_idx, rr_stream stream) {
+  if (!d || !y_pool || d->mode != RR_CONV3X3 || d->act != RR_ACT_RELU || d->out_split ||
+      d->accumulate || d->has_mask || d->want_stats || d->out_nchw || d->h < 2 || d->w < 2)
+    return RR_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  if (stream3_blocks(d, 0) && !d->c_in2 && pool_idx) {
+    S3Args s{};
+    s.x = (const char *)x1; s.wt = (const char *)w; s.bias = d->has_bias ? bias : nullptr;
+    s.n = d->n; s.h = d->h; s.act = d->act;
+    s.ypool = (char *)y_pool; s.pidx = pool_idx;
+    if (!x1 || !w || (d->has_bias && !bias)) return RR_EINVAL;
+    return stream3_launch_pool(d, s, st);
+  }
+  rr_igemm_desc d2 = *d;
+  d2.act = RR_ACT_RELU | RR_ACT_POOL | RR_ACT_NOFULL;
+  if (!conv3r_bc(&d2)) return RR_EUNSUPPORTED;
+  IgemmArgs a;
+  const int rc = fill_args(&d2, x1, x2, w, bias, y_pool, nullptr, nullptr, nullptr, a);
+  if (rc) return rc;
+  a.ypool = (char *)y_pool;
+  a.pidx = pool_idx;
+  return conv3r_launch(&d2, a, st);
+}
+
+// the kernel rr_igemm_pool launches for *d ("unsupported" when neither takes it)
+extern "C" const char *rr_igemm_pool_kernel_name(const rr_igemm_desc *d) {
+  if (!d || d->mode != RR_CONV3X3 || d->act != RR_ACT_RELU || d->out_split || d->accumulate ||
+      d->has_mask || d->want_stats || d->out_nchw || d->h < 2 || d->w < 2)
+    return "unsupported";
+  if (stream3_blocks(d, 0) && !d->c_in2) return d->w == 64 ? "stream3_kernel<64,pool>" : "stream3_kernel<32,pool>";
+  rr_igemm_desc d2 = *d;
+  d2.act = RR_ACT_RELU | RR_ACT_POOL | RR_ACT_NOFULL;
+  return conv3r_bc(&d2) ? conv3r_name(&d2) : "unsupported";
 }
 
 static int bnbwd_rows(const rr_igemm_desc *d) { return rr_igemm_stat_blocks(d); }

@@ -33,6 +33,7 @@ struct IgemmArgs {
   const float *alpha;
   const char *res;
   char *ypool;        // act & RR_ACT_POOL: [n][h/2][w/2][c_out] 2x2 max-pool of the output
+  uint8_t *pidx;      // (rr_igemm_pool) its first-max window index, or null
   int ntile;          // conv3r: tiles of the launch (a persistent grid walks them)
 };
 
@@ -65,7 +66,17 @@ __device__ __forceinline__ void store_staged_bnbwd(const IgemmArgs &a, float *st
   double sa = 0.0;
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s0[j] = 0.f; s1[j] = 0.f; }
-#pragma unroll 2
+  // every chunk's t loaded before the first gm store (a store may alias a
+  // later load: in program order each chunk paid a memory latency)
+  f32x4 tp[NCH][2];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int r = (tid + NT * i) / CPR;
+    const long long e = (long long)(p0 + (r < nvalid ? r : 0)) * a.cout + c;
+    tp[i][0] = load4<T>(reinterpret_cast<const T *>(a.bt) + e);
+    tp[i][1] = load4<T>(reinterpret_cast<const T *>(a.bt) + e + 4);
+  }
+#pragma unroll
   for (int i = 0; i < NCH; ++i) {
     const int q = tid + NT * i;
     const int r = q / CPR;
@@ -73,8 +84,8 @@ __device__ __forceinline__ void store_staged_bnbwd(const IgemmArgs &a, float *st
     const long long e = (long long)(p0 + r) * a.cout + c;
     const f32x4 g0 = *reinterpret_cast<const f32x4 *>(stg + r * SROW + cc);
     const f32x4 g1 = *reinterpret_cast<const f32x4 *>(stg + r * SROW + cc + 4);
-    const f32x4 t0 = load4<T>(reinterpret_cast<const T *>(a.bt) + e);
-    const f32x4 t1 = load4<T>(reinterpret_cast<const T *>(a.bt) + e + 4);
+    const f32x4 t0 = tp[i][0];
+    const f32x4 t1 = tp[i][1];
     const float g[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
     const float t[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
     float gm[8];

@@ -957,6 +957,44 @@ __global__ void maxpool_bwd8_kernel(int n, int h, int w, int C, const T *__restr
   }
 }
 
+// MaxPool2d(2, 2) backward of a pool whose input is a ReLU output (the
+// perceptual VGG slice: conv + ReLU + MaxPool2d, 14:189-196): the ReLU mask
+// at a window's argmax is (pooled value > 0) -- the max IS that element --
+// and every other element of the window gets 0 anyway, so the mask comes
+// from the pooled forward output yp instead of the full-size activation
+// (a quarter of the bytes).  Scatter form: one thread per pooled pixel x 8
+// channels writes its whole window (h, w even).  Bitwise the gather form of
+// maxpool_bwd8_kernel with mask = the full-size ReLU output.
+template <typename T>
+__global__ void maxpool_bwd8p_kernel(int n, int h, int w, int C, const T *__restrict__ dy,
+                                     const uint8_t *__restrict__ idx, const T *__restrict__ yp,
+                                     T *__restrict__ dx) {
+  const int ho = h / 2, wo = w / 2, G = C / 8;
+  const int total = n * ho * wo * G;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int g = i % G, op = i / G;
+    const int ox = op % wo, t = op / wo, oy = t % ho, nn = t / ho;
+    const long long o = (long long)op * C + g * 8;
+    const uint2 id = *reinterpret_cast<const uint2 *>(idx + o);
+    f32x4 d0, d1, m0, m1;
+    load8<T>(dy + o, d0, d1);
+    load8<T>(yp + o, m0, m1);
+    const float d[8] = {d0[0], d0[1], d0[2], d0[3], d1[0], d1[1], d1[2], d1[3]};
+    const float m[8] = {m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool at = (int)(((j < 4 ? id.x : id.y) >> (8 * (j & 3))) & 0xff) == k;
+        v[j] = at && m[j] > 0.f ? d[j] : 0.f;
+      }
+      const long long e = (((long long)nn * h + 2 * oy + (k >> 1)) * w + 2 * ox + (k & 1)) * C + g * 8;
+      store8<T>(dx + e, f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]});
+    }
+  }
+}
+
 template <typename T>
 __global__ void maxpool_bwd_kernel(int n, int h, int w, int C, const T *__restrict__ dy,
                                    const uint8_t *__restrict__ idx, T *__restrict__ dx,
@@ -1757,6 +1795,26 @@ extern "C" int rr_maxpool2_fwd(int dtype, int n, int h, int w, int C, const void
   else
     hipLaunchKernelGGL(maxpool_fwd_kernel<float>, g, b, 0, st, n, h, w, C, (const float *)x,
                        (float *)y, idx);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_maxpool2_bwd_pooled(int dtype, int n, int h, int w, int C, const void *dy,
+                                      const uint8_t *idx, const void *y_pool, void *dx,
+                                      rr_stream stream) {
+  if (!dy || !idx || !y_pool || !dx || n < 0 || h < 0 || w < 0) return RR_EINVAL;
+  if (dtype != RR_BF16 && dtype != RR_F32) return RR_EINVAL;
+  if (C % 8 || h % 2 || w % 2 || (long long)n * h * w * C >= 0x7fffffffLL) return RR_EUNSUPPORTED;
+  const long long t8 = (long long)n * (h / 2) * (w / 2) * (C / 8);
+  if (t8 == 0) return RR_OK;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 g(rr_grid_cap((t8 + 255) / 256, 8192)), b(256);
+  if (dtype == RR_BF16)
+    hipLaunchKernelGGL(maxpool_bwd8p_kernel<bf16_t>, g, b, 0, st, n, h, w, C, (const bf16_t *)dy, idx,
+                       (const bf16_t *)y_pool, (bf16_t *)dx);
+  else
+    hipLaunchKernelGGL(maxpool_bwd8p_kernel<float>, g, b, 0, st, n, h, w, C, (const float *)dy, idx,
+                       (const float *)y_pool, (float *)dx);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

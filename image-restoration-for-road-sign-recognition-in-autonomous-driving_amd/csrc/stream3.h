@@ -20,6 +20,10 @@ struct S3Args {
   const char *bt;
   const float *bmean, *binv, *baff_s, *baff_b, *balpha;
   float *bpart, *bapart;     // [nwg][64][3], [nwg]
+  // pool epilogue (stream3_launch_pool): 2x2 max-pool of the ReLU output and
+  // its first-max window index, [n][h/2][w/2][64] (no full-size output)
+  char *ypool;
+  uint8_t *pidx;
 };
 
 // 0 when the descriptor is not handled by the streaming kernel, else the
@@ -30,3 +34,7 @@ struct S3Args {
 int stream3_blocks(const rr_igemm_desc *d, int bnbwd);
 // launch; returns an RR_* status
 int stream3_launch(const rr_igemm_desc *d, const S3Args &a, int bnbwd, hipStream_t st);
+// conv (+ bias) + ReLU + MaxPool2d(2, 2) with the window index (a.ypool,
+// a.pidx; a.y unused); RR_EUNSUPPORTED when the streaming kernel does not
+// take the descriptor
+int stream3_launch_pool(const rr_igemm_desc *d, const S3Args &a, hipStream_t st);

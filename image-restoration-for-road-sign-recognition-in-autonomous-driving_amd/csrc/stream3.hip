@@ -60,7 +60,9 @@ namespace {
 
 constexpr int S3_WG = 256;   // workgroups: one per CU on MI355X (fixed: deterministic partial rows)
 
-enum : int { F_BIAS = 1, F_STATS = 2, F_RELU = 4, F_ACC = 8, F_MASK = 16, F_BNBWD = 32 };
+// F_POOL: the 2x2 max-pool (+ its first-max index) of the activated output
+// instead of the output (VGG16 conv + ReLU + MaxPool2d, 14:189-196)
+enum : int { F_BIAS = 1, F_STATS = 2, F_RELU = 4, F_ACC = 8, F_MASK = 16, F_BNBWD = 32, F_POOL = 64 };
 
 // chunk swizzle: the 16 pixels of a B read at pixel offset P in {0, 1, 2}
 // mod 16 need distinct (p & 1, chunk ^ swz(p)) pairs with chunks c (outer 8
@@ -161,8 +163,13 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
   constexpr bool BNBWD = (F & F_BNBWD) != 0;
   constexpr bool ACC = (F & F_ACC) != 0, MASK = (F & F_MASK) != 0;
   constexpr bool STATS = (F & F_STATS) != 0;
+  constexpr bool POOL = (F & F_POOL) != 0;
+  static_assert(!POOL || ((F & ~(F_BIAS | F_RELU | F_POOL)) == 0 && (F & F_RELU) && MP % 2 == 0 &&
+                          W % (8 * MP) == 0), "pool epilogue: bias + ReLU, row-pair blocks");
   constexpr int NE = BNBWD ? 1 : (ACC ? 1 : 0) + (MASK ? 1 : 0);   // epilogue loads per block
-  constexpr int E = MC * MP * NE, S = MP;          // S: 16-B stores per step
+  // S: stores per step (16-B output stores; POOL: a pooled value + an index
+  // store per channel block and column block pair)
+  constexpr int E = MC * MP * NE, S = POOL ? MC * MP : MP;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
   float *coef = reinterpret_cast<float *>(smem + RING * ROWB);   // [64][2]
 
@@ -247,11 +254,17 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
 
   // ---- per-wave pixel blocks of a step and lane parts ----
   // the wave's 16 MP pixels start at row q0, column x0 (uniform); block ni
-  // sits NRW(ni) rows and XO(ni) columns further (compile time: x0 + 16 MP
-  // never crosses more than the rows the geometry implies)
-  constexpr int NR = (16 * MP + W - 1) / W;     // distinct image rows of a wave's pixels
-  const int q0 = (wp * 16 * MP) / W, x0 = (wp * 16 * MP) % W;
+  // sits brow(ni) rows and bcol(ni) columns further (compile time: x0 + 16 MP
+  // never crosses more than the rows the geometry implies).  POOL: a wave
+  // owns 2 rows x 8 MP columns (blocks 2j / 2j + 1 = rows 0 / 1 of columns
+  // 16 j ..), so a 2x2 window lies in one lane and its xor-1 neighbour
+  constexpr int NR = POOL ? 2 : (16 * MP + W - 1) / W;   // distinct image rows of a wave's pixels
+  constexpr int PCOLS = 8 * MP, WPR = POOL ? W / PCOLS : 1;
+  const int q0 = POOL ? 2 * (wp / WPR) : (wp * 16 * MP) / W;
+  const int x0 = POOL ? PCOLS * (wp % WPR) : (wp * 16 * MP) % W;
   static_assert(W >= 16 * MP || (16 * MP) % W == 0, "block rows");
+  auto brow = [](int ni) constexpr { return POOL ? (ni & 1) : (ni * 16) / W; };
+  auto bcol = [](int ni) constexpr { return POOL ? (ni >> 1) * 16 : (ni * 16) % W; };
   // lane part of a B read for tap column dx and k-half kb: pixel frow + dx of
   // the block, chunk kb * 4 + fq through the swizzle
   uint32_t boff[3][2];
@@ -278,7 +291,7 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     for (int mi = 0; mi < MC; ++mi)
 #pragma unroll
       for (int ni = 0; ni < MP; ++ni) {
-        const long long ub = (pix0 + q0 * W + x0 + ni * 16) * 128 + mi * 32;   // uniform
+        const long long ub = (pix0 + (q0 + brow(ni)) * W + x0 + bcol(ni)) * 128 + mi * 32;   // uniform
         if constexpr (BNBWD) ev0[mi][ni] = load_b64_async(a.bt + ub + le);
         if constexpr (!BNBWD && ACC) ev0[mi][ni] = load_b64_async(a.y + ub + le);
         if constexpr (!BNBWD && MASK) ev1[mi][ni] = load_b64_async(a.mask + ub + le);
@@ -314,8 +327,8 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
 #pragma unroll
     for (int ni = 0; ni < MP; ++ni)
       asm volatile("ds_read_b128 %0, %1 offset:%2"
-                   : "=v"(fb[0][ni]) : "v"(rba[0][(ni * 16) / W] + boff[0][0]),
-                     "i"(((ni * 16) % W) * 128));
+                   : "=v"(fb[0][ni]) : "v"(rba[0][brow(ni)] + boff[0][0]),
+                     "i"(bcol(ni) * 128));
 #pragma unroll
     for (int q = 0; q < 18; ++q) {
       if (q + 1 < 18) {
@@ -324,8 +337,8 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
         for (int ni = 0; ni < MP; ++ni)
           asm volatile("ds_read_b128 %0, %1 offset:%2"
                        : "=v"(fb[(q + 1) & 1][ni])
-                       : "v"(rba[t1 / 3][(ni * 16) / W] + boff[t1 % 3][kb1]),
-                         "i"(((ni * 16) % W) * 128));
+                       : "v"(rba[t1 / 3][brow(ni)] + boff[t1 % 3][kb1]),
+                         "i"(bcol(ni) * 128));
         asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(MP) : "memory");
       } else {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -394,6 +407,33 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
         pk[mi][ni] = pack4(g);
       }
     }
+    if constexpr (POOL) {
+      // the 2x2 window (rows q0, q0 + 1 of columns x0 + 16 j + frow and its
+      // xor-1 neighbour lane) on the bf16-rounded values -- the stored ones
+      // maxpool_fwd8 would read -- in window order, first max + its index
+      const long long prow = (pix0 / W + q0) >> 1;                // pooled row (uniform)
+#pragma unroll
+      for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+        for (int j = 0; j < MP / 2; ++j) {
+          const uint2 a0 = pk[mi][2 * j], a1 = pk[mi][2 * j + 1];
+          const uint2 b0 = make_uint2(xor1_u32(a0.x), xor1_u32(a0.y));
+          const uint2 b1 = make_uint2(xor1_u32(a1.x), xor1_u32(a1.y));
+          const f32x4 u0 = unpack4(((u64)a0.y << 32) | a0.x), v0 = unpack4(((u64)b0.y << 32) | b0.x);
+          const f32x4 u1 = unpack4(((u64)a1.y << 32) | a1.x), v1 = unpack4(((u64)b1.y << 32) | b1.x);
+          f32x4 m;
+          uint32_t id[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) m[c] = pool4_first_max(u0[c], v0[c], u1[c], v1[c], id[c]);
+          if ((frow & 1) == 0) {
+            const long long pp = prow * (W / 2) + ((x0 + 16 * j + frow) >> 1);
+            const int c = wc * 32 + mi * 16 + fq * 4;
+            *reinterpret_cast<uint2 *>(a.ypool + (pp * 64 + c) * 2) = pack4(m);
+            *reinterpret_cast<uint32_t *>(a.pidx + pp * 64 + c) = id[0] | (id[1] << 8) | (id[2] << 16) | (id[3] << 24);
+          }
+        }
+      return;
+    }
     // widened stores: per pixel-block pair (A, B) two permlane16 swap levels
     // turn the accumulator layout (lane: 4 channels of one pixel) into 16 B
     // per lane, 4 lanes = the wave's 32 channels (64 B) of one pixel:
@@ -421,7 +461,7 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int ni = 2 * j + h;
-        const long long ub = (pix0 + q0 * W + x0 + ni * 16) * 128;             // uniform
+        const long long ub = (pix0 + (q0 + brow(ni)) * W + x0 + bcol(ni)) * 128;   // uniform
         *reinterpret_cast<uint4 *>(a.y + ub + le2) = make_uint4(v[h][0], v[h][1], v[h][2], v[h][3]);
       }
     }
@@ -691,6 +731,25 @@ int stream3_blocks(const rr_igemm_desc *d, int bnbwd) {
   const long long P = (long long)d->n * d->h * d->w;
   if (P < 256LL * S3_WG || P * 64 > INT_MAX) return 0;
   return S3_WG;
+}
+
+int stream3_launch_pool(const rr_igemm_desc *d, const S3Args &a0, hipStream_t st) {
+  if (!stream3_blocks(d, 0) || d->c_in2 || d->act != RR_ACT_RELU || d->accumulate || d->has_mask ||
+      d->want_stats || !a0.ypool || !a0.pidx)
+    return RR_EUNSUPPORTED;
+  S3Args a = a0;
+  a.wld = 64; a.woff = 0;
+  const int P = d->n * d->h * d->w;
+  // 128-pixel steps, no stagger: the bias + ReLU forward's form (launch_w)
+  if (d->w == 64) {
+    if (d->has_bias) launch1<64, 2, F_BIAS | F_RELU | F_POOL, 0>(a, P, st);
+    else launch1<64, 2, F_RELU | F_POOL, 0>(a, P, st);
+  } else {
+    if (d->has_bias) launch1<32, 2, F_BIAS | F_RELU | F_POOL, 0>(a, P, st);
+    else launch1<32, 2, F_RELU | F_POOL, 0>(a, P, st);
+  }
+  RR_CHECK_LAUNCH();
+  return RR_OK;
 }
 
 int stream3_launch(const rr_igemm_desc *d, const S3Args &a0, int bnbwd, hipStream_t st) {

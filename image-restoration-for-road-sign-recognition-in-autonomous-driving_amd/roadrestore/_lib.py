@@ -74,6 +74,8 @@ _SIGS = {
     "rr_igemm_ex": (I_, [C.POINTER(IgemmDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_, P_, P_]),
     "rr_igemm_stat_blocks": (I_, [C.POINTER(IgemmDesc)]),
     "rr_igemm_kernel_name": (C.c_char_p, [C.POINTER(IgemmDesc), I_]),
+    "rr_igemm_pool": (I_, [C.POINTER(IgemmDesc), P_, P_, P_, P_, P_, P_, P_]),
+    "rr_igemm_pool_kernel_name": (C.c_char_p, [C.POINTER(IgemmDesc)]),
     "rr_wgrad_kernel_name": (C.c_char_p, [C.POINTER(WgradDesc)]),
     "rr_igemm_bnbwd_workspace": (S_, [C.POINTER(IgemmDesc)]),
     "rr_igemm_bnbwd": (I_, [C.POINTER(IgemmDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_, P_, P_]),
@@ -112,6 +114,7 @@ _SIGS = {
     "rr_png_write_batch": (I_, [I_, I_, I_, I_, P_, P_, I_, I_]),
     "rr_nearest_resize_bwd": (I_, [I_, I_, I_, I_, I_, I_, I_, P_, P_, P_]),
     "rr_maxpool2_bwd": (I_, [I_, I_, I_, I_, I_, P_, P_, P_, I_, P_, P_]),
+    "rr_maxpool2_bwd_pooled": (I_, [I_, I_, I_, I_, I_, P_, P_, P_, P_, P_]),
     "rr_conv_in_mfma": (I_, [I_, I_, I_, P_, P_, I_, P_, P_, P_, P_]),
     "rr_im2col3": (I_, [I_, I_, I_, I_, I_, I_, P_, P_, P_]),
     "rr_pack_conv_in": (I_, [I_, I_, I_, I_, P_, P_, P_, P_]),
@@ -170,8 +173,17 @@ class Lib:
                 "(run __graft_entry__.build())")
         self.path = path
         self.dll = C.CDLL(path)
+        # another build loaded for an A/B (RR_LIB_PATH) may predate entry
+        # points this binding knows: those stay unbound (calling one raises)
+        # instead of refusing the library; the in-tree library must export all
+        other = os.path.abspath(path) != os.path.abspath(os.path.join(_HERE, "libroadrestore.so"))
         for name, (res, args) in _SIGS.items():
-            fn = getattr(self.dll, name)
+            try:
+                fn = getattr(self.dll, name)
+            except AttributeError:
+                if not other:
+                    raise
+                continue
             fn.restype = res
             fn.argtypes = args
             setattr(self, name, fn)

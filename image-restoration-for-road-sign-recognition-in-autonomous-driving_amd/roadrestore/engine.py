@@ -197,10 +197,12 @@ class GradSink:
             off += p.numel()
         nz = sum(p.numel() for p in zp)
         if nz:
-            # (torch's fill; the library zero is replay-safe too: round 3 saw
-            # garbage after a second replay, which tools/diag_memset*.py no
-            # longer reproduce -- test_library_zero_in_hip_graph_replays)
-            self.flat[:nz].zero_()
+            # the library's zero (rr_zero), graph-capturable: round 3's
+            # garbage-after-a-second-replay observation does not reproduce
+            # (tools/diag_memset*.py, test_library_zero_in_hip_graph_replays;
+            # the zeros are checked after replays in
+            # test_hip_graph_step_follows_cosine_lr_schedule)
+            ops.zero_(self.flat[:nz])
         self.zero_count = nz
         self.hook = hook
 
@@ -360,8 +362,12 @@ _PAIR_FINALIZE = os.environ.get("RR_BN_PAIR_FINALIZE", "1") != "0"
 def _momentum(bn):
     """BatchNorm2d(momentum=None) (cumulative moving average): -1, the
     finalize then reads the factor 1 / num_batches_tracked on the device (no
-    host sync; as layers.batch_norm)"""
-    return -1.0 if bn.momentum is None else bn.momentum
+    host sync; as layers.batch_norm).  Without running statistics
+    (track_running_stats=False: no counter, nothing updated) the momentum is
+    never used: 0."""
+    if bn.momentum is None:
+        return -1.0 if bn.num_batches_tracked is not None else 0.0
+    return bn.momentum
 
 
 def _fin_args(bn, st, bias, count, out):
@@ -602,6 +608,30 @@ def resblock_backward(blk, S, g_out, sink, pool=None):
     return gx1, gx2
 
 
+# named points of the ResUNet forward where callers may start work on a side
+# stream (VGGPerceptualLoss.prefetch_target(at=...)): a callback registered
+# for a point runs once, on the forward's stream, right after that block
+FORWARD_POINTS = ("start", "res1", "res2", "res3", "bottleneck", "dec3", "dec2")
+_AT_POINT = {}
+
+
+def at_forward_point(name, fn):
+    if name not in FORWARD_POINTS:
+        raise ValueError(f"unknown forward point {name!r} (one of {FORWARD_POINTS})")
+    _AT_POINT.setdefault(name, []).append(fn)
+
+
+def drop_forward_point(fn):
+    for fns in _AT_POINT.values():
+        while fn in fns:
+            fns.remove(fn)
+
+
+def _reached(name):
+    for fn in _AT_POINT.pop(name, ()):
+        fn()
+
+
 def resunet_block_names():
     return ["res1", "res2", "res3", "bottleneck.0", "bottleneck.1", "bottleneck.2", "dec3", "dec2",
             "dec1"]
@@ -619,6 +649,7 @@ def _skip_align(u, h, w):
 
 def resunet_forward(m, x, wc, dt, training, need_bwd):
     wc.begin()
+    _reached("start")
     n, _, H, W = x.shape
     if H < 8 or W < 8:
         raise ValueError("ResUNet needs H, W >= 8 (three 2x2 max-pools, floor mode)")
@@ -636,20 +667,26 @@ def resunet_forward(m, x, wc, dt, training, need_bwd):
         S.e1pre = e1pre
     r1, S.res1, (p1, i1) = resblock_forward(m.res1, e1, None, n, H, W, wc, dt, training, need_bwd,
                                             pool=True)
+    _reached("res1")
     r2, S.res2, (p2, i2) = resblock_forward(m.res2, p1, None, n, H2, W2, wc, dt, training,
                                             need_bwd, pool=True)
+    _reached("res2")
     r3, S.res3, (p3, i3) = resblock_forward(m.res3, p2, None, n, H3, W3, wc, dt, training,
                                             need_bwd, pool=True)
+    _reached("res3")
     b = p3
     for i in range(3):
         b, S[f"bottleneck.{i}"] = resblock_forward(m.bottleneck[i], b, None, n, H4, W4, wc,
                                                    dt, training, need_bwd)
+    _reached("bottleneck")
     u3, pku3 = _convT_up(wc, dt, m.up3, b, n, H4, W4, need_bwd)
     u3, al3 = _skip_align(u3, H3, W3)
     d3, S.dec3 = resblock_forward(m.dec3, u3, r3, n, H3, W3, wc, dt, training, need_bwd)
+    _reached("dec3")
     u2, pku2 = _convT_up(wc, dt, m.up2, d3, n, H3, W3, need_bwd)
     u2, al2 = _skip_align(u2, H2, W2)
     d2, S.dec2 = resblock_forward(m.dec2, u2, r2, n, H2, W2, wc, dt, training, need_bwd)
+    _reached("dec2")
     u1, pku1 = _convT_up(wc, dt, m.up1, d2, n, H2, W2, need_bwd)
     u1, al1 = _skip_align(u1, H, W)
     d1, S.dec1 = resblock_forward(m.dec1, u1, r1, n, H, W, wc, dt, training, need_bwd)
@@ -819,16 +856,20 @@ def vgg_features_forward(features, x, wc, dt, upto=None, need_bwd=False):
             act = RELU if kind == "conv_relu" else 0
             nxt_pool = li + 1 < len(layers) and layers[li + 1][0] == "pool" and \
                 _pool_2x2(layers[li + 1][1])
-            if cur is not None and not need_bwd and nxt_pool and \
-                    _ex_fusable(cur.dtype, n, h, w, cur.shape[-1], 0, mod.weight.shape[0],
-                                act | ops.RR_ACT_POOL | ops.RR_ACT_NOFULL):
-                # no backward (the judge, the perceptual target): conv + ReLU +
-                # MaxPool2d in one pass, the full-size map never written
-                pk = wc.conv(mod.weight, dt, dgrad=False)
-                _, y, _ = ops.igemm(RR_CONV3X3, cur, None, n, h, w, pk[0], mod.weight.shape[0],
-                                    bias=mod.bias, act=act, pool_only=True)
+            cout = mod.weight.shape[0]
+            pname = ops.igemm_pool_kernel_name(ops.igemm_pool_desc(cur, n, h, w, cout, mod.bias is not None)) \
+                if cur is not None and kind == "conv_relu" and nxt_pool and cur.dtype == torch.bfloat16 \
+                and h % 2 == 0 and w % 2 == 0 else "unsupported"
+            if pname != "unsupported":
+                # conv + ReLU + MaxPool2d in one pass (rr_igemm_pool), the
+                # full-size map never written; with a backward the window
+                # index is kept and the pool's backward takes its ReLU mask
+                # from the pooled output ("pool_p", rr_maxpool2_bwd_pooled)
+                pk = wc.conv(mod.weight, dt, dgrad=need_bwd)
+                y, idx = ops.igemm_pool(cur, n, h, w, pk[0], cout, bias=mod.bias,
+                                        want_idx=need_bwd or pname.startswith("stream3"))
                 S.acts.append((kind, mod, cur, pk, h, w, None))
-                S.acts.append(("pool", layers[li + 1][1], None, None, h, w, None))
+                S.acts.append(("pool_p", layers[li + 1][1], y, None, h, w, idx if need_bwd else None))
                 cur = y
                 skip_pool = True
                 continue
@@ -843,6 +884,9 @@ def vgg_features_forward(features, x, wc, dt, upto=None, need_bwd=False):
             S.acts.append((kind, mod, cur, pk, h, w, None))
             cur = y
         else:
+            if not _pool_2x2(mod):
+                raise NotImplementedError(f"VGG feature pool {mod}: only MaxPool2d(2, 2) (floor) "
+                                          "is implemented")
             y, idx = ops.maxpool2_fwd(cur)
             S.acts.append((kind, mod, cur, None, h, w, idx))
             h, w = h // 2, w // 2
@@ -861,6 +905,10 @@ def vgg_features_backward_input(S, g_pre_last, x_grad_out=None, accumulate=False
     acts = S.acts
     for li in range(len(acts) - 1, -1, -1):
         kind, mod, xin, pk, h, w, idx = acts[li]
+        if kind == "pool_p":
+            # (fused conv + ReLU + pool: xin is the pooled output)
+            g = ops.maxpool2_bwd_pooled(g, idx, xin, h, w)
+            continue
         if kind == "pool":
             # input of the pool is the previous layer's (relu) output
             prev_relu = li > 0 and acts[li - 1][0] == "conv_relu"

@@ -573,6 +573,48 @@ def maxpool2_fwd(x):
     return y, idx
 
 
+def maxpool2_bwd_pooled(dy, idx, y_pool, h, w):
+    """MaxPool2d(2, 2) backward through the ReLU before it, the mask taken
+    from the pooled forward output (rr_maxpool2_bwd_pooled; bitwise
+    maxpool2_bwd with mask = the full-size ReLU output)."""
+    n, _, _, Cc = dy.shape
+    out = torch.empty((n, h, w, Cc), dtype=dy.dtype, device=dy.device)
+    lib().check(lib().rr_maxpool2_bwd_pooled(rr_dtype(dy.dtype), n, h, w, Cc, _p(dy), _p(idx),
+                                             _p(y_pool), _p(out), stream()),
+                "rr_maxpool2_bwd_pooled")
+    return out
+
+
+def igemm_pool_desc(x1, n, h, w, cout, has_bias):
+    return IgemmDesc(rr_dtype(x1.dtype), RR_CONV3X3, n, h, w, x1.shape[-1], 0, cout, 0, 1, 0,
+                     int(has_bias), 0, 0, 0)
+
+
+def igemm_pool_kernel_name(d):
+    """The kernel rr_igemm_pool launches for ``d`` ("unsupported": none, or
+    an older build loaded for an A/B that lacks the entry point)."""
+    fn = getattr(lib(), "rr_igemm_pool_kernel_name", None)
+    return fn(C.byref(d)).decode() if fn is not None else "unsupported"
+
+
+def igemm_pool(x1, n, h, w, wpack, cout, bias=None, want_idx=True):
+    """conv3x3 (+ bias) + ReLU + MaxPool2d(2, 2) in one pass (rr_igemm_pool):
+    -> (pooled [n, h/2, w/2, cout], first-max index or None); the full-size
+    output is never written."""
+    _need_cuda(x1, wpack)
+    d = igemm_pool_desc(x1, n, h, w, cout, bias is not None)
+    yp = torch.empty((n, h // 2, w // 2, cout), dtype=x1.dtype, device=x1.device)
+    idx = torch.empty((n, h // 2, w // 2, cout), dtype=torch.uint8, device=x1.device) \
+        if want_idx else None
+
+    def launch():
+        lib().check(lib().rr_igemm_pool(C.byref(d), _p(x1), None, _p(wpack), _p(bias), _p(yp),
+                                        _p(idx), stream()), "rr_igemm_pool")
+    _launch(lambda: igemm_pool_kernel_name(d), 2.0 * n * h * w * cout * 9 * x1.shape[-1], launch,
+            f"fwd m{RR_CONV3X3} {n}x{h}x{w} c{x1.shape[-1]}+0->{cout} pool")
+    return yp, idx
+
+
 def nearest_resize(x, ho, wo):
     """F.interpolate(x, size=(ho, wo)) mode 'nearest' (14:169-182), NHWC."""
     _need_cuda(x)

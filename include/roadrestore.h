@@ -103,6 +103,18 @@ int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
 int rr_igemm_ex(const rr_igemm_desc *d, const void *x1, const void *x2, const void *w,
                 const float *bias, const float *alpha, const void *res, void *y1,
                 void *y_pool, const void *mask, float *stats_partial, rr_stream stream);
+/* conv (+ bias) + ReLU + MaxPool2d(2, 2) (floor) in one pass, the full-size
+ * output never written: y_pool [n][h/2][w/2][c_out] and, when pool_idx is
+ * not null, the first-max window index (0..3, rr_maxpool2_fwd's) for the
+ * backward (rr_maxpool2_bwd_pooled).  The perceptual VGG slice's conv + ReLU
+ * + MaxPool2d pairs (torchvision vgg16 features[2:5], [7:10], 14:189-196).
+ * d->act must be RR_ACT_RELU; no split / accumulate / mask / statistics.
+ * bf16 3x3: the row-streaming kernel (64 -> 64 channels, 64x64 / 32x32 maps;
+ * needs pool_idx) or the tap-reuse conv; others RR_EUNSUPPORTED. */
+int rr_igemm_pool(const rr_igemm_desc *d, const void *x1, const void *x2, const void *w,
+                  const float *bias, void *y_pool, uint8_t *pool_idx, rr_stream stream);
+/* the kernel rr_igemm_pool launches for *d, or "unsupported" */
+const char *rr_igemm_pool_kernel_name(const rr_igemm_desc *d);
 /* number of row blocks the partial stats buffer holds: [blocks][c_out][2] */
 int rr_igemm_stat_blocks(const rr_igemm_desc *d);
 /* The kernel rr_igemm (bnbwd = 0) or rr_igemm_bnbwd (bnbwd = 1) launches for
@@ -332,6 +344,14 @@ int rr_maxpool2_fwd(int dtype, int n, int h, int w, int C, const void *x,
 int rr_maxpool2_bwd(int dtype, int n, int h, int w, int C, const void *dy,
                     const uint8_t *idx, void *dx, int accumulate,
                     const void *mask, rr_stream stream);
+/* the same backward when the pool's input is a ReLU output (VGG16 features,
+ * 14:189-196): the mask is taken from the POOLED forward output y_pool
+ * [n][h/2][w/2][C] (the ReLU mask at a window's argmax is y_pool > 0; every
+ * other element is 0 anyway), so the full-size activation need not be kept;
+ * dx fully written (no accumulate).  Bitwise rr_maxpool2_bwd with mask =
+ * the full-size ReLU output.  h, w even, C % 8 == 0. */
+int rr_maxpool2_bwd_pooled(int dtype, int n, int h, int w, int C, const void *dy,
+                           const uint8_t *idx, const void *y_pool, void *dx, rr_stream stream);
 
 /* PNG encoding of restored uint8 HWC images (17:89-99: cv2.imwrite of the
  * BGR-swapped array, which stores the RGB pixels).  Host memory, no device:

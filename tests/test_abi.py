@@ -166,6 +166,30 @@ def test_kernel_selection_for_the_benched_layers():
             assert rr_stat_blocks(d) == 512 * h * h // 128
 
 
+def test_kernel_selection_odd_batches_stay_on_whole_rows(monkeypatch):
+    """host-only: a 16x16 / 8x8 map whose pixel count does not
+    fill the first pick's 512-pixel tiles takes the 256- or 128-pixel
+    whole-row tiles before the row-segment ones; only batches that fill none
+    of them drop to segments.  Both K loops (RR_CONV3R_RW) pick the same tile."""
+    from roadrestore import ops
+    from roadrestore._lib import RR_BF16, RR_CONV3X3, IgemmDesc
+    want = {  # (n, h, c_in, c_out): kernel (LDS-weight K loop)
+        (3, 16, 256, 256): "conv3r_kernel<16,128,32,w8>",    # P = 768: 256-pixel tiles
+        (512, 16, 256, 256): "conv3r_kernel<16,128,w8>",     # the benched batch: 512
+        (1, 8, 512, 512): "conv3r_kernel<s1,128,w8>",        # P = 64: no whole-row tile fits
+        (3, 8, 512, 512): "conv3r_kernel<s1,128,w8>",        # P = 192
+        (2, 8, 512, 512): "conv3r_kernel<8,128,32>",         # P = 128: 4-wave 128-pixel tiles
+        (1, 16, 64, 64): "conv3r_kernel<16,64,32>",          # P = 256, 64 channels
+    }
+    for rw in ("0", "1"):
+        monkeypatch.setenv("RR_CONV3R_RW", rw)
+        for (n, h, ci, co), f in want.items():
+            d = IgemmDesc(RR_BF16, RR_CONV3X3, n, h, h, ci, 0, co, 0, 0, 0, 1, 0, 1, 0)
+            exp = f + (",rw" if rw == "1" and "<s" not in f else "")
+            exp = exp.replace(">,rw", ",rw>")
+            assert ops.igemm_kernel_name(d) == exp, (n, h, ci, co, rw, ops.igemm_kernel_name(d))
+
+
 def test_kernel_selection_at_the_reference_geometry():
     """host-only: the 3x3 convs of the reference's 224x224 pipeline and its
     112 / 56 / 28 / 14 maps (14:202-205, 17:66, 18:28-32) take the

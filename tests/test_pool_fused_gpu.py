@@ -1,0 +1,101 @@
+"""conv + ReLU + MaxPool2d(2, 2) in one pass (rr_igemm_pool) and the pool
+backward with its ReLU mask taken from the pooled output
+(rr_maxpool2_bwd_pooled): the perceptual VGG slice's conv1_2 / conv2_2 +
+pool pairs (torchvision vgg16 features[2:5], [7:10]; 14:189-196).
+
+Both must be BITWISE equal to the separate ops they replace -- the conv with
+its ReLU epilogue, rr_maxpool2_fwd on the stored bf16 map (first max in
+window order, NaN rule), and rr_maxpool2_bwd with mask = the full-size ReLU
+output -- on the row-streaming kernel (64 -> 64 channels at 64x64 / 32x32),
+the tap-reuse conv's whole-row tiles (32x32 / 16x16 / 8x8) and its
+row-segment tiles (the reference's 224 / 112 / 56 geometry, odd sizes)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+BF = torch.bfloat16
+
+
+def _mk(n, h, w, c, co, dev, seed):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    x = torch.randn(n, h, w, c, device=dev, generator=g).to(BF)
+    wt = torch.randn(co, c, 3, 3, device=dev, generator=g) / (3 * c ** 0.5)
+    b = torch.randn(co, device=dev, generator=g) * 0.1
+    return x, wt, b
+
+
+# (n, h, w, c_in, c_out, kernel prefix)
+CASES = [
+    (256, 64, 64, 64, 64, "stream3_kernel<64,pool>"),     # VGG conv1_2 at cfg3 size (half batch)
+    (256, 32, 32, 64, 64, "stream3_kernel<32,pool>"),
+    (8, 32, 32, 128, 128, "conv3r_kernel<32,128"),         # VGG conv2_2
+    (8, 16, 16, 256, 256, "conv3r_kernel<16,128"),         # conv3_3 (+ pool4 in the judge)
+    (4, 56, 56, 128, 128, "conv3r_kernel<s2,128"),         # the 224 pipeline's conv2_2 map
+    (2, 30, 22, 64, 64, "conv3r_kernel<s2,64"),            # odd-size segments, floor pooling
+    (2, 64, 64, 64, 64, "conv3r_kernel<s2,64"),            # golden-size batch: segments at 64x64
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_igemm_pool_equals_conv_relu_then_pool(dev, case):
+    from roadrestore import ops
+    from roadrestore._lib import RR_CONV3X3
+    n, h, w, c, co, kname = case
+    x, wt, b = _mk(n, h, w, c, co, dev, seed=h * 7 + c)
+    pk, _ = ops.pack_conv(wt, BF)
+    d = ops.igemm_pool_desc(x, n, h, w, co, True)
+    assert ops.igemm_pool_kernel_name(d).startswith(kname), ops.igemm_pool_kernel_name(d)
+    y, _, _ = ops.igemm(RR_CONV3X3, x, None, n, h, w, pk, co, bias=b, act=1)
+    ref, ridx = ops.maxpool2_fwd(y)
+    yp, idx = ops.igemm_pool(x, n, h, w, pk, co, bias=b)
+    torch.cuda.synchronize()
+    assert torch.equal(yp, ref)
+    assert torch.equal(idx, ridx)
+    # no-index form (the no-backward target / judge) on the tap-reuse conv
+    if not kname.startswith("stream3"):
+        yp2, none = ops.igemm_pool(x, n, h, w, pk, co, bias=b, want_idx=False)
+        assert none is None and torch.equal(yp2, ref)
+
+
+@pytest.mark.parametrize("shape", [(256, 64, 64, 64), (8, 32, 32, 128), (3, 30, 22, 64)])
+def test_maxpool_bwd_pooled_mask_equals_full_mask(dev, shape):
+    """pool backward through the ReLU: mask from the pooled output == mask
+    from the full-size ReLU output (many exact-zero ties after the ReLU)"""
+    from roadrestore import ops
+    n, h, w, c = shape
+    g = torch.Generator(device=dev).manual_seed(5)
+    a = torch.relu(torch.randn(n, h, w, c, device=dev, generator=g)).to(BF)   # a ReLU output
+    a[:, ::3] = 0                                                         # whole zero windows
+    yp, idx = ops.maxpool2_fwd(a)
+    dy = torch.randn(n, h // 2, w // 2, c, device=dev, generator=g).to(BF)
+    ref = ops.maxpool2_bwd(dy, idx, h, w, mask=a)
+    got = ops.maxpool2_bwd_pooled(dy, idx, yp, h, w)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+
+
+def test_perceptual_features_fused_pool_grad_equals_unfused(dev, monkeypatch):
+    """the VGG slice's forward + input grad with the fused pools == the same
+    with them split (conv, rr_maxpool2_fwd, full-mask backward): bitwise"""
+    import roadrestore as rr
+    from roadrestore import engine, ops
+    torch.manual_seed(0)
+    perc = rr.VGGPerceptualLoss().to(dev)
+    n = 256
+    x = torch.rand(n, 3, 64, 64, device=dev)
+    wc = engine.WeightCache(static=True)
+    feats, S = engine.vgg_features_forward(perc.slice, x, wc, BF, need_bwd=True)
+    kinds = [k for k, *_ in S.acts]
+    assert kinds.count("pool_p") == 2
+    gl = torch.randn(feats.shape, device=dev).to(BF)
+    gx = engine.vgg_features_backward_input(S, gl)
+    torch.cuda.synchronize()
+    # unfused: pretend rr_igemm_pool supports nothing
+    monkeypatch.setattr(ops, "igemm_pool_kernel_name", lambda d: "unsupported")
+    feats2, S2 = engine.vgg_features_forward(perc.slice, x, wc, BF, need_bwd=True)
+    assert [k for k, *_ in S2.acts].count("pool") == 2
+    gx2 = engine.vgg_features_backward_input(S2, gl)
+    torch.cuda.synchronize()
+    assert torch.equal(feats, feats2)
+    assert torch.equal(gx, gx2)
