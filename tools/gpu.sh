@@ -19,6 +19,9 @@
 #                                                               -> <tag>_abstep.txt
 #   ablibs:PATH      graph-step A/B of this build vs another .so -> <tag>_ablibs.txt
 #   abconv:PATH      per-layer conv3r A/B of this build vs another .so -> <tag>_abconv.txt
+#   ablayers:PATH[;SET] per-layer times + output SHA-1 of this build vs another .so
+#                    (tools/layer_times.py SET = wgrad / conv3r) -> <tag>_ablayers_<SET>.txt
+#   gtrace           rocprofv3 kernel trace of the graph-replayed bench -> <tag>_graph_trace.json
 #   py:SCRIPT[;ARGS] python SCRIPT ARGS                         -> <tag>_py.log
 set -o pipefail
 TAG=$1; shift
@@ -96,6 +99,28 @@ run_step() {
       done
       unset RR_LIB_PATH SET
       cat ${O}_abconv.txt ;;
+    ablayers)
+      # per-layer times + output SHA-1 (tools/layer_times.py SET) of this build
+      # vs another .so, alternating processes, 3 rounds
+      local other=${arg%%;*} set=${arg#*;}
+      [ "$set" = "$arg" ] && set=wgrad
+      for i in 1 2 3; do
+        for L in cur other; do
+          if [ $L = other ]; then export RR_LIB_PATH=$other; else unset RR_LIB_PATH; fi
+          timeout -k 10 200 python -u tools/layer_times.py $set > ${O}_ablayers.log 2>&1 || { unset RR_LIB_PATH; return 1; }
+          sed "s/^/$L $i /" ${O}_ablayers.log >> ${O}_ablayers_${set}.txt
+        done
+      done
+      unset RR_LIB_PATH
+      grep total_ms ${O}_ablayers_${set}.txt ;;
+    gtrace)
+      # rocprofv3 kernel trace of the HIP-graph replays of the driver's bench
+      # command; tools/graph_trace.py: kernel sum vs wall per step
+      rm -rf ${O}_gt
+      timeout -k 10 300 rocprofv3 --kernel-trace -d ${O}_gt -o gt -- python bench.py --gpus 1 \
+        --steps 20 --warmup 5 --no-cpu-baseline --no-probe > ${O}_gtrace_bench.json 2> ${O}_gtrace.err || return 1
+      local db=$(find ${O}_gt -name "*.db" | head -1)
+      python tools/graph_trace.py "$db" ${O}_graph_trace.json 20 ;;
     py)
       local script=${arg%%;*} rest=""
       [ "$script" != "$arg" ] && rest=${arg#*;}
