@@ -842,7 +842,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     };
     // (in two halves of the wave's rows: the whole tile's operand, 64 VGPRs
     // on the 128 x 64 tiles, spilled next to the accumulators)
-    constexpr int RH = R / 2;                         // rows per half (even: row pairs stay whole)
+    constexpr int RH = R >= 4 ? R / 2 : R;            // rows per half (even: row pairs stay whole)
     constexpr int NQ = RH * NS * (NM / 2);
     uint4 opq[NQ];
     auto preload = [&](int oh) __attribute__((always_inline)) {
@@ -1015,7 +1015,10 @@ int r3_tpx(R3Pick k) { return (k.nwv / (k.bc / k.nw)) * 128; }
 R3Pick r3_pick(const rr_igemm_desc *d) {
   const long long P = (long long)d->n * d->h * d->w;
   const int W = d->w;
-  const bool square = d->h == W && (W == 8 || W == 16 || W == 32);
+  // RR_CONV3R_W64 (A/B): 0 = the 64x64 maps on row-segment tiles
+  const char *e64 = getenv("RR_CONV3R_W64");
+  const bool w64 = W == 64 && !(e64 && !atoi(e64));
+  const bool square = d->h == W && (W == 8 || W == 16 || W == 32 || w64);
   const char *e = getenv("RR_CONV3R_WG");
   const int nwv = e && (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : (d->c_out % 128 == 0 && W != 32 ? 8 : 4);
   if (square) {
@@ -1024,7 +1027,7 @@ R3Pick r3_pick(const rr_igemm_desc *d) {
     const char *re = getenv("RR_CONV3R_RW");
     const int rwm = re ? atoi(re) : 0;
     const int rw = ((d->c_in1 + d->c_in2) % 64 == 0) && (rwm == 1 || (rwm == 32 && W == 32)) &&
-                   !(W == 8 && d->c_out % 128 != 0);
+                   !(W == 8 && d->c_out % 128 != 0) && W != 64;
     // 128-channel column blocks where c_out % 256 == 0 too: 2-3 % faster per
     // layer than 256-channel ones at 16x16 / 8x8 once the row loop lost its
     // run-time switches (profiles/r4zk_conv3r_bc_ab.jsonl); the small-batch
@@ -1130,6 +1133,10 @@ static int conv3r_go(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
     hipLaunchKernelGGL((conv3r_kernel<0, BC, NW, NWV, HB, SG, 0>), grid, block, 0, st, a);
   } else {
     switch (d->w) {
+      case 64:
+        if constexpr (RW) return RR_EUNSUPPORTED;
+        else hipLaunchKernelGGL((conv3r_kernel<64, BC, NW, NWV, HB, 0, 0>), grid, block, 0, st, a);
+        break;
       case 32: hipLaunchKernelGGL((conv3r_kernel<32, BC, NW, NWV, HB, 0, RW>), grid, block, 0, st, a); break;
       case 16: hipLaunchKernelGGL((conv3r_kernel<16, BC, NW, NWV, HB, 0, RW>), grid, block, 0, st, a); break;
       default:
@@ -1185,7 +1192,7 @@ int conv3r_launch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
 const char *conv3r_name(const rr_igemm_desc *d) {
   if (!conv3r_bc(d)) return "invalid";
   const R3Pick k = r3_pick(d);
-  static char names[3][5][2][2][40];
+  static char names[4][5][2][2][40];
   static char segnames[2][2][2][40];
   char *n;
   if (k.sg) {
@@ -1195,7 +1202,7 @@ const char *conv3r_name(const rr_igemm_desc *d) {
     if (!n[0]) snprintf(n, 40, "conv3r_kernel<s%d,%d%s>", k.sg, k.bc, k.nwv == 8 ? ",w8" : "");
     return n;
   }
-  const int wi = d->w == 8 ? 0 : d->w == 16 ? 1 : 2;
+  const int wi = d->w == 8 ? 0 : d->w == 16 ? 1 : d->w == 32 ? 2 : 3;
   const int bi = k.bc == 64 ? (k.nw == 64 ? 0 : 4) : k.bc == 256 ? 3 : (k.nw == 64 ? 1 : 2);
   const int vi = k.nwv == 8;
   n = names[wi][bi][vi][k.rw != 0];

@@ -144,13 +144,13 @@ def test_kernel_selection_for_the_benched_layers():
     64x64 input) -- host-only queries, no launch: the row-streaming conv and
     weight grad on the 64-channel 64x64 / 32x32 layers, the tap-reuse conv
     (conv3r) on the wider 32x32 .. 8x8 layers and on dec1's 64 + 64 concat
-    (row-segment tiles, one pass), the LDS-halo weight grads on the 16x16 /
+    (64x64 whole-row tiles, one pass), the LDS-halo weight grads on the 16x16 /
     8x8 ones."""
     from roadrestore import ops
     from roadrestore._lib import RR_BF16, RR_CONV3X3, IgemmDesc, WgradDesc
     want = {  # (h, c_in1, c_in2, c_out): (fwd, wgrad)
         (64, 64, 0, 64): ("stream3_kernel<64>", "swgrad_kernel<64>"),
-        (64, 64, 64, 64): ("conv3r_kernel<s2,64>", "swgrad_kernel<64>"),  # one pass, fp32 sum
+        (64, 64, 64, 64): ("conv3r_kernel<64,64>", "swgrad_kernel<64>"),  # one pass, fp32 sum
         (32, 64, 0, 128): ("conv3r_kernel<32,128>", "swgrad_kernel<32>"),
         (32, 128, 64, 64): ("conv3r_kernel<32,64>", "swgrad_kernel<32>"),
         (16, 256, 0, 256): ("conv3r_kernel<16,128,w8>", "wgrad3_halo_kernel<16>"),

@@ -54,6 +54,8 @@ SHAPES = [
     (512, 8, 512, 0, 256, "conv3r_kernel<8,128,32>"), # 128 x 32 wave tiles: 512 workgroups
     (8, 8, 256, 0, 512, "conv3r_kernel<8,128,32>"),   # small batch: 128 x 32 tiles
     (8, 8, 128, 0, 128, "conv3r_kernel<8,128,32>"),
+    (2, 64, 64, 64, 64, "conv3r_kernel<64,64>"),      # dec1.c1 (concat) fwd: 2-row wave tiles
+    (2, 64, 128, 0, 128, "conv3r_kernel<64,128>"),
 ]
 # the 8-wave, one-per-CU variant (RR_CONV3R_WG=8, the default where
 # c_out % 128 == 0)
@@ -64,6 +66,8 @@ SHAPES_W8 = [
     (8, 16, 128, 0, 256, "conv3r_kernel<16,128,w8>"),
     (512, 8, 512, 0, 512, "conv3r_kernel<8,128,w8>"),
     (8, 8, 256, 0, 512, "conv3r_kernel<8,128,32,w8>"),
+    (2, 64, 64, 0, 128, "conv3r_kernel<64,128,w8>"),  # dec1.c1 dgrad (64 -> 64 + 64)
+    (2, 64, 64, 64, 64, "conv3r_kernel<64,64,32,w8>"),
 ]
 
 
@@ -119,7 +123,8 @@ def test_conv3r_fwd_bias_stats_relu(dev, shape, monkeypatch):
 
 
 @pytest.mark.parametrize("shape", [(2, 32, 128, 0, 128), (8, 16, 256, 0, 256), (8, 8, 512, 0, 512),
-                                   (512, 8, 512, 0, 512), (4, 32, 128, 0, 64)])
+                                   (512, 8, 512, 0, 512), (4, 32, 128, 0, 64), (2, 64, 128, 0, 64),
+                                   (2, 64, 64, 0, 128)])
 @pytest.mark.parametrize("acc,msk", [(True, False), (False, True), (True, True)])
 def test_conv3r_dgrad_epilogues(dev, shape, acc, msk, wg, monkeypatch):
     """dgrad epilogues: accumulate into y (the shortcut / identity grad), the
@@ -145,7 +150,8 @@ def test_conv3r_dgrad_epilogues(dev, shape, acc, msk, wg, monkeypatch):
 
 
 @pytest.mark.parametrize("shape,split", [((4, 16, 128, 0, 384), 256), ((4, 32, 64, 0, 192), 64),
-                                         ((4, 32, 64, 0, 192), 128)])
+                                         ((4, 32, 64, 0, 192), 128),
+                                         ((2, 64, 64, 0, 128), 64)])
 def test_conv3r_concat_split_dgrad(dev, shape, split, wg, monkeypatch):
     """the dgrad of a concat-input conv writes the two halves to two tensors
     (dec3.c1: 128 -> 256 + 128, dec2.c1: 64 -> 128 + 64 / 64 + 128)"""
@@ -167,7 +173,7 @@ def test_conv3r_concat_split_dgrad(dev, shape, split, wg, monkeypatch):
 
 
 @pytest.mark.parametrize("shape", [(2, 32, 128, 0, 128), (8, 16, 256, 0, 256), (8, 8, 512, 0, 512),
-                                   (4, 32, 128, 0, 64), (512, 8, 512, 0, 256)])
+                                   (4, 32, 128, 0, 64), (512, 8, 512, 0, 256), (2, 64, 128, 0, 64)])
 def test_conv3r_bnbwd(dev, shape, wg, monkeypatch):
     """conv dgrad + BN/PReLU backward reduce fused in the staged epilogue ==
     the halo kernel's fused path == the unfused sequence."""
@@ -207,6 +213,38 @@ def test_conv3r_bnbwd(dev, shape, wg, monkeypatch):
         assert rel(got[k], ref[k]) < 2e-2, k
         assert rel(got[k], halo[k]) < 1e-4, k
     assert rel(got["dt0"], halo["dt0"]) < 2e-3
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 64, 64, 64, 0), (2, 64, 64, 0, 128, 64)])
+def test_conv3r_w64_rows_equal_segments(dev, shape, wg, monkeypatch):
+    """64x64 maps: the whole-row tiles (2 output rows per wave) against the
+    row-segment tiles they replace (RR_CONV3R_W64=0) -- dec1.c1 forward with
+    BN statistics and its concat-split dgrad; the same fp32 sums per output
+    (same K order), so bitwise-equal outputs; statistics rows differ only in
+    which pixels share a partial row"""
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV3X3
+    monkeypatch.setenv("RR_CONV3R", "1")
+    n, w, c1, c2, co, split = shape
+    x = rnd(n, c1 + c2, w, w, seed=41)
+    wf, _ = rr.ops.pack_conv((rnd(co, c1 + c2, 3, 3, seed=42) / 24).to(dev), BF)
+    x1 = nhwc(x[:, :c1], dev)
+    x2 = nhwc(x[:, c1:], dev) if c2 else None
+    res = {}
+    for tag in ("1", "0"):
+        monkeypatch.setenv("RR_CONV3R_W64", tag)
+        name = rr.ops.igemm_kernel_name(_desc(n, w, c1, c2, co, split=split, stats=int(not split)))
+        assert name.startswith("conv3r_kernel<64," if tag == "1" else "conv3r_kernel<s2,"), name
+        if split:
+            y1, y2, _ = rr.ops.igemm(RR_CONV3X3, x1, x2, n, w, w, wf, co, split=split)
+            res[tag] = (torch.cat((y1, y2), -1), None)
+        else:
+            y, _, st = rr.ops.igemm(RR_CONV3X3, x1, x2, n, w, w, wf, co, stats=True)
+            res[tag] = (y, st.double().sum(0))
+        torch.cuda.synchronize()
+    assert torch.equal(res["1"][0], res["0"][0])
+    if not split:
+        assert rel(res["1"][1], res["0"][1]) < 1e-6
 
 
 def test_conv3r_stats_rows_deterministic(dev, wg, monkeypatch):

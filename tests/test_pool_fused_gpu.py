@@ -33,7 +33,7 @@ CASES = [
     (8, 16, 16, 256, 256, "conv3r_kernel<16,128"),         # conv3_3 (+ pool4 in the judge)
     (4, 56, 56, 128, 128, "conv3r_kernel<s2,128"),         # the 224 pipeline's conv2_2 map
     (2, 30, 22, 64, 64, "conv3r_kernel<s2,64"),            # odd-size segments, floor pooling
-    (2, 64, 64, 64, 64, "conv3r_kernel<s2,64"),            # golden-size batch: segments at 64x64
+    (2, 64, 64, 64, 64, "conv3r_kernel<64,64"),            # golden-size batch: 64x64 whole rows
 ]
 
 

@@ -63,8 +63,9 @@ def test_stream3_selected(dev, shape, monkeypatch):
     # the tap-reuse conv: 32x32 whole-row tiles (128-pixel partial rows),
     # else row-segment tiles (4 wave rows of 4 x 32 pixels per 16-row band)
     seg = n * -(-w // 32) * -(-h // 16) * 4
-    assert _blocks(n, h, w) == ((n * h * w) // 128 if w == 32 and h == w else seg)
-    assert _name(n, h, w) == ("conv3r_kernel<32,64>" if w == 32 and h == w else "conv3r_kernel<s2,64>")
+    whole = h == w and w in (32, 64)                 # (64x64: whole rows of 2-row wave tiles)
+    assert _blocks(n, h, w) == ((n * h * w) // 128 if whole else seg)
+    assert _name(n, h, w) == ("conv3r_kernel<%d,64>" % w if whole else "conv3r_kernel<s2,64>")
 
 
 @pytest.mark.parametrize("shape", SHAPES)
@@ -196,7 +197,7 @@ def test_stream3_concat_two_pass(dev, shape, stats, bias, act, monkeypatch):
         d = rr.ops.IgemmDesc(rr.ops.RR_BF16, RR_CONV3X3, n, h, w, 64, 64, 64, 0, act, 0,
                              int(bias), 0, int(stats), 0)
         name = rr.ops.igemm_kernel_name(d)
-        one_pass = "conv3r_kernel<32,64>" if w == 32 else "conv3r_kernel<s2,64>"
+        one_pass = "conv3r_kernel<%d,64>" % w if h == w else "conv3r_kernel<s2,64>"
         assert name == ("stream3_kernel<%d>" % w if tag == "1" else one_pass)
         tag = tag or "0"
         y, _, st = rr.ops.igemm(RR_CONV3X3, nhwc(x1, dev), nhwc(x2, dev), n, h, w, wf, 64,
