@@ -326,7 +326,15 @@ def main():
     prefetch_at = os.environ.get("RR_PERC_PREFETCH_AT", "now")
     prefetch_at = None if prefetch_at == "now" else prefetch_at
 
+    # the restorer's weight re-pack (after the previous step's AdamW) forked
+    # onto a side stream at the step start, overlapping the distortion +
+    # ToTensor instead of sitting in front of the first conv (A/B:
+    # RR_WEIGHT_PREFETCH=0)
+    wprefetch = os.environ.get("RR_WEIGHT_PREFETCH", "1") != "0"
+
     def step():
+        if wprefetch:
+            model.prefetch_weights()
         clean = to_tensor(clean_u8)
         if prefetch[0]:
             clean = perc.prefetch_target(clean, at=prefetch_at)

@@ -58,11 +58,14 @@ class WeightCache:
         self._plan = {}          # id(w) -> [w, dtype, dgrad], first-request order
         self._batch = None
         self._fresh = {}         # key -> (ver, packed), set by begin()
+        self._pending = None     # (event, fresh) of a prefetch() not yet joined
 
-    @staticmethod
-    def _ver(w, also=None):
+    def _ver(self, w, also=None):
+        # the fused optimizer's generation counts only for trained weights: a
+        # static cache (the frozen VGG) keyed on it re-packed in every
+        # captured step (2 x 12 us per replay, r5i trace)
         from .optim import GENERATION
-        return (w.data_ptr(), w._version, GENERATION[0],
+        return (w.data_ptr(), w._version, 0 if self.static else GENERATION[0],
                 None if also is None else (also.data_ptr(), also._version))
 
     def _get(self, w, dtype, kind, fn, also=None):
@@ -98,8 +101,38 @@ class WeightCache:
             self._c[key] = (ver, v)
         return v
 
+    def prefetch(self):
+        """Fork the next forward's batched re-pack onto a side stream now --
+        at the start of a training step, before the input pipeline (the
+        distortion + ToTensor, 14:31-64 / 14:199-202) is enqueued: the packs
+        depend on the weights only, so they overlap that work instead of
+        sitting in front of the first conv.  The next begin() joins them.
+        Only once the plan is known (after a first forward); False if nothing
+        was forked.  The pack outputs are persistent buffers (PackBatch), so
+        no allocation crosses streams."""
+        if self._pending is not None or not self._plan:
+            return False
+        w0 = next(iter(self._plan.values()))[0]
+        if not w0.is_cuda:
+            return False
+        side = _pack_stream(w0.device)
+        side.wait_stream(torch.cuda.current_stream(w0.device))
+        with torch.cuda.stream(side):
+            self.begin()
+            ev = torch.cuda.Event()
+            ev.record(side)
+        self._pending = (ev, self._fresh)
+        return True
+
     def begin(self):
-        """Start of a forward: one batched re-pack of every planned conv."""
+        """Start of a forward: one batched re-pack of every planned conv (or
+        the join of a prefetch() of it)."""
+        if self._pending is not None:
+            ev, fresh = self._pending
+            self._pending = None
+            torch.cuda.current_stream().wait_event(ev)
+            self._fresh = fresh
+            return
         self._fresh = {}
         if not self._plan:
             return
@@ -745,6 +778,15 @@ _RECOMPUTE_MASK = os.environ.get("RR_BN_RECOMPUTE_MASK", "1") != "0"
 # (same-box A/B) -- the concurrent kernels contend for the CUs and L2.
 _WGRAD_SIDE = os.environ.get("RR_WGRAD_SIDE_STREAM", "0") != "0"
 _SIDE = {}
+_PACK_SIDE = {}
+
+
+def _pack_stream(device):
+    """the stream WeightCache.prefetch() forks its re-pack onto"""
+    s = _PACK_SIDE.get(device)
+    if s is None:
+        s = _PACK_SIDE[device] = torch.cuda.Stream(device)
+    return s
 
 
 def _side_stream(device):

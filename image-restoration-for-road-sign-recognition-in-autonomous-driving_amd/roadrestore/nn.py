@@ -242,6 +242,14 @@ class _RRNet(tnn.Module):
             self._wc.drop_folds()      # running statistics may have moved (graph replays too)
         return self
 
+    def prefetch_weights(self):
+        """Start re-packing the weights for the next forward on a side stream
+        now (call at the start of a training step, after the previous
+        optimizer step and before the batch's input pipeline): the next
+        forward joins it instead of packing in front of its first conv.  A
+        no-op before the first forward.  Returns whether a pack was forked."""
+        return self._wc.prefetch()
+
     # data-parallel wrappers install a hook called as grad groups become final
     def set_grad_ready_hook(self, hook):
         self._grad_hook = hook

@@ -428,9 +428,10 @@ def test_hip_graph_training_step_matches_eager(dev, prefetch):
     capturable AdamW, weight re-packs) captured in a HIP graph and replayed
     must do exactly what the eager steps do (same kernels, device-side step
     count for the bias correction).  ``prefetch``: the captured step starts
-    F(clean) on the perceptual loss's side stream first (bench.py's schedule;
-    the frozen VGG packs come from before the capture) -- same results as the
-    eager steps without it."""
+    F(clean) on the perceptual loss's side stream first and the ResUNet's
+    weight re-pack on its own (bench.py's schedule; the frozen VGG packs come
+    from before the capture) -- same results as the eager steps without
+    them."""
     import roadrestore as rr
     from roadrestore.optim import flatten_parameters
     torch.manual_seed(3)
@@ -450,6 +451,8 @@ def test_hip_graph_training_step_matches_eager(dev, prefetch):
         opt = rr.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-4, capturable=capturable)
 
         def step():
+            if capturable and prefetch:
+                m.prefetch_weights()               # the weight re-pack on its side stream
             tgt = perc.prefetch_target(clean) if capturable and prefetch else clean
             opt.zero_grad(set_to_none=True)
             loss = rr.unified_loss(m(bad), tgt, perc, 0.1)
@@ -477,6 +480,39 @@ def test_hip_graph_training_step_matches_eager(dev, prefetch):
     for (na, pa), (nb, pb) in zip(ma.named_parameters(), mb.named_parameters()):
         d = (pa - pb).abs().max().item()
         assert d <= 1e-6 * max(1.0, pa.abs().max().item()), (na, d)
+
+
+def test_weight_prefetch_eager_steps_bitwise(dev):
+    """ResUNet.prefetch_weights() at the start of eager training steps (the
+    re-pack forked onto a side stream, joined by the forward) == the same
+    steps without it, bitwise; before the first forward it is a no-op."""
+    import roadrestore as rr
+    from roadrestore.optim import flatten_parameters
+    g = torch.Generator(device=dev).manual_seed(9)
+    clean = torch.rand((4, 3, 32, 32), generator=g, device=dev)
+    bad = (clean * 0.5 + 0.4).clamp(0, 1)
+    res = []
+    for pf in (False, True):
+        torch.manual_seed(7)
+        m = rr.ResUNet().to(dev)
+        m.compute_dtype = torch.bfloat16
+        m.train()
+        flatten_parameters(m)
+        opt = rr.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-4)
+        forked = []
+        for _ in range(3):
+            if pf:
+                forked.append(m.prefetch_weights())
+            opt.zero_grad(set_to_none=True)
+            loss = rr.L1Loss()(m(bad), clean)
+            loss.backward()
+            opt.step()
+        torch.cuda.synchronize()
+        if pf:
+            assert forked == [False, True, True]
+        res.append([p.detach().clone() for p in m.parameters()])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
 
 
 def test_hip_graph_step_follows_cosine_lr_schedule(dev):
