@@ -309,6 +309,9 @@ struct BnBwd {
   const float *aff_s, *aff_b, *alpha;
   const void *t0, *t1;
   const float *mean0, *inv0, *mean1, *inv1;
+  // rr_bn_bwd_apply_convout: g = the final 1x1 conv's input grad, recomputed
+  // from its fp32 NCHW output grad cody [n][3][h][w] and weights cow [3][C]
+  const float *cody, *cow;
 };
 
 template <typename T>
@@ -343,15 +346,17 @@ __device__ __forceinline__ f32x4 bwd_gm(const BnBwd &a, long long e, int c, f32x
 // affine_act_pool_kernel: v = t0*s0 + b0; q = t1*s1 + b1; v += q; relu), so
 // the block output is not read: out > 0 <=> v > 0.  s8/b8 hold BN0's forward
 // affine, sB/bB BN1's; tA/tB are the row's t0/t1 values.
-template <typename T, int MASK>
+template <typename T, int MASK, bool GIN = false>
 __device__ __forceinline__ void bwd_gm8(const BnBwd &a, long long e, const float *s8,
                                         const float *b8, float al, float *g, float &ag,
                                         const float *tA = nullptr, const float *tB = nullptr,
                                         const float *sB = nullptr, const float *bB = nullptr) {
-  f32x4 g0, g1;
-  load8<T>((const T *)a.g + e, g0, g1);
-  g[0] = g0[0]; g[1] = g0[1]; g[2] = g0[2]; g[3] = g0[3];
-  g[4] = g1[0]; g[5] = g1[1]; g[6] = g1[2]; g[7] = g1[3];
+  if constexpr (!GIN) {                 // (GIN: g already holds the upstream grad)
+    f32x4 g0, g1;
+    load8<T>((const T *)a.g + e, g0, g1);
+    g[0] = g0[0]; g[1] = g0[1]; g[2] = g0[2]; g[3] = g0[3];
+    g[4] = g1[0]; g[5] = g1[1]; g[6] = g1[2]; g[7] = g1[3];
+  }
   if constexpr (MASK == 3 || MASK == 5) {
     // + the MaxPool2d(2, 2) backward: the pooled grad goes to the window's
     // first max (rr_maxpool2_bwd's routing), added before the ReLU mask
@@ -476,7 +481,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwd a, float *__r
   }
 }
 
-template <typename T, int MASK, int NBN, bool GMO>
+// GCO: g recomputed from the final 1x1 conv's output grad (a.cody, a.cow:
+// 3 output channels), rounded to T as rr_conv_out_bwd would have stored it
+template <typename T, int MASK, int NBN, bool GMO, bool GCO = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(BnBwd a, const float *__restrict__ coef,
                                                             T *dt0, T *dt1, T *gmo) {
   const int G = a.C / 8;
@@ -515,11 +522,32 @@ __global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(BnBwd a, const float
     sB[k] = 0.f; bB[k] = 0.f;
   }
   const float al = MASK == 2 ? a.alpha[0] : 0.f;
+  float cw[GCO ? 3 : 1][8];
+  if constexpr (GCO) {
+#pragma unroll
+    for (int co = 0; co < 3; ++co)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) cw[co][k] = a.cow[co * a.C + c + k];
+  }
+  const long long hw = (long long)a.h * a.w;
   const long long rows = a.P;
   const long long stride = ((long long)gridDim.x * blockDim.x) / G;
   for (long long r = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / G; r < rows; r += stride) {
     const long long e = r * a.C + c;
     float gm[8], ag = 0.f, tv[2][8];
+    if constexpr (GCO) {
+      const long long nn = r / hw, rr = r - nn * hw;
+      float d[3];
+#pragma unroll
+      for (int co = 0; co < 3; ++co) d[co] = a.cody[(nn * 3 + co) * hw + rr];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float t = 0.f;
+#pragma unroll
+        for (int co = 0; co < 3; ++co) t += d[co] * cw[co][k];
+        gm[k] = Elt<T>::round(t);
+      }
+    }
 #pragma unroll
     for (int b = 0; b < NBN; ++b) {
       f32x4 u0, u1;
@@ -536,9 +564,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(BnBwd a, const float
         l[j][0] = u[0]; l[j][1] = u[1]; l[j][2] = u[2]; l[j][3] = u[3];
         l[j][4] = v[0]; l[j][5] = v[1]; l[j][6] = v[2]; l[j][7] = v[3];
       }
-      bwd_gm8<T, MASK>(a, e, l[0], l[1], al, gm, ag, tv[0], tv[NBN - 1], l[2], l[3]);
+      bwd_gm8<T, MASK, GCO>(a, e, l[0], l[1], al, gm, ag, tv[0], tv[NBN - 1], l[2], l[3]);
     } else {
-      bwd_gm8<T, MASK>(a, e, s8, b8, al, gm, ag, tv[0], tv[NBN - 1], sB, bB);
+      bwd_gm8<T, MASK, GCO>(a, e, s8, b8, al, gm, ag, tv[0], tv[NBN - 1], sB, bB);
     }
     if constexpr (GMO)
       store8<T>(gmo + e, f32x4{gm[0], gm[1], gm[2], gm[3]}, f32x4{gm[4], gm[5], gm[6], gm[7]});
@@ -979,6 +1007,7 @@ static BnBwd make_bnbwd(const rr_bnbwd_desc *d, const void *g, const void *aux,
   a.h = d->h; a.w = d->w; a.pdy = d->pool_dy; a.pidx = d->pool_idx;
   a.g = g; a.aux = aux; a.aff_s = aff_s; a.aff_b = aff_b; a.alpha = alpha;
   a.t0 = t0; a.t1 = t1; a.mean0 = mean0; a.inv0 = inv0; a.mean1 = mean1; a.inv1 = inv1;
+  a.cody = nullptr; a.cow = nullptr;
   return a;
 }
 
@@ -1084,6 +1113,36 @@ extern "C" int rr_bn_bwd_apply(const rr_bnbwd_desc *d, const void *g, const void
   else
     hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(grid), dim3(256), 0, st, a, coef,
                        (float *)dt0, (float *)dt1, (float *)gm_out);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+// the residual-tail BN backward apply of a block whose output feeds the final
+// 1x1 conv (ResUNet dec1, 14:149): g recomputed from that conv's output grad
+// (rr_conv_out_bwd_bnred reduced it without storing it); recomputed ReLU mask
+// (mask kind 4)
+extern "C" int rr_bn_bwd_apply_convout(const rr_bnbwd_desc *d, int h, int w, const float *dy,
+                                       const float *wt, int cout, const float *aff_s,
+                                       const float *aff_b, const void *t0, const float *mean0,
+                                       const float *invstd0, const void *t1, const float *mean1,
+                                       const float *invstd1, const float *coef, void *dt0, void *dt1,
+                                       rr_stream stream) {
+  int rc = bnbwd_check(d);
+  if (rc) return rc;
+  if (!dy || !wt || !aff_s || !aff_b || !t0 || !t1 || !coef || !dt0 || !dt1 || h <= 0 || w <= 0)
+    return RR_EINVAL;
+  if (d->mask_kind != 4 || d->nbn != 2 || d->P % ((long long)h * w)) return RR_EINVAL;
+  if (cout != 3) return RR_EUNSUPPORTED;
+  BnBwd a = make_bnbwd(d, nullptr, nullptr, aff_s, aff_b, nullptr, t0, mean0, invstd0, t1, mean1, invstd1);
+  a.h = h; a.w = w; a.cody = dy; a.cow = wt;
+  const int grid8 = rr_grid_cap((d->P * d->C / 8 + 255) / 256, 4096);
+  hipStream_t st = (hipStream_t)stream;
+  if (d->dtype == RR_BF16)
+    hipLaunchKernelGGL((bn_bwd_apply8_kernel<bf16_t, 4, 2, false, true>), dim3(grid8), dim3(256), 0, st, a, coef,
+                       (bf16_t *)dt0, (bf16_t *)dt1, (bf16_t *)nullptr);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply8_kernel<float, 4, 2, false, true>), dim3(grid8), dim3(256), 0, st, a, coef,
+                       (float *)dt0, (float *)dt1, (float *)nullptr);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

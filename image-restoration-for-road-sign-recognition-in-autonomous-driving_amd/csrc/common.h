@@ -35,6 +35,7 @@ template <> struct Elt<float> {
   static constexpr int dtype = RR_F32;
   __device__ __forceinline__ static float load(const float *p, long long i) { return p[i]; }
   __device__ __forceinline__ static void store(float *p, long long i, float v) { p[i] = v; }
+  __device__ __forceinline__ static float round(float v) { return v; }   // (the stored value)
 };
 template <> struct Elt<bf16_t> {
   static constexpr int size = 2;
@@ -45,6 +46,7 @@ template <> struct Elt<bf16_t> {
   __device__ __forceinline__ static void store(bf16_t *p, long long i, float v) {
     p[i].v = f32_to_bf16(v);
   }
+  __device__ __forceinline__ static float round(float v) { return bf16_to_f32(f32_to_bf16(v)); }
 };
 
 // 4 consecutive elements <-> float4

@@ -139,6 +139,18 @@ template <int N> __device__ __forceinline__ void vm_barrier_st(unsigned long lon
   tb += t2 - t1;
 }
 #define VM_BARRIER(N) vm_barrier_st<N>(st_vm, st_bar)
+// the wave's epilogue time (K loop end -> any return), written at scope exit
+struct C3EpiStamp {
+  unsigned long long *o = nullptr;
+  unsigned long long t1 = 0;
+  __device__ ~C3EpiStamp() {
+    if (o) {
+      unsigned long long t;
+      C3_STAMP(t);
+      o[7] = t - t1;
+    }
+  }
+};
 #else
 #define C3_STAMP(t) do {} while (0)
 #define VM_BARRIER(N) vm_barrier<N>()
@@ -153,6 +165,8 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   constexpr int NS = G::NS, R = G::R, NM = G::NM, WC = G::WC, RS = G::RS;
   constexpr int HW = W * W;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+  [[maybe_unused]] unsigned long long st_k0 = 0;
+  C3_STAMP(st_k0);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -305,6 +319,9 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   const int kc = a.cin / 32, nst = 3 * kc;
   [[maybe_unused]] unsigned long long st_vm = 0, st_bar = 0, st_row0 = 0, st_loop0 = 0, st_loop1 = 0, st_t = 0;
   C3_STAMP(st_loop0);
+#ifdef RR_CONV3R_STAMPS
+  C3EpiStamp epi_stamp;
+#endif
   if constexpr (RW) {
     // ---- RW K loop: every wave loads its own A fragments (its NM 1-KB
     // weight tiles per tap row dy) from global memory (L2) into registers,
@@ -607,6 +624,9 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     unsigned long long *o = rr_c3_stamps + ((long long)blockIdx.x * NWV + wv) * 8;
     o[0] = st_loop1 - st_loop0; o[1] = st_row0; o[2] = st_vm; o[3] = st_bar;
     o[4] = (unsigned long long)nst; o[5] = 1;
+    o[6] = st_loop0 - st_k0;                        // prologue (kernel entry -> K loop)
+    epi_stamp.o = o;
+    epi_stamp.t1 = st_loop1;
   }
 #endif
 

@@ -1375,6 +1375,36 @@ extern "C" const char *rr_igemm_pool_kernel_name(const rr_igemm_desc *d) {
   return conv3r_bc(&d2) ? conv3r_name(&d2) : "unsupported";
 }
 
+// the 3x3 dgrad plus the 1x1 dgrad of a second gradient into one output, one
+// pass: a ResidualBlock's input grad is conv_block[0]'s dgrad + shortcut[0]'s
+// dgrad (14:99-115) -- dec1 (64 + 64 -> 64): per concat half, instead of a
+// 3x3 dgrad and a 1x1 accumulate pass over both halves
+static bool dgrad_sc_ok(const rr_igemm_desc *d, int c_sc) {
+  return d && d->mode == RR_CONV3X3 && !d->act && !d->has_bias && !d->want_stats && !d->has_mask &&
+         !d->out_split && !d->accumulate && !d->out_nchw && !d->c_in2 && c_sc == 64 &&
+         stream3_blocks(d, 0);
+}
+
+extern "C" int rr_igemm_dgrad_sc(const rr_igemm_desc *d, const void *dy, const void *w,
+                                 const void *dy_sc, const void *w_sc, int c_sc, void *y,
+                                 rr_stream stream) {
+  if (!d || !dy || !w || !dy_sc || !w_sc || !y || c_sc <= 0) return RR_EINVAL;
+  if (d->mode != RR_CONV3X3 || d->act || d->has_bias || d->want_stats || d->has_mask ||
+      d->out_split || d->accumulate || d->out_nchw || d->c_in2)
+    return RR_EINVAL;
+  if (!dgrad_sc_ok(d, c_sc)) return RR_EUNSUPPORTED;
+  S3Args s{};
+  s.x = (const char *)dy; s.wt = (const char *)w; s.y = (char *)y;
+  s.n = d->n; s.h = d->h;
+  s.xsc = (const char *)dy_sc; s.wsc = (const char *)w_sc;
+  return stream3_launch_sc(d, s, (hipStream_t)stream);
+}
+
+extern "C" const char *rr_igemm_dgrad_sc_kernel_name(const rr_igemm_desc *d, int c_sc) {
+  if (!dgrad_sc_ok(d, c_sc)) return "unsupported";
+  return d->w == 64 ? "stream3_kernel<64,sc>" : "stream3_kernel<32,sc>";
+}
+
 static int bnbwd_rows(const rr_igemm_desc *d) { return rr_igemm_stat_blocks(d); }
 
 extern "C" size_t rr_igemm_bnbwd_workspace(const rr_igemm_desc *d) {

@@ -834,6 +834,124 @@ __global__ __launch_bounds__(256) void conv_out_bwd64_kernel(
   }
 }
 
+// the final conv's backward fused with the BN-backward reduce of the block
+// that produced its input (ResUNet dec1's residual tail, 14:99-115 + 14:149):
+// the final 1x1 conv's dW / db partials as conv_out_bwd64_kernel, and per
+// channel sum(gm), sum(gm xhat0), sum(gm xhat1) of gm = dL/d(block out)
+// masked by the block's ReLU (out > 0 <=> the pre-ReLU sum > 0), where
+// dL/d(block out) = the conv's input grad (rounded to T as rr_conv_out_bwd
+// stores it) -- never written: rr_bn_bwd_apply_convout recomputes it.  One
+// workgroup per BN partial row ([blocks][64][3], rr_bn_bwd_finalize's layout).
+template <typename T, int COUT>
+__global__ __launch_bounds__(256) void conv_out_bwd64_bnred_kernel(
+    int n, int h, int w, const float *__restrict__ dy, const T *__restrict__ x,
+    const float *__restrict__ wt, const T *__restrict__ t0, const float *__restrict__ mean0,
+    const float *__restrict__ inv0, const T *__restrict__ t1, const float *__restrict__ mean1,
+    const float *__restrict__ inv1, float *__restrict__ part, float *__restrict__ bnpart,
+    long long px_per_block) {
+  constexpr int CIN = 64;
+  __shared__ float red[4][COUT + 1][CIN];
+  __shared__ float bred[4][CIN][3];
+  const int cg = threadIdx.x & 7, pl = threadIdx.x >> 3;
+  const long long hw = (long long)h * w;
+  const long long P = (long long)n * hw;
+  const long long pb = blockIdx.x * px_per_block;
+  const long long pe = min(P, pb + px_per_block);
+  float wv[COUT][8], m0[8], i0[8], m1[8], i1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) wv[co][j] = wt[co * CIN + cg * 8 + j];
+    m0[j] = mean0[cg * 8 + j]; i0[j] = inv0[cg * 8 + j];
+    m1[j] = mean1[cg * 8 + j]; i1[j] = inv1[cg * 8 + j];
+  }
+  float sw[COUT][8], sb[COUT], bs[3][8];
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) {
+    sb[co] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sw[co][j] = 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { bs[0][j] = 0.f; bs[1][j] = 0.f; bs[2][j] = 0.f; }
+  auto one = [&](long long p) __attribute__((always_inline)) {
+    const long long nn = p / hw, r = p - nn * hw;
+    float d[COUT];
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) d[co] = dy[(nn * COUT + co) * hw + r];
+    const long long e = p * CIN + cg * 8;
+    f32x4 x0, x1, a0, a1, b0, b1;
+    load8<T>(x + e, x0, x1);
+    load8<T>(t0 + e, a0, a1);
+    load8<T>(t1 + e, b0, b1);
+    const float xv[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    const float ta[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    const float tb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int co = 0; co < COUT; ++co) {
+        t += d[co] * wv[co][j];
+        sw[co][j] += d[co] * xv[j];
+      }
+      const float gm = xv[j] > 0.f ? Elt<T>::round(t) : 0.f;
+      bs[0][j] += gm;
+      bs[1][j] += gm * ((ta[j] - m0[j]) * i0[j]);
+      bs[2][j] += gm * ((tb[j] - m1[j]) * i1[j]);
+    }
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) sb[co] += d[co];
+  };
+  long long p = pb + pl;
+  for (; p + 32 < pe; p += 64) {
+    one(p);
+    one(p + 32);
+  }
+  if (p < pe) one(p);
+  // over the 8 pixel lanes of this wave with the same cg (lane bits 3..5)
+  auto lanes8 = [](float v) __attribute__((always_inline)) {
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    return v;
+  };
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sw[co][j] = lanes8(sw[co][j]);
+    sb[co] = lanes8(sb[co]);
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bs[k][j] = lanes8(bs[k][j]);
+  const int wv_ = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane < 8) {
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[wv_][co][cg * 8 + j] = sw[co][j];
+      if (cg == 0) red[wv_][COUT][co] = sb[co];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) bred[wv_][cg * 8 + j][k] = bs[k][j];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < COUT * CIN + COUT; i += 256) {
+    const int co = i / CIN, ci = i - co * CIN;
+    part[(long long)blockIdx.x * (COUT + 1) * CIN + i] =
+        red[0][co][ci] + red[1][co][ci] + red[2][co][ci] + red[3][co][ci];
+  }
+  if (threadIdx.x < CIN * 3) {
+    const int c = threadIdx.x / 3, k = threadIdx.x - c * 3;
+    bnpart[(long long)blockIdx.x * CIN * 3 + threadIdx.x] =
+        bred[0][c][k] + bred[1][c][k] + bred[2][c][k] + bred[3][c][k];
+  }
+}
+
 __global__ void conv_out_bwd_finalize(int cin, int cout, int blocks, const double *__restrict__ part,
                                       float *dw, float *db) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over cout*cin + cout
@@ -1669,6 +1787,46 @@ extern "C" int rr_conv_out_bwd(int dtype, int n, int h, int w, int cin, int cout
   if (chunks < 0) return RR_ELAUNCH;
   hipLaunchKernelGGL(conv_out_bwd_finalize, dim3((cout * cin + cout + 255) / 256), dim3(256), 0,
                      st, cin, cout, chunks, (const double *)red, dw, db);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" size_t rr_conv_out_bwd_bnred_workspace(long long P, int cin, int cout) {
+  const int blocks = rr_bn_stats_blocks(P);
+  return (size_t)blocks * (cout + 1) * cin * sizeof(float) + rr_colreduce_bytes(blocks, (cout + 1) * cin);
+}
+
+extern "C" int rr_conv_out_bwd_bnred(const rr_bnbwd_desc *d, int n, int h, int w, int cout,
+                                     const float *dy, const void *x, const float *wt, const void *t0,
+                                     const float *mean0, const float *invstd0, const void *t1,
+                                     const float *mean1, const float *invstd1, float *dw, float *db,
+                                     float *bn_partial, void *ws, size_t ws_bytes, rr_stream stream) {
+  if (!d || !dy || !x || !wt || !t0 || !mean0 || !invstd0 || !t1 || !mean1 || !invstd1 || !dw || !db ||
+      !bn_partial)
+    return RR_EINVAL;
+  const long long P = (long long)n * h * w;
+  if (d->P != P || d->nbn != 2 || d->mask_kind != 4 || d->eval) return RR_EINVAL;
+  if (d->C != 64 || cout != 3) return RR_EUNSUPPORTED;
+  const int blocks = rr_bn_stats_blocks(P);
+  if (blocks != rr_bn_bwd_blocks(d)) return RR_EINVAL;
+  const size_t pbytes = (size_t)blocks * (cout + 1) * d->C * sizeof(float);
+  if (!ws || ws_bytes < rr_conv_out_bwd_bnred_workspace(P, d->C, cout)) return RR_EWORKSPACE;
+  const long long ppb = (P + blocks - 1) / blocks;
+  hipStream_t st = (hipStream_t)stream;
+  if (d->dtype == RR_BF16)
+    hipLaunchKernelGGL((conv_out_bwd64_bnred_kernel<bf16_t, 3>), dim3(blocks), dim3(256), 0, st, n, h, w, dy,
+                       (const bf16_t *)x, wt, (const bf16_t *)t0, mean0, invstd0, (const bf16_t *)t1, mean1,
+                       invstd1, (float *)ws, bn_partial, ppb);
+  else
+    hipLaunchKernelGGL((conv_out_bwd64_bnred_kernel<float, 3>), dim3(blocks), dim3(256), 0, st, n, h, w, dy,
+                       (const float *)x, wt, (const float *)t0, mean0, invstd0, (const float *)t1, mean1,
+                       invstd1, (float *)ws, bn_partial, ppb);
+  RR_CHECK_LAUNCH();
+  double *red = (double *)((char *)ws + pbytes);
+  const int chunks = rr_colreduce((const float *)ws, blocks, (cout + 1) * d->C, red, st);
+  if (chunks < 0) return RR_ELAUNCH;
+  hipLaunchKernelGGL(conv_out_bwd_finalize, dim3((cout * d->C + cout + 255) / 256), dim3(256), 0, st, d->C,
+                     cout, chunks, (const double *)red, dw, db);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

@@ -24,6 +24,9 @@ struct S3Args {
   // its first-max window index, [n][h/2][w/2][64] (no full-size output)
   char *ypool;
   uint8_t *pidx;
+  // 1x1 second source (stream3_launch_sc): NHWC bf16 [n][h][w][64] and its
+  // weights [64 out][64] (rows of the 1x1 dgrad pack)
+  const char *xsc, *wsc;
 };
 
 // 0 when the descriptor is not handled by the streaming kernel, else the
@@ -38,3 +41,6 @@ int stream3_launch(const rr_igemm_desc *d, const S3Args &a, int bnbwd, hipStream
 // a.pidx; a.y unused); RR_EUNSUPPORTED when the streaming kernel does not
 // take the descriptor
 int stream3_launch_pool(const rr_igemm_desc *d, const S3Args &a, hipStream_t st);
+// the plain 64 -> 64 dgrad plus a 1x1 dgrad of a.xsc with a.wsc into the same
+// accumulators (rr_igemm_dgrad_sc); RR_EUNSUPPORTED when not taken
+int stream3_launch_sc(const rr_igemm_desc *d, const S3Args &a, hipStream_t st);

@@ -55,6 +55,21 @@
 
 #include <climits>
 #include <cstdlib>
+#include <type_traits>
+
+// B fragments of the three tap columns: RR_S3_DPP=1 (a separate build, A/B)
+// reads the centre column once per (tap row, k half) and forms the dx = 0 / 2
+// operands by a DPP row rotate of it (lane = pixel within a 16-lane row) plus
+// the two edge pixels of each contiguous run of blocks (exec-masked reads): a
+// third of the LDS fragment traffic.  Measured 15 % slower on the stream3
+// layers and -1.1 % on the graph step (profiles/r5n_ablayers_s3.txt,
+// r5n_ablibs.txt): the LDS port was not the limiter, the 16 VALU rotates +
+// selects per block and tap column cost more than the reads they replace.
+// 0 (default): the 3 reads per (tap row, k half).  The MFMA order differs
+// (dy, kb, dx vs dy, dx, kb): both are the same 576-term fp32 dot product.
+#ifndef RR_S3_DPP
+#define RR_S3_DPP 0
+#endif
 
 namespace {
 
@@ -62,7 +77,11 @@ constexpr int S3_WG = 256;   // workgroups: one per CU on MI355X (fixed: determi
 
 // F_POOL: the 2x2 max-pool (+ its first-max index) of the activated output
 // instead of the output (VGG16 conv + ReLU + MaxPool2d, 14:189-196)
-enum : int { F_BIAS = 1, F_STATS = 2, F_RELU = 4, F_ACC = 8, F_MASK = 16, F_BNBWD = 32, F_POOL = 64 };
+// F_SC: a 1x1 dgrad of a second gradient (a.xsc, weights a.wsc) summed into
+// the accumulators -- the shortcut conv's dgrad of a ResidualBlock with a
+// concat input, 14:109-113 (rr_igemm_dgrad_sc)
+enum : int { F_BIAS = 1, F_STATS = 2, F_RELU = 4, F_ACC = 8, F_MASK = 16, F_BNBWD = 32, F_POOL = 64,
+             F_SC = 128 };
 
 // chunk swizzle: the 16 pixels of a B read at pixel offset P in {0, 1, 2}
 // mod 16 need distinct (p & 1, chunk ^ swz(p)) pairs with chunks c (outer 8
@@ -121,6 +140,12 @@ __device__ __forceinline__ u64 load_b64_async(const char *p) {
   asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
   return r;
 }
+// (16 B: a B fragment of the F_SC source)
+__device__ __forceinline__ i32x4 load_b128_async(const char *p) {
+  i32x4 r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
 // LDS reads outside the compiler's view: its waitcnt pass puts a vmcnt(0)
 // (drain all LDS-DMA) before a visible ds_read it cannot separate from the
 // DMA destination
@@ -150,6 +175,43 @@ __device__ __forceinline__ uint2 pack4(f32x4 g) {
   return o;
 }
 
+template <int N> using ic = std::integral_constant<int, N>;
+
+// a wave's MP 16-pixel blocks of a step: block ni sits brow(ni) image rows and
+// bcol(ni) columns from the wave's first pixel (POOL: 2 rows x 8 MP columns,
+// blocks 2j / 2j + 1 = rows 0 / 1 of columns 16 j ..).  Segments: maximal runs
+// of blocks that continue each other in one row (the DPP B operands, RR_S3_DPP)
+template <int W, int MP, bool POOL> struct S3Blk {
+  static constexpr int brow(int ni) { return POOL ? (ni & 1) : (ni * 16) / W; }
+  static constexpr int bcol(int ni) { return POOL ? (ni >> 1) * 16 : (ni * 16) % W; }
+  static constexpr bool needl(int ni) {
+    return !(ni > 0 && brow(ni - 1) == brow(ni) && bcol(ni - 1) + 16 == bcol(ni));
+  }
+  static constexpr bool needr(int ni) {
+    return !(ni + 1 < MP && brow(ni + 1) == brow(ni) && bcol(ni + 1) == bcol(ni) + 16);
+  }
+  static constexpr int nseg() {
+    int k = 0;
+    for (int ni = 0; ni < MP; ++ni) k += needl(ni) ? 1 : 0;
+    return k;
+  }
+  static constexpr int seg_of(int ni) {
+    int g = -1;
+    for (int j = 0; j <= ni; ++j) g += needl(j) ? 1 : 0;
+    return g;
+  }
+  static constexpr int seg_first(int g) {
+    for (int j = 0; j < MP; ++j)
+      if (needl(j) && seg_of(j) == g) return j;
+    return 0;
+  }
+  static constexpr int seg_last(int g) {
+    for (int j = seg_first(g); j < MP; ++j)
+      if (needr(j)) return j;
+    return MP - 1;
+  }
+};
+
 struct Cur {
   int kind, n, y0, c;   // virtual step: pre-load, or compute of output rows [y0, y0 + RPS) of image n
 };
@@ -164,12 +226,16 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
   constexpr bool ACC = (F & F_ACC) != 0, MASK = (F & F_MASK) != 0;
   constexpr bool STATS = (F & F_STATS) != 0;
   constexpr bool POOL = (F & F_POOL) != 0;
+  constexpr bool SC = (F & F_SC) != 0;
+  static_assert(!SC || (F == F_SC && STAG == 0), "the 1x1 second source: plain dgrad epilogue");
   static_assert(!POOL || ((F & ~(F_BIAS | F_RELU | F_POOL)) == 0 && (F & F_RELU) && MP % 2 == 0 &&
                           W % (8 * MP) == 0), "pool epilogue: bias + ReLU, row-pair blocks");
   constexpr int NE = BNBWD ? 1 : (ACC ? 1 : 0) + (MASK ? 1 : 0);   // epilogue loads per block
   // S: stores per step (16-B output stores; POOL: a pooled value + an index
   // store per channel block and column block pair)
-  constexpr int E = MC * MP * NE, S = POOL ? MC * MP : MP;
+  // (F_SC: its B fragments, 2 k-halves per pixel block, count with the
+  // epilogue loads: issued with them, waited for after the 3x3 MFMAs)
+  constexpr int E = MC * MP * NE + (SC ? 2 * MP : 0), S = POOL ? MC * MP : MP;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
   float *coef = reinterpret_cast<float *>(smem + RING * ROWB);   // [64][2]
 
@@ -194,6 +260,17 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
       for (int kb = 0; kb < 2; ++kb)
         wr[mi][tap][kb] =
             *reinterpret_cast<const bf16x8 *>(a.wt + ((co * 9 + tap) * a.wld + a.woff + kb * 32 + fq * 8) * 2);
+  }
+  // F_SC: the 1x1 weights [c_out][64] of the wave's output channels
+  bf16x8 wsr[SC ? MC : 1][2];
+  if constexpr (SC) {
+#pragma unroll
+    for (int mi = 0; mi < MC; ++mi) {
+      const int co = wc * 32 + mi * 16 + frow;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+        wsr[mi][kb] = *reinterpret_cast<const bf16x8 *>(a.wsc + (co * 64 + kb * 32 + fq * 8) * 2);
+    }
   }
   float al = 0.f;
   if constexpr (BNBWD) {
@@ -263,8 +340,9 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
   const int q0 = POOL ? 2 * (wp / WPR) : (wp * 16 * MP) / W;
   const int x0 = POOL ? PCOLS * (wp % WPR) : (wp * 16 * MP) % W;
   static_assert(W >= 16 * MP || (16 * MP) % W == 0, "block rows");
-  auto brow = [](int ni) constexpr { return POOL ? (ni & 1) : (ni * 16) / W; };
-  auto bcol = [](int ni) constexpr { return POOL ? (ni >> 1) * 16 : (ni * 16) % W; };
+  using BK = S3Blk<W, MP, POOL>;
+  auto brow = [](int ni) constexpr { return BK::brow(ni); };
+  auto bcol = [](int ni) constexpr { return BK::bcol(ni); };
   // lane part of a B read for tap column dx and k-half kb: pixel frow + dx of
   // the block, chunk kb * 4 + fq through the swizzle
   uint32_t boff[3][2];
@@ -285,8 +363,17 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
   for (int mi = 0; mi < MC; ++mi) { r0[mi] = f32x4{0.f, 0.f, 0.f, 0.f}; r1[mi] = r0[mi]; }
 
   u64 ev0[MC][MP], ev1[MC][MP];
+  i32x4 esc[SC ? MP : 1][2];                    // F_SC B fragments: pixel frow, channels kb * 32 + fq * 8
   f32x4 acc[MC][MP];
   auto load_e = [&](long long pix0) __attribute__((always_inline)) {
+    if constexpr (SC) {
+#pragma unroll
+      for (int ni = 0; ni < MP; ++ni) {
+        const long long ub = (pix0 + (q0 + brow(ni)) * W + x0 + bcol(ni)) * 128;   // uniform
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) esc[ni][kb] = load_b128_async(a.xsc + ub + frow * 128 + kb * 64 + fq * 16);
+      }
+    }
 #pragma unroll
     for (int mi = 0; mi < MC; ++mi)
 #pragma unroll
@@ -299,8 +386,14 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
   };
   auto wait_e = [&]() __attribute__((always_inline)) {
     // the epilogue loads are older than the DMAW DMAs issued after them
-    if constexpr (NE > 0) {
+    if constexpr (E > 0) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMAW) : "memory");
+      if constexpr (SC) {
+#pragma unroll
+        for (int ni = 0; ni < MP; ++ni)
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) asm volatile("" : "+v"(esc[ni][kb]));
+      }
 #pragma unroll
       for (int mi = 0; mi < MC; ++mi)
 #pragma unroll
@@ -310,7 +403,122 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
         }
     }
   };
+  // ---- DPP form of the B operands (RR_S3_DPP): contiguous runs of blocks
+  // in one image row ("segments"); the first block's left neighbour pixel and
+  // the last block's right one come from one exec-masked edge read per
+  // segment (lane frow 0: left, frow 15: right), the inner ones from the
+  // neighbouring block's rotated fragment ----
+  constexpr int NSEG = BK::nseg();
+  // lane part of segment g's edge read (k half kb): left of its first block
+  // (lane frow 0, the dx = 0 read of that lane) or right of its last (frow 15)
+  uint32_t eoff[NSEG][2];
+#pragma unroll
+  for (int g = 0; g < NSEG; ++g)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+      eoff[g][kb] = frow == 0 ? BK::bcol(BK::seg_first(g)) * 128 + boff[0][kb] : BK::bcol(BK::seg_last(g)) * 128 + boff[2][kb];
+  const bool edge_lane = frow == 0 || frow == 15;
+  const bool lane_l = frow == 0, lane_r = frow == 15;
+  i32x4 eg[2][NSEG];                            // [buffer][segment] edge pixels (lanes frow 0 / 15)
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int g = 0; g < NSEG; ++g) eg[b][g] = i32x4{0, 0, 0, 0};
+  auto rot = [](i32x4 v, auto CTRLc) __attribute__((always_inline)) {
+    constexpr int CTRL = decltype(CTRLc)::value;
+    return i32x4{__builtin_amdgcn_mov_dpp(v[0], CTRL, 0xf, 0xf, false),
+                 __builtin_amdgcn_mov_dpp(v[1], CTRL, 0xf, 0xf, false),
+                 __builtin_amdgcn_mov_dpp(v[2], CTRL, 0xf, 0xf, false),
+                 __builtin_amdgcn_mov_dpp(v[3], CTRL, 0xf, 0xf, false)};
+  };
+  auto sel = [](bool c, i32x4 a, i32x4 b) __attribute__((always_inline)) {
+    return i32x4{c ? a[0] : b[0], c ? a[1] : b[1], c ? a[2] : b[2], c ? a[3] : b[3]};
+  };
+  // 6 groups (tap row dy, k half kb), each: the centre fragments of the MP
+  // blocks + one edge read per segment, read one group ahead; then the three
+  // tap columns' MFMAs (order dy, kb, dx)
+  auto mfma_step_dpp = [&](int s0) __attribute__((always_inline)) {
+    uint32_t rba[3][NR];
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {
+        int r = s0 + q0 + k + dy;
+        r = r >= RING ? r - RING : r;
+        rba[dy][k] = sbase + r * ROWB + x0 * 128;
+      }
+    i32x4 cf[2][MP];                            // [buffer][block] centre-column fragments
+    auto rd = [&](int q) __attribute__((always_inline)) {
+      const int dy = q >> 1, kb = q & 1;
+#pragma unroll
+      for (int ni = 0; ni < MP; ++ni)
+        asm volatile("ds_read_b128 %0, %1 offset:%2"
+                     : "=v"(cf[q & 1][ni]) : "v"(rba[dy][brow(ni)] + boff[1][kb]), "i"(bcol(ni) * 128));
+      if (edge_lane) {
+#pragma unroll
+        for (int g = 0; g < NSEG; ++g)
+          asm volatile("ds_read_b128 %0, %1" : "=v"(eg[q & 1][g])
+                       : "v"(rba[dy][BK::brow(BK::seg_first(g))] + eoff[g][kb]));
+      }
+    };
+    constexpr int NRD = MP + NSEG;
+    static_assert(NRD <= 15, "lgkmcnt");
+    rd(0);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const int dy = q >> 1, kb = q & 1, b = q & 1;
+      if (q + 1 < 6) {
+        rd(q + 1);
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NRD) : "memory");
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+#pragma unroll
+      for (int ni = 0; ni < MP; ++ni) asm volatile("" : "+v"(cf[b][ni]));
+#pragma unroll
+      for (int g = 0; g < NSEG; ++g) asm volatile("" : "+v"(eg[b][g]));
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        i32x4 bv[MP];
+        if (dx == 1) {
+#pragma unroll
+          for (int ni = 0; ni < MP; ++ni) bv[ni] = cf[b][ni];
+        } else if (dx == 0) {
+          // pixel x - 1: lane l <- lane l - 1 of its 16-lane row (row_ror:1);
+          // lane 0 <- the previous block's lane 15 (its rotate's lane 0) or the edge
+#pragma unroll
+          for (int ni = 0; ni < MP; ++ni) bv[ni] = rot(cf[b][ni], ic<0x121>{});
+#pragma unroll
+          for (int ni = MP - 1; ni >= 0; --ni)
+            bv[ni] = sel(lane_l, BK::needl(ni) ? eg[b][BK::seg_of(ni)] : bv[ni > 0 ? ni - 1 : 0], bv[ni]);
+        } else {
+          // pixel x + 1: row_ror:15; lane 15 <- the next block's lane 0 or the edge
+#pragma unroll
+          for (int ni = 0; ni < MP; ++ni) bv[ni] = rot(cf[b][ni], ic<0x12F>{});
+#pragma unroll
+          for (int ni = 0; ni < MP; ++ni)
+            bv[ni] = sel(lane_r, BK::needr(ni) ? eg[b][BK::seg_of(ni)] : bv[ni + 1 < MP ? ni + 1 : ni], bv[ni]);
+        }
+        const int t = dy * 3 + dx;
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < MP; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                wr[mi][t][kb], __builtin_bit_cast(bf16x8, bv[ni]),
+                (q == 0 && dx == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[mi][ni], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  };
   auto mfma_step = [&](int s0) __attribute__((always_inline)) {
+    // (the 256-pixel steps keep the 3 reads: their extra fragment registers
+    // spill the statistics / 32-wide variants)
+    if constexpr (RR_S3_DPP && MP == 2) {
+      mfma_step_dpp(s0);
+      return;
+    }
     // ring slot of input row y0 - 1 + r is s0 + r (mod RING); s0 + r < 2 RING
     uint32_t rba[3][NR];                        // per tap row dy and image row: ring row base (uniform)
 #pragma unroll
@@ -520,7 +728,7 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     const long long pix0 = (long long)(cp.n * H + cp.y0) * W;
     if (late && pcomp) epilogue(ppix);          // its loads were waited for last iteration
     // epilogue loads BEFORE this iteration's DMA (see the vmcnt accounting)
-    if constexpr (NE > 0) {
+    if constexpr (E > 0) {
       if (comp) load_e(pix0);
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -536,6 +744,18 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
       // registers must not be live across the loop back-edge (it may copy
       // them there before the data has landed)
       wait_e();
+      if constexpr (SC) {
+        // + the 1x1 dgrad of the second gradient (after the 9 taps: the
+        // fp32 sum in one order, bitwise-reproducible)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < MP; ++ni)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  wsr[mi][kb], __builtin_bit_cast(bf16x8, esc[ni][kb]), acc[mi][ni], 0, 0, 0);
+      }
       if (!late) epilogue(pix0);
     }
     ppix = pix0;
@@ -731,6 +951,19 @@ int stream3_blocks(const rr_igemm_desc *d, int bnbwd) {
   const long long P = (long long)d->n * d->h * d->w;
   if (P < 256LL * S3_WG || P * 64 > INT_MAX) return 0;
   return S3_WG;
+}
+
+int stream3_launch_sc(const rr_igemm_desc *d, const S3Args &a0, hipStream_t st) {
+  if (!stream3_blocks(d, 0) || d->c_in2 || s3_flags(d, false) != 0 || !a0.xsc || !a0.wsc)
+    return RR_EUNSUPPORTED;
+  S3Args a = a0;
+  a.wld = 64; a.woff = 0;
+  const int P = d->n * d->h * d->w;
+  // 128-pixel steps, no stagger (the plain dgrad's form, launch_w)
+  if (d->w == 64) launch1<64, 2, F_SC, 0>(a, P, st);
+  else launch1<32, 2, F_SC, 0>(a, P, st);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
 }
 
 int stream3_launch_pool(const rr_igemm_desc *d, const S3Args &a0, hipStream_t st) {

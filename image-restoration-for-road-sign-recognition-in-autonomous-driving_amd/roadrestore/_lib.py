@@ -76,6 +76,8 @@ _SIGS = {
     "rr_igemm_kernel_name": (C.c_char_p, [C.POINTER(IgemmDesc), I_]),
     "rr_igemm_pool": (I_, [C.POINTER(IgemmDesc), P_, P_, P_, P_, P_, P_, P_]),
     "rr_igemm_pool_kernel_name": (C.c_char_p, [C.POINTER(IgemmDesc)]),
+    "rr_igemm_dgrad_sc": (I_, [C.POINTER(IgemmDesc), P_, P_, P_, P_, I_, P_, P_]),
+    "rr_igemm_dgrad_sc_kernel_name": (C.c_char_p, [C.POINTER(IgemmDesc), I_]),
     "rr_wgrad_kernel_name": (C.c_char_p, [C.POINTER(WgradDesc)]),
     "rr_igemm_bnbwd_workspace": (S_, [C.POINTER(IgemmDesc)]),
     "rr_igemm_bnbwd": (I_, [C.POINTER(IgemmDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_, P_, P_]),
@@ -129,6 +131,11 @@ _SIGS = {
     "rr_conv_out_fwd": (I_, [I_, I_, I_, I_, I_, I_, P_, P_, P_, P_, P_]),
     "rr_conv_out_bwd": (I_, [I_, I_, I_, I_, I_, I_, P_, P_, P_, P_, I_, P_, P_, P_, S_, P_]),
     "rr_conv_out_bwd_workspace": (S_, [I_, I_, I_, I_, I_]),
+    "rr_conv_out_bwd_bnred_workspace": (S_, [L_, I_, I_]),
+    "rr_conv_out_bwd_bnred": (I_, [C.POINTER(BnBwdDesc), I_, I_, I_, I_, P_, P_, P_, P_, P_, P_, P_, P_,
+                                   P_, P_, P_, P_, P_, S_, P_]),
+    "rr_bn_bwd_apply_convout": (I_, [C.POINTER(BnBwdDesc), I_, I_, P_, P_, I_, P_, P_, P_, P_, P_, P_, P_,
+                                     P_, P_, P_, P_, P_]),
     "rr_nchw_to_nhwc": (I_, [I_, I_, I_, I_, I_, P_, P_, P_]),
     "rr_nhwc_to_nchw": (I_, [I_, I_, I_, I_, I_, P_, P_, P_]),
     "rr_loss_fwd": (I_, [I_, I_, L_, P_, P_, P_, F_, I_, P_, S_, P_]),

@@ -553,9 +553,13 @@ def resblock_zero_grad_params(blk):
     return z
 
 
-def resblock_backward(blk, S, g_out, sink, pool=None):
+def resblock_backward(blk, S, g_out, sink, pool=None, convout=None):
     """``pool=(dy_pool, idx)``: the output also fed a 2x2 max-pool whose
-    backward is fused into the tail BN backward (no separate pass)."""
+    backward is fused into the tail BN backward (no separate pass).
+    ``convout=(final, dy)``: the output fed the final 1x1 conv ``final`` and
+    ``dy`` is that conv's output grad (``g_out`` None): its backward runs here,
+    fused with the tail BN's reduce where the library takes it (the conv's
+    input grad is then never stored)."""
     cb = blk.conv_block
     c1, bn1, pr, c2, bn2 = cb[0], cb[1], cb[2], cb[3], cb[4]
     n, h, w = S.n, S.h, S.w
@@ -587,13 +591,31 @@ def resblock_backward(blk, S, g_out, sink, pool=None):
         if _RECOMPUTE_MASK and cout % 8 == 0 and 256 % (cout // 8) == 0:
             rec = S.pair if S.get("pair") is not None else (torch.stack((S.s2, S.ss)),
                                                              torch.stack((S.sh2, S.shs)))
-        r = ops.bn_backward(g_out, S.t2, S.m2, S.i2, bn2.weight, mask_kind=1, aux=S.out, pool=pool,
-                            recompute=rec, t1=S.s, mean1=S.ms, inv1=S.is_, gamma1=sc1.weight,
-                            outs=dict(dgamma0=sink[bn2.weight], dbeta0=sink[bn2.bias],
-                                      dgamma1=sink[sc1.weight], dbeta1=sink[sc1.bias]),
-                            eval_mode=ev, dbias=(sink[c2.bias], sink[sc0.bias]) if ev else None)
+        outs2 = dict(dgamma0=sink[bn2.weight], dbeta0=sink[bn2.bias], dgamma1=sink[sc1.weight],
+                     dbeta1=sink[sc1.bias])
+        r = None
+        if convout is not None:
+            final, dy = convout
+            if _FUSED_CONVOUT_BN and rec is not None and not ev and pool is None:
+                r = ops.bn_backward_convout(dy, S.out, final.weight, S.t2, S.m2, S.i2, bn2.weight,
+                                            S.s, S.ms, S.is_, sc1.weight, rec, outs2,
+                                            dw=sink[final.weight], db=sink[final.bias])
+            if r is None:
+                g_out, _, _ = ops.conv_out_bwd(dy, S.out, final.weight, mask_relu=False,
+                                               dw=sink[final.weight], db=sink[final.bias])
+            sink.ready(_params(final))
+        if r is None:
+            r = ops.bn_backward(g_out, S.t2, S.m2, S.i2, bn2.weight, mask_kind=1, aux=S.out,
+                                pool=pool, recompute=rec, t1=S.s, mean1=S.ms, inv1=S.is_,
+                                gamma1=sc1.weight, outs=outs2, eval_mode=ev,
+                                dbias=(sink[c2.bias], sink[sc0.bias]) if ev else None)
         dt2, ds = r["dt0"], r["dt1"]
     else:
+        if convout is not None:
+            final, dy = convout
+            g_out, _, _ = ops.conv_out_bwd(dy, S.out, final.weight, mask_relu=False,
+                                           dw=sink[final.weight], db=sink[final.bias])
+            sink.ready(_params(final))
         gx1 = torch.empty_like(x1)
         r = ops.bn_backward(g_out, S.t2, S.m2, S.i2, bn2.weight, mask_kind=1, aux=S.out, pool=pool,
                             want_gm=True, gm_out=gx1,
@@ -627,6 +649,18 @@ def resblock_backward(blk, S, g_out, sink, pool=None):
             # [c_in][9][c_out] rows is not a pack the tap-reuse conv can
             # read -- its weight tiles sit behind the whole pack)
             half = 64 * 9 * cout
+            if _FUSED_SC_DGRAD:
+                # each half + the shortcut's 1x1 dgrad of it in the same pass
+                # (no 1.3 GB accumulate pass over both halves)
+                hs = 64 * cout
+                gx1 = ops.igemm_dgrad_sc(dt1, n, h, w, S.pk1[1][:half], 64, ds, S.pks[1][:hs])
+                gx2 = ops.igemm_dgrad_sc(dt1, n, h, w, S.pk1[1][half:], 64, ds, S.pks[1][hs:]) \
+                    if gx1 is not None else None
+                if gx2 is not None:
+                    if side is not None:
+                        torch.cuda.current_stream().wait_stream(side)
+                    sink.ready(_params(blk))
+                    return gx1, gx2
             gx1, _, _ = ops.igemm(RR_CONV3X3, dt1, None, n, h, w, S.pk1[1][:half], 64)
             gx2, _, _ = ops.igemm(RR_CONV3X3, dt1, None, n, h, w, S.pk1[1][half:], 64)
         else:
@@ -762,6 +796,11 @@ _FUSED_POOL = os.environ.get("RR_FUSED_POOL", "1") != "0"
 _FUSED_POOL_BWD = os.environ.get("RR_FUSED_POOL_BWD", "1") != "0"
 # A/B switch: dec1's concat dgrad as two 64 -> 64 row-streaming launches
 _SPLIT_DGRAD = os.environ.get("RR_SPLIT_DGRAD", "1") != "0"
+# A/B switch: the final conv's backward fused with dec1's tail BN reduce, its
+# input grad recomputed in the apply instead of stored (rr_conv_out_bwd_bnred)
+_FUSED_CONVOUT_BN = os.environ.get("RR_FUSED_CONVOUT_BN", "1") != "0"
+# A/B switch: ... each with the shortcut's 1x1 dgrad summed in (rr_igemm_dgrad_sc)
+_FUSED_SC_DGRAD = os.environ.get("RR_FUSED_SC_DGRAD", "1") != "0"
 
 
 def _streams_half(dtype, n, h, w):
@@ -800,10 +839,8 @@ def resunet_backward(m, S, g_out, sink):
     n = S.n
     (H, W), (H2, W2), (H3, W3), (H4, W4) = S.sizes
     al1, al2, al3 = S.aligned
-    g_d1, _, _ = ops.conv_out_bwd(g_out, S.d1, m.final.weight, mask_relu=False,
-                                  dw=sink[m.final.weight], db=sink[m.final.bias])
-    sink.ready(_params(m.final))
-    g_u1, g_r1 = resblock_backward(m.dec1, S.dec1, g_d1, sink)
+    # the final conv's backward runs inside dec1's (fused with its tail BN reduce)
+    g_u1, g_r1 = resblock_backward(m.dec1, S.dec1, None, sink, convout=(m.final, g_out))
     if al1:
         g_u1 = ops.nearest_resize_bwd(g_u1, 2 * H2, 2 * W2)
     g_d2 = _convT_bwd(m.up1, S.pku1, g_u1, S.d2, n, H2, W2, sink)

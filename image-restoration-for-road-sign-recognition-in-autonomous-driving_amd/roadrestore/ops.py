@@ -615,6 +615,36 @@ def igemm_pool(x1, n, h, w, wpack, cout, bias=None, want_idx=True):
     return yp, idx
 
 
+def igemm_dgrad_sc_kernel_name(d, c_sc):
+    f = getattr(lib(), "rr_igemm_dgrad_sc_kernel_name", None)    # (older builds: A/B runs)
+    return f(C.byref(d), c_sc).decode() if f is not None else "unsupported"
+
+
+def dgrad_sc_desc(dy, n, h, w, cout):
+    return IgemmDesc(rr_dtype(dy.dtype), RR_CONV3X3, n, h, w, dy.shape[-1], 0, cout, 0, 0, 0, 0, 0,
+                     0, 0)
+
+
+def igemm_dgrad_sc(dy, n, h, w, wpack, cout, dy_sc, wpack_sc):
+    """the 3x3 dgrad of ``dy`` + the 1x1 dgrad of ``dy_sc`` (rows ``wpack_sc``
+    of the 1x1 dgrad pack) into one [n, h, w, cout] output, one pass
+    (rr_igemm_dgrad_sc); None where the library does not take the shape."""
+    _need_cuda(dy, wpack, dy_sc, wpack_sc)
+    d = dgrad_sc_desc(dy, n, h, w, cout)
+    c_sc = dy_sc.shape[-1]
+    if igemm_dgrad_sc_kernel_name(d, c_sc) == "unsupported":
+        return None
+    y = torch.empty((n, h, w, cout), dtype=dy.dtype, device=dy.device)
+
+    def launch():
+        lib().check(lib().rr_igemm_dgrad_sc(C.byref(d), _p(dy), _p(wpack), _p(dy_sc), _p(wpack_sc),
+                                            c_sc, _p(y), stream()), "rr_igemm_dgrad_sc")
+    _launch(lambda: igemm_dgrad_sc_kernel_name(d, c_sc),
+            2.0 * n * h * w * cout * (9 * dy.shape[-1] + c_sc), launch,
+            f"fwd m{RR_CONV3X3} {n}x{h}x{w} c{dy.shape[-1]}+0->{cout} sc{c_sc}")
+    return y
+
+
 def nearest_resize(x, ho, wo):
     """F.interpolate(x, size=(ho, wo)) mode 'nearest' (14:169-182), NHWC."""
     _need_cuda(x)
@@ -815,6 +845,48 @@ def conv_out_bwd(dy_nchw, x, wt, mask_relu=False, want_dx=True, dw=None, db=None
                                       _p(dx), int(mask_relu), _p(dw), _p(db), _p(ws), ws.numel(),
                                       stream()), "rr_conv_out_bwd")
     return dx, dw, db
+
+
+def bn_backward_convout(dy_nchw, x, wt, t0, mean0, inv0, gamma0, t1, mean1, inv1, gamma1,
+                        recompute, outs, dw, db):
+    """The residual-tail BN backward (two BNs, recomputed ReLU mask: as
+    ``bn_backward(g, ..., mask_kind=1, recompute=...)``) of the block whose
+    output ``x`` feeds the final 1x1 conv, with g = that conv's input grad
+    never materialised: rr_conv_out_bwd_bnred (the conv's dw / db + the BN
+    reduce), rr_bn_bwd_finalize, rr_bn_bwd_apply_convout (g recomputed from
+    ``dy_nchw``).  Train mode only.  Returns dict(dt0, dt1); None where the
+    library does not take the shape (the caller runs conv_out_bwd +
+    bn_backward)."""
+    n, h, w, Cc = x.shape
+    cout = wt.shape[0]
+    if Cc != 64 or cout != 3 or not hasattr(lib(), "rr_conv_out_bwd_bnred"):
+        return None
+    P = n * h * w
+    dev = x.device
+    d = BnBwdDesc(rr_dtype(x.dtype), P, Cc, 4, 2, 0, 0, None, None)
+    blocks = lib().rr_bn_bwd_blocks(C.byref(d))
+    part = torch.empty(blocks * Cc * 3 + blocks, dtype=torch.float32, device=dev)
+    ws = _ws(lib().rr_conv_out_bwd_bnred_workspace(P, Cc, cout), dev)
+    dy = dy_nchw.contiguous()
+    w2 = wt.reshape(cout, Cc)
+    s = stream()
+    lib().check(lib().rr_conv_out_bwd_bnred(C.byref(d), n, h, w, cout, _p(dy), _p(x), _p(w2), _p(t0),
+                                            _p(mean0), _p(inv0), _p(t1), _p(mean1), _p(inv1), _p(dw),
+                                            _p(db), _p(part), _p(ws), ws.numel(), s),
+                "rr_conv_out_bwd_bnred")
+    coef = torch.empty(Cc * 6, dtype=torch.float32, device=dev)
+    lib().check(lib().rr_bn_bwd_finalize(C.byref(d), _p(part), _p(gamma0), _p(inv0), _p(gamma1),
+                                         _p(inv1), _p(outs["dgamma0"]), _p(outs["dbeta0"]),
+                                         _p(outs["dgamma1"]), _p(outs["dbeta1"]), None, _p(coef), s),
+                "rr_bn_bwd_finalize")
+    aff_s, aff_b = (q.contiguous() for q in recompute)
+    dt0 = torch.empty_like(x)
+    dt1 = torch.empty_like(x)
+    lib().check(lib().rr_bn_bwd_apply_convout(C.byref(d), h, w, _p(dy), _p(w2), cout, _p(aff_s),
+                                              _p(aff_b), _p(t0), _p(mean0), _p(inv0), _p(t1),
+                                              _p(mean1), _p(inv1), _p(coef), _p(dt0), _p(dt1), s),
+                "rr_bn_bwd_apply_convout")
+    return dict(dt0=dt0, dt1=dt1)
 
 
 def nchw_to_nhwc(x, dtype):

@@ -115,6 +115,20 @@ int rr_igemm_pool(const rr_igemm_desc *d, const void *x1, const void *x2, const 
                   const float *bias, void *y_pool, uint8_t *pool_idx, rr_stream stream);
 /* the kernel rr_igemm_pool launches for *d, or "unsupported" */
 const char *rr_igemm_pool_kernel_name(const rr_igemm_desc *d);
+/* y = the 3x3 dgrad of dy (d: mode RR_CONV3X3, c_in1 = dy's channels, c_out =
+ * y's; no bias / activation / statistics / mask / split / accumulate) + the
+ * 1x1 dgrad of a second gradient dy_sc [n][h][w][c_sc] with w_sc, the rows of
+ * y's channels in the 1x1 conv's dgrad pack ([c_out][c_sc], rr_pack_conv) --
+ * one pass, fp32 sum of both, rounded once.  A ResidualBlock's input grad =
+ * conv_block[0]'s dgrad + shortcut[0]'s dgrad (14:99-115; dec1's concat
+ * halves).  bf16, 64 -> 64 channels, c_sc = 64, the row-streaming kernel's
+ * maps (64x64 / 32x32); others RR_EUNSUPPORTED (the caller runs rr_igemm +
+ * an accumulating 1x1 rr_igemm).  Replaces the two torch autograd dgrads of
+ * nn.Conv2d at 14:99-113. */
+int rr_igemm_dgrad_sc(const rr_igemm_desc *d, const void *dy, const void *w, const void *dy_sc,
+                      const void *w_sc, int c_sc, void *y, rr_stream stream);
+/* the kernel rr_igemm_dgrad_sc launches for (*d, c_sc), or "unsupported" */
+const char *rr_igemm_dgrad_sc_kernel_name(const rr_igemm_desc *d, int c_sc);
 /* number of row blocks the partial stats buffer holds: [blocks][c_out][2] */
 int rr_igemm_stat_blocks(const rr_igemm_desc *d);
 /* The kernel rr_igemm (bnbwd = 0) or rr_igemm_bnbwd (bnbwd = 1) launches for
@@ -315,6 +329,29 @@ int rr_bn_bwd_finalize_rows(const rr_bnbwd_desc *d, int rows, const float *parti
                             const float *apartial, const float *gamma0, const float *invstd0,
                             float *dgamma0, float *dbeta0, float *dalpha, float *coef,
                             void *ws, size_t ws_bytes, rr_stream stream);
+/* the final 1x1 conv's backward (dw, db as rr_conv_out_bwd; its input grad g
+ * NOT stored) fused with the reduce of the residual-tail BN backward of the
+ * block that produced its input x (ResUNet dec1 -> final, 14:99-115, 14:149):
+ * bn_partial [rr_bn_bwd_blocks(d)][C][3] for rr_bn_bwd_finalize, gm = g
+ * rounded to the activation dtype, masked by x > 0 (x = the block output).
+ * d: mask_kind 4, nbn 2, P = n*h*w, C = 64 (t0 / t1: the block's two pre-BN
+ * tensors, as rr_bn_bwd_reduce); cout = 3.  The apply is
+ * rr_bn_bwd_apply_convout.  Replaces the autograd of nn.Conv2d(64, 3, 1) and
+ * the reduce half of BatchNorm2d's backward at 14:149 / 14:104-115. */
+size_t rr_conv_out_bwd_bnred_workspace(long long P, int cin, int cout);
+int rr_conv_out_bwd_bnred(const rr_bnbwd_desc *d, int n, int h, int w, int cout, const float *dy,
+                          const void *x, const float *wt, const void *t0, const float *mean0,
+                          const float *invstd0, const void *t1, const float *mean1,
+                          const float *invstd1, float *dw, float *db, float *bn_partial, void *ws,
+                          size_t ws_bytes, rr_stream stream);
+/* the apply of that BN backward (mask kind 4) with g recomputed from the
+ * final conv's fp32 NCHW output grad dy [n][cout][h][w] and weights wt
+ * [cout][C]: the 268 MB input grad is never written or read (cout = 3) */
+int rr_bn_bwd_apply_convout(const rr_bnbwd_desc *d, int h, int w, const float *dy, const float *wt,
+                            int cout, const float *aff_s, const float *aff_b, const void *t0,
+                            const float *mean0, const float *invstd0, const void *t1,
+                            const float *mean1, const float *invstd1, const float *coef,
+                            void *dt0, void *dt1, rr_stream stream);
 /* apply: dt_i = coef_a[c]*(gm - coef_b[c] - xhat_i*coef_c[c]); optional gm out */
 int rr_bn_bwd_apply(const rr_bnbwd_desc *d, const void *g, const void *aux,
                     const float *aff_s, const float *aff_b, const float *alpha,

@@ -43,7 +43,8 @@ CURVE_DELTA_TOL = 0.25
 BENCHED = {"stream3_kernel<64>", "stream3_kernel<32>", "swgrad_kernel<64>", "swgrad_kernel<32>",
            "conv3r_kernel<32,128>", "conv3r_kernel<32,64>",
            "conv3r_kernel<16,128,w8>", "conv3r_kernel<8,128,32,w8>", "wgrad3_halo_kernel<16>",
-           "wgrad3_halo_kernel<8>", "conv3r_kernel<64,64>"}
+           "wgrad3_halo_kernel<8>", "conv3r_kernel<64,64>", "stream3_kernel<64,sc>",
+           "stream3_kernel<64,pool>"}
 
 
 def _gold(name):

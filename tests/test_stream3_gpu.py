@@ -214,3 +214,44 @@ def test_stream3_concat_two_pass(dev, shape, stats, bias, act, monkeypatch):
         assert rel(s1[:, 1], (pre.double() ** 2).sum((0, 2, 3))) < 1e-5
         assert rel(s[:, 0], pre.double().sum((0, 2, 3))) < 4e-3
         assert rel(s[:, 1], (pre.double() ** 2).sum((0, 2, 3))) < 4e-3
+
+
+@pytest.mark.parametrize("shape", [(17, 64, 64), (65, 16, 64), (81, 32, 32)])
+def test_dgrad_sc_equals_dgrad_plus_shortcut(dev, shape):
+    """rr_igemm_dgrad_sc: per concat half, the 3x3 dgrad + the 1x1 shortcut
+    dgrad in one pass (dec1's input grad, 14:99-115) vs fp32 torch
+    (conv_transpose of both) and vs the two-step form it replaces (3x3 dgrad,
+    then the 1x1 dgrad accumulated in bf16): the one-pass sum is rounded once,
+    so it is at least as close to fp32."""
+    import roadrestore as rr
+    from roadrestore import ops
+    from roadrestore._lib import RR_CONV1X1, RR_CONV3X3
+    n, h, w = shape
+    dt = rnd(n, 64, h, w, seed=71).bfloat16().float()
+    dsc = rnd(n, 64, h, w, seed=72).bfloat16().float()
+    wt = (rnd(64, 128, 3, 3, seed=73) / 24.0).bfloat16().float()      # dec1.conv_block[0]
+    ws = (rnd(64, 128, 1, 1, seed=74) / 8.0).bfloat16().float()       # dec1.shortcut[0]
+    ref = F.conv_transpose2d(dt, wt, padding=1) + F.conv_transpose2d(dsc, ws)
+    _, wd = ops.pack_conv(wt.to(dev), BF)
+    _, wsd = ops.pack_conv(ws.to(dev), BF)
+    half, hs = 64 * 9 * 64, 64 * 64
+    d = ops.dgrad_sc_desc(nhwc(dt, dev), n, h, w, 64)
+    assert ops.igemm_dgrad_sc_kernel_name(d, 64) == "stream3_kernel<%d,sc>" % w
+    assert ops.igemm_dgrad_sc_kernel_name(d, 32) == "unsupported"
+    x, xs = nhwc(dt, dev), nhwc(dsc, dev)
+    g1 = ops.igemm_dgrad_sc(x, n, h, w, wd[:half], 64, xs, wsd[:hs])
+    g2 = ops.igemm_dgrad_sc(x, n, h, w, wd[half:], 64, xs, wsd[hs:])
+    # the two-step form (RR_FUSED_SC_DGRAD=0)
+    t1, _, _ = ops.igemm(RR_CONV3X3, x, None, n, h, w, wd[:half], 64)
+    t2, _, _ = ops.igemm(RR_CONV3X3, x, None, n, h, w, wd[half:], 64)
+    ops.igemm(RR_CONV1X1, xs, None, n, h, w, wsd, 128, out=t1, out2=t2, split=64, accumulate=True)
+    torch.cuda.synchronize()
+    got = torch.cat((nchw(g1), nchw(g2)), 1)
+    two = torch.cat((nchw(t1), nchw(t2)), 1)
+    e_got, e_two = rel(got, ref), rel(two, ref)
+    print(f"{shape}: one pass rel {e_got:.2e}, two-step rel {e_two:.2e}")
+    assert e_got < 4e-3 and e_got <= e_two * 1.05
+    assert rel(got, two) < 4e-3
+    # deterministic
+    g1b = ops.igemm_dgrad_sc(x, n, h, w, wd[:half], 64, xs, wsd[:hs])
+    assert torch.equal(g1, g1b)

@@ -7,6 +7,9 @@ RR_CONV3R_STAMPS) sums per wave the s_memtime segments of every stage:
   bar   the barrier after it
   rest  everything else in the loop (MFMA issue, B-row reads, DMA issue)
 
+and per wave the prologue (kernel entry -> K loop: first halo + weights) and
+the epilogue (K loop end -> return: statistics, bias, stores).
+
 Read the SHARES, not the totals: every stamp drains the LDS reads in flight.
 Usage: python tools/conv3r_stamps.py [NAME=v1,v2 ...] (env switches to sweep; cfg3 layers, B=512)."""
 import ctypes as C
@@ -48,8 +51,11 @@ def stamps(run):
     rest = loop - row0 - vm - bar
     per = lambda v: round(float(np.median(v / nst)), 1)   # noqa: E731
     tot = float(np.sum(loop))
+    pro, epi = r[:, 6], r[:, 7]
     return {"waves": int(len(r)), "cyc_per_stage": per(loop), "row0": per(row0), "vm": per(vm),
-            "bar": per(bar), "rest": per(rest),
+            "bar": per(bar), "rest": per(rest), "stages": int(np.median(nst)),
+            "loop_cyc": round(float(np.median(loop)), 0), "prologue_cyc": round(float(np.median(pro)), 0),
+            "epilogue_cyc": round(float(np.median(epi)), 0),
             "share": {k: round(float(np.sum(v)) / tot, 3)
                       for k, v in (("row0", row0), ("vm", vm), ("bar", bar), ("rest", rest))}}
 

@@ -3,7 +3,8 @@ one JSON line per layer (median of REPS HIP-event timings) with a SHA-1 of
 the output bytes, so two builds run in alternating processes
 (tools/gpu.sh ablayers:OTHER.so;SET) can be compared for time AND bitwise
 equality.  SET=wgrad: every 3x3 / 1x1 / convT weight grad of the ResUNet
-backward (14:96-186); SET=conv3r: the tap-reuse conv layers, fwd + dgrad.
+backward (14:96-186); SET=conv3r: the tap-reuse conv layers, fwd + dgrad;
+SET=s3: the row-streaming conv's variants at 64x64 / 32x32.
 
     python tools/layer_times.py [SET]
 """
@@ -165,5 +166,44 @@ elif SET == "bnbwd":
         print(json.dumps({"layer": name, "kernel": ops.igemm_kernel_name(
             ops.IgemmDesc(ops.RR_BF16, RR_CONV3X3, B, H, H, C, 0, C, 0, 0, 0, 0, 0, 0, 0), bnbwd=True),
             "ms": round(ms, 4), "tf": round(fl / ms / 1e9, 1), "sha": sha(gm)}), flush=True)
+elif SET == "s3":
+    # the row-streaming conv's variants (64 -> 64 channels): fwd + BN stats
+    # (res1 / dec1 / dec2 conv2), bias + ReLU (VGG conv1_2), plain / ReLU-mask /
+    # accumulate dgrads, the fused BN -> PReLU backward dgrad
+    for H in (64, 32):
+        x = torch.randn(B, H, H, 64, device=dev, generator=g).bfloat16()
+        wf, wd = ops.pack_conv(torch.randn(64, 64, 3, 3, device=dev, generator=g) / 24, torch.bfloat16)
+        bias = torch.randn(64, device=dev, generator=g)
+        mk = torch.randn(B, H, H, 64, device=dev, generator=g).bfloat16()
+        y0 = torch.randn(B, H, H, 64, device=dev, generator=g).bfloat16()
+        t1 = (torch.randn(B, H, H, 64, device=dev, generator=g) * 2 + 0.3).bfloat16()
+        tf = t1.float().reshape(-1, 64)
+        mean = tf.mean(0)
+        inv = 1.0 / torch.sqrt(tf.var(0, unbiased=False) + 1e-5)
+        s1 = torch.rand(64, device=dev, generator=g) + 0.5
+        sh1 = torch.rand(64, device=dev, generator=g) - 0.5
+        alpha = torch.tensor([0.23], device=dev)
+        fl = 2.0 * B * H * H * 64 * 64 * 9
+        row = {"layer": f"s3_{H}"}
+        hs = []
+        out = {}
+        yb = y0.clone()
+        cases = (("fwd_stats", lambda: ops.igemm(RR_CONV3X3, x, None, B, H, H, wf, 64, bias=bias, stats=True)),
+                 ("fwd_relu", lambda: ops.igemm(RR_CONV3X3, x, None, B, H, H, wf, 64, bias=bias, act=1)),
+                 ("dgrad", lambda: ops.igemm(RR_CONV3X3, x, None, B, H, H, wd, 64)),
+                 ("dgrad_mask", lambda: ops.igemm(RR_CONV3X3, x, None, B, H, H, wd, 64, mask=mk)),
+                 ("dgrad_acc", lambda: ops.igemm(RR_CONV3X3, x, None, B, H, H, wd, 64, out=yb, accumulate=True)),
+                 ("bnbwd", lambda: ops.igemm_bnbwd(RR_CONV3X3, x, B, H, H, wd, 64, t1, mean, inv, s1, sh1, alpha)))
+        for tag, fn in cases:
+            def run(fn=fn, tag=tag):
+                out[tag] = fn()
+            ms = timeit(run)
+            row[tag] = round(ms, 4)
+            tot_ms += ms
+            tot_fl += fl
+            if tag != "dgrad_acc":
+                hs.append(out[tag][0])
+        row["sha"] = sha(*hs)
+        print(json.dumps(row), flush=True)
 print(json.dumps({"set": SET, "total_ms": round(tot_ms, 4),
                   "tflops": round(tot_fl / tot_ms / 1e9, 1)}), flush=True)
