@@ -158,10 +158,17 @@ struct C3EpiStamp {
 
 template <int N> using ic = std::integral_constant<int, N>;
 
-template <int W, int BC, int NW, int NWV, int HB, int SG, int RW>
+// EPI: 0 = every epilogue (operand loads: accumulate / residual / ReLU mask,
+// PReLU, pool, the fused BN backward), 1 = bias, statistics, ReLU and the
+// concat split only -- the forward and plain dgrad of the training step.  The
+// specialised instance holds no operand registers (no spills) and carries no
+// operand branches: the plain epilogue's instruction stream is a third of the
+// general one's (989 vs the general path's share of 11.7 k instructions).
+template <int W, int BC, int NW, int NWV, int HB, int SG, int RW, int EPI = 0>
 __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) {
   using G = R3<W, BC, NW, NWV, HB, SG, RW>;
   constexpr bool BNREG = G::SEGM || RR_C3_BNREG == 1 || (RR_C3_BNREG == 0 && NWV == 8);
+  constexpr bool OPS = EPI == 0;
   constexpr int NS = G::NS, R = G::R, NM = G::NM, WC = G::WC, RS = G::RS;
   constexpr int HW = W * W;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
@@ -172,6 +179,12 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wc = wv % WC, wp = wv / WC;
   const int frow = lane & 15, fq = lane >> 4;
+
+  // (A/B) every other co-resident workgroup starts a.stagger x 8128 cycles
+  // late: the tiles' epilogue store bursts then alternate instead of landing
+  // on the whole chip at once (the later slots keep the offset)
+  if (a.stagger > 0 && ((((int)blockIdx.x >> 8) ^ (int)blockIdx.x) & 1))
+    for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(127);
 
   // XCD-aware tile order (as igemm3_halo_kernel): XCD b % 8 walks a
   // contiguous tile range, so column blocks of a pixel tile share its L2
@@ -688,7 +701,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
       vb[j] = __uint_as_float(t[1]);
     }
   };
-  if constexpr (BNREG) {
+  if constexpr (BNREG && OPS) {
     if (a.bpart) {
       // ---- fused BN -> PReLU backward (rr_igemm_bnbwd; IgemmArgs::bpart)
       // in registers: the accumulator is dL/d(PReLU out); per lane 8
@@ -793,7 +806,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
       return;
     }
   }
-  if (BNREG || !a.bpart) {
+  if (BNREG || !OPS || !a.bpart) {
     // ---- register epilogue: lane = 4 NHWC channels of one pixel per
     // accumulator tile ----
     if (a.stats) {
@@ -841,7 +854,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     // sizes) to a.ypool [n][h/2][w/2][c_out]; RR_ACT_NOFULL: only that.
     // Rows are finished in pairs (o, o + 1: a wave's first row is even), the
     // column pair is lane frow ^ 1 (same 8 channels after the swap)
-    const bool pool = (a.act & RR_ACT_POOL) != 0, full = (a.act & RR_ACT_NOFULL) == 0;
+    const bool pool = OPS && (a.act & RR_ACT_POOL) != 0, full = !OPS || (a.act & RR_ACT_NOFULL) == 0;
     const int ph = a.h >> 1, pw = a.w >> 1;
     // one epilogue operand of the whole wave tile -- the accumulate input,
     // else the residual, else the ReLU mask (uniform) -- is loaded before the
@@ -849,7 +862,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     // in program order, and loaded next to its use every 16-B group paid a
     // memory latency of its own (the 32x32 dgrads ran 30-70 % over the plain
     // conv).  A second operand (accumulate AND mask) still loads in place.
-    const int pre = a.accumulate ? 1 : (a.res ? 2 : (a.has_mask ? 3 : 0));
+    const int pre = !OPS ? 0 : (a.accumulate ? 1 : (a.res ? 2 : (a.has_mask ? 3 : 0)));
     // operand / destination address of tile (o, s), block pair pp (the
     // concat split is uniform per pair: split % 32 == 0)
     auto op_ptr = [&](int kind, int o, int s, int pp) __attribute__((always_inline)) -> const char * {
@@ -902,13 +915,13 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
             if (G::SEGM && p < 0) continue;
             bf16_t *dst = reinterpret_cast<bf16_t *>(const_cast<char *>(op_ptr(1, o, s, pp)));
             const int q = ((o % RH) * NS + s) * (NM / 2) + pp;
-            if (a.accumulate) {
+            if (OPS && a.accumulate) {
               f32x4 lo, hi;
               unpack8(opq[q], lo, hi);                      // (pre == 1)
               va += lo;
               vb += hi;
             }
-            if (a.res) {                                   // (rr_igemm_ex: y1's layout, no split)
+            if (OPS && a.res) {                            // (rr_igemm_ex: y1's layout, no split)
               f32x4 lo, hi;
               if (pre == 2) {
                 unpack8(opq[q], lo, hi);
@@ -923,7 +936,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
             if ((a.act & 3) == RR_ACT_RELU) {
 #pragma unroll
               for (int j = 0; j < 4; ++j) { va[j] = fmaxf(va[j], 0.f); vb[j] = fmaxf(vb[j], 0.f); }
-            } else if ((a.act & 3) == RR_ACT_PRELU) {
+            } else if (OPS && (a.act & 3) == RR_ACT_PRELU) {
               const float al = a.alpha[0];
 #pragma unroll
               for (int j = 0; j < 4; ++j) {
@@ -931,7 +944,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
                 vb[j] = vb[j] > 0.f ? vb[j] : al * vb[j];
               }
             }
-            if (a.has_mask) {
+            if (OPS && a.has_mask) {
               f32x4 ma, mb;
               if (pre == 3) {
                 unpack8(opq[q], ma, mb);
@@ -988,7 +1001,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     }
     return;
   }
-  if constexpr (!BNREG) {
+  if constexpr (!BNREG && OPS) {
     // ---- BN-backward epilogue: one 128-pixel group (= one wave row of the
     // grid) at a time as fp32 [128][BC] in LDS, then the staged store ----
     float *stg = reinterpret_cast<float *>(smem);
@@ -1143,6 +1156,26 @@ int conv3r_stat_blocks(const rr_igemm_desc *d) {
   return (int)(r3_ptiles(d, k) * (k.nwv / (k.bc / k.nw)));   // one row per wave row of a tile
 }
 
+// the plain epilogue (EPI 1: no operand loads, no PReLU / pool / fused BN
+// backward) wherever the call allows it; the register-weight K loop (an A/B
+// variant) keeps the general one.  RR_C3_PLAIN_EPI=0: a separate build with
+// the general epilogue everywhere (A/B)
+#ifndef RR_C3_PLAIN_EPI
+#define RR_C3_PLAIN_EPI 1
+#endif
+template <int W_, int BC, int NW, int NWV, int HB, int SG, int RW>
+static void c3_launch(const IgemmArgs &a, dim3 grid, dim3 block, hipStream_t st) {
+  const bool plain = !a.accumulate && !a.res && !a.has_mask && (a.act & 3) != RR_ACT_PRELU &&
+                     !(a.act & (RR_ACT_POOL | RR_ACT_NOFULL)) && !a.bpart;
+  if constexpr (!RW && RR_C3_PLAIN_EPI) {
+    if (plain) {
+      hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, RW, 1>), grid, block, 0, st, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, RW, 0>), grid, block, 0, st, a);
+}
+
 template <int BC, int NW, int NWV, int HB, int SG, int RW>
 static int conv3r_go(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   a.ncblk = a.cout / BC;
@@ -1150,20 +1183,20 @@ static int conv3r_go(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   if (nblk <= 0 || nblk > 0x7fffffffLL) return RR_EUNSUPPORTED;
   const dim3 grid((unsigned)nblk), block(64 * NWV);
   if constexpr (SG > 0) {
-    hipLaunchKernelGGL((conv3r_kernel<0, BC, NW, NWV, HB, SG, 0>), grid, block, 0, st, a);
+    c3_launch<0, BC, NW, NWV, HB, SG, 0>(a, grid, block, st);
   } else {
     switch (d->w) {
       case 64:
         if constexpr (RW) return RR_EUNSUPPORTED;
-        else hipLaunchKernelGGL((conv3r_kernel<64, BC, NW, NWV, HB, 0, 0>), grid, block, 0, st, a);
+        else c3_launch<64, BC, NW, NWV, HB, 0, 0>(a, grid, block, st);
         break;
-      case 32: hipLaunchKernelGGL((conv3r_kernel<32, BC, NW, NWV, HB, 0, RW>), grid, block, 0, st, a); break;
-      case 16: hipLaunchKernelGGL((conv3r_kernel<16, BC, NW, NWV, HB, 0, RW>), grid, block, 0, st, a); break;
+      case 32: c3_launch<32, BC, NW, NWV, HB, 0, RW>(a, grid, block, st); break;
+      case 16: c3_launch<16, BC, NW, NWV, HB, 0, RW>(a, grid, block, st); break;
       default:
         // (RW 4-wave 64 x 64 tiles of 8x8 pairs: 2 x 40 KB of halo, past two
         // workgroups per CU; the picker does not take it)
         if constexpr (RW && NWV == 4 && BC == 64 && NW == 64) return RR_EUNSUPPORTED;
-        else hipLaunchKernelGGL((conv3r_kernel<8, BC, NW, NWV, HB, 0, RW>), grid, block, 0, st, a);
+        else c3_launch<8, BC, NW, NWV, HB, 0, RW>(a, grid, block, st);
         break;
     }
   }

@@ -1225,6 +1225,8 @@ static int fill_args(const rr_igemm_desc *d, const void *x1, const void *x2, con
   a.out_nchw = d->out_nchw;
   const char *dbg_env = getenv("RR_IGEMM_DBG");
   a.dbg = dbg_env ? atoi(dbg_env) : 0;
+  const char *stg_env = getenv("RR_CONV3R_STAGGER");
+  a.stagger = stg_env ? atoi(stg_env) : 0;
   const char *xcd_env = getenv("RR_XCD_MAP");   // A/B switch (default on)
   a.xcd = xcd_env ? atoi(xcd_env) : 1;
   a.ncblk = 1;
