@@ -54,9 +54,11 @@
 // the fused BN/PReLU-backward dgrad epilogue runs in registers on the
 // row-segment tiles and the 8-wave whole-row tiles (16x16 / 8x8: 1-4 %
 // faster than staging it through the LDS one 128-pixel group at a time,
-// profiles/r5d_ablayers_bnbwd.txt), staged on the 4-wave whole-row tiles
-// (32x32: the register form 12 % slower there).  RR_C3_BNREG (a separate
-// build, A/B): 1 = registers everywhere, 2 = staged on every whole-row tile
+// profiles/r5d_ablayers_bnbwd.txt) and in the bnbwd-only instance (EPI 3,
+// spill-free); the general instance stages it on the 4-wave whole-row tiles
+// (32x32: its register form was 12 % slower there).  RR_C3_BNREG (a separate
+// build, A/B): 1 = registers everywhere, 2 = staged on every whole-row tile,
+// 3 = staged on the 4-wave tiles in EPI 3 too
 #ifndef RR_C3_BNREG
 #define RR_C3_BNREG 0
 #endif
@@ -160,15 +162,20 @@ template <int N> using ic = std::integral_constant<int, N>;
 
 // EPI: 0 = every epilogue (operand loads: accumulate / residual / ReLU mask,
 // PReLU, pool, the fused BN backward), 1 = bias, statistics, ReLU and the
-// concat split only -- the forward and plain dgrad of the training step.  The
-// specialised instance holds no operand registers (no spills) and carries no
-// operand branches: the plain epilogue's instruction stream is a third of the
-// general one's (989 vs the general path's share of 11.7 k instructions).
+// concat split only -- the forward and plain dgrad of the training step,
+// 2 = 1 + the accumulate / ReLU-mask operands (the identity-shortcut and VGG
+// dgrads), 3 = the fused BN -> PReLU backward only.  A specialised instance
+// holds no registers for the epilogues it cannot run (no spills) and carries
+// none of their branches: the plain epilogue's instruction stream is a third
+// of the general one's (989 vs the general path's share of 11.7 k).
 template <int W, int BC, int NW, int NWV, int HB, int SG, int RW, int EPI = 0>
 __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) {
   using G = R3<W, BC, NW, NWV, HB, SG, RW>;
-  constexpr bool BNREG = G::SEGM || RR_C3_BNREG == 1 || (RR_C3_BNREG == 0 && NWV == 8);
-  constexpr bool OPS = EPI == 0;
+  constexpr bool BNREG = G::SEGM || RR_C3_BNREG == 1 || (RR_C3_BNREG == 0 && (NWV == 8 || EPI == 3)) ||
+                         (RR_C3_BNREG == 3 && NWV == 8);
+  constexpr bool ALLOW_BN = EPI == 0 || EPI == 3;     // the fused BN backward (a.bpart)
+  constexpr bool ALLOW_OPS = EPI == 0 || EPI == 2;    // accumulate / ReLU-mask operands
+  constexpr bool ALLOW_EX = EPI == 0;                 // residual, PReLU, pool
   constexpr int NS = G::NS, R = G::R, NM = G::NM, WC = G::WC, RS = G::RS;
   constexpr int HW = W * W;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
@@ -701,7 +708,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
       vb[j] = __uint_as_float(t[1]);
     }
   };
-  if constexpr (BNREG && OPS) {
+  if constexpr (BNREG && ALLOW_BN) {
     if (a.bpart) {
       // ---- fused BN -> PReLU backward (rr_igemm_bnbwd; IgemmArgs::bpart)
       // in registers: the accumulator is dL/d(PReLU out); per lane 8
@@ -806,7 +813,8 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
       return;
     }
   }
-  if (BNREG || !OPS || !a.bpart) {
+  if constexpr (EPI == 3 && BNREG) return;           // (a.bpart: returned above)
+  if (EPI != 3 && (BNREG || !ALLOW_BN || !a.bpart)) {
     // ---- register epilogue: lane = 4 NHWC channels of one pixel per
     // accumulator tile ----
     if (a.stats) {
@@ -828,20 +836,42 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
             s2[m] += v * v;
           }
         }
+      // over the 16 pixel lanes by a reduce-scatter: V[k] = (s1, s2) of
+      // (m, j) = divmod(k / 2, 4); each step pairs lanes that differ in one bit
+      // of frow (row mirror: bit 3, half mirror: 2, xor 2: 1, xor 1: 0), the
+      // lane with the bit clear keeps the lower half of its values plus its
+      // partner's copy, the other the upper half: 8 NM - 2 adds instead of 32
+      // NM (four-step tree per value).  Lane frow ends with V[NV/16 frow ..]
+      constexpr int NV = 8 * NM;
+      float v[NV];
 #pragma unroll
       for (int m = 0; m < NM; ++m)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          s1[m][j] = row16_sum(s1[m][j]);
-          s2[m][j] = row16_sum(s2[m][j]);
-        }
-      if (frow == 0) {
+        for (int j = 0; j < 4; ++j) { v[(m * 4 + j) * 2] = s1[m][j]; v[(m * 4 + j) * 2 + 1] = s2[m][j]; }
+      auto rs_step = [&](int n, bool hi, auto CTRLc) __attribute__((always_inline)) {
+        constexpr int CTRL = decltype(CTRLc)::value;
 #pragma unroll
-        for (int m = 0; m < NM; ++m) {
-          float *sp = a.stats + ((long long)srow * a.cout + c0 + cb + m * 16 + fq * 4) * 2;
-          *reinterpret_cast<f32x4 *>(sp) = f32x4{s1[m][0], s2[m][0], s1[m][1], s2[m][1]};
-          *reinterpret_cast<f32x4 *>(sp + 4) = f32x4{s1[m][2], s2[m][2], s1[m][3], s2[m][3]};
+        for (int i = 0; i < NV / 2; ++i) {
+          if (i >= n / 2) break;
+          const float send = hi ? v[i] : v[i + n / 2];
+          const float keep = hi ? v[i + n / 2] : v[i];
+          v[i] = keep + dpp_f<CTRL>(send);
         }
+      };
+      rs_step(NV, (frow & 8) != 0, ic<DPP_MIRROR>{});
+      rs_step(NV / 2, (frow & 4) != 0, ic<DPP_HALF_MIRROR>{});
+      rs_step(NV / 4, (frow & 2) != 0, ic<DPP_XOR2>{});
+      rs_step(NV / 8, (frow & 1) != 0, ic<DPP_XOR1>{});
+      float *sp = a.stats + ((long long)srow * a.cout + c0 + cb) * 2;
+      if constexpr (NV / 16 == 2) {
+        // (s1, s2) of (m, j) = divmod(frow, 4)
+        const int ch = (frow >> 2) * 16 + fq * 4 + (frow & 3);
+        *reinterpret_cast<float2 *>(sp + ch * 2) = make_float2(v[0], v[1]);
+      } else {
+        static_assert(NV / 16 == 1, "16- or 32-value reductions");
+        // t = frow & 1 of (m, j) = divmod(frow / 2, 4)
+        const int ch = (frow >> 3) * 16 + fq * 4 + ((frow >> 1) & 3);
+        sp[ch * 2 + (frow & 1)] = v[0];
       }
     }
     f32x4 bv[NM];
@@ -854,7 +884,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     // sizes) to a.ypool [n][h/2][w/2][c_out]; RR_ACT_NOFULL: only that.
     // Rows are finished in pairs (o, o + 1: a wave's first row is even), the
     // column pair is lane frow ^ 1 (same 8 channels after the swap)
-    const bool pool = OPS && (a.act & RR_ACT_POOL) != 0, full = !OPS || (a.act & RR_ACT_NOFULL) == 0;
+    const bool pool = ALLOW_EX && (a.act & RR_ACT_POOL) != 0, full = !ALLOW_EX || (a.act & RR_ACT_NOFULL) == 0;
     const int ph = a.h >> 1, pw = a.w >> 1;
     // one epilogue operand of the whole wave tile -- the accumulate input,
     // else the residual, else the ReLU mask (uniform) -- is loaded before the
@@ -862,7 +892,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     // in program order, and loaded next to its use every 16-B group paid a
     // memory latency of its own (the 32x32 dgrads ran 30-70 % over the plain
     // conv).  A second operand (accumulate AND mask) still loads in place.
-    const int pre = !OPS ? 0 : (a.accumulate ? 1 : (a.res ? 2 : (a.has_mask ? 3 : 0)));
+    const int pre = (ALLOW_OPS && a.accumulate) ? 1 : ((ALLOW_EX && a.res) ? 2 : ((ALLOW_OPS && a.has_mask) ? 3 : 0));
     // operand / destination address of tile (o, s), block pair pp (the
     // concat split is uniform per pair: split % 32 == 0)
     auto op_ptr = [&](int kind, int o, int s, int pp) __attribute__((always_inline)) -> const char * {
@@ -915,13 +945,13 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
             if (G::SEGM && p < 0) continue;
             bf16_t *dst = reinterpret_cast<bf16_t *>(const_cast<char *>(op_ptr(1, o, s, pp)));
             const int q = ((o % RH) * NS + s) * (NM / 2) + pp;
-            if (OPS && a.accumulate) {
+            if (ALLOW_OPS && a.accumulate) {
               f32x4 lo, hi;
               unpack8(opq[q], lo, hi);                      // (pre == 1)
               va += lo;
               vb += hi;
             }
-            if (OPS && a.res) {                            // (rr_igemm_ex: y1's layout, no split)
+            if (ALLOW_EX && a.res) {                       // (rr_igemm_ex: y1's layout, no split)
               f32x4 lo, hi;
               if (pre == 2) {
                 unpack8(opq[q], lo, hi);
@@ -936,7 +966,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
             if ((a.act & 3) == RR_ACT_RELU) {
 #pragma unroll
               for (int j = 0; j < 4; ++j) { va[j] = fmaxf(va[j], 0.f); vb[j] = fmaxf(vb[j], 0.f); }
-            } else if (OPS && (a.act & 3) == RR_ACT_PRELU) {
+            } else if (ALLOW_EX && (a.act & 3) == RR_ACT_PRELU) {
               const float al = a.alpha[0];
 #pragma unroll
               for (int j = 0; j < 4; ++j) {
@@ -944,7 +974,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
                 vb[j] = vb[j] > 0.f ? vb[j] : al * vb[j];
               }
             }
-            if (OPS && a.has_mask) {
+            if (ALLOW_OPS && a.has_mask) {
               f32x4 ma, mb;
               if (pre == 3) {
                 unpack8(opq[q], ma, mb);
@@ -1001,7 +1031,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     }
     return;
   }
-  if constexpr (!BNREG && OPS) {
+  if constexpr (!BNREG && ALLOW_BN) {
     // ---- BN-backward epilogue: one 128-pixel group (= one wave row of the
     // grid) at a time as fp32 [128][BC] in LDS, then the staged store ----
     float *stg = reinterpret_cast<float *>(smem);
@@ -1170,6 +1200,15 @@ static void c3_launch(const IgemmArgs &a, dim3 grid, dim3 block, hipStream_t st)
   if constexpr (!RW && RR_C3_PLAIN_EPI) {
     if (plain) {
       hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, RW, 1>), grid, block, 0, st, a);
+      return;
+    }
+    const bool ex = a.res || (a.act & 3) == RR_ACT_PRELU || (a.act & (RR_ACT_POOL | RR_ACT_NOFULL));
+    if (a.bpart && !ex && !a.accumulate && !a.has_mask) {
+      hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, RW, 3>), grid, block, 0, st, a);
+      return;
+    }
+    if (!a.bpart && !ex) {
+      hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, RW, 2>), grid, block, 0, st, a);
       return;
     }
   }

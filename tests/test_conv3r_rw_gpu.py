@@ -173,10 +173,19 @@ def test_rw_bnbwd_bitwise(dev, shape, geom, monkeypatch):
     alpha = torch.tensor([0.23], device=dev)
 
     def run():
-        return ops.igemm_bnbwd(RR_CONV3X3, g2, n, w, w, wd, C, t1, mean, inv, s1, sh1, alpha)
+        gm, part, rows, arows = ops.igemm_bnbwd(RR_CONV3X3, g2, n, w, w, wd, C, t1, mean, inv, s1,
+                                                sh1, alpha)
+        r = ops.bn_backward_rows(gm, part, rows, arows, t1, mean, inv, gamma)
+        return gm, r["dgamma0"], r["dbeta0"], r["dalpha"], r["dt0"]
     o0, o1, _ = _both(monkeypatch, geom, _desc(n, w, cg, 0, C), run)
-    assert torch.equal(o0[0], o1[0]) and torch.equal(o0[1], o1[1]) and o0[2] == o1[2]
-    assert torch.equal(o0[3], o1[3]) if torch.is_tensor(o0[3]) else o0[3] == o1[3]
+    # the masked grad bitwise; the per-row partial sums of the register-weight
+    # loop (general epilogue, staged on the 4-wave tiles) and of the default
+    # bnbwd-only instance (in registers) are laid out differently, so the
+    # channel sums agree to fp32 rounding
+    assert torch.equal(o0[0], o1[0])
+    for a, b in zip(o0[1:4], o1[1:4]):
+        assert ((a - b).norm() / b.norm().clamp_min(1e-30)).item() < 1e-5
+    assert ((o0[4].float() - o1[4].float()).norm() / o1[4].float().norm()).item() < 1e-3
 
 
 @pytest.mark.parametrize("shape", [(4, 16, 256, 0, 256), (8, 32, 128, 0, 128), (64, 8, 512, 0, 512)])
