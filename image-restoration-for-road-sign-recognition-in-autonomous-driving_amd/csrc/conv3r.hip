@@ -164,7 +164,8 @@ template <int N> using ic = std::integral_constant<int, N>;
 // PReLU, pool, the fused BN backward), 1 = bias, statistics, ReLU and the
 // concat split only -- the forward and plain dgrad of the training step,
 // 2 = 1 + the accumulate / ReLU-mask operands (the identity-shortcut and VGG
-// dgrads), 3 = the fused BN -> PReLU backward only.  A specialised instance
+// dgrads), 3 = the fused BN -> PReLU backward only, 4 = 1 + the 2x2 max-pool
+// (the perceptual VGG's conv + ReLU + MaxPool2d, rr_igemm_pool).  A specialised instance
 // holds no registers for the epilogues it cannot run (no spills) and carries
 // none of their branches: the plain epilogue's instruction stream is a third
 // of the general one's (989 vs the general path's share of 11.7 k).
@@ -175,7 +176,8 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
                          (RR_C3_BNREG == 3 && NWV == 8);
   constexpr bool ALLOW_BN = EPI == 0 || EPI == 3;     // the fused BN backward (a.bpart)
   constexpr bool ALLOW_OPS = EPI == 0 || EPI == 2;    // accumulate / ReLU-mask operands
-  constexpr bool ALLOW_EX = EPI == 0;                 // residual, PReLU, pool
+  constexpr bool ALLOW_EX = EPI == 0;                 // residual, PReLU
+  constexpr bool ALLOW_POOL = EPI == 0 || EPI == 4;   // the 2x2 max-pool epilogue
   constexpr int NS = G::NS, R = G::R, NM = G::NM, WC = G::WC, RS = G::RS;
   constexpr int HW = W * W;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
@@ -884,7 +886,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     // sizes) to a.ypool [n][h/2][w/2][c_out]; RR_ACT_NOFULL: only that.
     // Rows are finished in pairs (o, o + 1: a wave's first row is even), the
     // column pair is lane frow ^ 1 (same 8 channels after the swap)
-    const bool pool = ALLOW_EX && (a.act & RR_ACT_POOL) != 0, full = !ALLOW_EX || (a.act & RR_ACT_NOFULL) == 0;
+    const bool pool = ALLOW_POOL && (a.act & RR_ACT_POOL) != 0, full = !ALLOW_POOL || (a.act & RR_ACT_NOFULL) == 0;
     const int ph = a.h >> 1, pw = a.w >> 1;
     // one epilogue operand of the whole wave tile -- the accumulate input,
     // else the residual, else the ReLU mask (uniform) -- is loaded before the
@@ -1203,6 +1205,11 @@ static void c3_launch(const IgemmArgs &a, dim3 grid, dim3 block, hipStream_t st)
       return;
     }
     const bool ex = a.res || (a.act & 3) == RR_ACT_PRELU || (a.act & (RR_ACT_POOL | RR_ACT_NOFULL));
+    if ((a.act & RR_ACT_POOL) && !a.res && (a.act & 3) != RR_ACT_PRELU && !a.accumulate && !a.has_mask &&
+        !a.bpart) {
+      hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, RW, 4>), grid, block, 0, st, a);
+      return;
+    }
     if (a.bpart && !ex && !a.accumulate && !a.has_mask) {
       hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, RW, 3>), grid, block, 0, st, a);
       return;

@@ -71,6 +71,20 @@
 #define RR_S3_DPP 0
 #endif
 
+#ifdef RR_S3_STAMPS
+// diagnostic build only (make s3stamps; tools/s3_stamps.py): per-wave sums of
+// the step loop's segments, read with rr_s3_stamps; never shipped
+__device__ unsigned long long rr_s3_stamps[256 * 8 * 8];
+#define S3_STAMP(t)                                                             \
+  do {                                                                          \
+    __builtin_amdgcn_sched_barrier(0);                                          \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");   \
+    __builtin_amdgcn_sched_barrier(0);                                          \
+  } while (0)
+#else
+#define S3_STAMP(t) do {} while (0)
+#endif
+
 namespace {
 
 constexpr int S3_WG = 256;   // workgroups: one per CU on MI355X (fixed: deterministic partial rows)
@@ -711,8 +725,12 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
   constexpr int YL = (D - 1) * DMAW + S * (D - 1) + E * (D - 1);  // steady state, late
   long long ppix = 0;                           // late half: the step whose epilogue is pending
   bool pcomp = false;
+  [[maybe_unused]] unsigned long long st_a = 0, st_b = 0, st_wait = 0, st_issue = 0, st_mfma = 0, st_epi = 0,
+                                      st_steps = 0, st_t0 = 0, st_t1 = 0;
+  S3_STAMP(st_t0);
 #pragma unroll 1
   while (cp.c < cend) {
+    S3_STAMP(st_a);
     if ((hist & FULL) == FULL) {
       if (late) wait_vm_barrier_c<YL < 63 ? YL : 63>();
       else wait_vm_barrier_c<YE < 63 ? YE : 63>();
@@ -724,6 +742,9 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
                                (E + S) * __builtin_popcount(inner);
       wait_vm_barrier(y);
     }
+    S3_STAMP(st_b);
+    st_wait += st_b - st_a;
+    st_a = st_b;
     const bool comp = cp.kind == S3_COMP;
     const long long pix0 = (long long)(cp.n * H + cp.y0) * W;
     if (late && pcomp) epilogue(ppix);          // its loads were waited for last iteration
@@ -737,8 +758,15 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     lslot += RPS;
     lslot = lslot >= RING ? lslot - RING : lslot;
     __builtin_amdgcn_sched_barrier(0);
+    S3_STAMP(st_b);
+    st_issue += st_b - st_a;
+    st_a = st_b;
     if (comp) {
       mfma_step(cslot);
+      S3_STAMP(st_b);
+      st_mfma += st_b - st_a;
+      st_a = st_b;
+      ++st_steps;
       // wait for the epilogue loads in the iteration that issued them: the
       // compiler does not know the asm loads are asynchronous, so their
       // registers must not be live across the loop back-edge (it may copy
@@ -757,6 +785,8 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
                   wsr[mi][kb], __builtin_bit_cast(bf16x8, esc[ni][kb]), acc[mi][ni], 0, 0, 0);
       }
       if (!late) epilogue(pix0);
+      S3_STAMP(st_b);
+      st_epi += st_b - st_a;
     }
     ppix = pix0;
     pcomp = comp;
@@ -766,6 +796,14 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     advance(cp);
   }
   if (late && pcomp) epilogue(ppix);            // the late half's last epilogue
+#ifdef RR_S3_STAMPS
+  S3_STAMP(st_t1);
+  if (lane == 0) {
+    unsigned long long *o = rr_s3_stamps + ((long long)blockIdx.x * 8 + wv) * 8;
+    o[0] = st_t1 - st_t0; o[1] = st_wait; o[2] = st_issue; o[3] = st_mfma; o[4] = st_epi; o[5] = st_steps;
+    o[6] = 1;
+  }
+#endif
   // drain the ring's trailing (dummy) DMA before the LDS is reused / released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -952,6 +990,18 @@ int stream3_blocks(const rr_igemm_desc *d, int bnbwd) {
   if (P < 256LL * S3_WG || P * 64 > INT_MAX) return 0;
   return S3_WG;
 }
+
+#ifdef RR_S3_STAMPS
+extern "C" int rr_s3_stamps_read(unsigned long long *host, int n, int clear) {
+  if (n > 256 * 8 * 8) n = 256 * 8 * 8;
+  if (host && hipMemcpyFromSymbol(host, HIP_SYMBOL(rr_s3_stamps), (size_t)n * 8) != hipSuccess) return -3;
+  if (clear) {
+    static unsigned long long z[256 * 8 * 8];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rr_s3_stamps), z, sizeof(z)) != hipSuccess) return -3;
+  }
+  return 0;
+}
+#endif
 
 int stream3_launch_sc(const rr_igemm_desc *d, const S3Args &a0, hipStream_t st) {
   if (!stream3_blocks(d, 0) || d->c_in2 || s3_flags(d, false) != 0 || !a0.xsc || !a0.wsc)
