@@ -627,11 +627,18 @@ __global__ void distort_blur_kernel(DistCfg a) {
 // of 256, where a workgroup's 256 pixels always belong to one image: the
 // per-pixel loop then visits the ~k..2k nonzero taps of the rotated line
 // kernel instead of testing all k * k, with no per-tap global loads
+//
+// The source rows the 256 pixels read (their row span + k - 1, reflect-101
+// applied at staging, columns -anc .. w - 1 + k - 1 - anc) are staged in LDS
+// when they fit: the tap loop then reads bytes at (row, x + j) with no
+// reflection and no global load (same values, same order: bit-identical)
+#define RR_BLUR_LDS 24576
 __global__ __launch_bounds__(256) void distort_blur_tiled_kernel(DistCfg a) {
 #pragma clang fp contract(off)
   __shared__ float tv[RR_DISTORT_KMAX * RR_DISTORT_KMAX];
   __shared__ int ti[RR_DISTORT_KMAX * RR_DISTORT_KMAX];
   __shared__ int wcount[4];
+  __shared__ uint8_t simg[RR_BLUR_LDS];
   const long long hw = (long long)a.h * a.w, total = hw * a.n;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   for (long long q0 = blockIdx.x * 256LL; q0 < total; q0 += (long long)gridDim.x * 256) {
@@ -647,6 +654,20 @@ __global__ __launch_bounds__(256) void distort_blur_tiled_kernel(DistCfg a) {
     const int pos = __popcll(m & ((1ull << lane) - 1ull));
     __syncthreads();                                         // the previous image's list is read
     if (lane == 0) wcount[wv] = __popcll(m);
+    const uint8_t *src = a.tmp + (long long)img * hw * a.c;
+    const int rem0 = (int)(q0 - (long long)img * hw);
+    const int ya = rem0 / a.w, yb = (rem0 + 255) / a.w;      // row span of the 256 pixels
+    const int pw = a.w + k - 1, nr = yb - ya + k;             // staged columns / rows
+    const bool lds = nr * pw * a.c <= RR_BLUR_LDS;           // uniform
+    if (lds) {
+      const int rowb = pw * a.c;
+      for (int e = t; e < nr * rowb; e += 256) {
+        const int r = e / rowb, rest = e - r * rowb;
+        const int cx = rest / a.c, ch = rest - cx * a.c;
+        const int yy = reflect101(ya - anc + r, a.h), xx = reflect101(cx - anc, a.w);
+        simg[e] = src[((long long)yy * a.w + xx) * a.c + ch];
+      }
+    }
     __syncthreads();
     int off = 0;
     for (int u = 0; u < wv; ++u) off += wcount[u];
@@ -655,14 +676,23 @@ __global__ __launch_bounds__(256) void distort_blur_tiled_kernel(DistCfg a) {
     __syncthreads();
     const long long q = q0 + t;
     const int rem = (int)(q - (long long)img * hw), y = rem / a.w, x = rem % a.w;
-    const uint8_t *src = a.tmp + (long long)img * hw * a.c;
     float s[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int u = 0; u < nt; ++u) {
-      const int ij = ti[u];
-      const float w = tv[u];
-      const int yy = reflect101(y + (ij >> 8) - anc, a.h), xx = reflect101(x + (ij & 255) - anc, a.w);
-      const uint8_t *px = src + ((long long)yy * a.w + xx) * a.c;
-      for (int c = 0; c < a.c; ++c) s[c] = s[c] + w * (float)px[c];
+    if (lds) {
+      const uint8_t *base = simg + ((y - ya) * pw + x) * a.c;
+      for (int u = 0; u < nt; ++u) {
+        const int ij = ti[u];
+        const float w = tv[u];
+        const uint8_t *px = base + ((ij >> 8) * pw + (ij & 255)) * a.c;
+        for (int c = 0; c < a.c; ++c) s[c] = s[c] + w * (float)px[c];
+      }
+    } else {
+      for (int u = 0; u < nt; ++u) {
+        const int ij = ti[u];
+        const float w = tv[u];
+        const int yy = reflect101(y + (ij >> 8) - anc, a.h), xx = reflect101(x + (ij & 255) - anc, a.w);
+        const uint8_t *px = src + ((long long)yy * a.w + xx) * a.c;
+        for (int c = 0; c < a.c; ++c) s[c] = s[c] + w * (float)px[c];
+      }
     }
     blur_store(a, p, q, s);
   }

@@ -693,10 +693,46 @@ extern "C" const char *rr_wgrad_kernel_name(const rr_wgrad_desc *d) {
   return tn[d->dtype == RR_BF16][pl.BA == 128][pl.BB == 128][mi];
 }
 
+// the reduce of *d's split partials: (CA, CB, taps, nsplit) of the slab
+static void reduce_shape(const rr_wgrad_desc *d, int &CA, int &CB, int &taps, int &nsplit) {
+  if (swgrad_ok(d)) {
+    CA = d->c_out; CB = d->c_in1 + d->c_in2; taps = 9; nsplit = swgrad_nsplit(d);
+  } else if (halo_ok(d)) {
+    CA = d->c_out; CB = d->c_in1 + d->c_in2; taps = 9; nsplit = halo_plan(d).nsplit;
+  } else {
+    const Plan pl = plan_of(d);
+    CA = pl.CA; CB = pl.CB; taps = pl.taps; nsplit = pl.nsplit;
+  }
+}
+
+static bool wgrad_desc_ok(const rr_wgrad_desc *d) {
+  return d->mode == RR_CONV3X3 || d->mode == RR_CONV1X1 || d->mode == RR_CONVT_UP;
+}
+
+extern "C" int rr_wgrad_reduce(const rr_wgrad_desc *d, const void *ws, size_t ws_bytes, float *dw,
+                               rr_stream stream) {
+  if (!d || !ws || !dw || !wgrad_desc_ok(d)) return RR_EINVAL;
+  if (d->c_in1 % 64 || d->c_in2 % 64 || d->c_out % 64) return RR_EUNSUPPORTED;
+  if (ws_bytes < rr_wgrad_workspace(d)) return RR_EWORKSPACE;
+  int CA, CB, taps, nsplit;
+  reduce_shape(d, CA, CB, taps, nsplit);
+  launch_reduce((const float *)ws, dw, CA, CB, taps, nsplit, d->accumulate, (hipStream_t)stream);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
 extern "C" int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
                         const void *x2, float *dw, void *ws, size_t ws_bytes,
                         rr_stream stream) {
-  if (!d || !dy || !x1 || !dw) return RR_EINVAL;
+  if (!dw) return RR_EINVAL;
+  const int rc = rr_wgrad_partial(d, dy, x1, x2, ws, ws_bytes, stream);
+  if (rc) return rc;
+  return rr_wgrad_reduce(d, ws, ws_bytes, dw, stream);
+}
+
+extern "C" int rr_wgrad_partial(const rr_wgrad_desc *d, const void *dy, const void *x1,
+                                const void *x2, void *ws, size_t ws_bytes, rr_stream stream) {
+  if (!d || !dy || !x1) return RR_EINVAL;
   if (d->mode != RR_CONV3X3 && d->mode != RR_CONV1X1 && d->mode != RR_CONVT_UP) return RR_EINVAL;
   if (d->c_in1 % 64 || d->c_in2 % 64 || d->c_out % 64) return RR_EUNSUPPORTED;
   if (d->c_in2 > 0 && (!x2 || d->mode == RR_CONVT_UP)) return RR_EINVAL;
@@ -727,8 +763,6 @@ extern "C" int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
   if (swgrad_ok(d)) {
     const int rc = swgrad_launch(d, dy, x1, x2, ws, st);
     if (rc) return rc;
-    launch_reduce((const float *)ws, dw, d->c_out, d->c_in1 + d->c_in2, 9, swgrad_nsplit(d),
-                  d->accumulate, st);
     RR_CHECK_LAUNCH();
     return RR_OK;
   }
@@ -773,13 +807,7 @@ extern "C" int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
       }
     }
     RR_CHECK_LAUNCH();
-    launch_reduce((const float *)ws, dw, ha.CA, ha.CB, 9, hp.nsplit, d->accumulate, st);
-    RR_CHECK_LAUNCH();
     return RR_OK;
   }
-  int rc = d->dtype == RR_BF16 ? launch_t<bf16_t>(d, pl, a, st) : launch_t<float>(d, pl, a, st);
-  if (rc) return rc;
-  launch_reduce((const float *)ws, dw, pl.CA, pl.CB, pl.taps, pl.nsplit, d->accumulate, st);
-  RR_CHECK_LAUNCH();
-  return RR_OK;
+  return d->dtype == RR_BF16 ? launch_t<bf16_t>(d, pl, a, st) : launch_t<float>(d, pl, a, st);
 }

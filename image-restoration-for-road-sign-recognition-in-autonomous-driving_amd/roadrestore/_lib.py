@@ -83,6 +83,8 @@ _SIGS = {
     "rr_igemm_bnbwd": (I_, [C.POINTER(IgemmDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_, P_, P_]),
     "rr_wgrad_workspace": (S_, [C.POINTER(WgradDesc)]),
     "rr_wgrad": (I_, [C.POINTER(WgradDesc), P_, P_, P_, P_, P_, S_, P_]),
+    "rr_wgrad_partial": (I_, [C.POINTER(WgradDesc), P_, P_, P_, P_, S_, P_]),
+    "rr_wgrad_reduce": (I_, [C.POINTER(WgradDesc), P_, S_, P_, P_]),
     "rr_pack_conv": (I_, [I_, I_, I_, I_, P_, P_, P_, P_]),
     "rr_pack_conv_elems": (L_, [I_, I_, I_, I_]),
     "rr_pack_conv_batch": (I_, [I_, I_, P_, L_, P_]),

@@ -59,6 +59,7 @@ class WeightCache:
         self._batch = None
         self._fresh = {}         # key -> (ver, packed), set by begin()
         self._pending = None     # (event, fresh) of a prefetch() not yet joined
+        self._misc = {}          # key -> (w, fn, also): the convT / first-conv / bias packs
 
     def _ver(self, w, also=None):
         # the fused optimizer's generation counts only for trained weights: a
@@ -72,6 +73,11 @@ class WeightCache:
         cap = torch.cuda.is_current_stream_capturing()
         key = (id(w), dtype, kind)
         ver = self._ver(w, also)
+        if not self.static and w.is_cuda:
+            self._misc[key] = (w, fn, also)        # (re-)recorded by every use
+        f = self._fresh.get(key)
+        if f is not None and f[0] == ver:
+            return f[1]                  # made by a prefetch() of this forward
         e = None if cap and not self.static else self._c.get(key)
         if e is not None and e[0] == ver:
             return e[1]
@@ -117,8 +123,18 @@ class WeightCache:
             return False
         side = _pack_stream(w0.device)
         side.wait_stream(torch.cuda.current_stream(w0.device))
+        main = torch.cuda.current_stream(w0.device)
         with torch.cuda.stream(side):
             self.begin()
+            # the small non-conv packs too (3 convT + 3 bias tiles + the
+            # first conv: ~5 us launches each in front of their layers)
+            misc, self._misc = self._misc, {}     # the packs the last forward asked for
+            for key, (w, fn, also) in misc.items():
+                v = fn()
+                for t in (v if isinstance(v, (tuple, list)) else (v,)):
+                    if isinstance(t, torch.Tensor):
+                        t.record_stream(main)
+                self._fresh[key] = (self._ver(w, also), v)
             ev = torch.cuda.Event()
             ev.record(side)
         self._pending = (ev, self._fresh)
@@ -329,11 +345,20 @@ def _conv3_bwd(conv, pk, gpre, xin1, xin2, n, h, w, sink, mask=None, want_dx=Tru
     return y1, y2
 
 
-def _convT_bwd(conv, pk, gu, xin, n, h, w, sink, mask=None):
-    """ConvTranspose2d(k2,s2) backward: gu on the (2h, 2w) grid; xin [n,h,w,cin]."""
+def _convT_bwd(conv, pk, gu, xin, n, h, w, sink, mask=None, side=False):
+    """ConvTranspose2d(k2,s2) backward: gu on the (2h, 2w) grid; xin [n,h,w,cin].
+    ``side``: the weight grad's reduce and the bias sum on the reduce stream
+    (joined by join_wgrad_reduces)."""
     cin, cout = conv.weight.shape[0], conv.weight.shape[1]
-    ops.wgrad(RR_CONVT_UP, gu, xin, None, n, h, w, cout, dw=sink[conv.weight])
-    ops.channel_sum(gu, out=sink[conv.bias])
+    rs = reduce_stream(gu.device) if side else None
+    ops.wgrad(RR_CONVT_UP, gu, xin, None, n, h, w, cout, dw=sink[conv.weight], reduce_stream=rs)
+    if rs is None:
+        ops.channel_sum(gu, out=sink[conv.bias])
+    else:
+        rs.wait_stream(torch.cuda.current_stream(gu.device))
+        with torch.cuda.stream(rs):
+            ops.channel_sum(gu, out=sink[conv.bias])
+        gu.record_stream(rs)
     gx, _, _ = ops.igemm(RR_CONVT_DOWN, gu, None, n, h, w, pk[1], cin, mask=mask)
     return gx
 
@@ -553,7 +578,7 @@ def resblock_zero_grad_params(blk):
     return z
 
 
-def resblock_backward(blk, S, g_out, sink, pool=None, convout=None):
+def resblock_backward(blk, S, g_out, sink, pool=None, convout=None, reduce_side=False):
     """``pool=(dy_pool, idx)``: the output also fed a 2x2 max-pool whose
     backward is fused into the tail BN backward (no separate pass).
     ``convout=(final, dy)``: the output fed the final 1x1 conv ``final`` and
@@ -575,10 +600,13 @@ def resblock_backward(blk, S, g_out, sink, pool=None, convout=None):
     ev = bool(S.get("eval"))
     side = _side_stream(g_out.device) if _WGRAD_SIDE and g_out.is_cuda else None
 
+    # (reduce_side: the caller joins the reduce stream, join_wgrad_reduces)
+    rs = reduce_stream(x1.device) if reduce_side and side is None and x1.is_cuda else None
+
     def wgrad(*args, **kw):
         # every operand stays referenced in this frame until the join below
         if side is None:
-            ops.wgrad(*args, **kw)
+            ops.wgrad(*args, reduce_stream=rs, **kw)
             return
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -816,7 +844,34 @@ _RECOMPUTE_MASK = os.environ.get("RR_BN_RECOMPUTE_MASK", "1") != "0"
 # block's gradients are declared ready).  Off: measured 29.2k vs 29.4k img/s
 # (same-box A/B) -- the concurrent kernels contend for the CUs and L2.
 _WGRAD_SIDE = os.environ.get("RR_WGRAD_SIDE_STREAM", "0") != "0"
+# A/B switch: the weight grads' split-K reduces (rr_wgrad_reduce) and the
+# convT bias sums on a side stream -- nothing in the backward reads them, so
+# they run beside the next dgrad instead of between it and its producer;
+# joined where the gradients are read (join_wgrad_reduces: the end of the
+# backward, each data-parallel bucket).  Off: the graph step measured 2.2 %
+# slower with it (14.52 vs 14.21 ms, 3 interleaved rounds,
+# profiles/r5u_abstep_reduce_side.txt) -- the reduce workgroups take CUs the
+# next dgrad's one-per-CU tiles are waiting for
+_WGRAD_REDUCE_SIDE = os.environ.get("RR_WGRAD_REDUCE_SIDE", "0") != "0"
 _SIDE = {}
+_REDUCE_SIDE = {}
+
+
+def reduce_stream(device):
+    """the stream the weight-grad reduces fork onto (one per device)"""
+    s = _REDUCE_SIDE.get(device)
+    if s is None:
+        s = _REDUCE_SIDE[device] = torch.cuda.Stream(device)
+    return s
+
+
+def join_wgrad_reduces(stream=None, device=None):
+    """``stream`` (default: the current one) waits for every weight-grad
+    reduce forked so far"""
+    for dev, s in _REDUCE_SIDE.items():
+        if device is not None and dev != device:
+            continue
+        (stream or torch.cuda.current_stream(dev)).wait_stream(s)
 _PACK_SIDE = {}
 
 
@@ -839,37 +894,39 @@ def resunet_backward(m, S, g_out, sink):
     n = S.n
     (H, W), (H2, W2), (H3, W3), (H4, W4) = S.sizes
     al1, al2, al3 = S.aligned
+    sd = _WGRAD_REDUCE_SIDE and g_out.is_cuda
     # the final conv's backward runs inside dec1's (fused with its tail BN reduce)
-    g_u1, g_r1 = resblock_backward(m.dec1, S.dec1, None, sink, convout=(m.final, g_out))
+    g_u1, g_r1 = resblock_backward(m.dec1, S.dec1, None, sink, convout=(m.final, g_out),
+                                   reduce_side=sd)
     if al1:
         g_u1 = ops.nearest_resize_bwd(g_u1, 2 * H2, 2 * W2)
-    g_d2 = _convT_bwd(m.up1, S.pku1, g_u1, S.d2, n, H2, W2, sink)
+    g_d2 = _convT_bwd(m.up1, S.pku1, g_u1, S.d2, n, H2, W2, sink, side=sd)
     sink.ready(_params(m.up1))
-    g_u2, g_r2 = resblock_backward(m.dec2, S.dec2, g_d2, sink)
+    g_u2, g_r2 = resblock_backward(m.dec2, S.dec2, g_d2, sink, reduce_side=sd)
     if al2:
         g_u2 = ops.nearest_resize_bwd(g_u2, 2 * H3, 2 * W3)
-    g_d3 = _convT_bwd(m.up2, S.pku2, g_u2, S.d3, n, H3, W3, sink)
+    g_d3 = _convT_bwd(m.up2, S.pku2, g_u2, S.d3, n, H3, W3, sink, side=sd)
     sink.ready(_params(m.up2))
-    g_u3, g_r3 = resblock_backward(m.dec3, S.dec3, g_d3, sink)
+    g_u3, g_r3 = resblock_backward(m.dec3, S.dec3, g_d3, sink, reduce_side=sd)
     if al3:
         g_u3 = ops.nearest_resize_bwd(g_u3, 2 * H4, 2 * W4)
-    g_b = _convT_bwd(m.up3, S.pku3, g_u3, S.b, n, H4, W4, sink)
+    g_b = _convT_bwd(m.up3, S.pku3, g_u3, S.b, n, H4, W4, sink, side=sd)
     sink.ready(_params(m.up3))
     for i in (2, 1, 0):
-        g_b, _ = resblock_backward(m.bottleneck[i], S[f"bottleneck.{i}"], g_b, sink)
+        g_b, _ = resblock_backward(m.bottleneck[i], S[f"bottleneck.{i}"], g_b, sink, reduce_side=sd)
     if _FUSED_POOL_BWD and g_b.dtype == torch.bfloat16 and H % 8 == 0 and W % 8 == 0:
         # each encoder block's output fed the skip concat and the pool: the
         # pool backward runs inside that block's tail BN backward
-        g_p2, _ = resblock_backward(m.res3, S.res3, g_r3, sink, pool=(g_b, S.i3))
-        g_p1, _ = resblock_backward(m.res2, S.res2, g_r2, sink, pool=(g_p2, S.i2))
-        g_e1, _ = resblock_backward(m.res1, S.res1, g_r1, sink, pool=(g_p1, S.i1))
+        g_p2, _ = resblock_backward(m.res3, S.res3, g_r3, sink, pool=(g_b, S.i3), reduce_side=sd)
+        g_p1, _ = resblock_backward(m.res2, S.res2, g_r2, sink, pool=(g_p2, S.i2), reduce_side=sd)
+        g_e1, _ = resblock_backward(m.res1, S.res1, g_r1, sink, pool=(g_p1, S.i1), reduce_side=sd)
     else:
         ops.maxpool2_bwd(g_b, S.i3, H3, W3, out=g_r3, accumulate=True)
-        g_p2, _ = resblock_backward(m.res3, S.res3, g_r3, sink)
+        g_p2, _ = resblock_backward(m.res3, S.res3, g_r3, sink, reduce_side=sd)
         ops.maxpool2_bwd(g_p2, S.i2, H2, W2, out=g_r2, accumulate=True)
-        g_p1, _ = resblock_backward(m.res2, S.res2, g_r2, sink)
+        g_p1, _ = resblock_backward(m.res2, S.res2, g_r2, sink, reduce_side=sd)
         ops.maxpool2_bwd(g_p1, S.i1, H, W, out=g_r1, accumulate=True)
-        g_e1, _ = resblock_backward(m.res1, S.res1, g_r1, sink)
+        g_e1, _ = resblock_backward(m.res1, S.res1, g_r1, sink, reduce_side=sd)
     pr = m.enc1[1]
     if g_e1.dtype == torch.bfloat16 and W % 8 == 0 and _FUSED_FIRST_WGRAD:
         # PReLU backward + first-conv wgrad in one pass over the image
@@ -879,6 +936,8 @@ def resunet_backward(m, S, g_out, sink):
         g_e1pre, _ = ops.prelu_bwd(g_e1, S.e1pre, pr.weight, dalpha=sink[pr.weight])
         ops.first_conv_wgrad(ops.im2col3(S.x, g_e1pre.dtype), g_e1pre, sink[m.enc1[0].weight],
                              sink[m.enc1[0].bias])
+    if sd:
+        join_wgrad_reduces(device=g_out.device)
     sink.ready(_params(m.enc1))
 
 

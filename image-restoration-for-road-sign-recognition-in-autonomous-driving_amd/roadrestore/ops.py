@@ -224,8 +224,13 @@ def igemm(mode, x1, x2, n, h, w, wpack, cout, bias=None, act=0, out=None, out2=N
     return out, out2, st
 
 
-def wgrad(mode, dy, x1, x2, n, h, w, cout, dw=None, accumulate=False, dw_shape=None):
-    """Weight grad (fp32, torch layout) of a conv / convT; see rr_wgrad."""
+def wgrad(mode, dy, x1, x2, n, h, w, cout, dw=None, accumulate=False, dw_shape=None,
+          reduce_stream=None):
+    """Weight grad (fp32, torch layout) of a conv / convT; see rr_wgrad.
+
+    ``reduce_stream``: the split-K reduce (rr_wgrad_reduce) runs there, after
+    the partial launch (rr_wgrad_partial) on the current stream; ``dw`` is
+    final once ``reduce_stream`` is joined."""
     _need_cuda(dy, x1)
     c1 = x1.shape[-1]
     c2 = x2.shape[-1] if x2 is not None else 0
@@ -236,8 +241,17 @@ def wgrad(mode, dy, x1, x2, n, h, w, cout, dw=None, accumulate=False, dw_shape=N
     ws = _ws(need, dy.device)
 
     def launch():
-        lib().check(lib().rr_wgrad(C.byref(d), _p(dy), _p(x1), _p(x2), _p(dw), _p(ws),
-                                   ws.numel(), stream()), "rr_wgrad")
+        if reduce_stream is None:
+            lib().check(lib().rr_wgrad(C.byref(d), _p(dy), _p(x1), _p(x2), _p(dw), _p(ws),
+                                       ws.numel(), stream()), "rr_wgrad")
+            return
+        lib().check(lib().rr_wgrad_partial(C.byref(d), _p(dy), _p(x1), _p(x2), _p(ws),
+                                           ws.numel(), stream()), "rr_wgrad_partial")
+        reduce_stream.wait_stream(torch.cuda.current_stream(dy.device))
+        with torch.cuda.stream(reduce_stream):
+            lib().check(lib().rr_wgrad_reduce(C.byref(d), _p(ws), ws.numel(), _p(dw),
+                                              reduce_stream.cuda_stream), "rr_wgrad_reduce")
+        ws.record_stream(reduce_stream)
     taps = 9 if mode == RR_CONV3X3 else (4 if mode == RR_CONVT_UP else 1)
     convT = mode == RR_CONVT_UP
     CA = c1 if convT else cout

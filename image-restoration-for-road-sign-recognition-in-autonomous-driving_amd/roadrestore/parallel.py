@@ -30,6 +30,8 @@ import os
 import torch
 import torch.distributed as dist
 
+from . import engine
+
 
 class _UniqueId(ctypes.Structure):
     _fields_ = [("internal", ctypes.c_char * 128)]     # NCCL_UNIQUE_ID_BYTES
@@ -197,14 +199,20 @@ class DataParallel:
             self.finish()
 
     def _reduce(self, view):
+        # the bucket's weight grads are final once the weight-grad reduces
+        # forked onto the reduce stream so far have run (engine.reduce_stream)
         if self.rccl is not None:
             self.comm_stream.wait_stream(torch.cuda.current_stream())
+            engine.join_wgrad_reduces(self.comm_stream)
             self.rccl.all_reduce_(view, self.comm_stream)   # joined in finish()
         elif self.comm_stream is not None:
             self.comm_stream.wait_stream(torch.cuda.current_stream())
+            engine.join_wgrad_reduces(self.comm_stream)
             with torch.cuda.stream(self.comm_stream):
                 self._pending.append(dist.all_reduce(view, group=self.pg, async_op=True))
         else:
+            if view.is_cuda:
+                engine.join_wgrad_reduces()
             self._pending.append(dist.all_reduce(view, group=self.pg, async_op=True))
 
     def finish(self):

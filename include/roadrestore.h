@@ -177,6 +177,15 @@ const char *rr_wgrad_kernel_name(const rr_wgrad_desc *d);
 int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
              const void *x2, float *dw, void *ws, size_t ws_bytes,
              rr_stream stream);
+/* rr_wgrad in its two launches: the weight-grad kernel writing the split
+ * partials into ws, and the fixed-order reduce of ws into dw (same result as
+ * rr_wgrad, bitwise).  The reduce may run on another stream once the partial
+ * launch has completed there (the training step puts it beside the next
+ * dgrad, off the critical path). */
+int rr_wgrad_partial(const rr_wgrad_desc *d, const void *dy, const void *x1,
+                     const void *x2, void *ws, size_t ws_bytes, rr_stream stream);
+int rr_wgrad_reduce(const rr_wgrad_desc *d, const void *ws, size_t ws_bytes, float *dw,
+                    rr_stream stream);
 
 /* weight packing (fp32 torch layout -> compute layout/dtype) */
 /* conv [co][ci][k][k] -> fwd [co][k*k][ci] and dgrad [ci][k*k flipped][co].
