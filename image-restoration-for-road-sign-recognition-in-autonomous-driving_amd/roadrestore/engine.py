@@ -271,6 +271,8 @@ class GradSink:
 
 
 
+_DIAG_SKIP_A1 = os.environ.get("RR_DIAG_SKIP_A1", "0") != "0"
+
 # A/B switch for the fused conv-dgrad + BN/PReLU backward reduce (default on)
 FUSE_BNBWD = os.environ.get("RR_FUSE_BNBWD", "1") not in ("0", "")
 
@@ -522,7 +524,10 @@ def resblock_forward(blk, x1, x2, n, h, w, wc, dt, training, need_bwd, pool=Fals
     pk1 = wc.conv(c1.weight, dt, dgrad=need_bwd)
     t1, _, st1 = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, pk1[0], cout, bias=c1.bias, stats=training)
     s1, sh1, m1, i1 = _bn_affine(bn1, st1, c1.bias, P, training, need_bwd=need_bwd)
-    a1 = ops.affine_act(t1, s1, sh1, alpha=pr.weight)
+    # (diagnostic, timing only -- results are wrong: RR_DIAG_SKIP_A1=1 feeds
+    # t1 to conv2 without the BN1 + PReLU pass, the upper bound of folding
+    # that pass into conv2's operand loads)
+    a1 = t1 if _DIAG_SKIP_A1 else ops.affine_act(t1, s1, sh1, alpha=pr.weight)
     pk2 = wc.conv(c2.weight, dt, dgrad=need_bwd)
     t2, _, st2 = ops.igemm(RR_CONV3X3, a1, None, n, h, w, pk2[0], cout, bias=c2.bias, stats=training)
     has_sc = block_has_shortcut(blk)

@@ -51,6 +51,14 @@ def main():
              "maxpool_us": timed(lambda: ops.maxpool2_fwd(y)),
              "fused_us": timed(lambda: ops.igemm_pool(x, n, h, h, pk, c, bias=b)),
              "fused_noidx_us": timed(lambda: ops.igemm_pool(x, n, h, h, pk, c, bias=b, want_idx=False))}
+        if h == 64:
+            # stream3's 256-pixel-step pool instance (RR_S3_POOL_MP=4, A/B)
+            os.environ["RR_S3_POOL_MP"] = "4"
+            r["fused_mp4_us"] = timed(lambda: ops.igemm_pool(x, n, h, h, pk, c, bias=b))
+            y4, i4 = ops.igemm_pool(x, n, h, h, pk, c, bias=b)
+            del os.environ["RR_S3_POOL_MP"]
+            y2, i2 = ops.igemm_pool(x, n, h, h, pk, c, bias=b)
+            r["mp4_equal"] = bool(torch.equal(y4, y2) and torch.equal(i4, i2))
         print(json.dumps(r), flush=True)
 
 
