@@ -410,10 +410,15 @@ __device__ __forceinline__ void bwd_gm8(const BnBwd &a, long long e, const float
   }
 }
 
-template <typename T, int MASK, int NBN>
+// GMO: gm (the masked upstream grad) is also stored, rounded to T, and the
+// sums are taken over the stored values -- the apply then reads gm alone
+// (rr_bn_bwd_reduce_gm: the identity-shortcut tail, whose gm is the block's
+// input grad anyway)
+template <typename T, int MASK, int NBN, bool GMO = false>
 __global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwd a, float *__restrict__ part,
                                                              float *__restrict__ apart,
-                                                             long long rows_per_block) {
+                                                             long long rows_per_block,
+                                                             T *__restrict__ gmo = nullptr) {
   extern __shared__ __attribute__((aligned(16))) float sm[];   // [R][C][3] + [256]
   const int TPR = a.C / 8;
   const int R = 256 / TPR;
@@ -451,6 +456,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwd a, float *__r
       t1[4] = u1[0]; t1[5] = u1[1]; t1[6] = u1[2]; t1[7] = u1[3];
     }
     bwd_gm8<T, MASK>(a, e, s8, b8, al, gm, asum, t0, t1, sB, bB);
+    if constexpr (GMO) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gm[k] = Elt<T>::round(gm[k]);
+      store8<T>(gmo + e, f32x4{gm[0], gm[1], gm[2], gm[3]}, f32x4{gm[4], gm[5], gm[6], gm[7]});
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       s[0][k] += gm[k];
@@ -1055,6 +1065,31 @@ extern "C" int rr_bn_bwd_reduce(const rr_bnbwd_desc *d, const void *g, const voi
   else
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, dim3(blocks), dim3(256), shm, st, a, partial,
                        d->mask_kind == 2 ? apart : nullptr, rpb);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+extern "C" int rr_bn_bwd_reduce_gm(const rr_bnbwd_desc *d, const void *g, const void *aux,
+                                   const void *t0, const float *mean0, const float *invstd0,
+                                   float *partial, void *gm_out, rr_stream stream) {
+  int rc = bnbwd_check(d);
+  if (rc) return rc;
+  if (!g || !aux || !t0 || !mean0 || !invstd0 || !partial || !gm_out) return RR_EINVAL;
+  if (d->nbn != 1 || (d->mask_kind != 1 && d->mask_kind != 3) || d->C % 8 || 256 % (d->C / 8))
+    return RR_EUNSUPPORTED;
+  const BnBwd a = make_bnbwd(d, g, aux, nullptr, nullptr, nullptr, t0, mean0, invstd0, nullptr,
+                             nullptr, nullptr);
+  const int blocks = reduce_blocks(d->P);
+  const long long rpb = (d->P + blocks - 1) / blocks;
+  const size_t shm8 = ((size_t)(256 / (d->C / 8)) * d->C * 3 + 256) * sizeof(float);
+  hipStream_t st = (hipStream_t)stream;
+#define RR_REDGM(TT, M) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<TT, M, 1, true>), dim3(blocks), dim3(256), shm8, st, a, partial, nullptr, rpb, (TT *)gm_out)
+  if (d->dtype == RR_BF16) {
+    if (d->mask_kind == 1) RR_REDGM(bf16_t, 1); else RR_REDGM(bf16_t, 3);
+  } else {
+    if (d->mask_kind == 1) RR_REDGM(float, 1); else RR_REDGM(float, 3);
+  }
+#undef RR_REDGM
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

@@ -61,7 +61,9 @@ enum : int { E_NONE = 0, E_ACC = 1, E_MASK = 2 };
 
 template <int MC, int KB, bool STATS, int MODE, bool NCHW, int EOP>
 __global__ __launch_bounds__(256, 2) void stream1_kernel(S1Args a) {
-  constexpr int D0 = KB <= 2 ? 4 : (KB <= 4 ? 3 : (KB <= 8 ? 2 : 1));
+  // (KB = 12 with the statistics registers keeps 1 block in flight: 2 spill
+  // 54 VGPRs)
+  constexpr int D0 = KB <= 2 ? 4 : (KB <= 4 ? 3 : (KB <= 8 || !STATS ? 2 : 1));
   constexpr int D = (EOP != E_NONE && MC >= 8) ? 2 : D0;
   constexpr int CW = 16 * MC;
   constexpr int NQ = MC / 2 > 0 ? MC / 2 : 1;

@@ -100,6 +100,7 @@ _SIGS = {
     "rr_bn_bwd_blocks": (I_, [C.POINTER(BnBwdDesc)]),
     "rr_bn_bwd_reduce": (I_, [C.POINTER(BnBwdDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_, P_, P_,
                               P_, P_]),
+    "rr_bn_bwd_reduce_gm": (I_, [C.POINTER(BnBwdDesc), P_, P_, P_, P_, P_, P_, P_, P_]),
     "rr_bn_bwd_finalize": (I_, [C.POINTER(BnBwdDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_, P_,
                                 P_, P_]),
     "rr_bn_bwd_finalize_rows_workspace": (S_, [I_, I_]),

@@ -9,6 +9,7 @@ CPU fallback: a missing library or device raises.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -415,6 +416,11 @@ def affine_act_pool(x, scale, shift, res=None, res_scale=None, res_shift=None, r
     return y, yp, idx
 
 
+# A/B switch: the identity-shortcut tail's BN backward stores gm in its
+# reduce and applies from it (rr_bn_bwd_reduce_gm); 0: gm from the apply
+_BN_GM_IN_REDUCE = os.environ.get("RR_BN_GM_IN_REDUCE", "1") != "0"
+
+
 def bn_backward(g, t0, mean0, inv0, gamma0, *, mask_kind=0, aux=None, aff_s=None, aff_b=None,
                 alpha=None, t1=None, mean1=None, inv1=None, gamma1=None, want_gm=False,
                 gm_out=None, outs=None, pool=None, recompute=None, eval_mode=False, dbias=None):
@@ -450,9 +456,20 @@ def bn_backward(g, t0, mean0, inv0, gamma0, *, mask_kind=0, aux=None, aff_s=None
     blocks = lib().rr_bn_bwd_blocks(C.byref(d))
     part = torch.empty(blocks * Cc * 3 + blocks, dtype=torch.float32, device=dev)
     s = stream()
-    lib().check(lib().rr_bn_bwd_reduce(C.byref(d), _p(g), _p(aux), _p(aff_s), _p(aff_b), _p(alpha),
-                                       _p(t0), _p(mean0), _p(inv0), _p(t1), _p(mean1), _p(inv1),
-                                       _p(part), s), "rr_bn_bwd_reduce")
+    # the identity-shortcut tail (gm is the block's input grad): the reduce
+    # stores gm and the apply reads it alone (rr_bn_bwd_reduce_gm)
+    gm_first = (_BN_GM_IN_REDUCE and (want_gm or gm_out is not None) and nbn == 1 and
+                d.mask_kind in (1, 3) and Cc % 8 == 0 and 256 % (Cc // 8) == 0)
+    if gm_first:
+        if gm_out is None:
+            gm_out = torch.empty_like(g)
+        lib().check(lib().rr_bn_bwd_reduce_gm(C.byref(d), _p(g), _p(aux), _p(t0), _p(mean0),
+                                              _p(inv0), _p(part), _p(gm_out), s),
+                    "rr_bn_bwd_reduce_gm")
+    else:
+        lib().check(lib().rr_bn_bwd_reduce(C.byref(d), _p(g), _p(aux), _p(aff_s), _p(aff_b),
+                                           _p(alpha), _p(t0), _p(mean0), _p(inv0), _p(t1),
+                                           _p(mean1), _p(inv1), _p(part), s), "rr_bn_bwd_reduce")
     o = outs or {}
     dg0 = o.get("dgamma0")
     if dg0 is None:
@@ -475,6 +492,14 @@ def bn_backward(g, t0, mean0, inv0, gamma0, *, mask_kind=0, aux=None, aff_s=None
                                          _p(coef), s), "rr_bn_bwd_finalize")
     dt0 = torch.empty_like(g)
     dt1 = torch.empty_like(g) if nbn == 2 else None
+    if gm_first:
+        da = BnBwdDesc(d.dtype, P, Cc, 0, 1, 0, 0, None, None)
+        _set_eval(da, eval_mode, dbias)
+        lib().check(lib().rr_bn_bwd_apply(C.byref(da), _p(gm_out), None, None, None, None,
+                                          _p(t0), _p(mean0), _p(inv0), None, None, None,
+                                          _p(coef), _p(dt0), None, None, s), "rr_bn_bwd_apply")
+        return dict(dt0=dt0, dt1=None, gm=gm_out, dgamma0=dg0, dbeta0=db0, dgamma1=dg1,
+                    dbeta1=db1, dalpha=dal)
     if want_gm and gm_out is None:
         gm_out = torch.empty_like(g)
     lib().check(lib().rr_bn_bwd_apply(C.byref(d), _p(g), _p(aux), _p(aff_s), _p(aff_b), _p(alpha),

@@ -324,6 +324,16 @@ int rr_bn_bwd_reduce(const rr_bnbwd_desc *d, const void *g, const void *aux,
                      const void *t0, const float *mean0, const float *invstd0,
                      const void *t1, const float *mean1, const float *invstd1,
                      float *partial, rr_stream stream);
+/* rr_bn_bwd_reduce for one BN behind a ReLU-masked identity residual tail
+ * (mask_kind 1, or 3 with the 2x2 max-pool backward; C % 8 == 0 and C / 8
+ * divides 256) that also stores gm = the masked upstream grad, rounded to the
+ * dtype -- the residual branch's input grad (ResidualBlock without a shortcut
+ * conv, 14:110-115) -- and sums the stored values.  The apply then reads gm
+ * alone (rr_bn_bwd_apply with mask_kind 0, g = gm) instead of the upstream
+ * grad, the pooled grad, its window index and the block output again. */
+int rr_bn_bwd_reduce_gm(const rr_bnbwd_desc *d, const void *g, const void *aux,
+                        const void *t0, const float *mean0, const float *invstd0,
+                        float *partial, void *gm_out, rr_stream stream);
 /* finalize: dgamma/dbeta (fp32, written) and the per-channel coefficients */
 int rr_bn_bwd_finalize(const rr_bnbwd_desc *d, const float *partial,
                        const float *gamma0, const float *invstd0,

@@ -629,6 +629,46 @@ def test_bn_backward_pool_fused(dev, dt, nbn):
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("pool", [False, True])
+@pytest.mark.parametrize("C", [64, 512])
+def test_bn_backward_gm_in_reduce(dev, dt, pool, C, monkeypatch):
+    """identity-shortcut tail (one BN, gm wanted): the reduce that stores gm
+    (rr_bn_bwd_reduce_gm) + the apply from gm alone == the apply that forms
+    gm itself -- gm bit for bit, the rest within the rounding of gm to the
+    storage dtype (fp32: to rounding); checked against fp64 torch too"""
+    from roadrestore import ops
+    n, h, w = 2, 8, 12
+    g = rnd(n, h, w, C, seed=41).to(dev, dt)
+    out = rnd(n, h, w, C, seed=42).to(dev, dt)
+    t0 = rnd(n, h, w, C, seed=43).to(dev, dt)
+    m0, i0 = rnd(C, seed=44).to(dev), (rnd(C, seed=45).abs() + 0.5).to(dev)
+    gam0 = rnd(C, seed=46).to(dev)
+    pl = None
+    if pool:
+        _, idx = ops.maxpool2_fwd(out)
+        pl = (rnd(n, h // 2, w // 2, C, seed=47).to(dev, dt), idx)
+    kw = dict(mask_kind=1, aux=out, want_gm=True, pool=pl)
+    monkeypatch.setattr(ops, "_BN_GM_IN_REDUCE", False)
+    ref = ops.bn_backward(g, t0, m0, i0, gam0, **kw)
+    monkeypatch.setattr(ops, "_BN_GM_IN_REDUCE", True)
+    got = ops.bn_backward(g, t0, m0, i0, gam0, **kw)
+    assert torch.equal(got["gm"], ref["gm"])
+    tol = 1e-5 if dt == torch.float32 else 1e-2
+    for k in ("dt0", "dgamma0", "dbeta0"):
+        a, b = got[k].float(), ref[k].float()
+        rel = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+        assert rel <= tol, (k, rel)
+    # fp64: dt = gamma inv (gm - mean(gm) - xhat mean(gm xhat)) on the stored gm
+    gm = got["gm"].double()
+    xh = (t0.double() - m0.double()) * i0.double()
+    P = n * h * w
+    dt_ref = gam0.double() * i0.double() * (gm - gm.sum((0, 1, 2)) / P -
+                                            xh * (gm * xh).sum((0, 1, 2)) / P)
+    rel = ((got["dt0"].double() - dt_ref).norm() / dt_ref.norm()).item()
+    assert rel <= (1e-5 if dt == torch.float32 else 1e-2), rel
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("pool", [False, True])
 @pytest.mark.parametrize("C", [64, 256])
 def test_bn_backward_recomputed_mask(dev, dt, pool, C):
     """mask kind 4 / 5: the BN-shortcut tail's ReLU mask recomputed from t0,
