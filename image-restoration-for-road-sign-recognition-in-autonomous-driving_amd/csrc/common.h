@@ -128,12 +128,22 @@ __device__ __forceinline__ uint32_t xor1_u32(uint32_t v) {
 // MaxPool2d(2, 2) of one window in window order (0,0) (0,1) (1,0) (1,1):
 // the value and the index of its FIRST occurrence (nn.MaxPool2d's routing of
 // the backward), a NaN replacing a number (maxpool_fwd8_kernel's rule)
+// take v over the running max m when v > m, or v is NaN and m is not:
+// !(v <= m) is "v > m or either is NaN", and m == m excludes a NaN m -- the
+// same truth table as (v > m || (v != v && m == m)) without the short-circuit,
+// so it compiles to compares + v_cndmask instead of exec-mask branches (the
+// branchy form cost ~14 instructions per window element in the pool
+// epilogues)
 __device__ __forceinline__ float pool4_first_max(float v0, float v1, float v2, float v3, uint32_t &id) {
   float m = v0;
-  id = 0;
-  if (v1 > m || (v1 != v1 && m == m)) { m = v1; id = 1; }
-  if (v2 > m || (v2 != v2 && m == m)) { m = v2; id = 2; }
-  if (v3 > m || (v3 != v3 && m == m)) { m = v3; id = 3; }
+  uint32_t k = 0;
+  bool t = !(v1 <= m) & (m == m);
+  m = t ? v1 : m; k = t ? 1u : k;
+  t = !(v2 <= m) & (m == m);
+  m = t ? v2 : m; k = t ? 2u : k;
+  t = !(v3 <= m) & (m == m);
+  m = t ? v3 : m; k = t ? 3u : k;
+  id = k;
   return m;
 }
 

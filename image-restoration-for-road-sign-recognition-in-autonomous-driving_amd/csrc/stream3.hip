@@ -1023,8 +1023,11 @@ int stream3_launch_pool(const rr_igemm_desc *d, const S3Args &a0, hipStream_t st
   S3Args a = a0;
   a.wld = 64; a.woff = 0;
   const int P = d->n * d->h * d->w;
-  // 128-pixel steps, no stagger: the bias + ReLU forward's form (launch_w);
-  // RR_S3_POOL_MP=4 (A/B): 256-pixel steps (4 rows, 2 row pairs) at W = 64
+  // 128-pixel steps, no stagger: the bias + ReLU forward's form (launch_w).
+  // RR_S3_POOL_MP=4 (A/B): 256-pixel steps (4 rows, 2 row pairs) at W = 64,
+  // bitwise equal and within the run order's noise (174 / 162 us measured
+  // first / second on one box, 179 / 178 us in the reverse order on another,
+  // profiles/r5zi_pool_bench.jsonl, r5zj_pool_bench.jsonl)
   const char *emp = getenv("RR_S3_POOL_MP");
   const bool mp4 = emp && atoi(emp) == 4;
   if (d->w == 64 && mp4) {

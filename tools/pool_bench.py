@@ -52,7 +52,8 @@ def main():
              "fused_us": timed(lambda: ops.igemm_pool(x, n, h, h, pk, c, bias=b)),
              "fused_noidx_us": timed(lambda: ops.igemm_pool(x, n, h, h, pk, c, bias=b, want_idx=False))}
         if h == 64:
-            # stream3's 256-pixel-step pool instance (RR_S3_POOL_MP=4, A/B)
+            # stream3's pool in the other step size (RR_S3_POOL_MP=2 / 4, A/B;
+            # the default is 128-pixel steps)
             os.environ["RR_S3_POOL_MP"] = "4"
             r["fused_mp4_us"] = timed(lambda: ops.igemm_pool(x, n, h, h, pk, c, bias=b))
             y4, i4 = ops.igemm_pool(x, n, h, h, pk, c, bias=b)
