@@ -287,7 +287,12 @@ __global__ void affine_act_pool_kernel(int n, int h, int w, int C, const T *__re
         Elt<T>::store(rt, j, vv[j]);
         const float sv = Elt<T>::load(rt, j);
         if (k == 0) { m[j] = sv; id[j] = 0; }
-        else if (sv > m[j] || (sv != sv && m[j] == m[j])) { m[j] = sv; id[j] = (uint8_t)k; }
+        else {
+          // branch-free first max (pool4_first_max's form: compares + selects)
+          const bool t = !(sv <= m[j]) & (m[j] == m[j]);
+          m[j] = t ? sv : m[j];
+          id[j] = t ? (uint8_t)k : id[j];
+        }
       }
     }
     store8<T>(yp + op * C + c, f32x4{m[0], m[1], m[2], m[3]}, f32x4{m[4], m[5], m[6], m[7]});

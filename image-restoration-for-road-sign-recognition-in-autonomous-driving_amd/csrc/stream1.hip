@@ -68,7 +68,11 @@ __global__ __launch_bounds__(256, 2) void stream1_kernel(S1Args a) {
   constexpr int CW = 16 * MC;
   constexpr int NQ = MC / 2 > 0 ? MC / 2 : 1;
   const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
+  // wave-uniform in SGPRs: the block loop's bounds and the epilogue's flag
+  // tests then branch on scalars instead of exec masks
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int flags = __builtin_amdgcn_readfirstlane(a.flags);
+  const bool fbias = (flags & G_BIAS) != 0, frelu = (flags & G_RELU) != 0;
   const int g = blockIdx.x % a.G, slice = blockIdx.x / a.G;
   const int gw = g * S1_NW + wv;                // wave within the slice
   const int NWT = a.G * S1_NW;
@@ -78,7 +82,7 @@ __global__ __launch_bounds__(256, 2) void stream1_kernel(S1Args a) {
 
   __shared__ __attribute__((aligned(16))) float sbias[CW];
   for (int c = threadIdx.x; c < CW; c += 256)
-    sbias[c] = (a.flags & G_BIAS) && cbase + c < a.cout ? a.bias[cbase + c] : 0.f;
+    sbias[c] = fbias && cbase + c < a.cout ? a.bias[cbase + c] : 0.f;
 
   // ---- A fragments: GEMM column cbase + mi*16 + frow, k = kb*32 + fq*8 ----
   bf16x8 wr[MC][KB];
@@ -175,7 +179,7 @@ __global__ __launch_bounds__(256, 2) void stream1_kernel(S1Args a) {
           const int c = cbase + mi * 16 + fq * 4 + j;
           if (c < a.cout) {
             float v = acc[mi][j] + sbias[c - cbase];
-            if (a.flags & G_RELU) v = fmaxf(v, 0.f);
+            if (frelu) v = fmaxf(v, 0.f);
             yo[((long long)n * a.cout + c) * a.hw + rem] = v;
           }
         }
@@ -198,7 +202,7 @@ __global__ __launch_bounds__(256, 2) void stream1_kernel(S1Args a) {
       }
       const int c = col_of(q);
       f32x4 v0 = f32x4{lo[0], lo[1], lo[2], lo[3]}, v1 = f32x4{hi[0], hi[1], hi[2], hi[3]};
-      if (a.flags & G_BIAS) {
+      if (fbias) {
         v0 += *reinterpret_cast<const f32x4 *>(sbias + (c - cbase));
         v1 += *reinterpret_cast<const f32x4 *>(sbias + (c - cbase) + 4);
       }
@@ -206,7 +210,7 @@ __global__ __launch_bounds__(256, 2) void stream1_kernel(S1Args a) {
         v0 += unpack_lo(bk.e[q]);
         v1 += unpack_hi(bk.e[q]);
       }
-      if (a.flags & G_RELU) {
+      if (frelu) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) { v0[j] = fmaxf(v0[j], 0.f); v1[j] = fmaxf(v1[j], 0.f); }
       }
