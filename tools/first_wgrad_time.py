@@ -1,7 +1,8 @@
-"""Kernel time of the fused first-conv backward (rr_conv_in_wgrad_act: PReLU
-backward + 3->64 weight grad from the image) at the cfg3 shape (B = 512, 64x64,
-bf16), HIP events over 20 launches, median of 5, plus a SHA-1 of (dw, db,
-dalpha) for a bitwise comparison of two builds.
+"""Kernel times of the first conv at the cfg3 shape (B = 512, 64x64, bf16):
+the fused backward (rr_conv_in_wgrad_act: PReLU backward + 3->64 weight grad
+from the image) and the forward (rr_conv_in_mfma: conv + bias + PReLU, both
+outputs), HIP events over 20 launches, median of 5, plus SHA-1s of the
+outputs for a bitwise comparison of two builds.
 
     python tools/first_wgrad_time.py [other.so]   # alternates this build / other, 3 rounds"""
 import hashlib
@@ -29,25 +30,37 @@ def child():
     db = torch.empty(64, device=dev)
     da = torch.empty(1, device=dev)
 
-    def f():
-        ops.first_conv_wgrad_act(x, g, t, 2, alpha, dw, db, dalpha=da)
-    for _ in range(3):
-        f()
-    torch.cuda.synchronize()
-    res = []
-    for _ in range(5):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(20):
+    def timed(f):
+        for _ in range(3):
             f()
-        e.record()
         torch.cuda.synchronize()
-        res.append(s.elapsed_time(e) / 20 * 1e3)
-    h = hashlib.sha1()
-    for v in (dw, db, da):
-        h.update(v.cpu().numpy().tobytes())
-    print(json.dumps({"lib": os.environ.get("RR_LIB_PATH", "cur"), "us": round(statistics.median(res), 1),
-                      "sha": h.hexdigest()[:12]}), flush=True)
+        res = []
+        for _ in range(5):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(20):
+                f()
+            e.record()
+            torch.cuda.synchronize()
+            res.append(s.elapsed_time(e) / 20 * 1e3)
+        return round(statistics.median(res), 1)
+
+    def sha(*ts):
+        h = hashlib.sha1()
+        for v in ts:
+            h.update(v.float().cpu().numpy().tobytes())
+        return h.hexdigest()[:12]
+    us = timed(lambda: ops.first_conv_wgrad_act(x, g, t, 2, alpha, dw, db, dalpha=da))
+    w1 = torch.randn(64, 3, 3, 3, device=dev, generator=g0) * 0.2
+    b1 = torch.randn(64, device=dev, generator=g0) * 0.1
+    wp = ops.pack_conv_in(w1, b1, torch.bfloat16)
+    out = {}
+
+    def fwd():
+        out["y"] = ops.first_conv_fwd(x, w1, b1, torch.bfloat16, wp, act=2, alpha=alpha, want_pre=True)
+    us_f = timed(fwd)
+    print(json.dumps({"lib": os.environ.get("RR_LIB_PATH", "cur"), "wgrad_us": us, "sha": sha(dw, db, da),
+                      "fwd_us": us_f, "fwd_sha": sha(*out["y"])}), flush=True)
 
 
 def main():
