@@ -163,6 +163,31 @@ def test_wgrad(dev, dt, k):
     close(dw.cpu(), wt.grad, dt, scale=wt.grad.abs().max().item())
 
 
+@pytest.mark.parametrize("shape", [(3, 3, 12, 10, 128, 64), (1, 3, 16, 16, 64, 128), (1, 3, 64, 64, 64, 64),
+                                   (1, 1, 32, 32, 64, 64), (2, 2, 8, 8, 128, 64)])
+def test_wgrad_partial_reduce_on_another_stream(dev, shape):
+    """rr_wgrad_partial + rr_wgrad_reduce, the reduce on a side stream
+    (ops.wgrad(reduce_stream=...)), == rr_wgrad bit for bit, accumulate too
+    (swgrad, halo, tiled and convT kernels)"""
+    import roadrestore as rr
+    from roadrestore._lib import RR_CONV1X1, RR_CONV3X3, RR_CONVT_UP
+    n, k, h, w, cin, cout = shape
+    mode = {3: RR_CONV3X3, 1: RR_CONV1X1, 2: RR_CONVT_UP}[k]
+    x = nhwc(rnd(n, cin, h, w, seed=61), dev, torch.bfloat16)
+    gh, gw = (2 * h, 2 * w) if k == 2 else (h, w)
+    g = nhwc(rnd(n, cout, gh, gw, seed=62), dev, torch.bfloat16)
+    shp = (cin, cout, 2, 2) if k == 2 else (cout, cin, k, k)
+    side = torch.cuda.Stream(dev)
+    for acc in (False, True):
+        base = rnd(*shp, seed=63).to(dev)
+        ref = rr.ops.wgrad(mode, g, x, None, n, h, w, cout, dw=base.clone(), accumulate=acc)
+        got = rr.ops.wgrad(mode, g, x, None, n, h, w, cout, dw=base.clone(), accumulate=acc,
+                           reduce_stream=side)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref), (shape, acc)
+
+
 @pytest.mark.parametrize("hw", [(8, 8), (16, 16), (12, 32), (2, 64), (1, 8, 8), (3, 8, 8), (1, 16, 16)])
 @pytest.mark.parametrize("halo", [True, False])
 def test_wgrad3_halo(dev, hw, halo, monkeypatch):
