@@ -321,10 +321,6 @@ def main():
     # (the kernel probe turns it off: per-kernel durations are taken without
     # a concurrent kernel sharing the chip)
     prefetch = [w_perc != 0.0 and os.environ.get("RR_PERC_PREFETCH", "1") != "0"]
-    # where the side stream forks off the step (A/B): "now" = before the
-    # distortion, or a point of the ResUNet forward (engine.FORWARD_POINTS)
-    prefetch_at = os.environ.get("RR_PERC_PREFETCH_AT", "now")
-    prefetch_at = None if prefetch_at == "now" else prefetch_at
 
     # the restorer's weight re-pack (after the previous step's AdamW) forked
     # onto a side stream at the step start, overlapping the distortion +
@@ -337,7 +333,7 @@ def main():
             model.prefetch_weights()
         clean = to_tensor(clean_u8)
         if prefetch[0]:
-            clean = perc.prefetch_target(clean, at=prefetch_at)
+            clean = perc.prefetch_target(clean)
         bad = to_tensor(distort(clean_u8))
         opt.zero_grad(set_to_none=True)
         out = model(bad)
@@ -488,6 +484,16 @@ def main():
                    "flop_per_image": FLOP_STEP_WITH_PERC if w_perc else FLOP_RESUNET_FWDBWD},
         "achieved_model_tflops": round(value * (FLOP_STEP_WITH_PERC if w_perc else
                                                 FLOP_RESUNET_FWDBWD) / 1e12, 2),
+        # the north star's step-level quantity (MFMA utilisation
+        # of ResUNet fwd+bwd): per-GPU img/s x the metric's FLOP per image
+        # (13.698 GFLOP, ResUNet fwd+bwd) / the dense MFMA peak, and the same
+        # with the perceptual loss's FLOP (18.270 GFLOP per image) counted;
+        # `roofline` stays the dominant kernel's fraction
+        "step_mfma_frac": round(value / world * FLOP_RESUNET_FWDBWD / 1e12 / PEAK[
+            "bf16" if dt == torch.bfloat16 else "f32"], 4),
+        "step_mfma_frac_with_perceptual": round(value / world * (FLOP_STEP_WITH_PERC if w_perc else
+                                                                 FLOP_RESUNET_FWDBWD) / 1e12 / PEAK[
+            "bf16" if dt == torch.bfloat16 else "f32"], 4),
         "loss": round(loss_v, 6),
         "repeats": len(windows),
         "window_ms_per_step": [round(w / a.steps * 1e3, 3) for w in windows],

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/roadrestore.h"
 
@@ -157,6 +158,28 @@ __device__ __forceinline__ float wave_sum(float v) {
   do {                                                      \
     if (hipGetLastError() != hipSuccess) return RR_ELAUNCH; \
   } while (0)
+
+// Kernel-path overrides for the parity tests, the library's one run-time
+// knob: RR_PATH="key=value[,key=value...]" (read per call).  Every default is
+// the measured-best path; the tests force a family off (conv3r=0,
+// stream3=0, stream1=0, swgrad=0, igemm_halo=0, wgrad_halo=0, ...) or a
+// workgroup kind (conv3r_wg=4/8, conv3r_segwg=4/8, conv3r_w64=0) to check
+// one shipped kernel against another on the same shape.  Unknown keys are
+// ignored; an unset variable costs one getenv.
+static inline int rr_path(const char *key, int dflt) {
+  const char *e = getenv("RR_PATH");
+  if (!e || !*e) return dflt;
+  const size_t kl = __builtin_strlen(key);
+  for (const char *p = e; *p;) {
+    const char *q = p;
+    while (*q && *q != ',') ++q;
+    const char *eq = p;
+    while (eq < q && *eq != '=') ++eq;
+    if (eq < q && (size_t)(eq - p) == kl && __builtin_memcmp(p, key, kl) == 0) return atoi(eq + 1);
+    p = *q ? q + 1 : q;
+  }
+  return dflt;
+}
 
 static inline int rr_grid_cap(long long want, int cap = 2048) {
   if (want < 1) return 1;

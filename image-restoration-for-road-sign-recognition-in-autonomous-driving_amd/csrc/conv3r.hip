@@ -51,21 +51,9 @@
 #include <cstdlib>
 #include <type_traits>
 
-// the fused BN/PReLU-backward dgrad epilogue runs in registers on the
-// row-segment tiles and the 8-wave whole-row tiles (16x16 / 8x8: 1-4 %
-// faster than staging it through the LDS one 128-pixel group at a time,
-// profiles/r5d_ablayers_bnbwd.txt) and in the bnbwd-only instance (EPI 3,
-// spill-free); the general instance stages it on the 4-wave whole-row tiles
-// (32x32: its register form was 12 % slower there).  RR_C3_BNREG (a separate
-// build, A/B): 1 = registers everywhere, 2 = staged on every whole-row tile,
-// 3 = staged on the 4-wave tiles in EPI 3 too
-#ifndef RR_C3_BNREG
-#define RR_C3_BNREG 0
-#endif
-
 namespace {
 
-template <int W, int BC, int NW, int NWV, int HB, int SG, int RW> struct R3 {
+template <int W, int BC, int NW, int NWV, int HB, int SG> struct R3 {
   // SG > 0: row-segment tiles of any H x W (W ignored): TR rows x 16 SG
   // columns of one image; out-of-image rows / columns are zero in the halo
   // and masked in the epilogue
@@ -96,11 +84,9 @@ template <int W, int BC, int NW, int NWV, int HB, int SG, int RW> struct R3 {
   static constexpr int SROW = BC + 4;
   static constexpr int STG = 128 * SROW * 4 + (NWV * BC * 2 + NWV) * 4 + 256;
   // [weights x2][halo x HB][guard block]: the shifted edge reads stay inside
-  // (row-segment tiles read inside their side blocks: no guard).  RW (the
-  // weights in registers, straight from the tiles in L2): [guard][halo x 2]
-  // [guard] -- the left-shifted read of the first block lands in the front one
-  static constexpr int HOFF = RW ? 1024 : 2 * WBYTES;            // halo base
-  static constexpr int KBYTES = RW ? 2048 + HB * HBYTES : 2 * WBYTES + HB * HBYTES + (SEGM ? 0 : 1024);
+  // (row-segment tiles read inside their side blocks: no guard)
+  static constexpr int HOFF = 2 * WBYTES;                        // halo base
+  static constexpr int KBYTES = 2 * WBYTES + HB * HBYTES + (SEGM ? 0 : 1024);
   static constexpr int BIAS = KBYTES;               // [BC] fp32 bias for the register epilogue
   static constexpr int LDS = KBYTES + BC * 4 > STG || SEGM ? KBYTES + BC * 4 : STG;
   static_assert(LDS <= 160 * 1024 && (NWV != 4 || 2 * LDS <= 160 * 1024), "LDS");
@@ -108,10 +94,8 @@ template <int W, int BC, int NW, int NWV, int HB, int SG, int RW> struct R3 {
   static_assert(HB == 1 || HB == 2, "halo buffers");
   static_assert(!SEGM || (SG == 1 || SG == 2), "segment width");
   static_assert(SEGM || PAIR || TR % W == 0 || W % TR == 0, "tile rows");
-  static_assert(RW || 2 * WBYTES >= 1024, "the edge read of the first halo block stays in LDS");
+  static_assert(2 * WBYTES >= 1024, "the edge read of the first halo block stays in LDS");
   static_assert(2 * NM + NS <= 15, "lgkmcnt of the row-0 wait");
-  static_assert(!RW || (HB == 2 && !SEGM && R % 2 == 0 && R >= 4 && 8 * NM <= 63),
-                "RW: double halo, whole rows, even R (the next stage's row 0 lands in slot 0), vmcnt range");
 };
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -169,11 +153,16 @@ template <int N> using ic = std::integral_constant<int, N>;
 // holds no registers for the epilogues it cannot run (no spills) and carries
 // none of their branches: the plain epilogue's instruction stream is a third
 // of the general one's (989 vs the general path's share of 11.7 k).
-template <int W, int BC, int NW, int NWV, int HB, int SG, int RW, int EPI = 0>
+template <int W, int BC, int NW, int NWV, int HB, int SG, int EPI = 0>
 __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) {
-  using G = R3<W, BC, NW, NWV, HB, SG, RW>;
-  constexpr bool BNREG = G::SEGM || RR_C3_BNREG == 1 || (RR_C3_BNREG == 0 && (NWV == 8 || EPI == 3)) ||
-                         (RR_C3_BNREG == 3 && NWV == 8);
+  using G = R3<W, BC, NW, NWV, HB, SG>;
+  // the fused BN/PReLU-backward dgrad epilogue runs in registers on the
+  // row-segment tiles and the 8-wave whole-row tiles (16x16 / 8x8: 1-4 %
+  // faster than staging it through the LDS one 128-pixel group at a time,
+  // profiles/r5d_ablayers_bnbwd.txt) and in the bnbwd-only instance (EPI 3,
+  // spill-free); the general instance stages it on the 4-wave whole-row tiles
+  // (32x32: its register form was 12 % slower there)
+  constexpr bool BNREG = G::SEGM || NWV == 8 || EPI == 3;
   constexpr bool ALLOW_BN = EPI == 0 || EPI == 3;     // the fused BN backward (a.bpart)
   constexpr bool ALLOW_OPS = EPI == 0 || EPI == 2;    // accumulate / ReLU-mask operands
   constexpr bool ALLOW_EX = EPI == 0;                 // residual, PReLU
@@ -188,12 +177,6 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wc = wv % WC, wp = wv / WC;
   const int frow = lane & 15, fq = lane >> 4;
-
-  // (A/B) every other co-resident workgroup starts a.stagger x 8128 cycles
-  // late: the tiles' epilogue store bursts then alternate instead of landing
-  // on the whole chip at once (the later slots keep the offset)
-  if (a.stagger > 0 && ((((int)blockIdx.x >> 8) ^ (int)blockIdx.x) & 1))
-    for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(127);
 
   // XCD-aware tile order (as igemm3_halo_kernel): XCD b % 8 walks a
   // contiguous tile range, so column blocks of a pixel tile share its L2
@@ -276,9 +259,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     for (int i = 0; i < G::NWG; ++i)
       __builtin_amdgcn_global_load_lds((const void *)(wst + wrow[i]), LDS_PTR(dst + wdst[i]), 16, 0, 0);
   };
-  // dummy (RW only): every piece reads the zero page (the chunk past the
-  // last keeps the DMA count of a stage uniform)
-  auto issue_h = [&](int ch, bool dummy = false) __attribute__((always_inline)) {
+  auto issue_h = [&](int ch) __attribute__((always_inline)) {
     const int ci0 = ch * 32;
     const bool first = ci0 < a.c1;                  // uniform
     const char *base = first ? a.x1 : a.x2;
@@ -288,7 +269,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     char *dst = smem + G::HOFF + (HB == 2 ? (ch & 1) * G::HBYTES : 0);
 #pragma unroll
     for (int i = 0; i < G::NHG; ++i) {
-      const long long off = hpix[i] >= 0 && !dummy ? ((long long)hpix[i] * cs + cl) * 2 + fq * 16 : zoff;
+      const long long off = hpix[i] >= 0 ? ((long long)hpix[i] * cs + cl) * 2 + fq * 16 : zoff;
       __builtin_amdgcn_global_load_lds((const void *)(base + off), LDS_PTR(dst + hdst[i]), 16, 0, 0);
     }
   };
@@ -344,198 +325,11 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
 #ifdef RR_CONV3R_STAMPS
   C3EpiStamp epi_stamp;
 #endif
-  if constexpr (RW) {
-    // ---- RW K loop: every wave loads its own A fragments (its NM 1-KB
-    // weight tiles per tap row dy) from global memory (L2) into registers,
-    // one stage ahead, through a ring of 4 fragment sets: stage st (phase p =
-    // st % 4) holds tap dy in set (dy - p) & 3; the next stage's dy = 0 goes
-    // into the spare set at the stage start, its dy = 1 / 2 into the sets of
-    // this stage's dy = 0 / 1 once their last rows (R - 1 / R) are done.  The
-    // LDS holds only the halo, double-buffered, so the only barrier is at the
-    // end of a 32-channel chunk (3 stages): the weights no longer need one per
-    // stage.  Per accumulator the MFMA order is the LDS-weight loop's, so the
-    // results are bitwise equal to it.  The A loads are ordinary (compiler-
-    // visible) global loads: the compiler's waitcnt pass counts them with the
-    // halo DMA; the chunk-end wait for the halo is counted here (8 NM loads
-    // issued after it) ----
-    typedef __attribute__((address_space(1))) const i32x4 gi32x4;
-    const long long run = (long long)(a.cout / 16) * 1024;   // one (chunk, dx, dy) run of tiles
-    // uniform tile base (SGPRs) + the lane's 16 B (one 32-bit VGPR) + m KB
-    // (the instruction offset): global_load_dwordx4 v, v_lane, s_base offset:m*1024
-    const char *wu = wtile + (long long)(c0 / 16 + wc * NM) * 1024;
-    const uint32_t l16 = (uint32_t)lane * 16;
-    i32x4 ar[4][NM];
-    auto load_a = [&](auto SETc, int st, int dy) __attribute__((always_inline)) {
-      constexpr int SET = decltype(SETc)::value;
-      const char *p = wu + ((long long)st * 3 + dy) * run;
-#pragma unroll
-      for (int m = 0; m < NM; ++m) ar[SET][m] = *(gi32x4 *)(p + l16 + m * 1024);
-    };
-    i32x4 bf[2][NS];
-    // B fragments of halo row `row` (of the wave's rows) at lane address ba
-    auto read_row = [&](int slot, uint32_t ba, int row) __attribute__((always_inline)) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bf[slot][s]) : "v"(ba), "i"((row * RS + s) * 1024));
-    };
-    // the halo DMA with the piece geometry recomputed at issue (uniform but
-    // for the lane's pixel): no per-piece pixel registers live in the loop
-    const int lanepix = G::PAIR ? (frow >> 3) * HW + (frow & 7) : frow;
-    auto issue_h_rw = [&](int ch, bool dummy) __attribute__((always_inline)) {
-      const int ci0 = ch * 32;
-      const bool first = ci0 < a.c1;                // uniform
-      const char *base = first ? a.x1 : a.x2;
-      const long long cs = first ? a.c1 : a.c2;
-      const long long cl = first ? ci0 : ci0 - a.c1;
-      const long long zoff = (long long)((uintptr_t)rr_zero_page - (uintptr_t)base) + fq * 16;
-      char *dst = smem + G::HOFF + (ch & 1) * G::HBYTES;
-#pragma unroll
-      for (int i = 0; i < G::NHG; ++i) {
-        int b = wv + NWV * i;
-        if (b >= G::HBLK) b -= NWV;                 // a duplicate of this wave's previous block
-        const int k = b / ((G::HS + 2) * RS);
-        const int rem = b - k * ((G::HS + 2) * RS);
-        const int hr = rem / RS, s = rem - (rem / RS) * RS;
-        int y, pb;
-        if constexpr (G::PAIR) {
-          y = hr - 1;
-          pb = ((n0 + 2 * k) * W + y) * W;
-        } else {
-          y = ys + hr - 1;
-          pb = ((n0 + k) * W + y) * W + 16 * s;
-        }
-        const bool ok = y >= 0 && y < W && !dummy;  // uniform
-        const long long off = ok ? ((long long)(pb + lanepix) * cs + cl) * 2 + fq * 16 : zoff;
-        __builtin_amdgcn_global_load_lds((const void *)(base + off), LDS_PTR(dst + b * 1024), 16, 0, 0);
-      }
-    };
-    auto stage = [&](auto DXc, auto PHc, int ch) __attribute__((always_inline)) {
-      constexpr int DX = decltype(DXc)::value, PH = decltype(PHc)::value;
-      constexpr int SA[3] = {(4 - PH) & 3, (5 - PH) & 3, (6 - PH) & 3};   // set of tap row dy
-      constexpr int SP = (7 - PH) & 3;                                     // spare set
-      const int st = ch * 3 + DX;
-      const int stn = st + 1 < nst ? st + 1 : st;   // (the last stage's prefetch re-reads itself)
-      const uint32_t hb = b_wave + (uint32_t)(ch & 1) * G::HBYTES;
-      // the lane part of a read at tap column dx and whether it is a padding
-      // column (recomputed per stage: nothing extra stays live in the loop)
-      auto lanecol = [&](int dx, bool &z) __attribute__((always_inline)) -> uint32_t {
-        if constexpr (G::PAIR) {
-          const int x = (frow & 7) + dx - 1;
-          const int xc = x < 0 ? 0 : (x > 7 ? 7 : x);
-          z = x != xc;
-          return fq * 256 + ((frow >> 3) * 8 + xc) * 16;
-        } else {
-          const int x = frow + dx - 1;
-          z = x < 0 || x > 15;
-          return x < 0 ? fq * 256 + 240 - 1024 : (x > 15 ? fq * 256 + 1024 : fq * 256 + x * 16);
-        }
-      };
-      bool zcol;
-      const uint32_t ba = hb + lanecol(DX, zcol);
-      const bool zlo = DX == 0 && zcol;               // left padding column (block s = 0)
-      const bool zhi = DX == 2 && zcol;               // right padding column (block NS - 1)
-      if constexpr (DX == 0) read_row(0, ba, 0);      // (DX > 0: read by the previous stage)
-      __builtin_amdgcn_sched_barrier(0);
-      load_a(ic<SP>{}, stn, 0);                       // the next stage's dy = 0 taps
-      if constexpr (DX == 0) issue_h_rw(ch + 1, ch + 1 >= kc);   // the next chunk's halo
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int ri = 0; ri < R + 2; ++ri) {
-        if (ri + 1 < R + 2) {
-          read_row((ri + 1) & 1, ba, ri + 1);
-          asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
-        } else if constexpr (DX < 2) {
-          // the next stage's row 0 (same chunk, next tap column) into slot 0
-          bool zn;
-          read_row(0, hb + lanecol(DX + 1, zn), 0);
-          asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NS) : "memory");
-        } else {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
-#pragma unroll
-        for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(bf[ri & 1][s]));
-        {
-          i32x4 &lo = bf[ri & 1][0];
-          i32x4 &hi = bf[ri & 1][NS - 1];
-          if (G::PAIR) {
-            if (zlo || zhi) lo = i32x4{0, 0, 0, 0};
-          } else {
-            if (zlo) lo = i32x4{0, 0, 0, 0};
-            if (zhi) hi = i32x4{0, 0, 0, 0};
-          }
-        }
-#pragma unroll
-        for (int dy = 0; dy < 3; ++dy) {
-          const int o = ri - dy;
-          if (o < 0 || o >= R) continue;
-#pragma unroll
-          for (int s = 0; s < NS; ++s)
-#pragma unroll
-            for (int m = 0; m < NM; ++m)
-              acc[o][s][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                  __builtin_bit_cast(bf16x8, ar[SA[dy]][m]), __builtin_bit_cast(bf16x8, bf[ri & 1][s]),
-                  acc[o][s][m], 0, 0, 0);
-        }
-        // tap rows dy = 0 / 1 are done after rows R - 1 / R: their sets take
-        // the next stage's dy = 1 / 2
-        if (ri == R - 1) {
-          __builtin_amdgcn_sched_barrier(0);
-          load_a(ic<SA[0]>{}, stn, 1);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        if (ri == R) {
-          __builtin_amdgcn_sched_barrier(0);
-          load_a(ic<SA[1]>{}, stn, 2);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      if constexpr (DX == 2) {
-        // the next chunk's halo (issued at this chunk's first stage, 8 NM A
-        // loads ago) has landed for every wave, and every wave is done with
-        // this chunk's buffer (the one the chunk after next loads into)
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(8 * NM) : "memory");
-      }
-    };
-    // prologue: chunk 0's halo, stage 0's A fragments (phase 0: sets 0, 1, 2)
-    issue_h_rw(0, false);
-    __builtin_amdgcn_sched_barrier(0);
-    load_a(ic<0>{}, 0, 0);
-    load_a(ic<1>{}, 0, 1);
-    load_a(ic<2>{}, 0, 2);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(3 * NM) : "memory");
-    // chunk q of a 4-chunk group starts at stage phase (3 q) % 4
-    auto chunk = [&](auto PHc, int ch) __attribute__((always_inline)) {
-      constexpr int PH = decltype(PHc)::value;
-      stage(ic<0>{}, ic<PH>{}, ch);
-      stage(ic<1>{}, ic<(PH + 1) & 3>{}, ch);
-      stage(ic<2>{}, ic<(PH + 2) & 3>{}, ch);
-    };
-    int ch = 0;
-    for (; ch + 4 <= kc; ch += 4) {
-      chunk(ic<0>{}, ch);
-      chunk(ic<3>{}, ch + 1);
-      chunk(ic<2>{}, ch + 2);
-      chunk(ic<1>{}, ch + 3);
-    }
-    if (ch < kc) {                                    // kc % 4 == 2 (RW takes even kc)
-      chunk(ic<0>{}, ch);
-      chunk(ic<3>{}, ch + 1);
-    }
-    // the last prefetches (and the dummy halo) land before the epilogue
-    // stages through the LDS
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-  } else {
   // prologue: chunk 0's halo, stage 0's weights
   issue_h(0);
   issue_w(0);
   vm_barrier<0>();
 
-  // diagnostics (RR_IGEMM_DBG, timing only -- results are wrong): bit2 no
-  // DMA in the K loop, bit0 no epilogue, bit4 no weight DMA, bit5 no halo
-  // DMA (per stage; nothing run-time-switched inside the row loop: each such
-  // switch is a scalar branch around every row's MFMA cluster)
-  const bool dbg_nodma = (a.dbg & 4) != 0;
   // (no wave priority around the MFMA clusters: +3.3 % when it was added
   // next to the run-time switches, profiles/r3aa_ab*.jsonl; without them it
   // measured -0.6 % at 224 and -0.2 % on the step, r4zd)
@@ -543,12 +337,12 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     const int ch = st / 3, dx = st - ch * 3;       // uniform
     C3_STAMP(st_t);
     // operands of the next stage (weights) and of the next chunk (halo)
-    const bool next_h = HB == 2 && dx == 0 && ch + 1 < kc && !dbg_nodma && !(a.dbg & 32);
-    const bool next_w = st + 1 < nst && !dbg_nodma && !(a.dbg & 16);
+    const bool next_h = HB == 2 && dx == 0 && ch + 1 < kc;
+    const bool next_w = st + 1 < nst;
     if (HB == 1 && dx == 0 && ch > 0) {
       // one halo buffer: every wave is past the previous chunk's last read
       // (the barrier that ended the last stage); load this chunk's halo
-      if (!dbg_nodma && !(a.dbg & 32)) issue_h(ch);
+      issue_h(ch);
       VM_BARRIER(0);
     }
 
@@ -639,7 +433,6 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
     if (next_h) VM_BARRIER(G::NHG);
     else VM_BARRIER(0);
   }
-  }   // (LDS-weight K loop)
 #ifdef RR_CONV3R_STAMPS
   C3_STAMP(st_loop1);
   if (lane == 0 && blockIdx.x < (1 << 18) / (8 * NWV)) {
@@ -652,17 +445,6 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   }
 #endif
 
-  if (a.dbg & 1) {
-    float t = 0.f;
-#pragma unroll
-    for (int o = 0; o < R; ++o)
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-#pragma unroll
-        for (int m = 0; m < NM; ++m) t += acc[o][s][m][0];
-    if (t == 1234.5f) a.y1[tid] = 1;                  // keep the accumulators live
-    return;
-  }
   const int cb = wc * NW;                           // the wave's first column in the block
   const int srow = pblk * G::WP + wp;               // the wave's statistics / partial row
   // output pixel of accumulator tile (o, s) for this lane; -1: outside the
@@ -1057,101 +839,81 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   }
 }
 
-// column block and per-wave channels for *d: BC = 256 / 128 / 64 by c_out,
-// except where that leaves fewer than 256 workgroups (one per CU): the
-// 8x8 256-channel layers (B = 512: 128 tiles) take 128 x 32 wave tiles.
-// sg > 0: row-segment tiles (any H x W)
-struct R3Pick { int bc, nw, nwv, hb, sg, rw; };
+// column block and per-wave channels for *d: BC = 128 / 64 by c_out, 128 x
+// 64 wave tiles, except where that leaves fewer than 256 workgroups (one per
+// CU): the 8x8 256-channel layers (B = 512: 128 tiles) take 128 x 32 wave
+// tiles.  sg > 0: row-segment tiles (any H x W)
+struct R3Pick { int bc, nw, nwv, hb, sg; };
 int r3_tpx(R3Pick k) { return (k.nwv / (k.bc / k.nw)) * 128; }
 
-// square 8 / 16 / 32 maps whose pixel count fills whole tiles take the
+// square 8 / 16 / 32 / 64 maps whose pixel count fills whole tiles take the
 // whole-row tiles; everything else (the reference's 224 / 112 / 56 / 28 /
 // 14 maps, odd sizes, small batches) the row-segment tiles: 32-column
-// segments x 4 rows per wave above W = 16, 16 x 8 at W <= 16
-// workgroups of whole-row tiles: one 8-wave workgroup per CU with a
+// segments x 4 rows per wave above W = 16, 16 x 8 at W <= 16.
+// Workgroups of whole-row tiles: one 8-wave workgroup per CU with a
 // double-buffered halo where c_out % 128 == 0 on the 16x16 / 8x8 maps
 // (5-12% faster there, profiles/r3i_ab.jsonl, r4z_conv3r_wg_ab.jsonl), else
 // 4-wave workgroups, 2 per CU (one's epilogue / DMA waits overlap the other's
 // MFMAs) with one halo buffer -- also at W = 32, where the 8-wave tiles were
-// 4-11 % slower once the row loop lost its run-time switches (r4z).
-// RR_CONV3R_WG=4 / 8 forces one kind (A/B).
-// RW (register weights, whole-row tiles with an even number of 32-channel
-// chunks): RR_CONV3R_RW=0 / 1 (A/B); RW tiles always double-buffer the halo
+// 4-11 % slower once the row loop lost its run-time switches (r4z).  The
+// 128-channel column blocks are 2-3 % faster per layer than 256-channel ones
+// at 16x16 / 8x8 (profiles/r4zk_conv3r_bc_ab.jsonl).  Test overrides
+// (RR_PATH, common.h): conv3r_wg=4 / 8 forces a workgroup kind,
+// conv3r_w64=0 puts the 64x64 maps on row-segment tiles, conv3r_segwg=4 / 8
+// the row-segment workgroup kind
 R3Pick r3_pick(const rr_igemm_desc *d) {
   const long long P = (long long)d->n * d->h * d->w;
   const int W = d->w;
-  // RR_CONV3R_W64 (A/B): 0 = the 64x64 maps on row-segment tiles
-  const char *e64 = getenv("RR_CONV3R_W64");
-  const bool w64 = W == 64 && !(e64 && !atoi(e64));
+  const bool w64 = W == 64 && rr_path("conv3r_w64", 1) != 0;
   const bool square = d->h == W && (W == 8 || W == 16 || W == 32 || w64);
-  const char *e = getenv("RR_CONV3R_WG");
-  const int nwv = e && (atoi(e) == 4 || atoi(e) == 8) ? atoi(e) : (d->c_out % 128 == 0 && W != 32 ? 8 : 4);
+  const int fwg = rr_path("conv3r_wg", 0);
+  const int nwv = fwg == 4 || fwg == 8 ? fwg : (d->c_out % 128 == 0 && W != 32 ? 8 : 4);
   if (square) {
-    // RR_CONV3R_RW: 0 = LDS weights, 1 = register weights, 32 = register
-    // weights with 128 x 32 wave tiles on the 32x32 maps only
-    const char *re = getenv("RR_CONV3R_RW");
-    const int rwm = re ? atoi(re) : 0;
-    const int rw = ((d->c_in1 + d->c_in2) % 64 == 0) && (rwm == 1 || (rwm == 32 && W == 32)) &&
-                   !(W == 8 && d->c_out % 128 != 0) && W != 64;
-    // 128-channel column blocks where c_out % 256 == 0 too: 2-3 % faster per
-    // layer than 256-channel ones at 16x16 / 8x8 once the row loop lost its
-    // run-time switches (profiles/r4zk_conv3r_bc_ab.jsonl); the small-batch
-    // 8x8 layers keep 128 x 32 wave tiles.  RR_CONV3R_BC256=1: the 256-channel
-    // blocks (A/B, LDS weights only)
-    const char *b256 = getenv("RR_CONV3R_BC256");
-    const int h8 = 2, h4 = rw ? 2 : 1;
     R3Pick c[3];
     int nc = 0;
     if (nwv == 8) {
       if (d->c_out % 256 == 0 && W == 8 && (P / 256) * (d->c_out / 256) < 256 && P % 256 == 0) {
-        c[nc++] = {128, 32, 8, h8, 0, rw};
-      } else if (d->c_out % 256 == 0 && b256 && atoi(b256) && !rw) {
-        c[nc++] = {256, 64, 8, h8, 0, 0};
+        c[nc++] = {128, 32, 8, 2, 0};
       } else if (d->c_out % 128 == 0) {
-        c[nc++] = {128, 64, 8, h8, 0, rw};
+        c[nc++] = {128, 64, 8, 2, 0};
       } else {
-        c[nc++] = {64, 32, 8, h8, 0, rw};
+        c[nc++] = {64, 32, 8, 2, 0};
       }
     } else if (d->c_out % 128 == 0) {
       // 128-channel column blocks of 128 x 64 wave tiles (256-pixel tiles);
       // below 512 workgroups (2 per CU) the 8x8 layers take 128 x 32 wave
       // tiles (128-pixel tiles)
-      if (W == 8 && (P / 256) * (d->c_out / 128) < 512 && P % 128 == 0) c[nc++] = {128, 32, 4, h4, 0, rw};
-      else c[nc++] = {128, 64, 4, h4, 0, rw};
+      if (W == 8 && (P / 256) * (d->c_out / 128) < 512 && P % 128 == 0) c[nc++] = {128, 32, 4, 1, 0};
+      else c[nc++] = {128, 64, 4, 1, 0};
     } else {
-      c[nc++] = {64, 64, 4, h4, 0, rw};
+      c[nc++] = {64, 64, 4, 1, 0};
     }
     // batches whose pixels do not fill the first pick's tiles: smaller
     // whole-row tiles before the row-segment ones (an odd batch of 16x16
     // 256-channel maps stays on whole rows)
     if (d->c_out % 128 == 0) {
-      c[nc++] = {128, 32, 8, h8, 0, rw};
-      c[nc++] = {128, 32, 4, h4, 0, rw};
+      c[nc++] = {128, 32, 8, 2, 0};
+      c[nc++] = {128, 32, 4, 1, 0};
     } else {
-      c[nc++] = {64, 32, 4, h4, 0, rw};
+      c[nc++] = {64, 32, 4, 1, 0};
     }
-    // RR_CONV3R_NW=32 (A/B): 128 x 32 wave tiles for the first pick
-    const char *nwe = getenv("RR_CONV3R_NW");
-    if (((nwe && atoi(nwe) == 32) || (rw && rwm == 32)) && c[0].bc <= 128) c[0].nw = 32;
     for (int i = 0; i < nc; ++i)
       if (P % r3_tpx(c[i]) == 0) return c[i];
   }
-  const char *se = getenv("RR_CONV3R_SEG");          // A/B: force 1 / 2 column blocks per segment
-  const int sg = se && (atoi(se) == 1 || atoi(se) == 2) ? atoi(se) : (W > 16 ? 2 : 1);
+  const int sg = W > 16 ? 2 : 1;
   // one 8-wave workgroup per CU with a double-buffered halo (the next
   // chunk loads during this one's stages) on the 128+-channel maps of
   // W <= 28 (the 28x28 / 14x14 layers: 9-12 % faster), 2 x 4-wave elsewhere
   // (the 224 / 112 / 56 layers: even or 5-10 % slower,
-  // profiles/r3v_ab224_segwg.jsonl); RR_CONV3R_SEGWG=4 / 8 forces one (A/B)
-  const char *sw = getenv("RR_CONV3R_SEGWG");
-  const int segwg = sw && (atoi(sw) == 4 || atoi(sw) == 8) ? atoi(sw)
-                                                           : (d->c_out % 128 == 0 && W <= 28 ? 8 : 4);
+  // profiles/r3v_ab224_segwg.jsonl)
+  const int fsw = rr_path("conv3r_segwg", 0);
+  const int segwg = fsw == 4 || fsw == 8 ? fsw : (d->c_out % 128 == 0 && W <= 28 ? 8 : 4);
   if (segwg == 8) {
-    if (sg == 2) return d->c_out % 128 == 0 ? R3Pick{128, 64, 8, 2, 2, 0} : R3Pick{64, 32, 8, 2, 2, 0};
-    return d->c_out % 128 == 0 ? R3Pick{128, 32, 8, 2, 1, 0} : R3Pick{64, 32, 8, 1, 1, 0};
+    if (sg == 2) return d->c_out % 128 == 0 ? R3Pick{128, 64, 8, 2, 2} : R3Pick{64, 32, 8, 2, 2};
+    return d->c_out % 128 == 0 ? R3Pick{128, 32, 8, 2, 1} : R3Pick{64, 32, 8, 1, 1};
   }
-  if (sg == 2) return d->c_out % 128 == 0 ? R3Pick{128, 64, 4, 1, 2, 0} : R3Pick{64, 64, 4, 1, 2, 0};
-  return d->c_out % 128 == 0 ? R3Pick{128, 32, 4, 1, 1, 0} : R3Pick{64, 32, 4, 1, 1, 0};
+  if (sg == 2) return d->c_out % 128 == 0 ? R3Pick{128, 64, 4, 1, 2} : R3Pick{64, 64, 4, 1, 2};
+  return d->c_out % 128 == 0 ? R3Pick{128, 32, 4, 1, 1} : R3Pick{64, 32, 4, 1, 1};
 }
 // row-segment tiles: rows per tile, column segments and row bands per image
 int r3_tr(R3Pick k) { return (k.nwv / (k.bc / k.nw)) * (8 / k.sg); }
@@ -1167,9 +929,10 @@ long long r3_ptiles(const rr_igemm_desc *d, R3Pick k) {
 
 }  // namespace
 
+// RR_PATH conv3r=0: the halo / tiled kernels instead (tests), conv3r=2:
+// whole-row tiles only
 int conv3r_bc(const rr_igemm_desc *d) {
-  const char *e = getenv("RR_CONV3R");              // A/B switch (per call): 0 = halo kernels,
-  const int mode = e ? atoi(e) : 1;                 // 2 = whole-row tiles only
+  const int mode = rr_path("conv3r", 1);
   if (mode == 0) return 0;
   if (!d || d->dtype != RR_BF16 || d->mode != RR_CONV3X3 || d->out_nchw) return 0;
   if (d->n <= 0 || d->h <= 0 || d->w <= 0) return 0;
@@ -1188,82 +951,54 @@ int conv3r_stat_blocks(const rr_igemm_desc *d) {
   return (int)(r3_ptiles(d, k) * (k.nwv / (k.bc / k.nw)));   // one row per wave row of a tile
 }
 
-// the plain epilogue (EPI 1: no operand loads, no PReLU / pool / fused BN
-// backward) wherever the call allows it; the register-weight K loop (an A/B
-// variant) keeps the general one.  RR_C3_PLAIN_EPI=0: a separate build with
-// the general epilogue everywhere (A/B)
-#ifndef RR_C3_PLAIN_EPI
-#define RR_C3_PLAIN_EPI 1
-#endif
-template <int W_, int BC, int NW, int NWV, int HB, int SG, int RW>
+// the specialised epilogue instances wherever the call allows one: EPI 1
+// (plain: bias / statistics / ReLU / split, no operand loads) for the
+// training step's forward and plain dgrads, 4 (+ pool), 3 (the fused BN
+// backward alone), 2 (+ accumulate / ReLU-mask operands); the general one
+// (0) otherwise
+template <int W_, int BC, int NW, int NWV, int HB, int SG>
 static void c3_launch(const IgemmArgs &a, dim3 grid, dim3 block, hipStream_t st) {
   const bool plain = !a.accumulate && !a.res && !a.has_mask && (a.act & 3) != RR_ACT_PRELU &&
                      !(a.act & (RR_ACT_POOL | RR_ACT_NOFULL)) && !a.bpart;
-  if constexpr (!RW && RR_C3_PLAIN_EPI) {
-    if (plain) {
-      hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, RW, 1>), grid, block, 0, st, a);
-      return;
-    }
-    const bool ex = a.res || (a.act & 3) == RR_ACT_PRELU || (a.act & (RR_ACT_POOL | RR_ACT_NOFULL));
-    if ((a.act & RR_ACT_POOL) && !a.res && (a.act & 3) != RR_ACT_PRELU && !a.accumulate && !a.has_mask &&
-        !a.bpart) {
-      hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, RW, 4>), grid, block, 0, st, a);
-      return;
-    }
-    if (a.bpart && !ex && !a.accumulate && !a.has_mask) {
-      hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, RW, 3>), grid, block, 0, st, a);
-      return;
-    }
-    if (!a.bpart && !ex) {
-      hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, RW, 2>), grid, block, 0, st, a);
-      return;
-    }
+  if (plain) {
+    hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, 1>), grid, block, 0, st, a);
+    return;
   }
-  hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, RW, 0>), grid, block, 0, st, a);
+  const bool ex = a.res || (a.act & 3) == RR_ACT_PRELU || (a.act & (RR_ACT_POOL | RR_ACT_NOFULL));
+  if ((a.act & RR_ACT_POOL) && !a.res && (a.act & 3) != RR_ACT_PRELU && !a.accumulate && !a.has_mask &&
+      !a.bpart) {
+    hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, 4>), grid, block, 0, st, a);
+    return;
+  }
+  if (a.bpart && !ex && !a.accumulate && !a.has_mask) {
+    hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, 3>), grid, block, 0, st, a);
+    return;
+  }
+  if (!a.bpart && !ex) {
+    hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, 2>), grid, block, 0, st, a);
+    return;
+  }
+  hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, 0>), grid, block, 0, st, a);
 }
 
-template <int BC, int NW, int NWV, int HB, int SG, int RW>
+template <int BC, int NW, int NWV, int HB, int SG>
 static int conv3r_go(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   a.ncblk = a.cout / BC;
-  const long long nblk = r3_ptiles(d, R3Pick{BC, NW, NWV, HB, SG, RW}) * a.ncblk;
+  const long long nblk = r3_ptiles(d, R3Pick{BC, NW, NWV, HB, SG}) * a.ncblk;
   if (nblk <= 0 || nblk > 0x7fffffffLL) return RR_EUNSUPPORTED;
   const dim3 grid((unsigned)nblk), block(64 * NWV);
   if constexpr (SG > 0) {
-    c3_launch<0, BC, NW, NWV, HB, SG, 0>(a, grid, block, st);
+    c3_launch<0, BC, NW, NWV, HB, SG>(a, grid, block, st);
   } else {
     switch (d->w) {
-      case 64:
-        if constexpr (RW) return RR_EUNSUPPORTED;
-        else c3_launch<64, BC, NW, NWV, HB, 0, 0>(a, grid, block, st);
-        break;
-      case 32: c3_launch<32, BC, NW, NWV, HB, 0, RW>(a, grid, block, st); break;
-      case 16: c3_launch<16, BC, NW, NWV, HB, 0, RW>(a, grid, block, st); break;
-      default:
-        // (RW 4-wave 64 x 64 tiles of 8x8 pairs: 2 x 40 KB of halo, past two
-        // workgroups per CU; the picker does not take it)
-        if constexpr (RW && NWV == 4 && BC == 64 && NW == 64) return RR_EUNSUPPORTED;
-        else c3_launch<8, BC, NW, NWV, HB, 0, RW>(a, grid, block, st);
-        break;
+      case 64: c3_launch<64, BC, NW, NWV, HB, 0>(a, grid, block, st); break;
+      case 32: c3_launch<32, BC, NW, NWV, HB, 0>(a, grid, block, st); break;
+      case 16: c3_launch<16, BC, NW, NWV, HB, 0>(a, grid, block, st); break;
+      default: c3_launch<8, BC, NW, NWV, HB, 0>(a, grid, block, st); break;
     }
   }
   RR_CHECK_LAUNCH();
   return RR_OK;
-}
-
-template <int RW>
-static int conv3r_go_rows(const R3Pick &k, const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
-  constexpr int H4 = RW ? 2 : 1;
-  if (k.nwv == 8) {
-    if constexpr (!RW)
-      if (k.bc == 256) return conv3r_go<256, 64, 8, 2, 0, 0>(d, a, st);
-    if (k.bc == 128 && k.nw == 64) return conv3r_go<128, 64, 8, 2, 0, RW>(d, a, st);
-    if (k.bc == 128) return conv3r_go<128, 32, 8, 2, 0, RW>(d, a, st);
-    return conv3r_go<64, 32, 8, 2, 0, RW>(d, a, st);
-  }
-  if (k.bc == 128 && k.nw == 64) return conv3r_go<128, 64, 4, H4, 0, RW>(d, a, st);
-  if (k.bc == 128) return conv3r_go<128, 32, 4, H4, 0, RW>(d, a, st);
-  if (k.nw == 64) return conv3r_go<64, 64, 4, H4, 0, RW>(d, a, st);
-  return conv3r_go<64, 32, 4, H4, 0, RW>(d, a, st);
 }
 
 int conv3r_launch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
@@ -1271,27 +1006,35 @@ int conv3r_launch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   const R3Pick k = r3_pick(d);
   if (k.sg == 2) {
     if (k.nwv == 8) {
-      if (k.bc == 128) return conv3r_go<128, 64, 8, 2, 2, 0>(d, a, st);
-      return conv3r_go<64, 32, 8, 2, 2, 0>(d, a, st);
+      if (k.bc == 128) return conv3r_go<128, 64, 8, 2, 2>(d, a, st);
+      return conv3r_go<64, 32, 8, 2, 2>(d, a, st);
     }
-    if (k.bc == 128) return conv3r_go<128, 64, 4, 1, 2, 0>(d, a, st);
-    return conv3r_go<64, 64, 4, 1, 2, 0>(d, a, st);
+    if (k.bc == 128) return conv3r_go<128, 64, 4, 1, 2>(d, a, st);
+    return conv3r_go<64, 64, 4, 1, 2>(d, a, st);
   }
   if (k.sg == 1) {
     if (k.nwv == 8) {
-      if (k.bc == 128) return conv3r_go<128, 32, 8, 2, 1, 0>(d, a, st);
-      return conv3r_go<64, 32, 8, 1, 1, 0>(d, a, st);
+      if (k.bc == 128) return conv3r_go<128, 32, 8, 2, 1>(d, a, st);
+      return conv3r_go<64, 32, 8, 1, 1>(d, a, st);
     }
-    if (k.bc == 128) return conv3r_go<128, 32, 4, 1, 1, 0>(d, a, st);
-    return conv3r_go<64, 32, 4, 1, 1, 0>(d, a, st);
+    if (k.bc == 128) return conv3r_go<128, 32, 4, 1, 1>(d, a, st);
+    return conv3r_go<64, 32, 4, 1, 1>(d, a, st);
   }
-  return k.rw ? conv3r_go_rows<1>(k, d, a, st) : conv3r_go_rows<0>(k, d, a, st);
+  if (k.nwv == 8) {
+    if (k.bc == 128 && k.nw == 64) return conv3r_go<128, 64, 8, 2, 0>(d, a, st);
+    if (k.bc == 128) return conv3r_go<128, 32, 8, 2, 0>(d, a, st);
+    return conv3r_go<64, 32, 8, 2, 0>(d, a, st);
+  }
+  if (k.bc == 128 && k.nw == 64) return conv3r_go<128, 64, 4, 1, 0>(d, a, st);
+  if (k.bc == 128) return conv3r_go<128, 32, 4, 1, 0>(d, a, st);
+  if (k.nw == 64) return conv3r_go<64, 64, 4, 1, 0>(d, a, st);
+  return conv3r_go<64, 32, 4, 1, 0>(d, a, st);
 }
 
 const char *conv3r_name(const rr_igemm_desc *d) {
   if (!conv3r_bc(d)) return "invalid";
   const R3Pick k = r3_pick(d);
-  static char names[4][5][2][2][40];
+  static char names[4][5][2][40];
   static char segnames[2][2][2][40];
   char *n;
   if (k.sg) {
@@ -1302,14 +1045,13 @@ const char *conv3r_name(const rr_igemm_desc *d) {
     return n;
   }
   const int wi = d->w == 8 ? 0 : d->w == 16 ? 1 : d->w == 32 ? 2 : 3;
-  const int bi = k.bc == 64 ? (k.nw == 64 ? 0 : 4) : k.bc == 256 ? 3 : (k.nw == 64 ? 1 : 2);
+  const int bi = k.bc == 64 ? (k.nw == 64 ? 0 : 4) : (k.nw == 64 ? 1 : 2);
   const int vi = k.nwv == 8;
-  n = names[wi][bi][vi][k.rw != 0];
+  n = names[wi][bi][vi];
   if (!n[0]) {
     // conv3r_kernel<W,BC> (128 x 64 wave tiles), <W,BC,32> (128 x 32); the
-    // 8-wave one-per-CU variant adds ",w8", the register-weight K loop ",rw"
-    snprintf(n, 40, "conv3r_kernel<%d,%d%s%s%s>", d->w, k.bc, k.nw == 32 ? ",32" : "", vi ? ",w8" : "",
-             k.rw ? ",rw" : "");
+    // 8-wave one-per-CU variant adds ",w8"
+    snprintf(n, 40, "conv3r_kernel<%d,%d%s%s>", d->w, k.bc, k.nw == 32 ? ",32" : "", vi ? ",w8" : "");
   }
   return n;
 }

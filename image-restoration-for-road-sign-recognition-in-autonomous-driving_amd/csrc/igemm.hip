@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs a) {
 
   const int kchunks = a.cin / BK;   // stages per tap
   const int nstage0 = a.taps * kchunks;
-  const int nstage = (a.dbg & 2) ? 2 * nstage0 : nstage0;
+  const int nstage = nstage0;
 
   auto issue = [&](int s_, int buf) {
     const int s = s_ >= nstage0 ? s_ - nstage0 : s_;
@@ -216,15 +216,6 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs a) {
   }
 
   // ---- epilogue --------------------------------------------------------
-  if (a.dbg & 1) {
-    float t = 0.f;
-#pragma unroll
-    for (int mi = 0; mi < MC; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < MP; ++ni) t += acc[mi][ni][0];
-    if (t == 1234.5f) a.y1[0] = 1;   // keep the accumulators live
-    return;
-  }
   if (!a.out_nchw && c0 + BC <= a.cout) {
     // ---- staged epilogue: fp32 tile through LDS, column-wise BN stats,
     // ---- 16-B row-contiguous global stores (one 1 KiB run per wave-store)
@@ -405,23 +396,12 @@ template <int W, int BP, int NT = 2 * BP> struct HaloGeom {
 // per CU, one tile's prologue / epilogue overlapping the other's MFMA loop.
 // BC = 128 double-buffers the halo, 1 workgroup per CU.
 // BP = 128 (256 threads, ~51 KB LDS at BC = 64): 3 workgroups per CU.
-// NT = BP (4 waves at BP = 256, RR_HALO_NT=256): each wave owns a 64 x 64
-// output tile (MC = MP = 4), a third fewer LDS operand reads per MFMA than
-// the 64 x 32 wave tile of NT = 2 BP, at 2 waves per SIMD.
 template <int BC, int BP, int NT = 2 * BP> struct HaloCfg {
   static constexpr int HB = BC <= 64 ? 1 : 2;
   static constexpr int OCC = NT == BP ? 2 : BP == 128 ? (BC <= 64 ? 3 : 2) : (BC <= 64 ? 4 : 2);   // min waves / SIMD
 };
 
-// DBGK (timing diagnostics only, RR_HALO_DBGK; results are wrong): bit0 no
-// barriers in the K loop, bit1 no fragment reads in the K loop (the first
-// stage's fragments reused), bit2 no global loads in the K loop, bit4 no
-// next-chunk halo loads (weights still loaded) -- bounds on what each costs;
-// bit5 alone: the unsplit staging (every wave loads both operands), correct
-// results, for same-box A/B against the role split; bit6 alone: the next
-// chunk's halo issued all at tap 0 (correct results; A/B of the spread);
-// bit7 alone: weights 3 stages ahead at BC = 128 (correct results)
-template <int BC, int W, int MODE, int BP, int NT = 2 * BP, int DBGK = 0>
+template <int BC, int W, int MODE, int BP, int NT = 2 * BP>
 __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_kernel(IgemmArgs a) {
   using T = bf16_t;
   using G = HaloGeom<W, BP, NT>;
@@ -518,9 +498,9 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
   // per tap): here each workgroup walks tiles blockIdx.x + k gridDim.x with
   // the NEXT tile's halo loading into registers while the current one
   // computes and stores; the 9 taps' weights (9 x 2 KB) are staged once.
-  if constexpr (BC < 64 && DBGK == 0) {
+  if constexpr (BC < 64) {
     const int ntile = a.P / BP;
-    if (kch == 1 && a.ncblk == 1 && !(a.dbg & 3) && (int)gridDim.x < ntile) {
+    if (kch == 1 && a.ncblk == 1 && (int)gridDim.x < ntile) {
       char *const wall = smem + G::HBYTES;
       for (int i = tid; i < 9 * WPIECES; i += NT) {
         const int tp = i / WPIECES, idx = i - tp * WPIECES;
@@ -622,11 +602,9 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
   }
 
   V hreg[G::LH];
-  // weights prefetched 2 stages ahead (register set = stage parity).  DBGK
-  // bit7 (BC = 128): 3 ahead, register set k % 3 holding W(k) (9 taps per
-  // chunk, so the set is TAP % 3) -- measured no faster (r2i_dbgk.jsonl)
-  constexpr bool W3 = HB == 2 && (DBGK & 128) != 0;
-  V wr0[LW], wr1[LW], wr2[W3 ? LW : 1];
+  // weights prefetched 2 stages ahead (register set = stage parity; 3
+  // ahead at BC = 128 measured no faster, r2i_dbgk.jsonl)
+  V wr0[LW], wr1[LW];
 
   auto load_halo = [&](int ch) __attribute__((always_inline)) {
     const int ci0 = ch * 64;
@@ -685,8 +663,7 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
         v.x = ok ? v.x : 0u; v.y = ok ? v.y : 0u; v.z = ok ? v.z : 0u; v.w = ok ? v.w : 0u;
       }
       if constexpr (decltype(setc)::value == 0) wr0[i] = v;
-      else if constexpr (decltype(setc)::value == 1) wr1[i] = v;
-      else wr2[i] = v;
+      else wr1[i] = v;
     }
   };
   // LDS weight buffer SET (stage parity) <- register set REG
@@ -700,7 +677,7 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
       const int r = 8 * (idx >> 6) + (idx & 7);
       if (WPIECES % NT == 0 || idx < WPIECES)
         *reinterpret_cast<V *>(d + ((idx >> 3) & 7) * WPLANE + r * 16) =
-            REG == 0 ? wr0[i] : (REG == 1 ? wr1[i] : wr2[i < (W3 ? LW : 1) ? i : 0]);
+            REG == 0 ? wr0[i] : wr1[i];
     }
   };
 
@@ -710,12 +687,9 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
 #pragma unroll
     for (int ni = 0; ni < MP; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // DBGK bit1: fragments read once (diagnostics)
-  bf16x8 dfa[(DBGK & 2) ? 2 : 1][MC], dfb[(DBGK & 2) ? 2 : 1][MP];
   // prologue: halo(0), weights(0) into LDS; weights(1) in flight
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
   // RS (role split, HB = 2): waves 0-3 stage the weights, waves 4-7 the
   // next chunk's halo.  vmcnt retires in issue order, so a wave that loaded
   // the (HBM, long-latency) halo at tap 0 and then waited for its weights
@@ -727,12 +701,11 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
   // (r2h_dbgk.jsonl) but 5-7 % slower at BC = 128 (the four weight waves
   // then carry 2 x 4 loads + LDS stores per stage and become the critical
   // path); BC = 64 at W = 64 / 8 spills with it (128-VGPR cap)
-  constexpr bool RS = NT == 512 && DBGK == 0 && BC == 64 && (W == 16 || W == 32);
+  constexpr bool RS = NT == 512 && BC == 64 && (W == 16 || W == 32);
   if constexpr (!RS) {
     load_halo(0);
     load_w(0, I0{});
     load_w(nst > 1 ? 1 : 0, I1{});
-    if constexpr (W3) load_w(nst > 2 ? 2 : nst - 1, I2{});
     store_halo(0);
     store_w(I0{}, I0{});
     __syncthreads();
@@ -747,13 +720,10 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
     constexpr int TAP = decltype(tapc)::value;
     constexpr int SET = decltype(setc)::value;        // == s & 1
     const int s = ch * 9 + TAP;
-    if constexpr ((DBGK & 4) == 0) {
-      if constexpr (W3) load_w(s + 3 < nst ? s + 3 : nst - 1, std::integral_constant<int, TAP % 3>{});
-      else load_w(s + 2 < nst ? s + 2 : nst - 1, setc);
-    }
-    if constexpr ((DBGK & 84) == 0 && HB == 2) {       // (BC = 64 at its VGPR cap: spills)
+    load_w(s + 2 < nst ? s + 2 : nst - 1, setc);
+    if constexpr (HB == 2) {       // (BC = 64 at its VGPR cap: spills)
       if constexpr (TAP < 7) load_halo_part(ch + 1 < kch ? ch + 1 : ch, tapc);
-    } else if constexpr (TAP == 0 && (DBGK & 20) == 0) {
+    } else if constexpr (TAP == 0) {
       if constexpr (HB == 2) load_halo(ch + 1 < kch ? ch + 1 : ch);
       else if (kch > 1) load_halo(ch + 1 < kch ? ch + 1 : ch);   // uniform: kch per launch
     }
@@ -762,19 +732,12 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 fa[MC], fb[MP];
-      if constexpr ((DBGK & 2) != 0) {
 #pragma unroll
-        for (int mi = 0; mi < MC; ++mi) fa[mi] = dfa[kk][mi];
+      for (int mi = 0; mi < MC; ++mi)
+        fa[mi] = *reinterpret_cast<const bf16x8 *>(sA + abase[mi] + kk * 4 * WPLANE);
 #pragma unroll
-        for (int ni = 0; ni < MP; ++ni) fb[ni] = dfb[kk][ni];
-      } else {
-#pragma unroll
-        for (int mi = 0; mi < MC; ++mi)
-          fa[mi] = *reinterpret_cast<const bf16x8 *>(sA + abase[mi] + kk * 4 * WPLANE);
-#pragma unroll
-        for (int ni = 0; ni < MP; ++ni)
-          fb[ni] = *reinterpret_cast<const bf16x8 *>(sB + bbase[ni] + kk * 4 * G::PLANE);
-      }
+      for (int ni = 0; ni < MP; ++ni)
+        fb[ni] = *reinterpret_cast<const bf16x8 *>(sB + bbase[ni] + kk * 4 * G::PLANE);
 #pragma unroll
       for (int mi = 0; mi < MC; ++mi)
 #pragma unroll
@@ -782,18 +745,18 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi], fb[ni], acc[mi][ni], 0, 0, 0);
     }
     if (s + 1 < nst)
-      store_w(std::integral_constant<int, SET ^ 1>{}, std::integral_constant<int, W3 ? (TAP + 1) % 3 : (SET ^ 1)>{});
+      store_w(std::integral_constant<int, SET ^ 1>{}, std::integral_constant<int, SET ^ 1>{});
     if constexpr (TAP == 8) {
       if (ch + 1 < kch) {
         if constexpr (HB == 1) {
-          if constexpr ((DBGK & 1) == 0) __syncthreads();   // every wave is done reading this chunk's halo
+          __syncthreads();   // every wave is done reading this chunk's halo
           store_halo(0);
         } else {
           store_halo((ch + 1) & 1);
         }
       }
     }
-    if constexpr ((DBGK & 1) == 0) __syncthreads();
+    __syncthreads();
   };
   auto chunk_even = [&](int ch) __attribute__((always_inline)) {          // 9 ch even: s & 1 == TAP & 1
     stage(ch, std::integral_constant<int, 0>{}, I0{});
@@ -817,27 +780,13 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
     stage(ch, std::integral_constant<int, 7>{}, I0{});
     stage(ch, std::integral_constant<int, 8>{}, I1{});
   };
-  if constexpr ((DBGK & 2) != 0) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-      for (int mi = 0; mi < MC; ++mi) dfa[kk][mi] = *reinterpret_cast<const bf16x8 *>(wbuf + abase[mi] + kk * 4 * WPLANE);
-#pragma unroll
-      for (int ni = 0; ni < MP; ++ni) dfb[kk][ni] = *reinterpret_cast<const bf16x8 *>(hbuf + bbase[ni] + kk * 4 * G::PLANE);
-    }
-  }
-  // diagnostics (RR_IGEMM_DBG, timing only -- results are wrong): bit1 runs
-  // the K loop twice, bit0 skips the epilogue
-  const int reps = (a.dbg & 2) ? 2 : 1;
   if constexpr (!RS) {
-    for (int rep = 0; rep < reps; ++rep) {
-      int ch = 0;
-      for (; ch + 2 <= kch; ch += 2) {
-        chunk_even(ch);
-        chunk_odd(ch + 1);
-      }
-      if (ch < kch) chunk_even(ch);
+    int ch = 0;
+    for (; ch + 2 <= kch; ch += 2) {
+      chunk_even(ch);
+      chunk_odd(ch + 1);
     }
+    if (ch < kch) chunk_even(ch);
   } else {
     // weight waves: half of them at BC = 128 (2 x 4 pieces vs 13 halo
     // pieces per thread), a quarter at BC = 64 (2 x 4 vs 8: the same
@@ -988,26 +937,15 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
         rs_store_w(I0{});
       }
       __syncthreads();
-      for (int rep = 0; rep < reps; ++rep) {
-        int ch = 0;
-        for (; ch + 2 <= kch; ch += 2) {
-          even(ch);
-          odd(ch + 1);
-        }
-        if (ch < kch) even(ch);
+      int ch = 0;
+      for (; ch + 2 <= kch; ch += 2) {
+        even(ch);
+        odd(ch + 1);
       }
+      if (ch < kch) even(ch);
     };
     if (wrole) rs_run(I0{});
     else rs_run(I1{});
-  }
-  if (a.dbg & 1) {
-    float t = 0.f;
-#pragma unroll
-    for (int mi = 0; mi < MC; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < MP; ++ni) t += acc[mi][ni][0];
-    if (t == 1234.5f) a.y1[tid] = 1;   // keep the accumulators live
-    return;
   }
 
   // ---- epilogue: fp32 tile into LDS, then the shared staged store ----
@@ -1072,20 +1010,10 @@ Tile pick_tile(const rr_igemm_desc *d) {
   return {64, 128};
 }
 
-// halo tile height: 256 pixels, or 128 (RR_HALO_BP=128) -- per call
-int halo_bp(const rr_igemm_desc *d) {
-  const char *e = getenv("RR_HALO_BP");
-  const int bp = e ? atoi(e) : 256;
-  if (bp != 128) return 256;
-  const int R = 128 / d->w;
-  if (R <= d->h ? (d->h % R) : (R % d->h || d->n % (R / d->h))) return 256;
-  return 128;
-}
-
 // halo path eligibility (bf16 3x3, whole-row 256-pixel tiles); returns BC or 0
 int halo_bc(const rr_igemm_desc *d) {
-  const char *e = getenv("RR_IGEMM_NOHALO");   // A/B switch (per call)
-  if ((e && atoi(e)) || d->dtype != RR_BF16 || d->mode != RR_CONV3X3) return 0;
+  // RR_PATH igemm_halo=0: the per-tap tiled kernel instead (tests)
+  if (!rr_path("igemm_halo", 1) || d->dtype != RR_BF16 || d->mode != RR_CONV3X3) return 0;
   // NCHW fp32 output only through the narrow 16-column tile (image grads)
   if (d->out_nchw && (d->c_out > 16 || d->want_stats || d->c_in2)) return 0;
   const int W = d->w;
@@ -1095,28 +1023,12 @@ int halo_bc(const rr_igemm_desc *d) {
   if (R <= d->h ? (d->h % R) : (R % d->h || d->n % (R / d->h))) return 0;
   if (d->c_in1 % 64 || d->c_in2 % 64) return 0;
   if (d->out_nchw) return 16;
-  // BC = 64 (2 WG/CU) when the K loop is a single 64-channel chunk: the
-  // per-tile prologue / epilogue then dominates and overlap wins
-  const char *e64 = getenv("RR_HALO_BC64_MAXCIN");
-  const int max64 = e64 ? atoi(e64) : 128;   // measured best (tools/ab_igemm.py)
+  // BC = 64 (2 WG/CU) up to 128 input channels: the per-tile prologue /
+  // epilogue then dominates and overlap wins (measured best, tools/ab_igemm.py)
   const bool wide_ok = d->c_out % 128 == 0 && (d->out_split == 0 || d->out_split % 128 == 0);
-  if (wide_ok && d->c_in1 + d->c_in2 > max64) return 128;
+  if (wide_ok && d->c_in1 + d->c_in2 > 128) return 128;
   if (d->c_out % 64 == 0) return 64;
   return 0;
-}
-
-template <int BC, int W, int BP, int NT>
-bool launch_halo_dbgk(const rr_igemm_desc *d, IgemmArgs &a, const dim3 &grid, const dim3 &block, hipStream_t st) {
-  const char *e = getenv("RR_HALO_DBGK");
-  const int k = e ? atoi(e) : 0;
-  if (!k || d->w != W) return false;
-  switch (k) {
-#define DK(v) case v: hipLaunchKernelGGL((igemm3_halo_kernel<BC, W, RR_CONV3X3, BP, NT, v>), grid, block, 0, st, a); break;
-    DK(1) DK(2) DK(3) DK(4) DK(16) DK(32) DK(64) DK(128) DK(192)
-#undef DK
-    default: return false;
-  }
-  return true;
 }
 
 template <int BC, int BP, int NT = 2 * BP>
@@ -1127,24 +1039,8 @@ int launch_halo(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   dim3 grid((unsigned)nblk), block(NT);
   // the image-grad tile runs persistent (2 workgroups per CU, each walking
   // tiles with the next halo in flight) when it has one K chunk
-  // (RR_IMGGRAD_PERSIST=0: one tile per workgroup, for A/B)
   if constexpr (BC < 64) {
-    const char *e = getenv("RR_IMGGRAD_PERSIST");            // per call (A/B)
-    const bool persist = !(e && atoi(e) == 0);
-    if (persist && a.cin == 64 && a.ncblk == 1 && !a.dbg && nblk > 512) grid = dim3(512);
-  }
-  if constexpr (BC == 128 && BP == 256 && NT == 512) {
-    if (launch_halo_dbgk<BC, 8, BP, NT>(d, a, grid, block, st) || launch_halo_dbgk<BC, 16, BP, NT>(d, a, grid, block, st) ||
-        launch_halo_dbgk<BC, 32, BP, NT>(d, a, grid, block, st)) {
-      RR_CHECK_LAUNCH();
-      return RR_OK;
-    }
-  }
-  if constexpr (BC == 64 && BP == 256 && NT == 512) {
-    if (launch_halo_dbgk<BC, 32, BP, NT>(d, a, grid, block, st) || launch_halo_dbgk<BC, 16, BP, NT>(d, a, grid, block, st)) {
-      RR_CHECK_LAUNCH();
-      return RR_OK;
-    }
+    if (a.cin == 64 && a.ncblk == 1 && nblk > 512) grid = dim3(512);
   }
   switch (d->w) {
     case 64: hipLaunchKernelGGL((igemm3_halo_kernel<BC, 64, RR_CONV3X3, BP, NT>), grid, block, 0, st, a); break;
@@ -1160,19 +1056,9 @@ template <typename T>
 int dispatch(const rr_igemm_desc *d, IgemmArgs &a, hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
     const int hb = halo_bc(d);
-    const int bp = (hb && hb <= 64) ? halo_bp(d) : 256;
-    if (bp == 128) {
-      if (hb == 64) return launch_halo<64, 128>(d, a, st);
-      if (hb == 16) return launch_halo<16, 128>(d, a, st);
-    } else {
-      if (hb == 128) return launch_halo<128, 256>(d, a, st);
-      if (hb == 64) {
-        const char *e = getenv("RR_HALO_NT");      // A/B switch (per call): 256 = 4-wave tiles
-        if (e && atoi(e) == 256) return launch_halo<64, 256, 256>(d, a, st);
-        return launch_halo<64, 256>(d, a, st);
-      }
-      if (hb == 16) return launch_halo<16, 256>(d, a, st);
-    }
+    if (hb == 128) return launch_halo<128, 256>(d, a, st);
+    if (hb == 64) return launch_halo<64, 256>(d, a, st);
+    if (hb == 16) return launch_halo<16, 256>(d, a, st);
   }
   const Tile t = pick_tile(d);
   if (t.bc == 128) return launch_mode<T, 128, 128, 2>(d, a, st);
@@ -1190,7 +1076,7 @@ extern "C" int rr_igemm_stat_blocks(const rr_igemm_desc *d) {
   if (const int r = conv3r_stat_blocks(d)) return r;
   const long long P = (long long)d->n * d->h * d->w;
   const int hb = halo_bc(d);
-  const int bp = hb ? (hb <= 64 ? halo_bp(d) : 256) : pick_tile(d).bp;
+  const int bp = hb ? 256 : pick_tile(d).bp;
   return (int)((P + bp - 1) / bp);
 }
 
@@ -1223,12 +1109,7 @@ static int fill_args(const rr_igemm_desc *d, const void *x1, const void *x2, con
   a.P = (int)P;
   a.cout_t = d->mode == RR_CONVT_UP ? d->c_out / 4 : d->c_out;
   a.out_nchw = d->out_nchw;
-  const char *dbg_env = getenv("RR_IGEMM_DBG");
-  a.dbg = dbg_env ? atoi(dbg_env) : 0;
-  const char *stg_env = getenv("RR_CONV3R_STAGGER");
-  a.stagger = stg_env ? atoi(stg_env) : 0;
-  const char *xcd_env = getenv("RR_XCD_MAP");   // A/B switch (default on)
-  a.xcd = xcd_env ? atoi(xcd_env) : 1;
+  a.xcd = 1;                                   // XCD-aware tile order
   a.ncblk = 1;
   a.bt = nullptr; a.bmean = a.binv = a.baff_s = a.baff_b = a.balpha = nullptr;
   a.bpart = a.bapart = nullptr;
@@ -1256,7 +1137,6 @@ extern "C" const char *rr_igemm_kernel_name(const rr_igemm_desc *d, int bnbwd) {
   if (conv3r_bc(d)) return conv3r_name(d);
   if (d->dtype == RR_BF16) {
     const int hb = halo_bc(d);
-    const int bp = (hb && hb <= 64) ? halo_bp(d) : 256;
     if (hb) {
       static const char *names[3][4] = {
           {"igemm3_halo_kernel<16,8>", "igemm3_halo_kernel<16,16>", "igemm3_halo_kernel<16,32>", "igemm3_halo_kernel<16,64>"},
@@ -1264,7 +1144,6 @@ extern "C" const char *rr_igemm_kernel_name(const rr_igemm_desc *d, int bnbwd) {
           {"igemm3_halo_kernel<128,8>", "igemm3_halo_kernel<128,16>", "igemm3_halo_kernel<128,32>", "igemm3_halo_kernel<128,64>"}};
       const int wi = d->w == 8 ? 0 : d->w == 16 ? 1 : d->w == 32 ? 2 : 3;
       const int bi = hb == 16 ? 0 : hb == 64 ? 1 : 2;
-      (void)bp;
       return names[bi][wi];
     }
   }

@@ -26,8 +26,6 @@ struct IgemmArgs {
   const char *bt;                              // pre-BN activation t [P][cout]
   const float *bmean, *binv, *baff_s, *baff_b, *balpha;
   float *bpart, *bapart;                       // [npblk][cout][3], [npblk][cout/64]
-  int dbg;            // diagnostics (RR_IGEMM_DBG): bit0 skip epilogue, bit1 K loop x2
-  int stagger;        // conv3r: start delay (x 8128 cycles) of every other resident workgroup
   int xcd;            // XCD-aware tile order (RR_XCD_MAP=0 disables)
   // rr_igemm_ex (conv3r register epilogue): PReLU alpha (act & 3 ==
   // RR_ACT_PRELU), residual added before the activation (act & RR_ACT_RES)

@@ -699,8 +699,9 @@ __global__ __launch_bounds__(256) void distort_blur_tiled_kernel(DistCfg a) {
 }
 
 static void launch_blur(const DistCfg &a, long long tp, hipStream_t st) {
-  const char *e = getenv("RR_BLUR_TILED");
-  if (((long long)a.h * a.w) % 256 == 0 && a.c <= 4 && !(e && !atoi(e)))
+  // the LDS-tiled form where whole 256-pixel tiles fit (RR_PATH
+  // blur_tiled=0: the per-pixel kernel, tests)
+  if (((long long)a.h * a.w) % 256 == 0 && a.c <= 4 && rr_path("blur_tiled", 1))
     hipLaunchKernelGGL(distort_blur_tiled_kernel, dim3(rr_grid_cap((tp + 255) / 256, 8192)), dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL(distort_blur_kernel, dim3(rr_grid_cap((tp + 255) / 256, 8192)), dim3(256), 0, st, a);

@@ -1524,10 +1524,9 @@ extern "C" int rr_pack_conv(int dtype, int c_out, int c_in, int k, const float *
 extern "C" int rr_pack_conv_batch(int dtype, int count, const rr_pack_job *jobs, long long total,
                                   rr_stream stream) {
   if (!jobs || count <= 0 || count > PACKB_MAX || total <= 0) return RR_EINVAL;
-  const char *e = getenv("RR_PACK_GRID");
   // ~total / 36 items (8 channels x 9 taps each, two phases); the 1x1 jobs
   // have 9x more per element, so size for ~total / 16 and grid-stride the rest
-  dim3 g(rr_grid_cap((total / 16 + 255) / 256, e ? atoi(e) : 8192)), b(256);
+  dim3 g(rr_grid_cap((total / 16 + 255) / 256, 8192)), b(256);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == RR_BF16)
     hipLaunchKernelGGL(pack_conv_batch_kernel<bf16_t>, g, b, 0, st, count, jobs, total);

@@ -354,14 +354,14 @@ int ilog2(int v) {
 }  // namespace
 
 int stream1_plan(const rr_igemm_desc *d, S1Plan *pl) {
-  const char *e = getenv("RR_STREAM1");           // A/B switch (default on)
-  if (e && !atoi(e)) return 0;
+  // RR_PATH stream1=0: the tiled igemm instead; stream1_minp=N: stream from
+  // N pixels (the tests' small shapes; default 131072, measured, r5ze)
+  if (!rr_path("stream1", 1)) return 0;
   if (!d || d->dtype != RR_BF16) return 0;
   const int mode = d->mode;
   if (mode != RR_CONV1X1 && mode != RR_CONVT_UP && mode != RR_CONVT_DOWN) return 0;
   const long long P = (long long)d->n * d->h * d->w;
-  const char *ep = getenv("RR_STREAM1_MINP");
-  const long long minp = ep ? atoll(ep) : 131072;
+  const long long minp = rr_path("stream1_minp", 131072);
   if (P < minp || P % 16 || P * 16 > 0x7fffffffLL) return 0;
   const int cin = d->c_in1 + d->c_in2;
   const int taps = mode == RR_CONVT_DOWN ? 4 : 1;

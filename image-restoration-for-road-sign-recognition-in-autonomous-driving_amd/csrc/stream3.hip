@@ -57,19 +57,11 @@
 #include <cstdlib>
 #include <type_traits>
 
-// B fragments of the three tap columns: RR_S3_DPP=1 (a separate build, A/B)
-// reads the centre column once per (tap row, k half) and forms the dx = 0 / 2
-// operands by a DPP row rotate of it (lane = pixel within a 16-lane row) plus
-// the two edge pixels of each contiguous run of blocks (exec-masked reads): a
-// third of the LDS fragment traffic.  Measured 15 % slower on the stream3
+// B fragments of the three tap columns: 3 reads per (tap row, k half).
+// Forming the dx = 0 / 2 operands by DPP row rotates of one centre read (a
+// third of the LDS fragment traffic) measured 15 % slower on the stream3
 // layers and -1.1 % on the graph step (profiles/r5n_ablayers_s3.txt,
-// r5n_ablibs.txt): the LDS port was not the limiter, the 16 VALU rotates +
-// selects per block and tap column cost more than the reads they replace.
-// 0 (default): the 3 reads per (tap row, k half).  The MFMA order differs
-// (dy, kb, dx vs dy, dx, kb): both are the same 576-term fp32 dot product.
-#ifndef RR_S3_DPP
-#define RR_S3_DPP 0
-#endif
+// r5n_ablibs.txt): the LDS port was not the limiter.
 
 #ifdef RR_S3_STAMPS
 // diagnostic build only (make s3stamps; tools/s3_stamps.py): per-wave sums of
@@ -193,37 +185,10 @@ template <int N> using ic = std::integral_constant<int, N>;
 
 // a wave's MP 16-pixel blocks of a step: block ni sits brow(ni) image rows and
 // bcol(ni) columns from the wave's first pixel (POOL: 2 rows x 8 MP columns,
-// blocks 2j / 2j + 1 = rows 0 / 1 of columns 16 j ..).  Segments: maximal runs
-// of blocks that continue each other in one row (the DPP B operands, RR_S3_DPP)
+// blocks 2j / 2j + 1 = rows 0 / 1 of columns 16 j ..)
 template <int W, int MP, bool POOL> struct S3Blk {
   static constexpr int brow(int ni) { return POOL ? (ni & 1) : (ni * 16) / W; }
   static constexpr int bcol(int ni) { return POOL ? (ni >> 1) * 16 : (ni * 16) % W; }
-  static constexpr bool needl(int ni) {
-    return !(ni > 0 && brow(ni - 1) == brow(ni) && bcol(ni - 1) + 16 == bcol(ni));
-  }
-  static constexpr bool needr(int ni) {
-    return !(ni + 1 < MP && brow(ni + 1) == brow(ni) && bcol(ni + 1) == bcol(ni) + 16);
-  }
-  static constexpr int nseg() {
-    int k = 0;
-    for (int ni = 0; ni < MP; ++ni) k += needl(ni) ? 1 : 0;
-    return k;
-  }
-  static constexpr int seg_of(int ni) {
-    int g = -1;
-    for (int j = 0; j <= ni; ++j) g += needl(j) ? 1 : 0;
-    return g;
-  }
-  static constexpr int seg_first(int g) {
-    for (int j = 0; j < MP; ++j)
-      if (needl(j) && seg_of(j) == g) return j;
-    return 0;
-  }
-  static constexpr int seg_last(int g) {
-    for (int j = seg_first(g); j < MP; ++j)
-      if (needr(j)) return j;
-    return MP - 1;
-  }
 };
 
 struct Cur {
@@ -417,122 +382,7 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
         }
     }
   };
-  // ---- DPP form of the B operands (RR_S3_DPP): contiguous runs of blocks
-  // in one image row ("segments"); the first block's left neighbour pixel and
-  // the last block's right one come from one exec-masked edge read per
-  // segment (lane frow 0: left, frow 15: right), the inner ones from the
-  // neighbouring block's rotated fragment ----
-  constexpr int NSEG = BK::nseg();
-  // lane part of segment g's edge read (k half kb): left of its first block
-  // (lane frow 0, the dx = 0 read of that lane) or right of its last (frow 15)
-  uint32_t eoff[NSEG][2];
-#pragma unroll
-  for (int g = 0; g < NSEG; ++g)
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-      eoff[g][kb] = frow == 0 ? BK::bcol(BK::seg_first(g)) * 128 + boff[0][kb] : BK::bcol(BK::seg_last(g)) * 128 + boff[2][kb];
-  const bool edge_lane = frow == 0 || frow == 15;
-  const bool lane_l = frow == 0, lane_r = frow == 15;
-  i32x4 eg[2][NSEG];                            // [buffer][segment] edge pixels (lanes frow 0 / 15)
-#pragma unroll
-  for (int b = 0; b < 2; ++b)
-#pragma unroll
-    for (int g = 0; g < NSEG; ++g) eg[b][g] = i32x4{0, 0, 0, 0};
-  auto rot = [](i32x4 v, auto CTRLc) __attribute__((always_inline)) {
-    constexpr int CTRL = decltype(CTRLc)::value;
-    return i32x4{__builtin_amdgcn_mov_dpp(v[0], CTRL, 0xf, 0xf, false),
-                 __builtin_amdgcn_mov_dpp(v[1], CTRL, 0xf, 0xf, false),
-                 __builtin_amdgcn_mov_dpp(v[2], CTRL, 0xf, 0xf, false),
-                 __builtin_amdgcn_mov_dpp(v[3], CTRL, 0xf, 0xf, false)};
-  };
-  auto sel = [](bool c, i32x4 a, i32x4 b) __attribute__((always_inline)) {
-    return i32x4{c ? a[0] : b[0], c ? a[1] : b[1], c ? a[2] : b[2], c ? a[3] : b[3]};
-  };
-  // 6 groups (tap row dy, k half kb), each: the centre fragments of the MP
-  // blocks + one edge read per segment, read one group ahead; then the three
-  // tap columns' MFMAs (order dy, kb, dx)
-  auto mfma_step_dpp = [&](int s0) __attribute__((always_inline)) {
-    uint32_t rba[3][NR];
-#pragma unroll
-    for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-      for (int k = 0; k < NR; ++k) {
-        int r = s0 + q0 + k + dy;
-        r = r >= RING ? r - RING : r;
-        rba[dy][k] = sbase + r * ROWB + x0 * 128;
-      }
-    i32x4 cf[2][MP];                            // [buffer][block] centre-column fragments
-    auto rd = [&](int q) __attribute__((always_inline)) {
-      const int dy = q >> 1, kb = q & 1;
-#pragma unroll
-      for (int ni = 0; ni < MP; ++ni)
-        asm volatile("ds_read_b128 %0, %1 offset:%2"
-                     : "=v"(cf[q & 1][ni]) : "v"(rba[dy][brow(ni)] + boff[1][kb]), "i"(bcol(ni) * 128));
-      if (edge_lane) {
-#pragma unroll
-        for (int g = 0; g < NSEG; ++g)
-          asm volatile("ds_read_b128 %0, %1" : "=v"(eg[q & 1][g])
-                       : "v"(rba[dy][BK::brow(BK::seg_first(g))] + eoff[g][kb]));
-      }
-    };
-    constexpr int NRD = MP + NSEG;
-    static_assert(NRD <= 15, "lgkmcnt");
-    rd(0);
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const int dy = q >> 1, kb = q & 1, b = q & 1;
-      if (q + 1 < 6) {
-        rd(q + 1);
-        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NRD) : "memory");
-      } else {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      }
-#pragma unroll
-      for (int ni = 0; ni < MP; ++ni) asm volatile("" : "+v"(cf[b][ni]));
-#pragma unroll
-      for (int g = 0; g < NSEG; ++g) asm volatile("" : "+v"(eg[b][g]));
-#pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        i32x4 bv[MP];
-        if (dx == 1) {
-#pragma unroll
-          for (int ni = 0; ni < MP; ++ni) bv[ni] = cf[b][ni];
-        } else if (dx == 0) {
-          // pixel x - 1: lane l <- lane l - 1 of its 16-lane row (row_ror:1);
-          // lane 0 <- the previous block's lane 15 (its rotate's lane 0) or the edge
-#pragma unroll
-          for (int ni = 0; ni < MP; ++ni) bv[ni] = rot(cf[b][ni], ic<0x121>{});
-#pragma unroll
-          for (int ni = MP - 1; ni >= 0; --ni)
-            bv[ni] = sel(lane_l, BK::needl(ni) ? eg[b][BK::seg_of(ni)] : bv[ni > 0 ? ni - 1 : 0], bv[ni]);
-        } else {
-          // pixel x + 1: row_ror:15; lane 15 <- the next block's lane 0 or the edge
-#pragma unroll
-          for (int ni = 0; ni < MP; ++ni) bv[ni] = rot(cf[b][ni], ic<0x12F>{});
-#pragma unroll
-          for (int ni = 0; ni < MP; ++ni)
-            bv[ni] = sel(lane_r, BK::needr(ni) ? eg[b][BK::seg_of(ni)] : bv[ni + 1 < MP ? ni + 1 : ni], bv[ni]);
-        }
-        const int t = dy * 3 + dx;
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int mi = 0; mi < MC; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < MP; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                wr[mi][t][kb], __builtin_bit_cast(bf16x8, bv[ni]),
-                (q == 0 && dx == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[mi][ni], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      }
-    }
-  };
   auto mfma_step = [&](int s0) __attribute__((always_inline)) {
-    // (the 256-pixel steps keep the 3 reads: their extra fragment registers
-    // spill the statistics / 32-wide variants)
-    if constexpr (RR_S3_DPP && MP == 2) {
-      mfma_step_dpp(s0);
-      return;
-    }
     // ring slot of input row y0 - 1 + r is s0 + r (mod RING); s0 + r < 2 RING
     uint32_t rba[3][NR];                        // per tap row dy and image row: ring row base (uniform)
 #pragma unroll
@@ -878,20 +728,6 @@ int s3_flags(const rr_igemm_desc *d, bool bnbwd) {
   }
 }
 
-// second pass of a 64 + 64-channel concat input: accumulate onto the first
-// pass, then the caller's epilogue (bias, statistics, ReLU)
-int s3_concat_flags(const rr_igemm_desc *d) {
-  if (d->accumulate || d->has_mask) return -1;
-  const int f = (d->has_bias ? F_BIAS : 0) | (d->want_stats ? F_STATS : 0) |
-                (d->act == RR_ACT_RELU ? F_RELU : 0);
-  switch (f) {
-    case 0: case F_BIAS: case F_STATS: case F_BIAS | F_STATS: case F_RELU: case F_BIAS | F_RELU:
-      return F_ACC | f;
-    default:
-      return -1;
-  }
-}
-
 template <int W, int MP, int F, int STG = -1>
 void launch1(const S3Args &a, int P, hipStream_t st) {
   // the late-epilogue stagger measured faster only for 256-pixel steps
@@ -906,57 +742,22 @@ int launch_w(const S3Args &a, int f, int P, hipStream_t st) {
   // the dgrad (no epilogue) and the bias + ReLU forward in 128-pixel steps
   // too: in the graph-captured step they beat the staggered 256-pixel form
   // by 0.8 % (profiles/r3an_ab_s3_mp4.txt; the stagger had been measured
-  // faster on eager launches).  RR_S3_MP4_MODE (A/B): 0 = 256-pixel steps +
-  // stagger; 2 = 128-pixel steps + stagger; 3 (default) = 128-pixel steps
-  const char *em = getenv("RR_S3_MP4_MODE");
-  const int m4 = em ? atoi(em) : 3;
-  if (m4 == 2 || m4 == 3) {
-    switch (f) {
-      case 0: m4 == 2 ? launch1<W, 2, 0, 1>(a, P, st) : launch1<W, 2, 0, 0>(a, P, st); RR_CHECK_LAUNCH(); return RR_OK;
-      case F_BIAS | F_RELU:
-        m4 == 2 ? launch1<W, 2, F_BIAS | F_RELU, 1>(a, P, st) : launch1<W, 2, F_BIAS | F_RELU, 0>(a, P, st);
-        RR_CHECK_LAUNCH();
-        return RR_OK;
-      default: break;
-    }
-  }
+  // faster on eager launches)
   switch (f) {
-    case 0: launch1<W, 4, 0>(a, P, st); break;
+    case 0: launch1<W, 2, 0, 0>(a, P, st); break;
+    case F_BIAS | F_RELU: launch1<W, 2, F_BIAS | F_RELU, 0>(a, P, st); break;
     case F_BIAS: launch1<W, 4, F_BIAS>(a, P, st); break;
-    case F_STATS:
-    case F_BIAS | F_STATS: {
-      // the BN-statistics forward in 128-pixel steps: with 256-pixel steps
-      // (mode 0) the statistics registers pushed the kernel past 256 VGPRs
-      // (10 spilled at W = 64, 26 at W = 32: scratch traffic in the step
-      // loop, 224 us vs 139 us for the non-statistics 64x64 forward); 128-pixel
-      // steps fit in 220 (graph step +1.3 %, profiles/r3am_ab_s3_stats.txt).
-      // RR_S3_STATS_MODE (A/B): 0 = 256-pixel steps, no stagger; 1 = 256 +
-      // stagger; 2 = 128-pixel steps + stagger; 3 (default) = 128-pixel steps
-      const char *e = getenv("RR_S3_STATS_MODE");
-      const int m = e ? atoi(e) : 3;
-      if (f == F_STATS) {
-        if (m == 1) launch1<W, 4, F_STATS, 1>(a, P, st);
-        else if (m == 2) launch1<W, 2, F_STATS, 1>(a, P, st);
-        else if (m == 3) launch1<W, 2, F_STATS, 0>(a, P, st);
-        else launch1<W, 4, F_STATS>(a, P, st);
-      } else {
-        if (m == 1) launch1<W, 4, F_BIAS | F_STATS, 1>(a, P, st);
-        else if (m == 2) launch1<W, 2, F_BIAS | F_STATS, 1>(a, P, st);
-        else if (m == 3) launch1<W, 2, F_BIAS | F_STATS, 0>(a, P, st);
-        else launch1<W, 4, F_BIAS | F_STATS>(a, P, st);
-      }
-      break;
-    }
+    // the BN-statistics forward in 128-pixel steps: with 256-pixel steps the
+    // statistics registers pushed the kernel past 256 VGPRs (10 spilled at
+    // W = 64, 26 at W = 32: scratch traffic in the step loop, 224 us vs 139
+    // us for the non-statistics 64x64 forward); 128-pixel steps fit in 220
+    // (graph step +1.3 %, profiles/r3am_ab_s3_stats.txt)
+    case F_STATS: launch1<W, 2, F_STATS, 0>(a, P, st); break;
+    case F_BIAS | F_STATS: launch1<W, 2, F_BIAS | F_STATS, 0>(a, P, st); break;
     case F_RELU: launch1<W, 4, F_RELU>(a, P, st); break;
-    case F_BIAS | F_RELU: launch1<W, 4, F_BIAS | F_RELU>(a, P, st); break;
     case F_ACC: launch1<W, 2, F_ACC>(a, P, st); break;
     case F_MASK: launch1<W, 2, F_MASK>(a, P, st); break;
     case F_ACC | F_MASK: launch1<W, 2, F_ACC | F_MASK>(a, P, st); break;
-    case F_ACC | F_BIAS: launch1<W, 2, F_ACC | F_BIAS>(a, P, st); break;
-    case F_ACC | F_STATS: launch1<W, 2, F_ACC | F_STATS>(a, P, st); break;
-    case F_ACC | F_BIAS | F_STATS: launch1<W, 2, F_ACC | F_BIAS | F_STATS>(a, P, st); break;
-    case F_ACC | F_RELU: launch1<W, 2, F_ACC | F_RELU>(a, P, st); break;
-    case F_ACC | F_BIAS | F_RELU: launch1<W, 2, F_ACC | F_BIAS | F_RELU>(a, P, st); break;
     case F_BNBWD: launch1<W, 2, F_BNBWD>(a, P, st); break;
     default: return RR_EUNSUPPORTED;
   }
@@ -967,22 +768,16 @@ int launch_w(const S3Args &a, int f, int P, hipStream_t st) {
 }  // namespace
 
 int stream3_blocks(const rr_igemm_desc *d, int bnbwd) {
-  const char *e = getenv("RR_STREAM3");
-  if (e && !atoi(e)) return 0;
+  // RR_PATH stream3=0: the tap-reuse / halo kernels instead (tests)
+  if (!rr_path("stream3", 1)) return 0;
   if (d->dtype != RR_BF16 || d->mode != RR_CONV3X3) return 0;
   if (d->c_in1 != 64 || d->c_out != 64 || d->out_split || d->out_nchw) return 0;
   if (d->w != 64 && d->w != 32) return 0;
-  if (d->c_in2 == 64) {
-    // concat input (dec1: 64 + 64 -> 64): two passes, the second accumulating
-    // onto the first's bf16 half -- only with RR_STREAM3_CONCAT=1 (A/B).  By
-    // default the tap-reuse conv takes the layer in one pass with the whole
-    // K = 1152 sum in fp32: the same graph-step time (profiles/
-    // r4j_abstep_concat_splitdgrad.txt) without the extra bf16 rounding
-    const char *ec = getenv("RR_STREAM3_CONCAT");
-    if (!(ec && atoi(ec)) || bnbwd || s3_concat_flags(d) < 0) return 0;
-  } else if (d->c_in2 != 0 || s3_flags(d, bnbwd != 0) < 0) {
-    return 0;
-  }
+  // (a concat input, dec1's 64 + 64 -> 64, goes to the tap-reuse conv in
+  // one pass with the whole K = 1152 sum in fp32: the same graph-step time
+  // as two streaming passes, profiles/r4j_abstep_concat_splitdgrad.txt,
+  // without a bf16 rounding of the half sum)
+  if (d->c_in2 != 0 || s3_flags(d, bnbwd != 0) < 0) return 0;
   // eligibility independent of the step size: whole 256-pixel steps (the
   // larger one) and at least one per workgroup
   if (d->h % (256 / d->w)) return 0;
@@ -1023,17 +818,10 @@ int stream3_launch_pool(const rr_igemm_desc *d, const S3Args &a0, hipStream_t st
   S3Args a = a0;
   a.wld = 64; a.woff = 0;
   const int P = d->n * d->h * d->w;
-  // 128-pixel steps, no stagger: the bias + ReLU forward's form (launch_w).
-  // RR_S3_POOL_MP=4 (A/B): 256-pixel steps (4 rows, 2 row pairs) at W = 64,
-  // bitwise equal and within the run order's noise (174 / 162 us measured
-  // first / second on one box, 179 / 178 us in the reverse order on another,
-  // profiles/r5zi_pool_bench.jsonl, r5zj_pool_bench.jsonl)
-  const char *emp = getenv("RR_S3_POOL_MP");
-  const bool mp4 = emp && atoi(emp) == 4;
-  if (d->w == 64 && mp4) {
-    if (d->has_bias) launch1<64, 4, F_BIAS | F_RELU | F_POOL, 0>(a, P, st);
-    else launch1<64, 4, F_RELU | F_POOL, 0>(a, P, st);
-  } else if (d->w == 64) {
+  // 128-pixel steps, no stagger: the bias + ReLU forward's form (launch_w;
+  // 256-pixel steps at W = 64 were bitwise equal and within the run order's
+  // noise, profiles/r5zi_pool_bench.jsonl, r5zj_pool_bench.jsonl)
+  if (d->w == 64) {
     if (d->has_bias) launch1<64, 2, F_BIAS | F_RELU | F_POOL, 0>(a, P, st);
     else launch1<64, 2, F_RELU | F_POOL, 0>(a, P, st);
   } else {
@@ -1049,18 +837,6 @@ int stream3_launch(const rr_igemm_desc *d, const S3Args &a0, int bnbwd, hipStrea
   S3Args a = a0;
   const int P = d->n * d->h * d->w;
   auto go = [&](const S3Args &x, int f) { return d->w == 64 ? launch_w<64>(x, f, P, st) : launch_w<32>(x, f, P, st); };
-  if (d->c_in2 == 64) {
-    // conv(cat(x1, x2)) = conv(x1, W[:, :64]) + conv(x2, W[:, 64:]): pass 1
-    // writes the x1 half (bf16), pass 2 adds the x2 half and applies the
-    // epilogue to the sum (statistics of the pre-bias sum, as one pass)
-    S3Args p1 = a;
-    p1.x2 = nullptr; p1.bias = nullptr; p1.stats = nullptr; p1.mask = nullptr;
-    p1.wld = 128; p1.woff = 0; p1.accumulate = 0;
-    if (const int rc = go(p1, 0)) return rc;
-    S3Args p2 = a;
-    p2.x = a.x2; p2.x2 = nullptr; p2.wld = 128; p2.woff = 64; p2.accumulate = 1;
-    return go(p2, s3_concat_flags(d));
-  }
   S3Args p = a;
   p.wld = 64; p.woff = 0;
   return go(p, s3_flags(d, bnbwd != 0));

@@ -14,7 +14,6 @@ struct SWArgs {
   int n, h;                  // w is the template width
   int nwg_ps;                // workgroups per (dy slice, input slice) pair
   int nsteps;                // 128-pixel steps (n h w / 128)
-  unsigned long long *ts;    // debug phase timestamps [nwg][4] or null
 };
 
 // nonzero when the descriptor is handled by the streaming kernel

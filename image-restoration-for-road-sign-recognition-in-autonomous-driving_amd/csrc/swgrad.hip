@@ -120,10 +120,6 @@ __global__ __launch_bounds__(512, 2) void swgrad_kernel(SWArgs a) {
   const bool first = ci0 < a.c1;
   const char *const xsrc = (first ? a.x1 : a.x2) + (first ? ci0 : ci0 - a.c1) * 2;
   const int xpb = (first ? a.c1 : a.c2) * 2;              // bytes per source pixel
-  auto stamp = [&](int k) __attribute__((always_inline)) {
-    if (a.ts && tid == 0) a.ts[blockIdx.x * 4 + k] = __builtin_amdgcn_s_memrealtime();
-  };
-  stamp(0);
 
   // ---- halo columns: zeroed once, never written by the DMA ----
   for (int u = tid; u < RING * 16; u += 512) {
@@ -283,7 +279,6 @@ __global__ __launch_bounds__(512, 2) void swgrad_kernel(SWArgs a) {
     advance(cp);
     return cp.c < cend;
   };
-  stamp(1);
 #pragma unroll 1
   while (true) {
     if (!step(std::integral_constant<int, 0>())) break;
@@ -292,7 +287,6 @@ __global__ __launch_bounds__(512, 2) void swgrad_kernel(SWArgs a) {
     if (!step(std::integral_constant<int, 3>())) break;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  stamp(2);
 
   // ---- partial dW: split r of the [nwg_ps][64][9][c1 + c2] slabs reduced by
   // rr_wgrad's reduce (wgrad.hip).  Staged through LDS in two halves (m) so
@@ -318,7 +312,6 @@ __global__ __launch_bounds__(512, 2) void swgrad_kernel(SWArgs a) {
     }
     __syncthreads();
   }
-  stamp(3);
 }
 
 }  // namespace
@@ -326,8 +319,8 @@ __global__ __launch_bounds__(512, 2) void swgrad_kernel(SWArgs a) {
 static int sw_slices(const rr_wgrad_desc *d) { return (d->c_in1 + d->c_in2) / 64 * (d->c_out / 64); }
 
 int swgrad_ok(const rr_wgrad_desc *d) {
-  const char *e = getenv("RR_SWGRAD");
-  if (e && !atoi(e)) return 0;
+  // RR_PATH swgrad=0: the halo / tiled weight grads instead (tests)
+  if (!rr_path("swgrad", 1)) return 0;
   if (d->dtype != RR_BF16 || d->mode != RR_CONV3X3 || d->c_out % 64 || d->c_out > 128) return 0;
   if (d->w != 64 && d->w != 32) return 0;
   if (d->c_in1 % 64 || d->c_in2 % 64 || d->c_in1 + d->c_in2 > 192 || d->c_in1 <= 0) return 0;
@@ -354,34 +347,9 @@ int swgrad_launch(const rr_wgrad_desc *d, const void *dy, const void *x1, const 
   a.h = d->h;
   a.nwg_ps = SW_WG / S;
   a.nsteps = (int)((long long)d->n * d->h * d->w / 128);
-  // RR_SW_TS=1: per-workgroup phase times to stderr (debug; synchronizes)
-  static unsigned long long *tsb = nullptr;
-  const bool ts = getenv("RR_SW_TS") != nullptr;
-  if (ts && !tsb && hipMalloc(&tsb, SW_WG * 4 * 8) != hipSuccess) tsb = nullptr;
-  a.ts = ts ? tsb : nullptr;
   const dim3 grid(a.nwg_ps * S), block(512);
   if (d->w == 64) hipLaunchKernelGGL(swgrad_kernel<64>, grid, block, 0, st, a);
   else hipLaunchKernelGGL(swgrad_kernel<32>, grid, block, 0, st, a);
   RR_CHECK_LAUNCH();
-  if (a.ts) {
-    static unsigned long long h[SW_WG * 4];
-    const int nb = a.nwg_ps * S;
-    (void)hipStreamSynchronize(st);
-    (void)hipMemcpy(h, tsb, nb * 4 * 8, hipMemcpyDeviceToHost);
-    unsigned long long t0 = ~0ull, t3 = 0;
-    for (int b = 0; b < nb; ++b) {
-      t0 = h[b * 4] < t0 ? h[b * 4] : t0;
-      t3 = h[b * 4 + 3] > t3 ? h[b * 4 + 3] : t3;
-    }
-    double ph[3] = {0, 0, 0}, mx[3] = {0, 0, 0};
-    for (int b = 0; b < nb; ++b)
-      for (int k = 0; k < 3; ++k) {
-        const double dt = (h[b * 4 + k + 1] - h[b * 4 + k]) * 0.01;
-        ph[k] += dt / nb;
-        mx[k] = dt > mx[k] ? dt : mx[k];
-      }
-    fprintf(stderr, "swgrad ts: total %.1f us  prologue %.1f/%.1f  loop %.1f/%.1f  epilogue %.1f/%.1f (mean/max)\n",
-            (t3 - t0) * 0.01, ph[0], mx[0], ph[1], mx[1], ph[2], mx[2]);
-  }
   return RR_OK;
 }

@@ -39,7 +39,7 @@ struct WgradArgs {
   int split_len;           // pixels per split (multiple of BKP)
   int nablk, nbblk;
   FastDiv fd_w, fd_hw;
-  int xcd;                 // XCD-aware workgroup order (RR_XCD_MAP)
+  int xcd;                 // XCD-aware workgroup order (always on)
 };
 
 // XCD-aware order (workgroup b runs on XCD b % 8): XCD x takes the
@@ -281,19 +281,20 @@ struct Halo3Args {
   int stages;              // total 64-pixel stages (P / 64)
   int split_stages;        // stages per split
   int nablk, nbblk;
-  int xcd;                 // XCD-aware workgroup order (RR_XCD_MAP)
+  int xcd;                 // XCD-aware workgroup order (always on)
 };
 
 // MA: 16-row MFMA blocks of dy channels per wave (the wave tile is 16 MA dy
 // channels x 64 / MA x channels).  MA = 4: each wave owns all 64 dy channels
 // of the tile and 16 x channels, so per 32-pixel step it reads 4 A fragments
 // (reused over the 9 taps) and 9 B fragments -- 13 transposed fragment reads
-// per 36 MFMAs instead of the 2 x 2 tile's 20 (MA = 2): the LDS read port, at
-// ~2x the MFMA time on the 2 x 2 tile, was what bound this kernel
-// PF: stages of global prefetch in flight (2: two register sets, a stage's
-// loads issued two compute phases before their LDS write)
-template <int W, int MA, int PF>
+// per 36 MFMAs instead of the 2 x 2 tile's 20: the LDS read port, at ~2x the
+// MFMA time on the 2 x 2 tile, was what bound this kernel.  Two stages of
+// global prefetch in flight (two register sets, a stage's loads issued two
+// compute phases before their LDS write; one stage measured slower)
+template <int W>
 __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
+  constexpr int MA = 4;
   constexpr int MB = 4 / MA;                   // 16-column x blocks per wave
   constexpr int WA = 4 / MA;                   // waves along the dy channels
   constexpr int R = 64 / W;                    // image rows per stage
@@ -327,7 +328,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
   const int hw = a.h * a.w;
 
   typedef uint4 V;
-  V ra[LA], rb[LB], ra2[PF == 2 ? LA : 1], rb2[PF == 2 ? LB : 1];
+  V ra[LA], rb[LB], ra2[LA], rb2[LB];
   auto gload_to = [&](int st, V *ra, V *rb) __attribute__((always_inline)) {
     const int p0 = st * 64;                    // first pixel of the stage
     const int nn = p0 / hw;
@@ -423,20 +424,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
       }
     }
   };
-  if constexpr (PF == 1) {
-    if (nst > 0) {
-      gload(sbeg);
-      swrite(0);
-      __syncthreads();
-    }
-    for (int s = 0; s < nst; ++s) {
-      const int buf = s & 1;
-      if (s + 1 < nst) gload(sbeg + s + 1);
-      compute(buf);
-      if (s + 1 < nst) swrite(buf ^ 1);
-      __syncthreads();
-    }
-  } else {
+  {
     // register set (ra2, rb2) holds the odd stages, (ra, rb) the even ones
     if (nst > 0) {
       gload(sbeg);
@@ -630,8 +618,7 @@ static bool halo_ok(const rr_wgrad_desc *d) {
   if (!(d->w == 8 || d->w == 16 || d->w == 32 || d->w == 64)) return false;
   if (d->h % (64 / d->w)) return false;
   if (d->c_out % 64 || d->c_in1 % 64 || d->c_in2 % 64) return false;
-  const char *e = getenv("RR_WGRAD_NOHALO");
-  return !(e && atoi(e));
+  return rr_path("wgrad_halo", 1) != 0;   // RR_PATH wgrad_halo=0: the tiled kernel (tests)
 }
 
 struct HaloPlan { int stages, split_stages, nsplit; };
@@ -641,11 +628,10 @@ static HaloPlan halo_plan(const rr_wgrad_desc *d) {
   const long long P = (long long)d->n * d->h * d->w;
   p.stages = (int)(P / 64);
   const int tiles = (d->c_out / 64) * ((d->c_in1 + d->c_in2) / 64);
-  static const int target = [] {
-    const char *e = getenv("RR_WGRAD_HALO_WGS");
-    return e ? atoi(e) : 512;
-  }();
-  int want = (target + tiles - 1) / tiles;          // ~target workgroups (512 = one full wave at 2 blocks/CU, measured best)
+  // ~512 workgroups (one full wave at 2 blocks/CU, measured best: 256 and
+  // 1024 were 2.5 % / 1.5 % slower on the step, r5y / r5zc)
+  const int target = 512;
+  int want = (target + tiles - 1) / tiles;
   int maxs = (p.stages + 3) / 4;                    // >= 4 stages per split
   int ns = want < maxs ? want : maxs;
   if (ns < 1) ns = 1;
@@ -755,8 +741,7 @@ extern "C" int rr_wgrad_partial(const rr_wgrad_desc *d, const void *dy, const vo
   a.P = (int)P;
   a.split_len = pl.split_len;
   a.nablk = pl.nablk; a.nbblk = pl.nbblk;
-  const char *xcd_env = getenv("RR_XCD_MAP");
-  a.xcd = xcd_env ? atoi(xcd_env) : 1;
+  a.xcd = 1;                                   // XCD-aware workgroup order
   a.fd_w = make_fastdiv((uint32_t)d->w);
   a.fd_hw = make_fastdiv((uint32_t)(d->h * d->w));
   hipStream_t st = (hipStream_t)stream;
@@ -778,33 +763,11 @@ extern "C" int rr_wgrad_partial(const rr_wgrad_desc *d, const void *dy, const vo
     ha.nablk = ha.CA / 64; ha.nbblk = ha.CB / 64;
     ha.xcd = a.xcd;
     const dim3 grid((unsigned)(ha.nablk * ha.nbblk * hp.nsplit)), block(256);
-    // RR_WGRAD_HALO_MA=2: the 2 x 2 wave tiles (A/B)
-    const char *mae = getenv("RR_WGRAD_HALO_MA");
-    const int ma = mae && atoi(mae) == 2 ? 2 : 4;
-    // RR_WGRAD_HALO_PF=1: one stage of global prefetch (A/B)
-    const char *pfe = getenv("RR_WGRAD_HALO_PF");
-    const int pf = pfe && atoi(pfe) == 1 ? 1 : 2;
-    if (ma == 4 && pf == 2) {
-      switch (d->w) {
-        case 64: hipLaunchKernelGGL((wgrad3_halo_kernel<64, 4, 2>), grid, block, 0, st, ha); break;
-        case 32: hipLaunchKernelGGL((wgrad3_halo_kernel<32, 4, 2>), grid, block, 0, st, ha); break;
-        case 16: hipLaunchKernelGGL((wgrad3_halo_kernel<16, 4, 2>), grid, block, 0, st, ha); break;
-        default: hipLaunchKernelGGL((wgrad3_halo_kernel<8, 4, 2>), grid, block, 0, st, ha); break;
-      }
-    } else if (ma == 4) {
-      switch (d->w) {
-        case 64: hipLaunchKernelGGL((wgrad3_halo_kernel<64, 4, 1>), grid, block, 0, st, ha); break;
-        case 32: hipLaunchKernelGGL((wgrad3_halo_kernel<32, 4, 1>), grid, block, 0, st, ha); break;
-        case 16: hipLaunchKernelGGL((wgrad3_halo_kernel<16, 4, 1>), grid, block, 0, st, ha); break;
-        default: hipLaunchKernelGGL((wgrad3_halo_kernel<8, 4, 1>), grid, block, 0, st, ha); break;
-      }
-    } else {
-      switch (d->w) {
-        case 64: hipLaunchKernelGGL((wgrad3_halo_kernel<64, 2, 1>), grid, block, 0, st, ha); break;
-        case 32: hipLaunchKernelGGL((wgrad3_halo_kernel<32, 2, 1>), grid, block, 0, st, ha); break;
-        case 16: hipLaunchKernelGGL((wgrad3_halo_kernel<16, 2, 1>), grid, block, 0, st, ha); break;
-        default: hipLaunchKernelGGL((wgrad3_halo_kernel<8, 2, 1>), grid, block, 0, st, ha); break;
-      }
+    switch (d->w) {
+      case 64: hipLaunchKernelGGL((wgrad3_halo_kernel<64>), grid, block, 0, st, ha); break;
+      case 32: hipLaunchKernelGGL((wgrad3_halo_kernel<32>), grid, block, 0, st, ha); break;
+      case 16: hipLaunchKernelGGL((wgrad3_halo_kernel<16>), grid, block, 0, st, ha); break;
+      default: hipLaunchKernelGGL((wgrad3_halo_kernel<8>), grid, block, 0, st, ha); break;
     }
     RR_CHECK_LAUNCH();
     return RR_OK;

@@ -13,6 +13,20 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # RR_LIB_PATH: load another build of the same ABI (A/B of two builds on one box)
 LIB_PATH = os.environ.get("RR_LIB_PATH") or os.path.join(_HERE, "libroadrestore.so")
 
+
+
+def path_flag(key: str, default: int) -> int:
+    """The stack's one A/B and test knob, shared with the library
+    (csrc/common.h rr_path): RR_PATH="key=value[,key=value...]".  Every
+    default is the measured-best path; the Python schedule reads its fusion
+    keys (fused_pool=0, split_dgrad=0, ...) once at import."""
+    for item in os.environ.get("RR_PATH", "").split(","):
+        k, sep, v = item.partition("=")
+        if sep and k.strip() == key:
+            return int(v)
+    return default
+
+
 RR_F32, RR_BF16 = 0, 1
 RR_CONV3X3, RR_CONV1X1, RR_CONVT_UP, RR_CONVT_DOWN = 0, 1, 2, 3
 RR_ACT_NONE, RR_ACT_RELU, RR_ACT_PRELU, RR_ACT_RES, RR_ACT_POOL, RR_ACT_NOFULL = 0, 1, 2, 4, 8, 16

@@ -18,12 +18,11 @@ Reference schedules mirrored (file:line in the reference repo):
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
 from . import ops
-from ._lib import RR_CONV1X1, RR_CONV3X3, RR_CONVT_DOWN, RR_CONVT_UP
+from ._lib import RR_CONV1X1, RR_CONV3X3, RR_CONVT_DOWN, RR_CONVT_UP, path_flag
 
 RELU = 1
 
@@ -69,12 +68,16 @@ class WeightCache:
         return (w.data_ptr(), w._version, 0 if self.static else GENERATION[0],
                 None if also is None else (also.data_ptr(), also._version))
 
-    def _get(self, w, dtype, kind, fn, also=None):
+    def _get(self, w, dtype, kind, fn, also=None, record=True):
         cap = torch.cuda.is_current_stream_capturing()
         key = (id(w), dtype, kind)
         ver = self._ver(w, also)
-        if not self.static and w.is_cuda:
-            self._misc[key] = (w, fn, also)        # (re-)recorded by every use
+        # the non-conv packs (re-)recorded by every use for the next
+        # prefetch(); conv packs are the plan's (the batched re-pack), so a
+        # conv reaching here (the first forward, before the plan exists) is
+        # not recorded again as a per-layer pack
+        if record and not self.static and w.is_cuda:
+            self._misc[key] = (w, fn, also)
         f = self._fresh.get(key)
         if f is not None and f[0] == ver:
             return f[1]                  # made by a prefetch() of this forward
@@ -124,8 +127,11 @@ class WeightCache:
         side = _pack_stream(w0.device)
         side.wait_stream(torch.cuda.current_stream(w0.device))
         main = torch.cuda.current_stream(w0.device)
+        # the packs are built into local dicts and published to _fresh / _c
+        # only by the next begin(), after its wait on the side stream: until
+        # then nothing on the main stream can see buffers still being written
         with torch.cuda.stream(side):
-            self.begin()
+            fresh, cache = self._repack()
             # the small non-conv packs too (3 convT + 3 bias tiles + the
             # first conv: ~5 us launches each in front of their layers)
             misc, self._misc = self._misc, {}     # the packs the last forward asked for
@@ -134,30 +140,37 @@ class WeightCache:
                 for t in (v if isinstance(v, (tuple, list)) else (v,)):
                     if isinstance(t, torch.Tensor):
                         t.record_stream(main)
-                self._fresh[key] = (self._ver(w, also), v)
+                fresh[key] = (self._ver(w, also), v)
             ev = torch.cuda.Event()
             ev.record(side)
-        self._pending = (ev, self._fresh)
+        self._pending = (ev, fresh, cache)
         return True
 
     def begin(self):
         """Start of a forward: one batched re-pack of every planned conv (or
         the join of a prefetch() of it)."""
         if self._pending is not None:
-            ev, fresh = self._pending
+            ev, fresh, cache = self._pending
             self._pending = None
             torch.cuda.current_stream().wait_event(ev)
-            self._fresh = fresh
-            return
-        self._fresh = {}
+        else:
+            fresh, cache = self._repack()
+        self._fresh = fresh
+        self._c.update(cache)
+
+    def _repack(self):
+        """The batched re-pack of every planned conv when any is stale or a
+        graph is being captured: (fresh, cache) entries for the caller to
+        publish (nothing is published here)."""
+        fresh, cache = {}, {}
         if not self._plan:
-            return
+            return fresh, cache
         cap = torch.cuda.is_current_stream_capturing()
         ent = list(self._plan.values())
         keys = [(id(w), dt, "conv+d" if dg else "conv") for w, dt, dg in ent]
         vers = [self._ver(w) for w, _, _ in ent]
         if cap and self.static and all(self._c.get(k, (None,))[0] == v for k, v in zip(keys, vers)):
-            return                                   # conv() hits the pre-capture packs
+            return fresh, cache                      # conv() hits the pre-capture packs
         ok = self._batch is not None and self._batch.valid() and \
             self._batch.entries == [tuple(e) for e in ent]
         if not ok and not cap and all(w.is_contiguous() for w, _, _ in ent) and \
@@ -167,14 +180,15 @@ class WeightCache:
             self._batch = ops.PackBatch([tuple(e) for e in ent])
             ok = True
         if not cap and all(self._c.get(k, (None,))[0] == v for k, v in zip(keys, vers)):
-            return
+            return fresh, cache
         if not ok:
-            return                                   # per-layer packs instead
+            return fresh, cache                      # per-layer packs instead
         outs = self._batch.run()
         for k, v, o in zip(keys, vers, outs):
-            self._fresh[k] = (v, o)
+            fresh[k] = (v, o)
             if not cap:
-                self._c[k] = (v, o)
+                cache[k] = (v, o)
+        return fresh, cache
 
     def conv(self, w, dtype, dgrad):
         kind = "conv+d" if dgrad else "conv"
@@ -191,7 +205,7 @@ class WeightCache:
             self._batch = None
         elif dgrad and not p[2]:
             p[2] = True
-        return self._get(w, dtype, kind, lambda: ops.pack_conv(w, dtype, True, dgrad))
+        return self._get(w, dtype, kind, lambda: ops.pack_conv(w, dtype, True, dgrad), record=False)
 
     def convT(self, w, dtype, down):
         kind = "convT+d" if down else "convT"
@@ -270,11 +284,8 @@ class GradSink:
         return out
 
 
-
-_DIAG_SKIP_A1 = os.environ.get("RR_DIAG_SKIP_A1", "0") != "0"
-
 # A/B switch for the fused conv-dgrad + BN/PReLU backward reduce (default on)
-FUSE_BNBWD = os.environ.get("RR_FUSE_BNBWD", "1") not in ("0", "")
+FUSE_BNBWD = path_flag("fuse_bnbwd", 1) != 0
 
 def _params(*mods):
     out = []
@@ -416,7 +427,7 @@ def _bn_affine(bn, st, bias, count, training, out=None, need_bwd=False):
 
 
 # A/B switch: the tail BN and the shortcut BN finalized by one launch
-_PAIR_FINALIZE = os.environ.get("RR_BN_PAIR_FINALIZE", "1") != "0"
+_PAIR_FINALIZE = path_flag("bn_pair_finalize", 1) != 0
 
 
 def _momentum(bn):
@@ -440,9 +451,9 @@ def block_has_shortcut(blk):
     return len(blk.shortcut) > 0
 
 
-# A/B switch: eval-mode BN folded into the conv weights (RR_FOLD_BN=0: conv +
-# separate BN affine passes, as in training)
-_FOLD_BN = os.environ.get("RR_FOLD_BN", "1") != "0"
+# A/B switch: eval-mode BN folded into the conv weights (RR_PATH fold_bn=0:
+# conv + separate BN affine passes, as in training)
+_FOLD_BN = path_flag("fold_bn", 1) != 0
 
 
 def resblock_forward_eval_folded(blk, x1, x2, n, h, w, wc, dt, pool=False):
@@ -524,10 +535,7 @@ def resblock_forward(blk, x1, x2, n, h, w, wc, dt, training, need_bwd, pool=Fals
     pk1 = wc.conv(c1.weight, dt, dgrad=need_bwd)
     t1, _, st1 = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, pk1[0], cout, bias=c1.bias, stats=training)
     s1, sh1, m1, i1 = _bn_affine(bn1, st1, c1.bias, P, training, need_bwd=need_bwd)
-    # (diagnostic, timing only -- results are wrong: RR_DIAG_SKIP_A1=1 feeds
-    # t1 to conv2 without the BN1 + PReLU pass, the upper bound of folding
-    # that pass into conv2's operand loads)
-    a1 = t1 if _DIAG_SKIP_A1 else ops.affine_act(t1, s1, sh1, alpha=pr.weight)
+    a1 = ops.affine_act(t1, s1, sh1, alpha=pr.weight)
     pk2 = wc.conv(c2.weight, dt, dgrad=need_bwd)
     t2, _, st2 = ops.igemm(RR_CONV3X3, a1, None, n, h, w, pk2[0], cout, bias=c2.bias, stats=training)
     has_sc = block_has_shortcut(blk)
@@ -603,19 +611,11 @@ def resblock_backward(blk, S, g_out, sink, pool=None, convout=None, reduce_side=
     # eval-mode BatchNorm: running statistics, no batch-statistic terms, and
     # the conv biases feeding the BNs get their (non-zero) grads
     ev = bool(S.get("eval"))
-    side = _side_stream(g_out.device) if _WGRAD_SIDE and g_out.is_cuda else None
-
     # (reduce_side: the caller joins the reduce stream, join_wgrad_reduces)
-    rs = reduce_stream(x1.device) if reduce_side and side is None and x1.is_cuda else None
+    rs = reduce_stream(x1.device) if reduce_side and x1.is_cuda else None
 
     def wgrad(*args, **kw):
-        # every operand stays referenced in this frame until the join below
-        if side is None:
-            ops.wgrad(*args, reduce_stream=rs, **kw)
-            return
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            ops.wgrad(*args, **kw)
+        ops.wgrad(*args, reduce_stream=rs, **kw)
     if has_sc:
         sc0, sc1 = blk.shortcut[0], blk.shortcut[1]
         # the ReLU mask from t2 and s as the forward formed the output (mask
@@ -690,8 +690,6 @@ def resblock_backward(blk, S, g_out, sink, pool=None, convout=None, reduce_side=
                 gx2 = ops.igemm_dgrad_sc(dt1, n, h, w, S.pk1[1][half:], 64, ds, S.pks[1][hs:]) \
                     if gx1 is not None else None
                 if gx2 is not None:
-                    if side is not None:
-                        torch.cuda.current_stream().wait_stream(side)
                     sink.ready(_params(blk))
                     return gx1, gx2
             gx1, _, _ = ops.igemm(RR_CONV3X3, dt1, None, n, h, w, S.pk1[1][:half], 64)
@@ -702,34 +700,8 @@ def resblock_backward(blk, S, g_out, sink, pool=None, convout=None, reduce_side=
                   accumulate=True)
     else:
         ops.igemm(RR_CONV3X3, dt1, None, n, h, w, S.pk1[1], cin, out=gx1, accumulate=True)
-    if side is not None:
-        torch.cuda.current_stream().wait_stream(side)
     sink.ready(_params(blk))
     return gx1, gx2
-
-
-# named points of the ResUNet forward where callers may start work on a side
-# stream (VGGPerceptualLoss.prefetch_target(at=...)): a callback registered
-# for a point runs once, on the forward's stream, right after that block
-FORWARD_POINTS = ("start", "res1", "res2", "res3", "bottleneck", "dec3", "dec2")
-_AT_POINT = {}
-
-
-def at_forward_point(name, fn):
-    if name not in FORWARD_POINTS:
-        raise ValueError(f"unknown forward point {name!r} (one of {FORWARD_POINTS})")
-    _AT_POINT.setdefault(name, []).append(fn)
-
-
-def drop_forward_point(fn):
-    for fns in _AT_POINT.values():
-        while fn in fns:
-            fns.remove(fn)
-
-
-def _reached(name):
-    for fn in _AT_POINT.pop(name, ()):
-        fn()
 
 
 def resunet_block_names():
@@ -749,7 +721,6 @@ def _skip_align(u, h, w):
 
 def resunet_forward(m, x, wc, dt, training, need_bwd):
     wc.begin()
-    _reached("start")
     n, _, H, W = x.shape
     if H < 8 or W < 8:
         raise ValueError("ResUNet needs H, W >= 8 (three 2x2 max-pools, floor mode)")
@@ -767,26 +738,20 @@ def resunet_forward(m, x, wc, dt, training, need_bwd):
         S.e1pre = e1pre
     r1, S.res1, (p1, i1) = resblock_forward(m.res1, e1, None, n, H, W, wc, dt, training, need_bwd,
                                             pool=True)
-    _reached("res1")
     r2, S.res2, (p2, i2) = resblock_forward(m.res2, p1, None, n, H2, W2, wc, dt, training,
                                             need_bwd, pool=True)
-    _reached("res2")
     r3, S.res3, (p3, i3) = resblock_forward(m.res3, p2, None, n, H3, W3, wc, dt, training,
                                             need_bwd, pool=True)
-    _reached("res3")
     b = p3
     for i in range(3):
         b, S[f"bottleneck.{i}"] = resblock_forward(m.bottleneck[i], b, None, n, H4, W4, wc,
                                                    dt, training, need_bwd)
-    _reached("bottleneck")
     u3, pku3 = _convT_up(wc, dt, m.up3, b, n, H4, W4, need_bwd)
     u3, al3 = _skip_align(u3, H3, W3)
     d3, S.dec3 = resblock_forward(m.dec3, u3, r3, n, H3, W3, wc, dt, training, need_bwd)
-    _reached("dec3")
     u2, pku2 = _convT_up(wc, dt, m.up2, d3, n, H3, W3, need_bwd)
     u2, al2 = _skip_align(u2, H2, W2)
     d2, S.dec2 = resblock_forward(m.dec2, u2, r2, n, H2, W2, wc, dt, training, need_bwd)
-    _reached("dec2")
     u1, pku1 = _convT_up(wc, dt, m.up1, d2, n, H2, W2, need_bwd)
     u1, al1 = _skip_align(u1, H, W)
     d1, S.dec1 = resblock_forward(m.dec1, u1, r1, n, H, W, wc, dt, training, need_bwd)
@@ -820,20 +785,22 @@ def resunet_zero_grad_params(m):
     return z
 
 
-# A/B switch for the fused first-conv backward (RR_FUSED_FIRST_WGRAD=0: the
-# prelu_bwd + im2col + wgrad sequence)
-_FUSED_FIRST_WGRAD = os.environ.get("RR_FUSED_FIRST_WGRAD", "1") != "0"
-# A/B switch for the residual tail + max-pool fusion (RR_FUSED_POOL=0: separate pool)
-_FUSED_POOL = os.environ.get("RR_FUSED_POOL", "1") != "0"
+# A/B and test switches (RR_PATH, _lib.path_flag; the unfused forms are the
+# paths of the shapes / dtypes the fused kernels do not take).  The fused
+# first-conv backward (first_wgrad=0: the prelu_bwd + im2col + wgrad
+# sequence)
+_FUSED_FIRST_WGRAD = path_flag("first_wgrad", 1) != 0
+# the residual tail + max-pool fusion (fused_pool=0: separate pool)
+_FUSED_POOL = path_flag("fused_pool", 1) != 0
 # A/B switch for the encoder max-pool backward fused into the tail BN backward
-_FUSED_POOL_BWD = os.environ.get("RR_FUSED_POOL_BWD", "1") != "0"
+_FUSED_POOL_BWD = path_flag("fused_pool_bwd", 1) != 0
 # A/B switch: dec1's concat dgrad as two 64 -> 64 row-streaming launches
-_SPLIT_DGRAD = os.environ.get("RR_SPLIT_DGRAD", "1") != "0"
+_SPLIT_DGRAD = path_flag("split_dgrad", 1) != 0
 # A/B switch: the final conv's backward fused with dec1's tail BN reduce, its
 # input grad recomputed in the apply instead of stored (rr_conv_out_bwd_bnred)
-_FUSED_CONVOUT_BN = os.environ.get("RR_FUSED_CONVOUT_BN", "1") != "0"
+_FUSED_CONVOUT_BN = path_flag("convout_bn", 1) != 0
 # A/B switch: ... each with the shortcut's 1x1 dgrad summed in (rr_igemm_dgrad_sc)
-_FUSED_SC_DGRAD = os.environ.get("RR_FUSED_SC_DGRAD", "1") != "0"
+_FUSED_SC_DGRAD = path_flag("sc_dgrad", 1) != 0
 
 
 def _streams_half(dtype, n, h, w):
@@ -843,12 +810,11 @@ def _streams_half(dtype, n, h, w):
     return ops.igemm_kernel_name(d).startswith("stream3")
 # A/B switch: the BN-shortcut tail's ReLU mask recomputed from t2 and the
 # shortcut's pre-BN output (read anyway) instead of read from the block output
-_RECOMPUTE_MASK = os.environ.get("RR_BN_RECOMPUTE_MASK", "1") != "0"
-# A/B switch: a residual block's weight grads on a side stream, concurrent
-# with the dgrad / BN-backward chain they do not feed (joined before the
-# block's gradients are declared ready).  Off: measured 29.2k vs 29.4k img/s
-# (same-box A/B) -- the concurrent kernels contend for the CUs and L2.
-_WGRAD_SIDE = os.environ.get("RR_WGRAD_SIDE_STREAM", "0") != "0"
+_RECOMPUTE_MASK = path_flag("recompute_mask", 1) != 0
+# (a residual block's weight grads on a side stream, concurrent with the
+# dgrad / BN-backward chain they do not feed, measured 29.2k vs 29.4k img/s
+# in a same-box A/B -- the concurrent kernels contend for the CUs and L2 --
+# and was removed in round 6)
 # A/B switch: the weight grads' split-K reduces (rr_wgrad_reduce) and the
 # convT bias sums on a side stream -- nothing in the backward reads them, so
 # they run beside the next dgrad instead of between it and its producer;
@@ -857,8 +823,7 @@ _WGRAD_SIDE = os.environ.get("RR_WGRAD_SIDE_STREAM", "0") != "0"
 # slower with it (14.52 vs 14.21 ms, 3 interleaved rounds,
 # profiles/r5u_abstep_reduce_side.txt) -- the reduce workgroups take CUs the
 # next dgrad's one-per-CU tiles are waiting for
-_WGRAD_REDUCE_SIDE = os.environ.get("RR_WGRAD_REDUCE_SIDE", "0") != "0"
-_SIDE = {}
+_WGRAD_REDUCE_SIDE = path_flag("wgrad_reduce_side", 0) != 0
 _REDUCE_SIDE = {}
 
 
@@ -885,13 +850,6 @@ def _pack_stream(device):
     s = _PACK_SIDE.get(device)
     if s is None:
         s = _PACK_SIDE[device] = torch.cuda.Stream(device)
-    return s
-
-
-def _side_stream(device):
-    s = _SIDE.get(device)
-    if s is None:
-        s = _SIDE[device] = torch.cuda.Stream(device)
     return s
 
 

@@ -493,46 +493,31 @@ class VGGPerceptualLoss(tnn.Module):
         self._side = None
         self._pending = None
 
-    def prefetch_target(self, y, at=None):
+    def prefetch_target(self, y):
         """Start F(y), the target's features (no gradient flows into y), on a
         side stream, so it runs concurrently with what the caller launches
         next -- the distortion and the restorer's forward, which F(y) does not
         depend on.  The next perceptual / unified loss on this same ``y`` joins
         it (stream-ordered, also inside a HIP-graph capture).  Returns the
-        tensor to pass to the loss.
-
-        ``at``: where the side stream forks off the caller's stream -- None
-        (now), or the name of a point of the next ResUNet forward
-        (engine.FORWARD_POINTS, e.g. "res1": after that block), so the
-        target's HBM-bound 64x64 layers overlap the restorer's MFMA-bound
-        deeper ones instead of its own 64x64 layers."""
+        tensor to pass to the loss.  (Forking later, at a block of the
+        restorer's forward, measured within 0.4 % of forking here,
+        profiles/r5x_abstep_perc_prefetch_at.txt.)"""
         y = y.float().contiguous()
         self._join()
         if self._side is None or self._side.device != y.device:
             self._side = torch.cuda.Stream(device=y.device)
         box = {}
-
-        def start():
-            self._side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(self._side):
-                box["fy"], _ = engine.vgg_features_forward(self.slice, y, self._wc,
-                                                           self.compute_dtype)
-                box["ev"] = torch.cuda.Event()
-                box["ev"].record(self._side)
-        if at is None:
-            start()
-        else:
-            engine.at_forward_point(at, start)
-        self._pending = (y, box, start)
+        self._side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self._side):
+            box["fy"], _ = engine.vgg_features_forward(self.slice, y, self._wc, self.compute_dtype)
+            box["ev"] = torch.cuda.Event()
+            box["ev"].record(self._side)
+        self._pending = (y, box)
         return y
 
     def _join(self):
         p, self._pending = self._pending, None
         if p is not None:
-            if "ev" not in p[1]:
-                # no forward reached the fork point: fork here
-                engine.drop_forward_point(p[2])
-                p[2]()
             torch.cuda.current_stream().wait_event(p[1]["ev"])
         return p
 

@@ -9,11 +9,10 @@ CPU fallback: a missing library or device raises.
 from __future__ import annotations
 
 import ctypes as C
-import os
 
 import torch
 
-from ._lib import (RR_ACT_NOFULL, RR_ACT_POOL, RR_ACT_PRELU, RR_ACT_RES, RR_BF16, RR_F32, RR_CONV1X1, RR_CONV3X3,
+from ._lib import (path_flag, RR_ACT_NOFULL, RR_ACT_POOL, RR_ACT_PRELU, RR_ACT_RES, RR_BF16, RR_F32, RR_CONV1X1, RR_CONV3X3,
                    RR_CONVT_DOWN, RR_CONVT_UP, RR_DISTORT_KMAX, BnBwdDesc, DistortParam, IgemmDesc, PackJob, WgradDesc, lib)
 
 __all__ = [
@@ -242,7 +241,9 @@ def wgrad(mode, dy, x1, x2, n, h, w, cout, dw=None, accumulate=False, dw_shape=N
     ws = _ws(need, dy.device)
 
     def launch():
-        if reduce_stream is None:
+        # (an A/B build loaded through RR_LIB_PATH may predate the split
+        # entry points: the one-launch form then, on the current stream)
+        if reduce_stream is None or not hasattr(lib(), "rr_wgrad_partial"):
             lib().check(lib().rr_wgrad(C.byref(d), _p(dy), _p(x1), _p(x2), _p(dw), _p(ws),
                                        ws.numel(), stream()), "rr_wgrad")
             return
@@ -418,7 +419,7 @@ def affine_act_pool(x, scale, shift, res=None, res_scale=None, res_shift=None, r
 
 # A/B switch: the identity-shortcut tail's BN backward stores gm in its
 # reduce and applies from it (rr_bn_bwd_reduce_gm); 0: gm from the apply
-_BN_GM_IN_REDUCE = os.environ.get("RR_BN_GM_IN_REDUCE", "1") != "0"
+_BN_GM_IN_REDUCE = path_flag("bn_gm_in_reduce", 1) != 0
 
 
 def bn_backward(g, t0, mean0, inv0, gamma0, *, mask_kind=0, aux=None, aff_s=None, aff_b=None,
@@ -459,7 +460,8 @@ def bn_backward(g, t0, mean0, inv0, gamma0, *, mask_kind=0, aux=None, aff_s=None
     # the identity-shortcut tail (gm is the block's input grad): the reduce
     # stores gm and the apply reads it alone (rr_bn_bwd_reduce_gm)
     gm_first = (_BN_GM_IN_REDUCE and (want_gm or gm_out is not None) and nbn == 1 and
-                d.mask_kind in (1, 3) and Cc % 8 == 0 and 256 % (Cc // 8) == 0)
+                d.mask_kind in (1, 3) and Cc % 8 == 0 and 256 % (Cc // 8) == 0 and
+                hasattr(lib(), "rr_bn_bwd_reduce_gm"))      # (absent from older A/B builds)
     if gm_first:
         if gm_out is None:
             gm_out = torch.empty_like(g)

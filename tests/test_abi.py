@@ -166,11 +166,11 @@ def test_kernel_selection_for_the_benched_layers():
             assert rr_stat_blocks(d) == 512 * h * h // 128
 
 
-def test_kernel_selection_odd_batches_stay_on_whole_rows(monkeypatch):
+def test_kernel_selection_odd_batches_stay_on_whole_rows():
     """host-only: a 16x16 / 8x8 map whose pixel count does not
     fill the first pick's 512-pixel tiles takes the 256- or 128-pixel
     whole-row tiles before the row-segment ones; only batches that fill none
-    of them drop to segments.  Both K loops (RR_CONV3R_RW) pick the same tile."""
+    of them drop to segments."""
     from roadrestore import ops
     from roadrestore._lib import RR_BF16, RR_CONV3X3, IgemmDesc
     want = {  # (n, h, c_in, c_out): kernel (LDS-weight K loop)
@@ -181,13 +181,9 @@ def test_kernel_selection_odd_batches_stay_on_whole_rows(monkeypatch):
         (2, 8, 512, 512): "conv3r_kernel<8,128,32>",         # P = 128: 4-wave 128-pixel tiles
         (1, 16, 64, 64): "conv3r_kernel<16,64,32>",          # P = 256, 64 channels
     }
-    for rw in ("0", "1"):
-        monkeypatch.setenv("RR_CONV3R_RW", rw)
-        for (n, h, ci, co), f in want.items():
-            d = IgemmDesc(RR_BF16, RR_CONV3X3, n, h, h, ci, 0, co, 0, 0, 0, 1, 0, 1, 0)
-            exp = f + (",rw" if rw == "1" and "<s" not in f else "")
-            exp = exp.replace(">,rw", ",rw>")
-            assert ops.igemm_kernel_name(d) == exp, (n, h, ci, co, rw, ops.igemm_kernel_name(d))
+    for (n, h, ci, co), f in want.items():
+        d = IgemmDesc(RR_BF16, RR_CONV3X3, n, h, h, ci, 0, co, 0, 0, 0, 1, 0, 1, 0)
+        assert ops.igemm_kernel_name(d) == f, (n, h, ci, co, ops.igemm_kernel_name(d))
 
 
 def test_kernel_selection_at_the_reference_geometry():

@@ -2,7 +2,7 @@
 layers on 32x32 / 16x16 / 8x8 maps (ResUNet res2 / res3 / dec2 / dec3 /
 bottleneck, VGG16 conv2_x / conv3_x; their dgrads with the concat split and
 the fused BN/PReLU backward) vs fp32 torch and vs the LDS-halo kernel it
-replaces (RR_CONV3R=0).  Inputs are bf16-exact, so against fp32 torch the
+replaces (RR_PATH conv3r=0).  Inputs are bf16-exact, so against fp32 torch the
 only error is the bf16 rounding of the output; vs the halo kernel the same
 fp32 sums in another order, rounded once.  Shapes cover every tile geometry:
 a tile inside an image (W = 32: 16 or 8 rows, top and bottom zero rows),
@@ -11,6 +11,7 @@ inputs."""
 import pytest
 import torch
 import torch.nn.functional as F
+from rrpath import set_path  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -41,7 +42,7 @@ def _desc(n, w, c1, c2, co, split=0, act=0, acc=0, bias=0, mask=0, stats=0, h=No
                      bias, mask, stats, 0)
 
 
-# (n, w, c1, c2, c_out, kernel) -- 4-wave workgroups (2 per CU; RR_CONV3R_WG=4,
+# (n, w, c1, c2, c_out, kernel) -- 4-wave workgroups (2 per CU; RR_PATH conv3r_wg=4,
 # the default where c_out % 128 != 0)
 SHAPES = [
     (4, 32, 64, 0, 128, "conv3r_kernel<32,128>"),     # res2.c1 / VGG conv2_1
@@ -57,7 +58,7 @@ SHAPES = [
     (2, 64, 64, 64, 64, "conv3r_kernel<64,64>"),      # dec1.c1 (concat) fwd: 2-row wave tiles
     (2, 64, 128, 0, 128, "conv3r_kernel<64,128>"),
 ]
-# the 8-wave, one-per-CU variant (RR_CONV3R_WG=8, the default where
+# the 8-wave, one-per-CU variant (RR_PATH conv3r_wg=8, the default where
 # c_out % 128 == 0)
 SHAPES_W8 = [
     (4, 32, 64, 0, 128, "conv3r_kernel<32,128,w8>"),
@@ -73,26 +74,26 @@ SHAPES_W8 = [
 
 @pytest.fixture(params=["4", "8"])
 def wg(request, monkeypatch):
-    monkeypatch.setenv("RR_CONV3R_WG", request.param)
+    set_path(monkeypatch, "conv3r_wg", request.param)
     return request.param
 
 
 @pytest.mark.parametrize("shape", SHAPES + [s + ("w8",) for s in SHAPES_W8])
 def test_conv3r_selected(dev, shape, monkeypatch):
-    monkeypatch.setenv("RR_CONV3R_WG", "4")
+    set_path(monkeypatch, "conv3r_wg", "4")
     if len(shape) == 7:
-        monkeypatch.setenv("RR_CONV3R_WG", "8")
+        set_path(monkeypatch, "conv3r_wg", "8")
         shape = shape[:6]
     from roadrestore import ops
     n, w, c1, c2, co, name = shape
     assert ops.igemm_kernel_name(_desc(n, w, c1, c2, co, bias=1, stats=1)) == name
-    monkeypatch.setenv("RR_CONV3R", "0")
+    set_path(monkeypatch, "conv3r", "0")
     assert not ops.igemm_kernel_name(_desc(n, w, c1, c2, co, bias=1, stats=1)).startswith("conv3r")
 
 
 @pytest.mark.parametrize("shape", SHAPES + SHAPES_W8)
 def test_conv3r_fwd_bias_stats_relu(dev, shape, monkeypatch):
-    monkeypatch.setenv("RR_CONV3R_WG", "8" if shape in SHAPES_W8 else "4")
+    set_path(monkeypatch, "conv3r_wg", "8" if shape in SHAPES_W8 else "4")
     import roadrestore as rr
     from roadrestore._lib import RR_CONV3X3
     n, w, c1, c2, co, _ = shape
@@ -106,7 +107,7 @@ def test_conv3r_fwd_bias_stats_relu(dev, shape, monkeypatch):
     x2 = nhwc(x[:, c1:], dev) if c2 else None
     outs = {}
     for tag in ("1", "0"):
-        monkeypatch.setenv("RR_CONV3R", tag)
+        set_path(monkeypatch, "conv3r", tag)
         y, _, st = rr.ops.igemm(RR_CONV3X3, x1, x2, n, w, w, wf, co, bias=b.to(dev), stats=True)
         yr, _, _ = rr.ops.igemm(RR_CONV3X3, x1, x2, n, w, w, wf, co, bias=b.to(dev), act=1)
         torch.cuda.synchronize()
@@ -131,7 +132,7 @@ def test_conv3r_dgrad_epilogues(dev, shape, acc, msk, wg, monkeypatch):
     ReLU-backward mask (VGG dgrads), both."""
     import roadrestore as rr
     from roadrestore._lib import RR_CONV3X3
-    monkeypatch.setenv("RR_CONV3R", "1")
+    set_path(monkeypatch, "conv3r", "1")
     n, w, c1, _, co = shape
     x = rnd(n, c1, w, w, seed=11).bfloat16().float()
     wt = (rnd(co, c1, 3, 3, seed=12) / (3 * c1 ** 0.5)).bfloat16().float()
@@ -164,7 +165,7 @@ def test_conv3r_concat_split_dgrad(dev, shape, split, wg, monkeypatch):
     wf, _ = rr.ops.pack_conv(wt.to(dev), BF)
     outs = {}
     for tag in ("1", "0"):
-        monkeypatch.setenv("RR_CONV3R", tag)
+        set_path(monkeypatch, "conv3r", tag)
         y1, y2, _ = rr.ops.igemm(RR_CONV3X3, nhwc(x, dev), None, n, w, w, wf, co, split=split)
         torch.cuda.synchronize()
         outs[tag] = torch.cat((nchw(y1), nchw(y2)), 1)
@@ -193,13 +194,13 @@ def test_conv3r_bnbwd(dev, shape, wg, monkeypatch):
     s1 = gamma * inv
     sh1 = beta - mean * s1
     alpha = torch.tensor([0.23], device=dev)
-    monkeypatch.setenv("RR_CONV3R", "0")
+    set_path(monkeypatch, "conv3r", "0")
     da1, _, _ = ops.igemm(RR_CONV3X3, g2, None, n, w, w, wd, C)
     ref = ops.bn_backward(da1, t1, mean, inv, gamma, mask_kind=2, aux=t1, aff_s=s1, aff_b=sh1,
                           alpha=alpha)
     res = {}
     for tag in ("0", "1"):
-        monkeypatch.setenv("RR_CONV3R", tag)
+        set_path(monkeypatch, "conv3r", tag)
         gm, part, rows, arows = ops.igemm_bnbwd(RR_CONV3X3, g2, n, w, w, wd, C, t1, mean, inv, s1,
                                                 sh1, alpha)
         if tag == "1":
@@ -218,13 +219,13 @@ def test_conv3r_bnbwd(dev, shape, wg, monkeypatch):
 @pytest.mark.parametrize("shape", [(2, 64, 64, 64, 64, 0), (2, 64, 64, 0, 128, 64)])
 def test_conv3r_w64_rows_equal_segments(dev, shape, wg, monkeypatch):
     """64x64 maps: the whole-row tiles (2 output rows per wave) against the
-    row-segment tiles they replace (RR_CONV3R_W64=0) -- dec1.c1 forward with
+    row-segment tiles they replace (RR_PATH conv3r_w64=0) -- dec1.c1 forward with
     BN statistics and its concat-split dgrad; the same fp32 sums per output
     (same K order), so bitwise-equal outputs; statistics rows differ only in
     which pixels share a partial row"""
     import roadrestore as rr
     from roadrestore._lib import RR_CONV3X3
-    monkeypatch.setenv("RR_CONV3R", "1")
+    set_path(monkeypatch, "conv3r", "1")
     n, w, c1, c2, co, split = shape
     x = rnd(n, c1 + c2, w, w, seed=41)
     wf, _ = rr.ops.pack_conv((rnd(co, c1 + c2, 3, 3, seed=42) / 24).to(dev), BF)
@@ -232,7 +233,7 @@ def test_conv3r_w64_rows_equal_segments(dev, shape, wg, monkeypatch):
     x2 = nhwc(x[:, c1:], dev) if c2 else None
     res = {}
     for tag in ("1", "0"):
-        monkeypatch.setenv("RR_CONV3R_W64", tag)
+        set_path(monkeypatch, "conv3r_w64", tag)
         name = rr.ops.igemm_kernel_name(_desc(n, w, c1, c2, co, split=split, stats=int(not split)))
         assert name.startswith("conv3r_kernel<64," if tag == "1" else "conv3r_kernel<s2,"), name
         if split:
@@ -252,7 +253,7 @@ def test_conv3r_stats_rows_deterministic(dev, wg, monkeypatch):
     outputs and statistics"""
     import roadrestore as rr
     from roadrestore._lib import RR_CONV3X3
-    monkeypatch.setenv("RR_CONV3R", "1")
+    set_path(monkeypatch, "conv3r", "1")
     n, w, c, co = 8, 16, 256, 256
     x = nhwc(rnd(n, c, w, w, seed=31), dev)
     wf, _ = rr.ops.pack_conv((rnd(co, c, 3, 3, seed=32) / 48).to(dev), BF)
@@ -281,7 +282,7 @@ SHAPES_SEG = [
 def _seg_rows(n, h, w, co, name):
     sg = int(name.split("<s")[1][0])
     bc = int(name.split(",")[1].rstrip(">"))
-    w8 = ",w8" in name                          # RR_CONV3R_SEGWG=8: 8-wave workgroups
+    w8 = ",w8" in name                          # conv3r_segwg=8: 8-wave workgroups
     nw = 64 if (sg == 2 and (bc == 128 or not w8)) else 32
     wp = (8 if w8 else 4) // (bc // nw)
     tr = wp * (8 // sg)
@@ -289,7 +290,7 @@ def _seg_rows(n, h, w, co, name):
 
 
 def _seg_name_ok(got, name):
-    # RR_CONV3R_SEGWG=4 / 8 in the environment switch the workgroup kind
+    # RR_PATH conv3r_segwg=4 / 8 switches the workgroup kind
     base = name.replace(",w8", "")
     return got in (base, base[:-1] + ",w8>")
 
@@ -299,7 +300,7 @@ def test_conv3r_seg_fwd_bias_stats_relu(dev, shape, monkeypatch):
     import roadrestore as rr
     from roadrestore._lib import RR_CONV3X3
     n, h, w, c1, c2, co, name = shape
-    monkeypatch.setenv("RR_CONV3R", "1")
+    set_path(monkeypatch, "conv3r", "1")
     name_got = rr.ops.igemm_kernel_name(_desc(n, w, c1, c2, co, bias=1, stats=1, h=h))
     assert _seg_name_ok(name_got, name), name_got
     cin = c1 + c2
@@ -312,7 +313,7 @@ def test_conv3r_seg_fwd_bias_stats_relu(dev, shape, monkeypatch):
     x2 = nhwc(x[:, c1:], dev) if c2 else None
     outs = {}
     for tag in ("1", "0"):
-        monkeypatch.setenv("RR_CONV3R", tag)
+        set_path(monkeypatch, "conv3r", tag)
         y, _, st = rr.ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf, co, bias=b.to(dev), stats=True)
         yr, _, _ = rr.ops.igemm(RR_CONV3X3, x1, x2, n, h, w, wf, co, bias=b.to(dev), act=1)
         torch.cuda.synchronize()
@@ -334,7 +335,7 @@ def test_conv3r_seg_fwd_bias_stats_relu(dev, shape, monkeypatch):
 def test_conv3r_seg_dgrad_epilogues(dev, shape, acc, msk, monkeypatch):
     import roadrestore as rr
     from roadrestore._lib import RR_CONV3X3
-    monkeypatch.setenv("RR_CONV3R", "1")
+    set_path(monkeypatch, "conv3r", "1")
     n, h, w, c1, _, co = shape
     x = rnd(n, c1, h, w, seed=11).bfloat16().float()
     wt = (rnd(co, c1, 3, 3, seed=12) / (3 * c1 ** 0.5)).bfloat16().float()
@@ -363,7 +364,7 @@ def test_conv3r_seg_concat_split_dgrad(dev, shape, split, monkeypatch):
     wt = (rnd(co, c1, 3, 3, seed=22) / (3 * c1 ** 0.5)).bfloat16().float()
     ref = F.conv2d(x, wt, None, padding=1)
     wf, _ = rr.ops.pack_conv(wt.to(dev), BF)
-    monkeypatch.setenv("RR_CONV3R", "1")
+    set_path(monkeypatch, "conv3r", "1")
     assert rr.ops.igemm_kernel_name(_desc(n, w, c1, 0, co, split=split, h=h)).startswith("conv3r_kernel<s")
     y1, y2, _ = rr.ops.igemm(RR_CONV3X3, nhwc(x, dev), None, n, h, w, wf, co, split=split)
     torch.cuda.synchronize()
@@ -393,13 +394,13 @@ def test_conv3r_seg_bnbwd(dev, shape, monkeypatch):
     s1 = gamma * inv
     sh1 = beta - mean * s1
     alpha = torch.tensor([0.23], device=dev)
-    monkeypatch.setenv("RR_CONV3R", "0")
+    set_path(monkeypatch, "conv3r", "0")
     da1, _, _ = ops.igemm(RR_CONV3X3, g2, None, n, h, w, wd, C)
     ref = ops.bn_backward(da1, t1, mean, inv, gamma, mask_kind=2, aux=t1, aff_s=s1, aff_b=sh1,
                           alpha=alpha)
     res = {}
     for tag in ("0", "1"):
-        monkeypatch.setenv("RR_CONV3R", tag)
+        set_path(monkeypatch, "conv3r", tag)
         gm, part, rows, arows = ops.igemm_bnbwd(RR_CONV3X3, g2, n, h, w, wd, C, t1, mean, inv, s1,
                                                 sh1, alpha)
         if tag == "1":
@@ -419,7 +420,7 @@ def test_conv3r_seg_bnbwd(dev, shape, monkeypatch):
 def test_conv3r_seg_deterministic(dev, monkeypatch):
     import roadrestore as rr
     from roadrestore._lib import RR_CONV3X3
-    monkeypatch.setenv("RR_CONV3R", "1")
+    set_path(monkeypatch, "conv3r", "1")
     n, h, w, c, co = 2, 56, 56, 128, 256
     x = nhwc(rnd(n, c, h, w, seed=31), dev)
     wf, _ = rr.ops.pack_conv((rnd(co, c, 3, 3, seed=32) / 48).to(dev), BF)
@@ -438,7 +439,7 @@ def test_conv3r_ex_prelu_and_residual(dev, shape, monkeypatch):
     import roadrestore as rr
     from roadrestore import ops
     from roadrestore._lib import RR_ACT_PRELU, RR_ACT_RES, RR_CONV3X3
-    monkeypatch.setenv("RR_CONV3R", "1")
+    set_path(monkeypatch, "conv3r", "1")
     n, h, w, c1, c2, co = shape
     cin = c1 + c2
     x = rnd(n, cin, h, w, seed=61).bfloat16().float()
@@ -485,7 +486,7 @@ def test_conv3r_ex_pool(dev, shape, monkeypatch):
     output, vs fp32 torch on bf16-exact inputs"""
     from roadrestore import ops
     from roadrestore._lib import RR_CONV3X3
-    monkeypatch.setenv("RR_CONV3R", "1")
+    set_path(monkeypatch, "conv3r", "1")
     n, h, w, c1, c2, co = shape
     cin = c1 + c2
     x = rnd(n, cin, h, w, seed=71).bfloat16().float()
@@ -515,36 +516,3 @@ def test_conv3r_ex_pool(dev, shape, monkeypatch):
     assert y.data_ptr() == base.data_ptr()
     assert rel(nchw(y), F.relu(pre + r)) < 4e-3
     assert torch.equal(nchw(yp), F.max_pool2d(nchw(y), 2))
-
-
-
-
-@pytest.mark.parametrize("shape", [(2, 32, 128, 0, 256), (8, 16, 128, 0, 256), (512, 8, 512, 0, 512)])
-def test_conv3r_bc256_variant(dev, shape, monkeypatch):
-    """RR_CONV3R_BC256=1 (A/B): the 256-channel column blocks of 8-wave
-    workgroups (the round-3 default where c_out % 256 == 0) against fp32
-    torch, and bitwise against the 128-channel default: every output sums the
-    same taps in the same stage / row order, only the tile shape differs."""
-    import roadrestore as rr
-    from roadrestore._lib import RR_CONV3X3
-    monkeypatch.setenv("RR_CONV3R", "1")
-    monkeypatch.setenv("RR_CONV3R_WG", "8")
-    n, w, c1, c2, co = shape
-    x = rnd(n, c1, w, w, seed=21).bfloat16().float()
-    wt = (rnd(co, c1, 3, 3, seed=22) / (3 * c1 ** 0.5)).bfloat16().float()
-    b = rnd(co, seed=23)
-    pre = F.conv2d(x, wt, None, padding=1)
-    wf, _ = rr.ops.pack_conv(wt.to(dev), BF)
-    x1 = nhwc(x, dev)
-    outs = {}
-    for tag in ("1", "0"):
-        monkeypatch.setenv("RR_CONV3R_BC256", tag)
-        name = rr.ops.igemm_kernel_name(_desc(n, w, c1, c2, co, bias=1, stats=1))
-        assert name.startswith("conv3r") and (",256" in name or "<%d,256" % w in name) == (tag == "1"), name
-        y, _, st = rr.ops.igemm(RR_CONV3X3, x1, None, n, w, w, wf, co, bias=b.to(dev), stats=True)
-        torch.cuda.synchronize()
-        outs[tag] = (nchw(y), st.double().sum(0).cpu())
-    ref = pre + b[None, :, None, None]
-    assert rel(outs["1"][0], ref) < 4e-3
-    assert torch.equal(outs["1"][0], outs["0"][0])
-    assert rel(outs["1"][1], outs["0"][1]) < 1e-12

@@ -10,6 +10,7 @@ import pytest
 import torch
 
 from oracle import imgproc_cpu as I
+from rrpath import set_path  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -220,7 +221,7 @@ def test_random_distortion_draws_on_device(dev):
 def test_blur_tiled_equals_untiled(dev, mode, monkeypatch):
     """The LDS-compacted blur (h * w a multiple of 256: nonzero taps listed
     once per workgroup) is byte-identical to the per-pixel tap scan
-    (RR_BLUR_TILED=0) over every (degree, angle) the draws can produce."""
+    (RR_PATH blur_tiled=0) over every (degree, angle) the draws can produce."""
     from roadrestore import imgproc, ops
     from roadrestore._lib import RR_DISTORT_BLUR
     n = 11 * 24
@@ -235,7 +236,7 @@ def test_blur_tiled_equals_untiled(dev, mode, monkeypatch):
         p.ksize = 5 + i % 11
     outs = []
     for tiled in ("1", "0"):
-        monkeypatch.setenv("RR_BLUR_TILED", tiled)
+        set_path(monkeypatch, "blur_tiled", tiled)
         outs.append(ops.distort_u8(x, params, table[idx], mode=mode, seed=seed))
     assert torch.equal(outs[0], outs[1])
 

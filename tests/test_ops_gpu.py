@@ -5,6 +5,7 @@ relative tolerances of bf16 storage."""
 import pytest
 import torch
 import torch.nn.functional as F
+from rrpath import set_path  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -82,7 +83,7 @@ def test_conv3x3_halo(dev, shape, halo, monkeypatch):
     only error is the bf16 rounding of the output."""
     import roadrestore as rr
     from roadrestore._lib import RR_CONV3X3
-    monkeypatch.setenv("RR_IGEMM_NOHALO", "0" if halo else "1")
+    set_path(monkeypatch, "igemm_halo", 1 if halo else 0)
     n, h, w, c1, c2, cout, split = shape
     cin = c1 + c2
     x = rnd(n, cin, h, w, seed=41).bfloat16().float()
@@ -198,7 +199,7 @@ def test_wgrad3_halo(dev, hw, halo, monkeypatch):
     with clamped loads and LDS writes no stage reads."""
     import roadrestore as rr
     from roadrestore._lib import RR_CONV3X3
-    monkeypatch.setenv("RR_WGRAD_NOHALO", "0" if halo else "1")
+    set_path(monkeypatch, "wgrad_halo", 1 if halo else 0)
     n = 5
     if len(hw) == 3:
         n, hw = hw[0], hw[1:]

@@ -1,15 +1,16 @@
 """Wave-streaming 1x1 / convT GEMM (csrc/stream1.hip) vs fp32 torch and vs
-the tiled igemm kernel (RR_STREAM1=0), for every mode and epilogue the
+the tiled igemm kernel (RR_PATH stream1=0), for every mode and epilogue the
 ResUNet step routes through it: shortcut conv fwd with BN statistics
 (14:109-112), its dgrad into a concat split with accumulate, the relu-mask
 epilogue, the fp32 NCHW final conv (14:149), ConvTranspose2d(2, 2) fwd
 (14:137-147) and its dgrad.  Inputs are bf16-exact, so against fp32 torch the
-only error is the bf16 rounding of the output.  RR_STREAM1_MINP lowers the
+only error is the bf16 rounding of the output.  RR_PATH stream1_minp lowers the
 pixel-count threshold so small shapes take the streaming path (uneven block
 counts per wave, partial last rounds)."""
 import pytest
 import torch
 import torch.nn.functional as F
+from rrpath import set_path  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -47,7 +48,7 @@ SHAPES = [(4, 32, 32), (11, 16, 16), (137, 16, 16)]
 
 @pytest.fixture
 def small_ok(monkeypatch):
-    monkeypatch.setenv("RR_STREAM1_MINP", "1024")
+    set_path(monkeypatch, "stream1_minp", "1024")
 
 
 @pytest.mark.parametrize("shape", SHAPES)
@@ -70,7 +71,7 @@ def test_stream1_conv1x1_stats(dev, small_ok, shape, c1, c2, co, monkeypatch):
     assert _name(RR_CONV1X1, n, h, w, c1, c2, co, bias=1, stats=1).startswith(want)
     res = {}
     for tag in ("1", "0"):
-        monkeypatch.setenv("RR_STREAM1", tag)
+        set_path(monkeypatch, "stream1", tag)
         y, _, st = rr.ops.igemm(RR_CONV1X1, nhwc(x1, dev), nhwc(x2, dev) if c2 else None, n, h, w,
                                 wf, co, bias=b.to(dev), stats=True)
         torch.cuda.synchronize()
@@ -175,7 +176,7 @@ def test_stream1_convT(dev, small_ok, shape, cin, cout, monkeypatch):
     assert _name(RR_CONVT_DOWN, n, h, w, cout, 0, cin, mask=1).startswith("igemm_kernel")
     res = {}
     for tag in ("1", "0"):
-        monkeypatch.setenv("RR_STREAM1", tag)
+        set_path(monkeypatch, "stream1", tag)
         y, _, _ = rr.ops.igemm(RR_CONVT_UP, nhwc(x, dev), None, n, h, w, wu, 4 * cout, bias=b4)
         gx, _, _ = rr.ops.igemm(RR_CONVT_DOWN, nhwc(g, dev), None, n, h, w, wdn, cin,
                                 mask=nhwc(m, dev))

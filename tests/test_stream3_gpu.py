@@ -1,12 +1,13 @@
 """Row-streaming 3x3 conv (csrc/stream3.hip): the 64 -> 64 channel bf16 conv
 at W = 64 / 32 (ResUNet res1 / dec1 / dec2, VGG16 conv1_2) vs fp32 torch and
-vs the tiled halo kernel (RR_STREAM3=0).  Shapes put workgroup row ranges
+vs the tiled halo kernel (RR_PATH stream3=0).  Shapes put workgroup row ranges
 across image boundaries (uneven splits, short images) so the ring's
 pre-load steps and zero-padding rows are exercised.  Inputs are bf16-exact,
 so against fp32 torch the only error is the bf16 rounding of the output."""
 import pytest
 import torch
 import torch.nn.functional as F
+from rrpath import set_path  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -54,12 +55,12 @@ def _name(n, h, w):
 @pytest.mark.parametrize("shape", SHAPES)
 def test_stream3_selected(dev, shape, monkeypatch):
     """the streaming kernel owns these shapes (256 partial rows), and the
-    RR_STREAM3=0 switch hands them back to the tiled kernel"""
+    RR_PATH stream3=0 switch hands them back to the tiled kernel"""
     n, h, w = shape
     assert _blocks(n, h, w) == 256 and _name(n, h, w).startswith("stream3")
     # too small for one step per workgroup / not whole steps: a tiled kernel
     assert not _name(n // 2 if n * h * w // 2 < 65536 else 1, h, w).startswith("stream3")
-    monkeypatch.setenv("RR_STREAM3", "0")
+    set_path(monkeypatch, "stream3", "0")
     # the tap-reuse conv: 32x32 whole-row tiles (128-pixel partial rows),
     # else row-segment tiles (4 wave rows of 4 x 32 pixels per 16-row band)
     seg = n * -(-w // 32) * -(-h // 16) * 4
@@ -80,7 +81,7 @@ def test_stream3_fwd_stats(dev, shape, monkeypatch):
     wf, _ = rr.ops.pack_conv(wt.to(dev), BF)
     outs = {}
     for tag in ("1", "0"):
-        monkeypatch.setenv("RR_STREAM3", tag)
+        set_path(monkeypatch, "stream3", tag)
         y, _, st = rr.ops.igemm(RR_CONV3X3, nhwc(x, dev), None, n, h, w, wf, 64, bias=b.to(dev),
                                 stats=True)
         yr, _, _ = rr.ops.igemm(RR_CONV3X3, nhwc(x, dev), None, n, h, w, wf, 64, bias=b.to(dev),
@@ -105,7 +106,7 @@ def test_stream3_load_epilogue(dev, shape, acc, msk, act, monkeypatch):
     backward mask (VGG conv1_2 dgrad), both; plain and ReLU without bias."""
     import roadrestore as rr
     from roadrestore._lib import RR_CONV3X3
-    monkeypatch.setenv("RR_STREAM3", "1")
+    set_path(monkeypatch, "stream3", "1")
     n, h, w = shape
     x = rnd(n, 64, h, w, seed=11).bfloat16().float()
     wt = (rnd(64, 64, 3, 3, seed=12) / 24.0).bfloat16().float()
@@ -145,13 +146,13 @@ def test_stream3_bnbwd(dev, shape, monkeypatch):
     s1 = gamma * inv
     sh1 = beta - mean * s1
     alpha = torch.tensor([0.23], device=dev)
-    monkeypatch.setenv("RR_STREAM3", "0")
+    set_path(monkeypatch, "stream3", "0")
     da1, _, _ = ops.igemm(RR_CONV3X3, g2, None, n, h, w, wd, C)
     ref = ops.bn_backward(da1, t1, mean, inv, gamma, mask_kind=2, aux=t1, aff_s=s1, aff_b=sh1,
                           alpha=alpha)
     res = {}
     for tag in ("0", "1"):
-        monkeypatch.setenv("RR_STREAM3", tag)
+        set_path(monkeypatch, "stream3", tag)
         gm, part, rows, arows = ops.igemm_bnbwd(RR_CONV3X3, g2, n, h, w, wd, C, t1, mean, inv, s1,
                                                 sh1, alpha)
         if tag == "1":
@@ -168,14 +169,12 @@ def test_stream3_bnbwd(dev, shape, monkeypatch):
 
 @pytest.mark.parametrize("shape", [(16, 64, 64), (17, 64, 64), (81, 32, 32)])
 @pytest.mark.parametrize("stats,bias,act", [(True, True, 0), (False, True, 1), (False, False, 0)])
-def test_stream3_concat_two_pass(dev, shape, stats, bias, act, monkeypatch):
-    """64 + 64-channel concat input (ResUNet dec1 conv1, 14:144,174-177).
-    Default: the tap-reuse conv in ONE pass (the K = 1152 sum in fp32),
-    against fp32 torch on the concatenation at the single-rounding bound.
-    RR_STREAM3_CONCAT=1 (A/B): two streaming passes, the second accumulating
-    onto the first's bf16 half and applying bias / statistics / ReLU to the
-    sum (its extra bf16 rounding of the first half gets the looser bound);
-    the statistics are of the pre-bias sum either way."""
+def test_stream3_concat_one_pass(dev, shape, stats, bias, act, monkeypatch):
+    """64 + 64-channel concat input (ResUNet dec1 conv1, 14:144,174-177):
+    the tap-reuse conv in ONE pass (the K = 1152 sum in fp32, no bf16
+    rounding of a half sum; the two-pass streaming form was removed in round
+    6), against fp32 torch on the concatenation at the single-rounding bound;
+    the statistics are of the pre-bias sum."""
     import roadrestore as rr
     from roadrestore._lib import RR_CONV3X3
     n, h, w = shape
@@ -188,28 +187,17 @@ def test_stream3_concat_two_pass(dev, shape, stats, bias, act, monkeypatch):
     if act:
         ref = F.relu(ref)
     wf, _ = rr.ops.pack_conv(wt.to(dev), BF)
-    outs = {}
-    for tag in ("1", None):
-        if tag is None:
-            monkeypatch.delenv("RR_STREAM3_CONCAT", raising=False)
-        else:
-            monkeypatch.setenv("RR_STREAM3_CONCAT", tag)
-        d = rr.ops.IgemmDesc(rr.ops.RR_BF16, RR_CONV3X3, n, h, w, 64, 64, 64, 0, act, 0,
-                             int(bias), 0, int(stats), 0)
-        name = rr.ops.igemm_kernel_name(d)
-        one_pass = "conv3r_kernel<%d,64>" % w if h == w else "conv3r_kernel<s2,64>"
-        assert name == ("stream3_kernel<%d>" % w if tag == "1" else one_pass)
-        tag = tag or "0"
-        y, _, st = rr.ops.igemm(RR_CONV3X3, nhwc(x1, dev), nhwc(x2, dev), n, h, w, wf, 64,
-                                bias=b.to(dev) if bias else None, act=act, stats=stats)
-        torch.cuda.synchronize()
-        outs[tag] = (nchw(y), st.double().sum(0).cpu() if stats else None)
-    y1, s1 = outs["0"]                          # the default one-pass conv
+    d = rr.ops.IgemmDesc(rr.ops.RR_BF16, RR_CONV3X3, n, h, w, 64, 64, 64, 0, act, 0,
+                         int(bias), 0, int(stats), 0)
+    one_pass = "conv3r_kernel<%d,64>" % w if h == w else "conv3r_kernel<s2,64>"
+    assert rr.ops.igemm_kernel_name(d) == one_pass
+    y, _, st = rr.ops.igemm(RR_CONV3X3, nhwc(x1, dev), nhwc(x2, dev), n, h, w, wf, 64,
+                            bias=b.to(dev) if bias else None, act=act, stats=stats)
+    torch.cuda.synchronize()
+    y1 = nchw(y)
     assert rel(y1, ref) < 4e-3
-    y, s = outs["1"]
-    assert rel(y, ref) < 6e-3
-    assert rel(y, y1) < 4e-3
     if stats:
+        s1 = st.double().sum(0).cpu()
         assert rel(s1[:, 0], pre.double().sum((0, 2, 3))) < 1e-5
         assert rel(s1[:, 1], (pre.double() ** 2).sum((0, 2, 3))) < 1e-5
         assert rel(s[:, 0], pre.double().sum((0, 2, 3))) < 4e-3
@@ -241,7 +229,7 @@ def test_dgrad_sc_equals_dgrad_plus_shortcut(dev, shape):
     x, xs = nhwc(dt, dev), nhwc(dsc, dev)
     g1 = ops.igemm_dgrad_sc(x, n, h, w, wd[:half], 64, xs, wsd[:hs])
     g2 = ops.igemm_dgrad_sc(x, n, h, w, wd[half:], 64, xs, wsd[hs:])
-    # the two-step form (RR_FUSED_SC_DGRAD=0)
+    # the two-step form (RR_PATH sc_dgrad=0)
     t1, _, _ = ops.igemm(RR_CONV3X3, x, None, n, h, w, wd[:half], 64)
     t2, _, _ = ops.igemm(RR_CONV3X3, x, None, n, h, w, wd[half:], 64)
     ops.igemm(RR_CONV1X1, xs, None, n, h, w, wsd, 128, out=t1, out2=t2, split=64, accumulate=True)

@@ -2,11 +2,12 @@
 128-channel output gradients (64-channel dy slices): eligibility mirror, parity against fp32 torch on
 bf16-exact inputs (products exact in fp32, only the summation order
 differs), concat second sources, accumulate, and agreement with the tiled
-LDS-halo kernel (RR_SWGRAD=0).  Shapes cover partial images per workgroup,
+LDS-halo kernel (RR_PATH swgrad=0).  Shapes cover partial images per workgroup,
 several images per workgroup and ragged step ranges."""
 import pytest
 import torch
 import torch.nn.functional as F
+from rrpath import set_path  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -63,7 +64,7 @@ def test_swgrad_accumulate_and_tiled(dev, shape, monkeypatch):
     _, _, acc = run(dev, n, h, w, c1, c2, cout, seed=80, dw=base.clone(), accumulate=True)
     _, _, one = run(dev, n, h, w, c1, c2, cout, seed=80)
     torch.testing.assert_close(acc, base + one, rtol=0, atol=1e-4)
-    monkeypatch.setenv("RR_SWGRAD", "0")
+    set_path(monkeypatch, "swgrad", "0")
     _, _, tiled = run(dev, n, h, w, c1, c2, cout, seed=80)
     rel = ((one - tiled).norm() / tiled.norm()).item()
     assert rel < 2e-5, rel
