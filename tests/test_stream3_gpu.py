@@ -200,8 +200,6 @@ def test_stream3_concat_one_pass(dev, shape, stats, bias, act, monkeypatch):
         s1 = st.double().sum(0).cpu()
         assert rel(s1[:, 0], pre.double().sum((0, 2, 3))) < 1e-5
         assert rel(s1[:, 1], (pre.double() ** 2).sum((0, 2, 3))) < 1e-5
-        assert rel(s[:, 0], pre.double().sum((0, 2, 3))) < 4e-3
-        assert rel(s[:, 1], (pre.double() ** 2).sum((0, 2, 3))) < 4e-3
 
 
 @pytest.mark.parametrize("shape", [(17, 64, 64), (65, 16, 64), (81, 32, 32)])
