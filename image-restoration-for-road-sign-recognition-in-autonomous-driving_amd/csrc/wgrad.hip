@@ -447,19 +447,21 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
     }
   }
 
-  // partial[split][a][tap][b]
+  // partial[split][a / 4][tap][b][a % 4]: the accumulator's own layout (a
+  // lane holds 4 consecutive dy channels of one x channel), one 16-B store
+  // per lane and (i, j, tap), 16 lanes = 256 contiguous bytes -- 36 dwordx4
+  // stores per wave instead of 144 dword ones into 64-B pieces
+  // (rr_wgrad_reduce maps the layout back: launch_reduce's alayout)
 #pragma unroll
   for (int i = 0; i < MA; ++i)
 #pragma unroll
     for (int j = 0; j < MB; ++j) {
       const int b = b0 + wb * 16 * MB + j * 16 + gi;
+      const int a4 = (a0 + wa * 16 * MA + i * 16) / 4 + g;
 #pragma unroll
       for (int t = 0; t < 9; ++t)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int ar = a0 + wa * 16 * MA + i * 16 + g * 4 + e;
-          a.partial[(((long long)split * a.CA + ar) * 9 + t) * a.CB + b] = acc[i][j][t][e];
-        }
+        *reinterpret_cast<f32x4 *>(a.partial + ((((long long)split * (a.CA / 4) + a4) * 9 + t) * a.CB + b) * 4) =
+            acc[i][j][t];
     }
 }
 
@@ -492,10 +494,12 @@ __global__ void wgrad_reduce(const float *__restrict__ partial, float *__restric
 // Split-parallel variant: G split groups x (256/G) float4 output columns per
 // block; group g sums splits g, g+G, ... and the groups are combined in LDS in
 // fixed order (deterministic).  Needs slab % 4 == 0.
+// alayout 1: the slabs are [a / 4][tap][b][a % 4] (wgrad3_halo_kernel), 0:
+// [a][tap][b]; the split sum is elementwise either way (same order)
 template <int G>
 __global__ __launch_bounds__(256) void wgrad_reduce_g(const float *__restrict__ partial,
                                                        float *__restrict__ dw, int CA, int CB,
-                                                       int taps, int nsplit, int accumulate) {
+                                                       int taps, int nsplit, int accumulate, int alayout) {
   constexpr int NC = 256 / G;                  // float4 columns per block
   __shared__ float4 red[G][NC];
   const long long slab = (long long)CA * CB * taps;
@@ -527,6 +531,18 @@ __global__ __launch_bounds__(256) void wgrad_reduce_g(const float *__restrict__ 
     s.x += u.x; s.y += u.y; s.z += u.z; s.w += u.w;
   }
   const float v[4] = {s.x, s.y, s.z, s.w};
+  if (alayout) {
+    const int b = (int)(o4 % CB);
+    const long long at = o4 / CB;
+    const int t = (int)(at % taps);
+    const int a4 = (int)(at / taps);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long long di = ((long long)(a4 * 4 + e) * CB + b) * taps + t;
+      dw[di] = accumulate ? dw[di] + v[e] : v[e];
+    }
+    return;
+  }
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const long long o = o4 * 4 + e;
@@ -540,7 +556,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_g(const float *__restrict__ 
 }
 
 static void launch_reduce(const float *ws, float *dw, int CA, int CB, int taps, int nsplit,
-                          int accumulate, hipStream_t st) {
+                          int accumulate, int alayout, hipStream_t st) {
   const long long total = (long long)CA * CB * taps;
   if (total % 4) {
     hipLaunchKernelGGL(wgrad_reduce, dim3(rr_grid_cap((total + 255) / 256, 8192)), dim3(256), 0, st,
@@ -552,11 +568,11 @@ static void launch_reduce(const float *ws, float *dw, int CA, int CB, int taps, 
   while (G < 16 && G * 2 <= nsplit && (total / 4 + 256 / G - 1) / (256 / G) < 1024) G *= 2;
   const unsigned nb = (unsigned)((total / 4 + 256 / G - 1) / (256 / G));
   switch (G) {
-    case 1: hipLaunchKernelGGL(wgrad_reduce_g<1>, dim3(nb), dim3(256), 0, st, ws, dw, CA, CB, taps, nsplit, accumulate); break;
-    case 2: hipLaunchKernelGGL(wgrad_reduce_g<2>, dim3(nb), dim3(256), 0, st, ws, dw, CA, CB, taps, nsplit, accumulate); break;
-    case 4: hipLaunchKernelGGL(wgrad_reduce_g<4>, dim3(nb), dim3(256), 0, st, ws, dw, CA, CB, taps, nsplit, accumulate); break;
-    case 8: hipLaunchKernelGGL(wgrad_reduce_g<8>, dim3(nb), dim3(256), 0, st, ws, dw, CA, CB, taps, nsplit, accumulate); break;
-    default: hipLaunchKernelGGL(wgrad_reduce_g<16>, dim3(nb), dim3(256), 0, st, ws, dw, CA, CB, taps, nsplit, accumulate); break;
+    case 1: hipLaunchKernelGGL(wgrad_reduce_g<1>, dim3(nb), dim3(256), 0, st, ws, dw, CA, CB, taps, nsplit, accumulate, alayout); break;
+    case 2: hipLaunchKernelGGL(wgrad_reduce_g<2>, dim3(nb), dim3(256), 0, st, ws, dw, CA, CB, taps, nsplit, accumulate, alayout); break;
+    case 4: hipLaunchKernelGGL(wgrad_reduce_g<4>, dim3(nb), dim3(256), 0, st, ws, dw, CA, CB, taps, nsplit, accumulate, alayout); break;
+    case 8: hipLaunchKernelGGL(wgrad_reduce_g<8>, dim3(nb), dim3(256), 0, st, ws, dw, CA, CB, taps, nsplit, accumulate, alayout); break;
+    default: hipLaunchKernelGGL(wgrad_reduce_g<16>, dim3(nb), dim3(256), 0, st, ws, dw, CA, CB, taps, nsplit, accumulate, alayout); break;
   }
 }
 
@@ -702,7 +718,8 @@ extern "C" int rr_wgrad_reduce(const rr_wgrad_desc *d, const void *ws, size_t ws
   if (ws_bytes < rr_wgrad_workspace(d)) return RR_EWORKSPACE;
   int CA, CB, taps, nsplit;
   reduce_shape(d, CA, CB, taps, nsplit);
-  launch_reduce((const float *)ws, dw, CA, CB, taps, nsplit, d->accumulate, (hipStream_t)stream);
+  const int alayout = !swgrad_ok(d) && halo_ok(d);   // wgrad3_halo_kernel's slab layout
+  launch_reduce((const float *)ws, dw, CA, CB, taps, nsplit, d->accumulate, alayout, (hipStream_t)stream);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }
