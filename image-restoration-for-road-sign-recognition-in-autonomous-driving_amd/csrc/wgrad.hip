@@ -248,7 +248,22 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs a) {
     __syncthreads();
   }
 
-  // partial[split][a][tap][b]
+  // partial[split][a / 4][tap][b][a % 4] where a.CA % 4 == 0: the
+  // accumulator's own layout, one 16-B store per lane and block (as
+  // wgrad3_halo_kernel; rr_wgrad_reduce maps it back), else [split][a][tap][b]
+  if (a.CA % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < MA; ++i)
+#pragma unroll
+      for (int j = 0; j < MB; ++j) {
+        const int b = b0 + wb * (BB / 2) + j * 16 + gi;
+        const int a4 = (a0 + wa * (BA / 2) + i * 16) / 4 + g;
+        if (b >= a.CB || b - b0 >= bvalid || a4 * 4 >= a.CA) continue;
+        *reinterpret_cast<f32x4 *>(a.partial + ((((long long)split * (a.CA / 4) + a4) * a.taps + tap) * a.CB + b) * 4) =
+            acc[i][j];
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < MA; ++i)
 #pragma unroll
@@ -494,8 +509,9 @@ __global__ void wgrad_reduce(const float *__restrict__ partial, float *__restric
 // Split-parallel variant: G split groups x (256/G) float4 output columns per
 // block; group g sums splits g, g+G, ... and the groups are combined in LDS in
 // fixed order (deterministic).  Needs slab % 4 == 0.
-// alayout 1: the slabs are [a / 4][tap][b][a % 4] (wgrad3_halo_kernel), 0:
-// [a][tap][b]; the split sum is elementwise either way (same order)
+// alayout 1: the slabs are [a / 4][tap][b][a % 4] (wgrad3_halo_kernel, and
+// wgrad_kernel where CA % 4 == 0), 0: [a][tap][b]; the split sum is
+// elementwise either way (same order)
 template <int G>
 __global__ __launch_bounds__(256) void wgrad_reduce_g(const float *__restrict__ partial,
                                                        float *__restrict__ dw, int CA, int CB,
@@ -594,12 +610,25 @@ Plan plan_of(const rr_wgrad_desc *d) {
   p.nbblk = (p.CB + p.BB - 1) / p.BB;
   const long long P = (long long)d->n * d->h * d->w;
   const long long tiles = (long long)p.nablk * p.nbblk * p.taps;
-  long long want = (1024 + tiles - 1) / tiles;                  // ~1024 workgroups
-  long long maxs = (P + 4 * BKP_PLAN - 1) / (4 * BKP_PLAN);     // >= 4 stages per split
-  long long ns = want < maxs ? want : maxs;
-  if (ns < 1) ns = 1;
-  long long len = (P + ns - 1) / ns;
-  len = (len + BKP_PLAN - 1) / BKP_PLAN * BKP_PLAN;
+  // ~1024 workgroups; ~512 for the bf16 1x1 / convT weight grads whose split
+  // partials (nsplit x the weight, written and read back in fp32) would be
+  // more than an eighth of the activation bytes at 1024 -- on the 16x16 /
+  // 8x8 maps they moved more bytes than the activations (1x1 / convT layers
+  // 10-30 % faster at 512, r6h); elsewhere 512 lost parallelism (up1, dec2.sc)
+  auto split_len = [&](long long target) {
+    const long long want = (target + tiles - 1) / tiles;
+    const long long maxs = (P + 4 * BKP_PLAN - 1) / (4 * BKP_PLAN);   // >= 4 stages per split
+    long long ns = want < maxs ? want : maxs;
+    if (ns < 1) ns = 1;
+    long long len = (P + ns - 1) / ns;
+    return (len + BKP_PLAN - 1) / BKP_PLAN * BKP_PLAN;
+  };
+  long long len = split_len(1024);
+  if (d->dtype == RR_BF16 && d->mode != RR_CONV3X3) {
+    const long long part = (P + len - 1) / len * p.CA * p.CB * p.taps * 4;
+    const long long act = 2 * P * (convT ? d->c_in1 + 4LL * d->c_out : (long long)d->c_out + d->c_in1 + d->c_in2);
+    if (8 * part > act) len = split_len(512);
+  }
   p.split_len = (int)len;
   p.nsplit = (int)((P + len - 1) / len);
   return p;
@@ -718,7 +747,7 @@ extern "C" int rr_wgrad_reduce(const rr_wgrad_desc *d, const void *ws, size_t ws
   if (ws_bytes < rr_wgrad_workspace(d)) return RR_EWORKSPACE;
   int CA, CB, taps, nsplit;
   reduce_shape(d, CA, CB, taps, nsplit);
-  const int alayout = !swgrad_ok(d) && halo_ok(d);   // wgrad3_halo_kernel's slab layout
+  const int alayout = !swgrad_ok(d) && CA % 4 == 0;   // the halo / tiled kernels' slab layout
   launch_reduce((const float *)ws, dw, CA, CB, taps, nsplit, d->accumulate, alayout, (hipStream_t)stream);
   RR_CHECK_LAUNCH();
   return RR_OK;
