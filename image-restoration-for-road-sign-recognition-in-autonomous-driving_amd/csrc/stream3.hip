@@ -261,10 +261,21 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     al = a.balpha[0];
     __syncthreads();
   }
+  // BNBWD: the wave's (s, b) coefficients in registers for the whole loop
+  // (two LDS round trips with a full lgkmcnt wait per step otherwise)
+  f32x4 bk[BNBWD ? MC : 1][2];
+  if constexpr (BNBWD) {
+#pragma unroll
+    for (int mi = 0; mi < MC; ++mi) lds_read_2x4(coef + (wc * 32 + mi * 16 + fq * 4) * 2, bk[mi][0], bk[mi][1]);
+  }
+  // the bias in registers for the whole loop (read from the LDS per step,
+  // behind a full lgkmcnt wait, until round 6)
+  f32x4 biar[(F & F_BIAS) ? MC : 1];
   if constexpr ((F & F_BIAS) != 0) {
-    // the bias is read from LDS per step (8 fewer VGPRs held over the loop)
     if (tid < 64) coef[tid] = a.bias[tid];
     __syncthreads();
+#pragma unroll
+    for (int mi = 0; mi < MC; ++mi) biar[mi] = lds_read_4(coef + wc * 32 + mi * 16 + fq * 4);
   }
 
   // ---- LDS-DMA pieces: a 1-KB piece lies in one ring row, so its row and
@@ -433,11 +444,10 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     uint2 pk[MC][MP];
 #pragma unroll
     for (int mi = 0; mi < MC; ++mi) {
-      const int c = wc * 32 + mi * 16 + fq * 4;
-      f32x4 k01, k23;                           // (s, b) of channels c .. c + 3
-      if constexpr (BNBWD) lds_read_2x4(coef + c * 2, k01, k23);
+      f32x4 k01, k23;                           // (s, b) of the lane's 4 channels
+      if constexpr (BNBWD) { k01 = bk[mi][0]; k23 = bk[mi][1]; }
       f32x4 bia;
-      if constexpr ((F & F_BIAS) != 0) bia = lds_read_4(coef + c);
+      if constexpr ((F & F_BIAS) != 0) bia = biar[mi];
 #pragma unroll
       for (int ni = 0; ni < MP; ++ni) {
         f32x4 g = acc[mi][ni];
