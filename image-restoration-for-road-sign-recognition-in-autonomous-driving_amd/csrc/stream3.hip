@@ -279,34 +279,43 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
   }
 
   // ---- LDS-DMA pieces: a 1-KB piece lies in one ring row, so its row and
-  // chunk are wave-uniform; the lane's plane / pixel is fixed ----
+  // chunk are wave-uniform; the lane's plane / pixel is fixed.  A wave's
+  // DMAW consecutive pieces lie in ONE ring row (a row is a whole multiple of
+  // them), so the row's terms (image row, validity, source base, ring slot)
+  // are formed once per step, and the lane's padding select is arithmetic:
+  // the scalar unit, shared by the CU's 8 waves, and an exec-mask region per
+  // piece had made the DMA issue ~16 % of a step (profiles/r6h_s3_stamps.jsonl) ----
+  static_assert((ROWB / 1024) % DMAW == 0, "a wave's pieces share one ring row");
   const long long zoff = (long long)((uintptr_t)rr_zero_page - (uintptr_t)a.x);   // zero source
-  int drow[DMAW], dchk[DMAW], dofs[DMAW];
+  const int drow = (wv * DMAW * 1024) / ROWB;       // the wave's ring row within a step (uniform)
+  int dchk[DMAW];
+  long long dofs[DMAW];                             // lane source offset in the row, or -1 (padding)
 #pragma unroll
   for (int i = 0; i < DMAW; ++i) {
     const int piece = (wv * DMAW + i) * 1024;
-    drow[i] = piece / ROWB;
-    dchk[i] = piece - drow[i] * ROWB;
+    dchk[i] = piece - drow * ROWB;
     const int o = dchk[i] + lane * 16;
     const int px = o / 128, x = px - 1, chunk = ((o / 16) & 7) ^ s3_swz(px & 15);
     dofs[i] = (x >= 0 && x < W) ? x * 128 + chunk * 16 : -1;
   }
   // DMA of virtual step `cu` into the ring rows starting at slot `slot`
   auto issue = [&](int slot, const Cur &cu, bool live) __attribute__((always_inline)) {
+    const int y = cu.kind == S3_PRE ? cu.y0 - RPS + 1 + drow : cu.y0 + 1 + drow;
+    const bool rok = live & (y >= 0) & (y < H) & ((cu.kind != S3_PRE) | (drow >= RPS - 2));   // uniform
+    // (an invalid row reads the zero page: its base makes every lane's
+    // candidate land there)
+    const long long rbase = rok ? ((long long)(cu.n * H + y) * W) * 128 : zoff;
+    int s = slot + drow;
+    s = s >= RING ? s - RING : s;
+    char *const dst = smem + s * ROWB;
 #pragma unroll
     for (int i = 0; i < DMAW; ++i) {
-      const int r = drow[i];
-      const int y = cu.kind == S3_PRE ? cu.y0 - RPS + 1 + r : cu.y0 + 1 + r;
-      const bool rok = live & (y >= 0) & (y < H) & ((cu.kind != S3_PRE) | (r >= RPS - 2));   // uniform
-      const long long rbase = ((long long)(cu.n * H + y) * W) * 128;
-      // one base pointer + selected offsets (no pointer select / branch: two
-      // exec-masked DMA instructions would break the vmcnt accounting)
-      long long off = dofs[i] >= 0 ? rbase + dofs[i] : zoff;
-      off = rok ? off : zoff;
-      int s = slot + r;
-      s = s >= RING ? s - RING : s;
-      __builtin_amdgcn_global_load_lds((const void *)(a.x + off),
-                                       LDS_PTR(smem + s * ROWB + dchk[i]), 16, 0, 0);
+      // one base pointer + a selected offset (no pointer select / branch:
+      // two exec-masked DMA instructions would break the vmcnt accounting)
+      const long long m = dofs[i] >> 63;            // -1: padding lane
+      const long long cand = rok ? rbase + dofs[i] : zoff;
+      const long long off = (cand & ~m) | (zoff & m);
+      __builtin_amdgcn_global_load_lds((const void *)(a.x + off), LDS_PTR(dst + dchk[i]), 16, 0, 0);
     }
   };
   auto advance = [&](Cur &cu) __attribute__((always_inline)) {
