@@ -84,6 +84,18 @@ run_step() {
       done
       unset RR_LIB_PATH
       cat ${O}_ablibs.txt ;;
+    abinf)
+      # cfg5 bf16 inference of this build vs another .so, alternating
+      # processes, 3 rounds (images/s, restore / judge ms per 1k images)
+      for i in 1 2 3; do
+        for L in cur other; do
+          if [ $L = other ]; then export RR_LIB_PATH=$arg; else unset RR_LIB_PATH; fi
+          timeout -k 10 300 python tools/bench_inference.py --images 4096 --dtype bf16 > ${O}_abinf.log 2>&1 || { unset RR_LIB_PATH; return 1; }
+          tail -1 ${O}_abinf.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); s=d['stage_ms_per_1k_images']; print('$L', d['images_per_sec'], s['restore'], s['judge'], d['roofline']['restore']['frac'])" >> ${O}_abinf.txt
+        done
+      done
+      unset RR_LIB_PATH
+      cat ${O}_abinf.txt ;;
     abconv)
       # per-layer conv3r A/B of this build vs another .so (cfg3 and the 224
       # set), alternating processes, 3 rounds
