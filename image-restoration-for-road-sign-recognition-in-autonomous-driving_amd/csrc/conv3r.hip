@@ -149,7 +149,10 @@ template <int N> using ic = std::integral_constant<int, N>;
 // concat split only -- the forward and plain dgrad of the training step,
 // 2 = 1 + the accumulate / ReLU-mask operands (the identity-shortcut and VGG
 // dgrads), 3 = the fused BN -> PReLU backward only, 4 = 1 + the 2x2 max-pool
-// (the perceptual VGG's conv + ReLU + MaxPool2d, rr_igemm_pool).  A specialised instance
+// (the perceptual VGG's conv + ReLU + MaxPool2d, rr_igemm_pool), 5 = 4 + the
+// residual and PReLU (the BN-folded eval forward of the restore path,
+// rr_igemm_ex: the general instance sat at 256 VGPRs with scratch spills on
+// the row-segment tiles of the cfg5 geometry).  A specialised instance
 // holds no registers for the epilogues it cannot run (no spills) and carries
 // none of their branches: the plain epilogue's instruction stream is a third
 // of the general one's (989 vs the general path's share of 11.7 k).
@@ -165,8 +168,8 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3r_kernel(IgemmArgs a) 
   constexpr bool BNREG = G::SEGM || NWV == 8 || EPI == 3;
   constexpr bool ALLOW_BN = EPI == 0 || EPI == 3;     // the fused BN backward (a.bpart)
   constexpr bool ALLOW_OPS = EPI == 0 || EPI == 2;    // accumulate / ReLU-mask operands
-  constexpr bool ALLOW_EX = EPI == 0;                 // residual, PReLU
-  constexpr bool ALLOW_POOL = EPI == 0 || EPI == 4;   // the 2x2 max-pool epilogue
+  constexpr bool ALLOW_EX = EPI == 0 || EPI == 5;     // residual, PReLU
+  constexpr bool ALLOW_POOL = EPI == 0 || EPI == 4 || EPI == 5;   // the 2x2 max-pool epilogue
   constexpr int NS = G::NS, R = G::R, NM = G::NM, WC = G::WC, RS = G::RS;
   constexpr int HW = W * W;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
@@ -976,6 +979,10 @@ static void c3_launch(const IgemmArgs &a, dim3 grid, dim3 block, hipStream_t st)
   }
   if (!a.bpart && !ex) {
     hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, 2>), grid, block, 0, st, a);
+    return;
+  }
+  if (!a.bpart && !a.accumulate && !a.has_mask) {
+    hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, 5>), grid, block, 0, st, a);
     return;
   }
   hipLaunchKernelGGL((conv3r_kernel<W_, BC, NW, NWV, HB, SG, 0>), grid, block, 0, st, a);
