@@ -1129,9 +1129,10 @@ extern "C" const char *rr_igemm_kernel_name(const rr_igemm_desc *d, int bnbwd) {
   if (d->act > RR_ACT_RELU) {
     // (the pool epilogue needs a 2x2 window: rr_igemm_ex refuses such maps)
     if ((d->act & RR_ACT_POOL) && (d->h < 2 || d->w < 2)) return "unsupported";
+    if (!bnbwd && stream3_ex_ok(d)) return stream3_name(d, "");
     return !bnbwd && conv3r_bc(d) ? conv3r_name(d) : "unsupported";
   }
-  if (stream3_blocks(d, bnbwd)) return d->w == 64 ? "stream3_kernel<64>" : "stream3_kernel<32>";
+  if (stream3_blocks(d, bnbwd)) return stream3_name(d, "");
   S1Plan pl;
   if (!bnbwd && stream1_plan(d, &pl)) return stream1_name(pl);
   if (conv3r_bc(d)) return conv3r_name(d);
@@ -1174,7 +1175,7 @@ extern "C" int rr_igemm(const rr_igemm_desc *d, const void *x1, const void *x2,
     s.x = a.x1; s.x2 = a.x2; s.wt = a.wt; s.bias = a.bias; s.y = a.y1;
     s.mask = d->has_mask ? a.mask : nullptr;
     s.stats = a.stats;
-    s.n = d->n; s.h = d->h; s.act = d->act; s.accumulate = d->accumulate;
+    s.n = d->n; s.h = d->h; s.w = d->w; s.act = d->act; s.accumulate = d->accumulate;
     return stream3_launch(d, s, 0, st);
   }
   S1Plan pl;
@@ -1200,6 +1201,17 @@ extern "C" int rr_igemm_ex(const rr_igemm_desc *d, const void *x1, const void *x
   if ((d->act & RR_ACT_POOL) && (!y_pool || d->out_split || d->h < 2 || d->w < 2)) return RR_EINVAL;
   if ((d->act & RR_ACT_NOFULL) && (!(d->act & RR_ACT_POOL) || d->accumulate || d->want_stats))
     return RR_EINVAL;
+  if (d->act > RR_ACT_RELU && stream3_ex_ok(d)) {
+    // the 64 -> 64 maps the streaming kernel takes (whole rows, or column
+    // strips of the reference's 224 maps)
+    if (!x1 || !w || !bias || (!y1 && !(d->act & RR_ACT_NOFULL))) return RR_EINVAL;
+    S3Args s{};
+    s.x = (const char *)x1; s.wt = (const char *)w; s.bias = bias;
+    s.y = (d->act & RR_ACT_NOFULL) ? nullptr : (char *)y1;
+    s.n = d->n; s.h = d->h; s.w = d->w; s.act = d->act;
+    s.alpha = alpha; s.res = (const char *)res; s.ypool = (char *)y_pool;
+    return stream3_launch_ex(d, s, (hipStream_t)stream);
+  }
   if (d->act > RR_ACT_RELU && !conv3r_bc(d)) return RR_EUNSUPPORTED;
   // (y1 unused with RR_ACT_NOFULL: fill_args wants a pointer)
   void *y1a = (d->act & RR_ACT_NOFULL) ? y_pool : y1;
@@ -1226,10 +1238,10 @@ extern "C" int rr_igemm_pool(const rr_igemm_desc *d, const void *x1, const void 
       d->accumulate || d->has_mask || d->want_stats || d->out_nchw || d->h < 2 || d->w < 2)
     return RR_EINVAL;
   hipStream_t st = (hipStream_t)stream;
-  if (stream3_blocks(d, 0) && !d->c_in2 && pool_idx) {
+  if (stream3_blocks(d, 0) && !d->c_in2 && (pool_idx ? !stream3_strips(d) : d->has_bias)) {
     S3Args s{};
     s.x = (const char *)x1; s.wt = (const char *)w; s.bias = d->has_bias ? bias : nullptr;
-    s.n = d->n; s.h = d->h; s.act = d->act;
+    s.n = d->n; s.h = d->h; s.w = d->w; s.act = d->act;
     s.ypool = (char *)y_pool; s.pidx = pool_idx;
     if (!x1 || !w || (d->has_bias && !bias)) return RR_EINVAL;
     return stream3_launch_pool(d, s, st);
@@ -1250,7 +1262,7 @@ extern "C" const char *rr_igemm_pool_kernel_name(const rr_igemm_desc *d) {
   if (!d || d->mode != RR_CONV3X3 || d->act != RR_ACT_RELU || d->out_split || d->accumulate ||
       d->has_mask || d->want_stats || d->out_nchw || d->h < 2 || d->w < 2)
     return "unsupported";
-  if (stream3_blocks(d, 0) && !d->c_in2) return d->w == 64 ? "stream3_kernel<64,pool>" : "stream3_kernel<32,pool>";
+  if (stream3_blocks(d, 0) && !d->c_in2) return stream3_name(d, "pool");
   rr_igemm_desc d2 = *d;
   d2.act = RR_ACT_RELU | RR_ACT_POOL | RR_ACT_NOFULL;
   return conv3r_bc(&d2) ? conv3r_name(&d2) : "unsupported";
@@ -1263,7 +1275,7 @@ extern "C" const char *rr_igemm_pool_kernel_name(const rr_igemm_desc *d) {
 static bool dgrad_sc_ok(const rr_igemm_desc *d, int c_sc) {
   return d && d->mode == RR_CONV3X3 && !d->act && !d->has_bias && !d->want_stats && !d->has_mask &&
          !d->out_split && !d->accumulate && !d->out_nchw && !d->c_in2 && c_sc == 64 &&
-         stream3_blocks(d, 0);
+         stream3_blocks(d, 0) && !stream3_strips(d);
 }
 
 extern "C" int rr_igemm_dgrad_sc(const rr_igemm_desc *d, const void *dy, const void *w,
@@ -1276,14 +1288,14 @@ extern "C" int rr_igemm_dgrad_sc(const rr_igemm_desc *d, const void *dy, const v
   if (!dgrad_sc_ok(d, c_sc)) return RR_EUNSUPPORTED;
   S3Args s{};
   s.x = (const char *)dy; s.wt = (const char *)w; s.y = (char *)y;
-  s.n = d->n; s.h = d->h;
+  s.n = d->n; s.h = d->h; s.w = d->w;
   s.xsc = (const char *)dy_sc; s.wsc = (const char *)w_sc;
   return stream3_launch_sc(d, s, (hipStream_t)stream);
 }
 
 extern "C" const char *rr_igemm_dgrad_sc_kernel_name(const rr_igemm_desc *d, int c_sc) {
   if (!dgrad_sc_ok(d, c_sc)) return "unsupported";
-  return d->w == 64 ? "stream3_kernel<64,sc>" : "stream3_kernel<32,sc>";
+  return stream3_name(d, "sc");
 }
 
 static int bnbwd_rows(const rr_igemm_desc *d) { return rr_igemm_stat_blocks(d); }

@@ -14,7 +14,7 @@ struct S3Args {
   char *y;                   // NHWC bf16 output [n][h][w][64]
   const char *mask;          // relu-backward mask (NHWC bf16) or null
   float *stats;              // [nwg][64][2] pre-bias partial sums or null
-  int n, h;                  // w is the template width
+  int n, h, w;               // w: the image width (the template width, or a multiple: column strips)
   int act, accumulate;
   // BN -> PReLU backward epilogue (rr_igemm_bnbwd), bt != null selects it
   const char *bt;
@@ -27,6 +27,9 @@ struct S3Args {
   // 1x1 second source (stream3_launch_sc): NHWC bf16 [n][h][w][64] and its
   // weights [64 out][64] (rows of the 1x1 dgrad pack)
   const char *xsc, *wsc;
+  // eval epilogues (stream3_launch_ex): PReLU alpha [1], identity residual NHWC bf16
+  const float *alpha;
+  const char *res;
 };
 
 // 0 when the descriptor is not handled by the streaming kernel, else the
@@ -35,6 +38,10 @@ struct S3Args {
 // beyond the supported flag sets, so the partial-row count a caller sizes
 // from the plain descriptor matches the launch.
 int stream3_blocks(const rr_igemm_desc *d, int bnbwd);
+// 1 when the streaming kernel walks *d in column strips (maps wider than 64):
+// only the plain / bias / eval flag sets have strip instances (no statistics,
+// operands, BN backward, 1x1 second source or pool window index)
+int stream3_strips(const rr_igemm_desc *d);
 // launch; returns an RR_* status
 int stream3_launch(const rr_igemm_desc *d, const S3Args &a, int bnbwd, hipStream_t st);
 // conv (+ bias) + ReLU + MaxPool2d(2, 2) with the window index (a.ypool,
@@ -44,3 +51,11 @@ int stream3_launch_pool(const rr_igemm_desc *d, const S3Args &a, hipStream_t st)
 // the plain 64 -> 64 dgrad plus a 1x1 dgrad of a.xsc with a.wsc into the same
 // accumulators (rr_igemm_dgrad_sc); RR_EUNSUPPORTED when not taken
 int stream3_launch_sc(const rr_igemm_desc *d, const S3Args &a, hipStream_t st);
+// the BN-folded eval epilogues of rr_igemm_ex (d->act: PReLU, or ReLU with the
+// identity residual and / or the 2x2 max-pool, no window index) on the
+// streaming kernel: stream3_ex_ok() != 0 when it takes *d
+int stream3_ex_ok(const rr_igemm_desc *d);
+int stream3_launch_ex(const rr_igemm_desc *d, const S3Args &a, hipStream_t st);
+// "stream3_kernel<64>" / "<32>" (whole rows) or "<s64>" / "<s32>" (column
+// strips) + the suffix
+const char *stream3_name(const rr_igemm_desc *d, const char *suffix);

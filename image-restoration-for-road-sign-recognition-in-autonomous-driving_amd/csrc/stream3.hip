@@ -86,8 +86,14 @@ constexpr int S3_WG = 256;   // workgroups: one per CU on MI355X (fixed: determi
 // F_SC: a 1x1 dgrad of a second gradient (a.xsc, weights a.wsc) summed into
 // the accumulators -- the shortcut conv's dgrad of a ResidualBlock with a
 // concat input, 14:109-113 (rr_igemm_dgrad_sc)
+// F_PRELU / F_RES: the BN-folded eval forward's epilogues (rr_igemm_ex,
+// 17:84-86 through 14:96-115): PReLU(conv + b) of conv1, act(conv + b + x)
+// of an identity-shortcut conv2 (the residual added after the bias, as the
+// tap-reuse conv's register epilogue); F_PFULL: with F_POOL, the full-size
+// output is stored too (an encoder block's skip tensor); F_PNOIDX: with
+// F_POOL, no window index (nothing runs backward)
 enum : int { F_BIAS = 1, F_STATS = 2, F_RELU = 4, F_ACC = 8, F_MASK = 16, F_BNBWD = 32, F_POOL = 64,
-             F_SC = 128 };
+             F_SC = 128, F_PRELU = 256, F_RES = 512, F_PFULL = 1024, F_PNOIDX = 2048 };
 
 // chunk swizzle: the 16 pixels of a B read at pixel offset P in {0, 1, 2}
 // mod 16 need distinct (p & 1, chunk ^ swz(p)) pairs with chunks c (outer 8
@@ -191,11 +197,17 @@ template <int W, int MP, bool POOL> struct S3Blk {
   static constexpr int bcol(int ni) { return POOL ? (ni >> 1) * 16 : (ni * 16) % W; }
 };
 
+// virtual step: pre-load, or compute of output rows [y0, y0 + RPS) of the
+// column (image img, columns [xs, xs + W)); a column is a whole image on the
+// 32 / 64-wide maps, a W-wide strip of it on the wider ones (column-strip
+// mode: the strip's left / right neighbour pixels are its halo)
 struct Cur {
-  int kind, n, y0, c;   // virtual step: pre-load, or compute of output rows [y0, y0 + RPS) of image n
+  int kind, img, xs, y0, c;
 };
 
-template <int W, int MP, int F, int STAG>
+// SM: column-strip mode (a.w a multiple of W); whole rows (a.w == W) keep
+// the width a compile-time constant
+template <int W, int MP, int F, int STAG, bool SM>
 __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
   using G = S3Geo<W, MP>;
   constexpr int RPS = G::RPS, ROWB = G::ROWB, RING = G::RING, D = G::D;
@@ -206,15 +218,19 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
   constexpr bool STATS = (F & F_STATS) != 0;
   constexpr bool POOL = (F & F_POOL) != 0;
   constexpr bool SC = (F & F_SC) != 0;
+  constexpr bool RES = (F & F_RES) != 0, PRELU = (F & F_PRELU) != 0;
+  constexpr bool PFULL = (F & F_PFULL) != 0, PIDX = POOL && !(F & F_PNOIDX);
   static_assert(!SC || (F == F_SC && STAG == 0), "the 1x1 second source: plain dgrad epilogue");
-  static_assert(!POOL || ((F & ~(F_BIAS | F_RELU | F_POOL)) == 0 && (F & F_RELU) && MP % 2 == 0 &&
-                          W % (8 * MP) == 0), "pool epilogue: bias + ReLU, row-pair blocks");
-  constexpr int NE = BNBWD ? 1 : (ACC ? 1 : 0) + (MASK ? 1 : 0);   // epilogue loads per block
-  // S: stores per step (16-B output stores; POOL: a pooled value + an index
-  // store per channel block and column block pair)
+  static_assert(!POOL || ((F & ~(F_BIAS | F_RELU | F_POOL | F_RES | F_PFULL | F_PNOIDX)) == 0 && (F & F_RELU) &&
+                          MP % 2 == 0 && W % (8 * MP) == 0), "pool epilogue: bias + ReLU, row-pair blocks");
+  static_assert(!(RES && (ACC || BNBWD || STATS)) && !(PRELU && (F & F_RELU)), "epilogue flag set");
+  constexpr int NE = BNBWD ? 1 : (ACC ? 1 : 0) + (MASK ? 1 : 0) + (RES ? 1 : 0);   // epilogue loads per block
+  // S: stores per step (16-B output stores; POOL: a pooled value (+ an index)
+  // store per channel block and column block pair, + the full output's)
   // (F_SC: its B fragments, 2 k-halves per pixel block, count with the
   // epilogue loads: issued with them, waited for after the 3x3 MFMAs)
-  constexpr int E = MC * MP * NE + (SC ? 2 * MP : 0), S = POOL ? MC * MP : MP;
+  constexpr int E = MC * MP * NE + (SC ? 2 * MP : 0);
+  constexpr int S = POOL ? (MC * MP / 2) * (PIDX ? 2 : 1) + (PFULL ? MP : 0) : MP;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
   float *coef = reinterpret_cast<float *>(smem + RING * ROWB);   // [64][2]
 
@@ -224,7 +240,8 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
   const int wc = wv & 1, wp = wv >> 1;
   const int frow = lane & 15, fq = lane >> 4;
   const int H = a.h;
-  const int spi = H / RPS;                      // compute steps per image
+  const int IW = SM ? a.w : W;                  // image width: W (whole rows) or a multiple of it (strips)
+  const int spi = H / RPS;                      // compute steps per column
   const int cbeg = (int)((long long)blockIdx.x * nsteps / S3_WG);
   const int cend = (int)((long long)(blockIdx.x + 1) * nsteps / S3_WG);
 
@@ -271,6 +288,7 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
   // the bias in registers for the whole loop (read from the LDS per step,
   // behind a full lgkmcnt wait, until round 6)
   f32x4 biar[(F & F_BIAS) ? MC : 1];
+  const float alp = PRELU ? a.alpha[0] : 0.f;   // (resident with the weights: the vmcnt(0) below)
   if constexpr ((F & F_BIAS) != 0) {
     if (tid < 64) coef[tid] = a.bias[tid];
     __syncthreads();
@@ -288,23 +306,33 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
   static_assert((ROWB / 1024) % DMAW == 0, "a wave's pieces share one ring row");
   const long long zoff = (long long)((uintptr_t)rr_zero_page - (uintptr_t)a.x);   // zero source
   const int drow = (wv * DMAW * 1024) / ROWB;       // the wave's ring row within a step (uniform)
+  static_assert(DMAW <= 8, "piece bits");
   int dchk[DMAW];
-  long long dofs[DMAW];                             // lane source offset in the row, or -1 (padding)
+  int dofs[DMAW];                                   // lane source offset from the column's pixel 0
+  // lane pixel of piece i: bit i inside the column, bit 8 + i its left
+  // neighbour, bit 16 + i its right one (one register for all pieces)
+  uint32_t dcode = 0;
 #pragma unroll
   for (int i = 0; i < DMAW; ++i) {
     const int piece = (wv * DMAW + i) * 1024;
     dchk[i] = piece - drow * ROWB;
     const int o = dchk[i] + lane * 16;
     const int px = o / 128, x = px - 1, chunk = ((o / 16) & 7) ^ s3_swz(px & 15);
-    dofs[i] = (x >= 0 && x < W) ? x * 128 + chunk * 16 : -1;
+    dofs[i] = x * 128 + chunk * 16;
+    dcode |= (x >= 0 && x < W ? 1u : 0u) << i;
+    dcode |= (x == -1 ? 1u : 0u) << (8 + i);
+    dcode |= (x == W ? 1u : 0u) << (16 + i);
   }
   // DMA of virtual step `cu` into the ring rows starting at slot `slot`
   auto issue = [&](int slot, const Cur &cu, bool live) __attribute__((always_inline)) {
     const int y = cu.kind == S3_PRE ? cu.y0 - RPS + 1 + drow : cu.y0 + 1 + drow;
     const bool rok = live & (y >= 0) & (y < H) & ((cu.kind != S3_PRE) | (drow >= RPS - 2));   // uniform
+    // the column's neighbour pixels are real ones inside the image (strips)
+    const bool lm = SM && cu.xs > 0, rm = SM && cu.xs + W < IW;                              // uniform
+    const uint32_t okb = (dcode | (lm ? dcode >> 8 : 0u) | (rm ? dcode >> 16 : 0u)) & 0xffu;
     // (an invalid row reads the zero page: its base makes every lane's
     // candidate land there)
-    const long long rbase = rok ? ((long long)(cu.n * H + y) * W) * 128 : zoff;
+    const long long rbase = rok ? ((long long)(cu.img * H + y) * IW + cu.xs) * 128 : zoff;
     int s = slot + drow;
     s = s >= RING ? s - RING : s;
     char *const dst = smem + s * ROWB;
@@ -312,7 +340,7 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     for (int i = 0; i < DMAW; ++i) {
       // one base pointer + a selected offset (no pointer select / branch:
       // two exec-masked DMA instructions would break the vmcnt accounting)
-      const long long m = dofs[i] >> 63;            // -1: padding lane
+      const long long m = ((okb >> i) & 1u) ? 0LL : -1LL;   // -1: padding lane
       const long long cand = rok ? rbase + dofs[i] : zoff;
       const long long off = (cand & ~m) | (zoff & m);
       __builtin_amdgcn_global_load_lds((const void *)(a.x + off), LDS_PTR(dst + dchk[i]), 16, 0, 0);
@@ -324,7 +352,12 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     } else {
       ++cu.c;
       cu.y0 += RPS;
-      if (cu.y0 == H) { cu.y0 = 0; ++cu.n; cu.kind = S3_PRE; }
+      if (cu.y0 == H) {
+        cu.y0 = 0;
+        cu.xs += W;
+        if (cu.xs == IW) { cu.xs = 0; ++cu.img; }
+        cu.kind = S3_PRE;
+      }
     }
   };
 
@@ -368,7 +401,7 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     if constexpr (SC) {
 #pragma unroll
       for (int ni = 0; ni < MP; ++ni) {
-        const long long ub = (pix0 + (q0 + brow(ni)) * W + x0 + bcol(ni)) * 128;   // uniform
+        const long long ub = (pix0 + (q0 + brow(ni)) * IW + x0 + bcol(ni)) * 128;   // uniform
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) esc[ni][kb] = load_b128_async(a.xsc + ub + frow * 128 + kb * 64 + fq * 16);
       }
@@ -377,9 +410,10 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     for (int mi = 0; mi < MC; ++mi)
 #pragma unroll
       for (int ni = 0; ni < MP; ++ni) {
-        const long long ub = (pix0 + (q0 + brow(ni)) * W + x0 + bcol(ni)) * 128 + mi * 32;   // uniform
+        const long long ub = (pix0 + (q0 + brow(ni)) * IW + x0 + bcol(ni)) * 128 + mi * 32;   // uniform
         if constexpr (BNBWD) ev0[mi][ni] = load_b64_async(a.bt + ub + le);
         if constexpr (!BNBWD && ACC) ev0[mi][ni] = load_b64_async(a.y + ub + le);
+        if constexpr (RES) ev0[mi][ni] = load_b64_async(a.res + ub + le);
         if constexpr (!BNBWD && MASK) ev1[mi][ni] = load_b64_async(a.mask + ub + le);
       }
   };
@@ -397,7 +431,7 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
       for (int mi = 0; mi < MC; ++mi)
 #pragma unroll
         for (int ni = 0; ni < MP; ++ni) {
-          if constexpr (BNBWD || ACC) asm volatile("" : "+v"(ev0[mi][ni]));
+          if constexpr (BNBWD || ACC || RES) asm volatile("" : "+v"(ev0[mi][ni]));
           if constexpr (MASK && !BNBWD) asm volatile("" : "+v"(ev1[mi][ni]));
         }
     }
@@ -449,7 +483,9 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     }
   };
   // epilogue: lane = pixel (frow) x 4 channels of each 16 x 16 block
-  auto epilogue = [&](long long pix0) __attribute__((always_inline)) {
+  // (pix0: the step's first output pixel, rowg: its image row over the batch,
+  // xs: the column's first image column)
+  auto epilogue = [&](long long pix0, int rowg, int xs) __attribute__((always_inline)) {
     uint2 pk[MC][MP];
 #pragma unroll
     for (int mi = 0; mi < MC; ++mi) {
@@ -485,9 +521,14 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
             r1[mi] += g * g;
           }
           if constexpr ((F & F_BIAS) != 0) g += bia;
+          if constexpr (RES) g += unpack4(ev0[mi][ni]);
           if constexpr ((F & F_RELU) != 0) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) g[j] = fmaxf(g[j], 0.f);
+          }
+          if constexpr (PRELU) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) g[j] = g[j] > 0.f ? g[j] : alp * g[j];
           }
           if constexpr (MASK) {
             const f32x4 mk = unpack4(ev1[mi][ni]);
@@ -502,7 +543,7 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
       // the 2x2 window (rows q0, q0 + 1 of columns x0 + 16 j + frow and its
       // xor-1 neighbour lane) on the bf16-rounded values -- the stored ones
       // maxpool_fwd8 would read -- in window order, first max + its index
-      const long long prow = (pix0 / W + q0) >> 1;                // pooled row (uniform)
+      const long long prow = (rowg + q0) >> 1;                    // pooled row (uniform)
 #pragma unroll
       for (int mi = 0; mi < MC; ++mi)
 #pragma unroll
@@ -517,13 +558,14 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
 #pragma unroll
           for (int c = 0; c < 4; ++c) m[c] = pool4_first_max(u0[c], v0[c], u1[c], v1[c], id[c]);
           if ((frow & 1) == 0) {
-            const long long pp = prow * (W / 2) + ((x0 + 16 * j + frow) >> 1);
+            const long long pp = prow * (IW / 2) + ((xs + x0 + 16 * j + frow) >> 1);
             const int c = wc * 32 + mi * 16 + fq * 4;
             *reinterpret_cast<uint2 *>(a.ypool + (pp * 64 + c) * 2) = pack4(m);
-            *reinterpret_cast<uint32_t *>(a.pidx + pp * 64 + c) = id[0] | (id[1] << 8) | (id[2] << 16) | (id[3] << 24);
+            if constexpr (PIDX)
+              *reinterpret_cast<uint32_t *>(a.pidx + pp * 64 + c) = id[0] | (id[1] << 8) | (id[2] << 16) | (id[3] << 24);
           }
         }
-      return;
+      if constexpr (!PFULL) return;
     }
     // widened stores: per pixel-block pair (A, B) two permlane16 swap levels
     // turn the accumulator layout (lane: 4 channels of one pixel) into 16 B
@@ -552,7 +594,7 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int ni = 2 * j + h;
-        const long long ub = (pix0 + (q0 + brow(ni)) * W + x0 + bcol(ni)) * 128;   // uniform
+        const long long ub = (pix0 + (q0 + brow(ni)) * IW + x0 + bcol(ni)) * 128;   // uniform
         *reinterpret_cast<uint4 *>(a.y + ub + le2) = make_uint4(v[h][0], v[h][1], v[h][2], v[h][3]);
       }
     }
@@ -562,10 +604,14 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
   // compiler's own wait for them would otherwise drain the prologue DMAs
   __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0) (gfx9 encoding)
   Cur ld;
-  ld.c = cbeg;
-  ld.n = cbeg / spi;
-  ld.y0 = (cbeg - ld.n * spi) * RPS;
-  ld.kind = S3_PRE;
+  {
+    const int col = cbeg / spi, ns = IW / W;    // column, columns per image
+    ld.c = cbeg;
+    ld.img = col / ns;
+    ld.xs = (col - ld.img * ns) * W;
+    ld.y0 = (cbeg - col * spi) * RPS;
+    ld.kind = S3_PRE;
+  }
   Cur cp = ld;
   int lslot = 0;                                // ring slot of the loader's step
 #pragma unroll
@@ -593,6 +639,7 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
   constexpr int YE = (D - 1) * DMAW + S + (E + S) * (D - 1);      // steady state, early
   constexpr int YL = (D - 1) * DMAW + S * (D - 1) + E * (D - 1);  // steady state, late
   long long ppix = 0;                           // late half: the step whose epilogue is pending
+  int prowg = 0, pxs = 0;
   bool pcomp = false;
   [[maybe_unused]] unsigned long long st_a = 0, st_b = 0, st_wait = 0, st_issue = 0, st_mfma = 0, st_epi = 0,
                                       st_steps = 0, st_t0 = 0, st_t1 = 0;
@@ -615,8 +662,9 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     st_wait += st_b - st_a;
     st_a = st_b;
     const bool comp = cp.kind == S3_COMP;
-    const long long pix0 = (long long)(cp.n * H + cp.y0) * W;
-    if (late && pcomp) epilogue(ppix);          // its loads were waited for last iteration
+    const int rowg = cp.img * H + cp.y0;
+    const long long pix0 = (long long)rowg * IW + cp.xs;
+    if (late && pcomp) epilogue(ppix, prowg, pxs);   // its loads were waited for last iteration
     // epilogue loads BEFORE this iteration's DMA (see the vmcnt accounting)
     if constexpr (E > 0) {
       if (comp) load_e(pix0);
@@ -653,18 +701,20 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
               acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                   wsr[mi][kb], __builtin_bit_cast(bf16x8, esc[ni][kb]), acc[mi][ni], 0, 0, 0);
       }
-      if (!late) epilogue(pix0);
+      if (!late) epilogue(pix0, rowg, cp.xs);
       S3_STAMP(st_b);
       st_epi += st_b - st_a;
     }
     ppix = pix0;
+    prowg = rowg;
+    pxs = cp.xs;
     pcomp = comp;
     cslot += RPS;
     cslot = cslot >= RING ? cslot - RING : cslot;
     hist = (hist << 1) | (comp ? 1u : 0u);
     advance(cp);
   }
-  if (late && pcomp) epilogue(ppix);            // the late half's last epilogue
+  if (late && pcomp) epilogue(ppix, prowg, pxs);   // the late half's last epilogue
 #ifdef RR_S3_STAMPS
   S3_STAMP(st_t1);
   if (lane == 0) {
@@ -747,13 +797,13 @@ int s3_flags(const rr_igemm_desc *d, bool bnbwd) {
   }
 }
 
-template <int W, int MP, int F, int STG = -1>
+template <int W, int MP, int F, int STG = -1, bool SM = false>
 void launch1(const S3Args &a, int P, hipStream_t st) {
   // the late-epilogue stagger measured faster only for 256-pixel steps
   // without the BN-statistics registers (it keeps acc live across the loop
   // back-edge: the stats variants spill with it)
   constexpr int STAG = STG >= 0 ? STG : ((MP == 4 && !(F & F_STATS)) ? 1 : 0);
-  hipLaunchKernelGGL((stream3_kernel<W, MP, F, STAG>), dim3(S3_WG), dim3(512), 0, st, a, P / (64 * MP));
+  hipLaunchKernelGGL((stream3_kernel<W, MP, F, STAG, SM>), dim3(S3_WG), dim3(512), 0, st, a, P / (64 * MP));
 }
 
 template <int W>
@@ -778,31 +828,158 @@ int launch_w(const S3Args &a, int f, int P, hipStream_t st) {
     case F_MASK: launch1<W, 2, F_MASK>(a, P, st); break;
     case F_ACC | F_MASK: launch1<W, 2, F_ACC | F_MASK>(a, P, st); break;
     case F_BNBWD: launch1<W, 2, F_BNBWD>(a, P, st); break;
+    // the eval epilogues (stream3_launch_ex), 128-pixel steps
+    case F_BIAS | F_PRELU: launch1<W, 2, F_BIAS | F_PRELU, 0>(a, P, st); break;
+    case F_BIAS | F_RES | F_RELU: launch1<W, 2, F_BIAS | F_RES | F_RELU, 0>(a, P, st); break;
+    case F_BIAS | F_RES | F_RELU | F_POOL | F_PFULL | F_PNOIDX:
+      launch1<W, 2, F_BIAS | F_RES | F_RELU | F_POOL | F_PFULL | F_PNOIDX, 0>(a, P, st); break;
+    case F_BIAS | F_RELU | F_POOL | F_PFULL | F_PNOIDX:
+      launch1<W, 2, F_BIAS | F_RELU | F_POOL | F_PFULL | F_PNOIDX, 0>(a, P, st); break;
+    case F_BIAS | F_RELU | F_POOL | F_PNOIDX: launch1<W, 2, F_BIAS | F_RELU | F_POOL | F_PNOIDX, 0>(a, P, st); break;
     default: return RR_EUNSUPPORTED;
   }
   RR_CHECK_LAUNCH();
   return RR_OK;
 }
 
+// column-strip mode: the flag sets it has instances for -- the plain conv /
+// dgrad, bias (+ ReLU), and the BN-folded eval epilogues of the reference's
+// 224 pipeline (17:84-86, 18:46-47); the training epilogues (statistics,
+// operands, BN backward, the window index) stay on the tap-reuse conv there
+bool s3_strip_flags(int f) {
+  switch (f) {
+    case 0: case F_BIAS: case F_BIAS | F_RELU: case F_BIAS | F_PRELU: case F_BIAS | F_RES | F_RELU:
+    case F_BIAS | F_RES | F_RELU | F_POOL | F_PFULL | F_PNOIDX:
+    case F_BIAS | F_RELU | F_POOL | F_PFULL | F_PNOIDX:
+    case F_BIAS | F_RELU | F_POOL | F_PNOIDX:
+      return true;
+    default:
+      return false;
+  }
+}
+
+int launch_strips(const S3Args &a, int f, int P, hipStream_t st) {
+  // 32-wide strips, 128-pixel steps (4 rows), no stagger
+  switch (f) {
+    case 0: launch1<32, 2, 0, 0, true>(a, P, st); break;
+    case F_BIAS: launch1<32, 2, F_BIAS, 0, true>(a, P, st); break;
+    case F_BIAS | F_RELU: launch1<32, 2, F_BIAS | F_RELU, 0, true>(a, P, st); break;
+    case F_BIAS | F_PRELU: launch1<32, 2, F_BIAS | F_PRELU, 0, true>(a, P, st); break;
+    case F_BIAS | F_RES | F_RELU: launch1<32, 2, F_BIAS | F_RES | F_RELU, 0, true>(a, P, st); break;
+    case F_BIAS | F_RES | F_RELU | F_POOL | F_PFULL | F_PNOIDX:
+      launch1<32, 2, F_BIAS | F_RES | F_RELU | F_POOL | F_PFULL | F_PNOIDX, 0, true>(a, P, st); break;
+    case F_BIAS | F_RELU | F_POOL | F_PFULL | F_PNOIDX:
+      launch1<32, 2, F_BIAS | F_RELU | F_POOL | F_PFULL | F_PNOIDX, 0, true>(a, P, st); break;
+    case F_BIAS | F_RELU | F_POOL | F_PNOIDX:
+      launch1<32, 2, F_BIAS | F_RELU | F_POOL | F_PNOIDX, 0, true>(a, P, st); break;
+    default: return RR_EUNSUPPORTED;
+  }
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+// column width of the streaming kernel on a w-wide map: the whole row at w =
+// 32 / 64, else 32-pixel column strips (the reference's 224 maps: 7 strips;
+// a strip's neighbour columns are its halo, read again by the next strip --
+// 34 / 32 of the input), 0: not taken
+int s3_col(int w) {
+  if (w == 32 || w == 64) return w;
+  if (w > 64 && w % 32 == 0) return 32;
+  return 0;
+}
+
+bool s3_is_strip(const rr_igemm_desc *d) { return s3_col(d->w) != d->w; }
+
+// launch flag set f of *d: whole rows or strips
+int s3_go(const rr_igemm_desc *d, const S3Args &a, int f, int P, hipStream_t st) {
+  if (s3_is_strip(d)) return launch_strips(a, f, P, st);
+  if (d->w == 64) return launch_w<64>(a, f, P, st);
+  return launch_w<32>(a, f, P, st);
+}
+
 }  // namespace
 
-int stream3_blocks(const rr_igemm_desc *d, int bnbwd) {
+int stream3_geom_ok(const rr_igemm_desc *d) {
   // RR_PATH stream3=0: the tap-reuse / halo kernels instead (tests)
   if (!rr_path("stream3", 1)) return 0;
   if (d->dtype != RR_BF16 || d->mode != RR_CONV3X3) return 0;
   if (d->c_in1 != 64 || d->c_out != 64 || d->out_split || d->out_nchw) return 0;
-  if (d->w != 64 && d->w != 32) return 0;
+  const int cw = s3_col(d->w);
+  // column strips: RR_PATH stream3_strips=0 leaves the wide maps to the
+  // tap-reuse conv's row-segment tiles
+  if (!cw || (cw != d->w && !rr_path("stream3_strips", 1))) return 0;
+  // eligibility independent of the step size: whole 256-pixel steps (the
+  // larger one) and at least one per workgroup
+  if (d->h % (256 / cw)) return 0;
+  const long long P = (long long)d->n * d->h * d->w;
+  // (every element offset is 64-bit: the cfg5 chunks of 1024 224x224 images
+  // are 6.6 GB per tensor)
+  if (P < 256LL * S3_WG || P > INT_MAX / 2) return 0;
+  return S3_WG;
+}
+
+int stream3_blocks(const rr_igemm_desc *d, int bnbwd) {
+  if (!stream3_geom_ok(d)) return 0;
   // (a concat input, dec1's 64 + 64 -> 64, goes to the tap-reuse conv in
   // one pass with the whole K = 1152 sum in fp32: the same graph-step time
   // as two streaming passes, profiles/r4j_abstep_concat_splitdgrad.txt,
   // without a bf16 rounding of the half sum)
-  if (d->c_in2 != 0 || s3_flags(d, bnbwd != 0) < 0) return 0;
-  // eligibility independent of the step size: whole 256-pixel steps (the
-  // larger one) and at least one per workgroup
-  if (d->h % (256 / d->w)) return 0;
-  const long long P = (long long)d->n * d->h * d->w;
-  if (P < 256LL * S3_WG || P * 64 > INT_MAX) return 0;
+  const int f = s3_flags(d, bnbwd != 0);
+  if (d->c_in2 != 0 || f < 0 || (s3_is_strip(d) && !s3_strip_flags(f))) return 0;
   return S3_WG;
+}
+
+int stream3_strips(const rr_igemm_desc *d) { return stream3_geom_ok(d) && s3_is_strip(d); }
+
+const char *stream3_name(const rr_igemm_desc *d, const char *suffix) {
+  static const char *names[4][5] = {
+      {"stream3_kernel<64>", "stream3_kernel<64,pool>", "stream3_kernel<64,sc>", "stream3_kernel<64,ex>", "stream3_kernel<64,bnbwd>"},
+      {"stream3_kernel<32>", "stream3_kernel<32,pool>", "stream3_kernel<32,sc>", "stream3_kernel<32,ex>", "stream3_kernel<32,bnbwd>"},
+      {"stream3_kernel<s64>", "stream3_kernel<s64,pool>", "stream3_kernel<s64,sc>", "stream3_kernel<s64,ex>", "stream3_kernel<s64,bnbwd>"},
+      {"stream3_kernel<s32>", "stream3_kernel<s32,pool>", "stream3_kernel<s32,sc>", "stream3_kernel<s32,ex>", "stream3_kernel<s32,bnbwd>"}};
+  const int cw = s3_col(d->w);
+  const int r = (cw == d->w ? 0 : 2) + (cw == 64 ? 0 : 1);   // (strips: 32 wide)
+  int c = 0;
+  if (suffix && suffix[0]) {
+    switch (suffix[0]) {
+      case 'p': c = 1; break;
+      case 's': c = 2; break;
+      case 'e': c = 3; break;
+      default: c = 4; break;
+    }
+  }
+  return names[r][c];
+}
+
+// the eval flag set of an rr_igemm_ex call, or -1
+static int s3_ex_flags(const rr_igemm_desc *d) {
+  if (!d->has_bias || d->want_stats || d->accumulate || d->has_mask) return -1;
+  const int act = d->act;
+  const bool prelu = (act & 3) == RR_ACT_PRELU, relu = (act & 3) == RR_ACT_RELU;
+  const bool res = (act & RR_ACT_RES) != 0, pool = (act & RR_ACT_POOL) != 0, full = !(act & RR_ACT_NOFULL);
+  if (prelu) return res || pool ? -1 : F_BIAS | F_PRELU;
+  if (!relu) return -1;
+  if (res && !pool) return F_BIAS | F_RES | F_RELU;
+  if (res && pool && full) return F_BIAS | F_RES | F_RELU | F_POOL | F_PFULL | F_PNOIDX;
+  if (!res && pool) return F_BIAS | F_RELU | F_POOL | F_PNOIDX | (full ? F_PFULL : 0);
+  return -1;
+}
+
+int stream3_ex_ok(const rr_igemm_desc *d) {
+  if (!stream3_geom_ok(d) || d->c_in2 != 0) return 0;
+  if ((d->act & RR_ACT_POOL) && (d->h % 2 || d->w % 2)) return 0;
+  return s3_ex_flags(d) >= 0 ? S3_WG : 0;
+}
+
+int stream3_launch_ex(const rr_igemm_desc *d, const S3Args &a0, hipStream_t st) {
+  const int f = s3_ex_flags(d);
+  if (!stream3_ex_ok(d) || f < 0 || !a0.x || !a0.wt || !a0.bias || ((f & F_PRELU) && !a0.alpha) ||
+      ((f & F_RES) && !a0.res) || ((f & F_POOL) && !a0.ypool) || (((f & F_PFULL) || !(f & F_POOL)) && !a0.y))
+    return RR_EUNSUPPORTED;
+  S3Args a = a0;
+  a.wld = 64; a.woff = 0; a.w = d->w;
+  const int P = d->n * d->h * d->w;
+  return s3_go(d, a, f, P, st);
 }
 
 #ifdef RR_S3_STAMPS
@@ -818,10 +995,10 @@ extern "C" int rr_s3_stamps_read(unsigned long long *host, int n, int clear) {
 #endif
 
 int stream3_launch_sc(const rr_igemm_desc *d, const S3Args &a0, hipStream_t st) {
-  if (!stream3_blocks(d, 0) || d->c_in2 || s3_flags(d, false) != 0 || !a0.xsc || !a0.wsc)
+  if (!stream3_blocks(d, 0) || d->c_in2 || s3_flags(d, false) != 0 || !a0.xsc || !a0.wsc || s3_is_strip(d))
     return RR_EUNSUPPORTED;
   S3Args a = a0;
-  a.wld = 64; a.woff = 0;
+  a.wld = 64; a.woff = 0; a.w = d->w;
   const int P = d->n * d->h * d->w;
   // 128-pixel steps, no stagger (the plain dgrad's form, launch_w)
   if (d->w == 64) launch1<64, 2, F_SC, 0>(a, P, st);
@@ -832,11 +1009,13 @@ int stream3_launch_sc(const rr_igemm_desc *d, const S3Args &a0, hipStream_t st) 
 
 int stream3_launch_pool(const rr_igemm_desc *d, const S3Args &a0, hipStream_t st) {
   if (!stream3_blocks(d, 0) || d->c_in2 || d->act != RR_ACT_RELU || d->accumulate || d->has_mask ||
-      d->want_stats || !a0.ypool || !a0.pidx)
+      d->want_stats || !a0.ypool || (!a0.pidx && !d->has_bias) || (a0.pidx && s3_is_strip(d)))
     return RR_EUNSUPPORTED;
   S3Args a = a0;
-  a.wld = 64; a.woff = 0;
+  a.wld = 64; a.woff = 0; a.w = d->w;
   const int P = d->n * d->h * d->w;
+  if (!a0.pidx)   // (the eval judge: no window index)
+    return s3_go(d, a, F_BIAS | F_RELU | F_POOL | F_PNOIDX, P, st);
   // 128-pixel steps, no stagger: the bias + ReLU forward's form (launch_w;
   // 256-pixel steps at W = 64 were bitwise equal and within the run order's
   // noise, profiles/r5zi_pool_bench.jsonl, r5zj_pool_bench.jsonl)
@@ -855,8 +1034,7 @@ int stream3_launch(const rr_igemm_desc *d, const S3Args &a0, int bnbwd, hipStrea
   if (!stream3_blocks(d, bnbwd)) return RR_EUNSUPPORTED;
   S3Args a = a0;
   const int P = d->n * d->h * d->w;
-  auto go = [&](const S3Args &x, int f) { return d->w == 64 ? launch_w<64>(x, f, P, st) : launch_w<32>(x, f, P, st); };
-  S3Args p = a;
-  p.wld = 64; p.woff = 0;
-  return go(p, s3_flags(d, bnbwd != 0));
+  a.wld = 64; a.woff = 0; a.w = d->w;
+  const int f = s3_flags(d, bnbwd != 0);
+  return s3_go(d, a, f, P, st);
 }

@@ -509,8 +509,9 @@ def resblock_forward_eval_folded(blk, x1, x2, n, h, w, wc, dt, pool=False):
 
 def _ex_fusable(dtype, n, h, w, c1, c2, cout, act):
     """rr_igemm_ex takes the epilogue ``act`` on this conv with the kernel the
-    plain conv would run anyway (the tap-reuse conv; on the 64x64 maps the
-    row-streaming kernel keeps the layer and the activation stays a pass)."""
+    plain conv would run anyway: the tap-reuse conv, or the row-streaming
+    kernel on the 64 -> 64 maps it takes (whole rows at 32 / 64, column strips
+    at the reference's 224; its eval epilogues, stream3.hip F_PRELU / F_RES)."""
     if dtype != torch.bfloat16:
         return False
     if act & ops.RR_ACT_POOL and (h < 2 or w < 2):
@@ -520,7 +521,7 @@ def _ex_fusable(dtype, n, h, w, c1, c2, cout, act):
                                                 0, 1, 0, 0, 0))
     plain = ops.igemm_kernel_name(ops.IgemmDesc(rd, RR_CONV3X3, n, h, w, c1, c2, cout, 0, 0,
                                                 0, 1, 0, 0, 0))
-    return fused.startswith("conv3r") and fused == plain
+    return (fused.startswith("conv3r") or fused.startswith("stream3")) and fused == plain
 
 
 def resblock_forward(blk, x1, x2, n, h, w, wc, dt, training, need_bwd, pool=False):

@@ -190,7 +190,8 @@ def test_kernel_selection_at_the_reference_geometry():
     """host-only: the 3x3 convs of the reference's 224x224 pipeline and its
     112 / 56 / 28 / 14 maps (14:202-205, 17:66, 18:28-32) take the
     row-segment tiles of the tap-reuse conv (32-column segments above W = 16,
-    16-column at 14x14), one statistics row per wave row of a tile"""
+    16-column at 14x14), one statistics row per wave row of a tile (the
+    row-streaming kernel's column strips have no statistics epilogue)"""
     from roadrestore import ops
     from roadrestore._lib import RR_BF16, RR_CONV3X3, IgemmDesc
     want = {  # (h, c_in1, c_in2, c_out): (kernel, rows per image)
@@ -209,15 +210,18 @@ def test_kernel_selection_at_the_reference_geometry():
 
 def test_igemm_ex_kernel_selection():
     """host-only: rr_igemm_ex's fused PReLU / residual epilogues run on the
-    tap-reuse conv only; other descriptors report "unsupported" (the engine
-    then keeps the activation pass)"""
+    tap-reuse conv or, for the 64 -> 64 maps it takes, the row-streaming
+    kernel (column strips at 224); other descriptors report "unsupported" (the
+    engine then keeps the activation pass)"""
     from roadrestore import ops
-    from roadrestore._lib import RR_ACT_PRELU, RR_ACT_RES, RR_BF16, RR_CONV3X3, RR_F32, IgemmDesc
+    from roadrestore._lib import RR_ACT_POOL, RR_ACT_PRELU, RR_ACT_RES, RR_BF16, RR_CONV3X3, RR_F32, IgemmDesc
 
     def name(dt, h, c, act, bnbwd=False):
         return ops.igemm_kernel_name(IgemmDesc(dt, RR_CONV3X3, 4, h, h, c, 0, c, 0, act, 0, 1, 0, 0, 0),
                                      bnbwd=bnbwd)
-    assert name(RR_BF16, 224, 64, RR_ACT_PRELU) == "conv3r_kernel<s2,64>"
+    assert name(RR_BF16, 224, 64, RR_ACT_PRELU) == "stream3_kernel<s32>"
+    assert name(RR_BF16, 224, 64, 1 | RR_ACT_RES | RR_ACT_POOL) == "stream3_kernel<s32>"
+    assert name(RR_BF16, 224, 128, RR_ACT_PRELU) == "conv3r_kernel<s2,128>"
     assert name(RR_BF16, 16, 256, 1 | RR_ACT_RES).startswith("conv3r_kernel<16,128")
     assert name(RR_F32, 224, 64, RR_ACT_PRELU) == "unsupported"
     assert name(RR_BF16, 224, 64, RR_ACT_PRELU, bnbwd=True) == "unsupported"
@@ -304,3 +308,34 @@ def test_saved_forward_state_lives_with_its_handle():
     del h
     gc.collect()
     assert T.saved_state_count() == n0
+
+
+def test_stream3_column_strips_selected(monkeypatch):
+    """host-only: the row-streaming kernel's column-strip mode -- 32-wide
+    strips of any 32-multiple width above 64 (the reference's 224) -- for the
+    plain / bias / ReLU and eval flag sets; the training epilogues stay on the
+    tap-reuse conv's row-segment tiles, and RR_PATH stream3_strips=0 hands the
+    wide maps back to them"""
+    from rrpath import set_path
+    from roadrestore import ops
+    from roadrestore._lib import RR_BF16, RR_CONV3X3, IgemmDesc
+
+    def name(n, h, w, c1=64, c2=0, co=64, stats=0, mask=0, bnbwd=False):
+        return ops.igemm_kernel_name(IgemmDesc(RR_BF16, RR_CONV3X3, n, h, w, c1, c2, co, 0, 0, 0, 1, mask,
+                                               stats, 0), bnbwd=bnbwd)
+    assert name(2, 224, 224) == "stream3_kernel<s32>"
+    assert name(10, 40, 224) == "stream3_kernel<s32>"
+    assert name(5, 128, 128) == "stream3_kernel<s32>"
+    assert name(2, 224, 224, stats=1) == "conv3r_kernel<s2,64>"    # training epilogues: tap-reuse
+    assert name(2, 224, 224, mask=1) == "conv3r_kernel<s2,64>"
+    assert name(2, 224, 224, bnbwd=True) == "conv3r_kernel<s2,64>"
+    assert name(16, 64, 64, stats=1) == "stream3_kernel<64>"
+    assert name(4, 104, 160) == "stream3_kernel<s32>"
+    assert name(16, 64, 64) == "stream3_kernel<64>"
+    assert name(1, 224, 224) == "conv3r_kernel<s2,64>"        # P < 256 steps of 256 pixels
+    assert name(2, 220, 224) == "conv3r_kernel<s2,64>"        # h % 8: no whole steps
+    assert name(8, 112, 112) == "conv3r_kernel<s2,64>"        # 112 % 32: no strip width
+    assert name(2, 224, 224, 64, 64) == "conv3r_kernel<s2,64>"   # concat: one tap-reuse pass
+    set_path(monkeypatch, "stream3_strips", "0")
+    assert name(2, 224, 224) == "conv3r_kernel<s2,64>"
+    assert name(16, 64, 64) == "stream3_kernel<64>"

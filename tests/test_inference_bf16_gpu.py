@@ -4,8 +4,9 @@ times:
 
   GTSRB-sized uint8 crops -> Resize((224, 224)) + ToTensor (PIL-exact)
     -> ResUNet.eval() in bf16: every BN folded into its conv, the 3x3 convs on
-       the tap-reuse kernel's row-segment tiles with the rr_igemm_ex
-       epilogues (PReLU, residual, fused 2x2 max-pool)
+       the tap-reuse kernel's row-segment tiles -- the 64 -> 64 ones at 224 on
+       the row-streaming kernel's 32-wide column strips -- with the
+       rr_igemm_ex epilogues (PReLU, residual, fused 2x2 max-pool)
     -> clamp, x255, uint8 truncation
     -> Resize + ToTensor + Normalize(ImageNet) -> VGG16 in bf16 (conv + ReLU +
        max-pool in one epilogue, the full-size map never written) -> Top-1.
@@ -105,13 +106,22 @@ def test_inference_pipeline_bf16_224(dev):
         finally:
             ops.LAUNCH_LOG = None
 
-        # ---- the kernels: every 3x3 conv with >= 32 input channels runs on
-        # the tap-reuse kernel's row-segment tiles (224 is not a whole-row
-        # map), and the inference epilogues are taken ----
+        # ---- the kernels: the 64 -> 64 3x3 convs at 224 run on the
+        # row-streaming kernel's column strips (restore: res1 conv1 + PReLU,
+        # res1 conv2 + residual + ReLU + pool, dec1 conv2; judge: conv1_2 +
+        # ReLU + pool), every other 3x3 conv with >= 32 input channels on the
+        # tap-reuse kernel's row-segment tiles (224 is not a whole-row map),
+        # and the inference epilogues are taken ----
         conv3 = [(k, t) for k, t in log if t.startswith(f"fwd m{RR_CONV3X3} ")]
         wide = [(k, t) for k, t in conv3 if int(t.split(" c")[1].split("+")[0]) >= 32]
         assert wide, log
-        bad = [(k, t) for k, t in wide if not k.startswith("conv3r_kernel<s")]
+
+        def is64(t):
+            return "x224x224 c64+0->64" in t
+        strips = [(k, t) for k, t in wide if is64(t)]
+        assert len(strips) == 4, strips                                        # 3 restore + judge conv1_2
+        bad = [(k, t) for k, t in strips if not k.startswith("stream3_kernel<s32")]
+        bad += [(k, t) for k, t in wide if not is64(t) and not k.startswith("conv3r_kernel<s")]
         assert not bad, bad
         ex_r = [t for _, t in log[:n_restore] if " ex" in t]
         # (the judge's conv + ReLU + MaxPool2d pairs: rr_igemm_pool, tag "... pool")
