@@ -96,6 +96,17 @@ run_step() {
       done
       unset RR_LIB_PATH
       cat ${O}_abinf.txt ;;
+    abinfenv)
+      # cfg5 bf16 inference per value of an environment switch, alternating,
+      # 3 rounds: abinfenv:RR_PATH=conv3r_segwg=4,conv3r_segwg=8
+      local name=${arg%%=*} vals=${arg#*=}
+      for i in 1 2 3; do
+        for v in ${vals//,/ }; do
+          env $name=$v timeout -k 10 300 python tools/bench_inference.py --images 4096 --dtype bf16 > ${O}_abinf.log 2>&1 || return 1
+          tail -1 ${O}_abinf.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); s=d['stage_ms_per_1k_images']; print('$name=$v', d['images_per_sec'], s['restore'], s['judge'], d['roofline']['restore']['frac'])" >> ${O}_abinfenv.txt
+        done
+      done
+      cat ${O}_abinfenv.txt ;;
     abconv)
       # per-layer conv3r A/B of this build vs another .so (cfg3 and the 224
       # set), alternating processes, 3 rounds
