@@ -440,6 +440,7 @@ def test_conv3r_ex_prelu_and_residual(dev, shape, monkeypatch):
     from roadrestore import ops
     from roadrestore._lib import RR_ACT_PRELU, RR_ACT_RES, RR_CONV3X3
     set_path(monkeypatch, "conv3r", "1")
+    set_path(monkeypatch, "stream3", "0")       # (the 224 64 -> 64 maps: stream3's column strips)
     n, h, w, c1, c2, co = shape
     cin = c1 + c2
     x = rnd(n, cin, h, w, seed=61).bfloat16().float()
@@ -487,6 +488,7 @@ def test_conv3r_ex_pool(dev, shape, monkeypatch):
     from roadrestore import ops
     from roadrestore._lib import RR_CONV3X3
     set_path(monkeypatch, "conv3r", "1")
+    set_path(monkeypatch, "stream3", "0")       # (the 224 64 -> 64 maps: stream3's column strips)
     n, h, w, c1, c2, co = shape
     cin = c1 + c2
     x = rnd(n, cin, h, w, seed=71).bfloat16().float()
