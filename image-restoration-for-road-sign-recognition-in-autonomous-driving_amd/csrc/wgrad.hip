@@ -299,36 +299,50 @@ struct Halo3Args {
   int xcd;                 // XCD-aware workgroup order (always on)
 };
 
-// MA: 16-row MFMA blocks of dy channels per wave (the wave tile is 16 MA dy
-// channels x 64 / MA x channels).  MA = 4: each wave owns all 64 dy channels
-// of the tile and 16 x channels, so per 32-pixel step it reads 4 A fragments
-// (reused over the 9 taps) and 9 B fragments -- 13 transposed fragment reads
-// per 36 MFMAs instead of the 2 x 2 tile's 20: the LDS read port, at ~2x the
-// MFMA time on the 2 x 2 tile, was what bound this kernel.  Two stages of
-// global prefetch in flight (two register sets, a stage's loads issued two
-// compute phases before their LDS write; one stage measured slower)
+// MA = 4: each wave owns all 64 dy channels of the tile and 16 x channels, so
+// per 32-pixel step it reads 4 A fragments (reused over the 9 taps) and 9 B
+// fragments -- 13 transposed fragment reads per 36 MFMAs.
+//
+// Operands arrive by LDS-DMA (global_load_lds_dwordx4, round 6): a stage is
+// the dy tile [64 px][64 ch] and the x halo [(R+2) rows][(W+2) cols][64 ch] as
+// 1-KB pieces of 8 LDS rows, the padding pixels from the zero page, three
+// stage buffers (two at W = 64), every wave issuing the same number of pieces
+// per stage (counted vmcnt waits + a raw barrier).  Until round 6 the stage
+// went global -> registers -> ds_write: two register sets of staging (48
+// VGPRs), per-element bounds branches, and rows padded to 136 B that left
+// every transposed read 2-way bank-conflicted (41 % of the LDS cycles,
+// profiles/r6w_pmc_stalls.json).  The rows are now 128 B with the 32-B column
+// blocks XOR-swizzled so the 8 rows one ds_read_b64_tr_b16 half-wave touches
+// land on disjoint 8-bank windows: dy rows by pixel bits 1 and 3 (the tiled
+// kernel's wg_off), halo rows by their column (W >= 16: the half-wave reads
+// columns {x..x+3, x+8..x+11} of one row) or by column bit 1 and row parity
+// (W = 8: columns {x..x+3} of two consecutive rows).  The DMA writes a row's
+// 16-B slots in lane order, so a lane fetches the chunk its slot holds.
+__device__ __forceinline__ s16x4 tr_read(uint32_t addr) {
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+
 template <int W>
 __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
   constexpr int MA = 4;
-  constexpr int MB = 4 / MA;                   // 16-column x blocks per wave
-  constexpr int WA = 4 / MA;                   // waves along the dy channels
   constexpr int R = 64 / W;                    // image rows per stage
   constexpr int HW2 = W + 2;
   constexpr int HROWS = (R + 2) * HW2;         // halo pixel rows
-  // 64 bf16 channels per row, padded 128 -> 136 B: the 8 rows one
-  // ds_read_b64_tr_b16 half-wave touches ({0..3, 8..11} or {0..3, 10..13}
-  // plus any base) start 34 banks apart and never overlap, and every tap's
-  // address is the lane's base + a compile-time offset
-  constexpr int RS = 136;
+  constexpr int RS = 128;                      // 64 bf16 channels per LDS row
+  constexpr int NB = (HROWS + 7) / 8;          // 1-KB halo pieces (8 rows each)
+  constexpr int NJ = 8 + NB;                   // pieces per stage (dy: 8)
+  constexpr int NI = (NJ + 3) / 4;             // DMA instructions per wave per stage
   constexpr int A_BYTES = 64 * RS;
-  constexpr int B_BYTES = ((HROWS * RS + 15) / 16) * 16;
-  constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int LA = 64 * 8 / 256;             // 16-B pieces per thread (A)
-  constexpr int LB = (HROWS * 8 + 255) / 256;  // (B halo)
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  constexpr int STAGE = A_BYTES + NB * 8 * RS;
+  constexpr int NSTG = 3 * STAGE <= 80 * 1024 ? 3 : 2;   // two workgroups per CU
+  static_assert(NI <= 16, "piece classes");
+  __shared__ __attribute__((aligned(16))) char smem[NSTG * STAGE];
 
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wa = wv % WA, wb = wv / WA;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wb = wv;                           // the wave's 16 x channels (all 64 dy channels)
   int bid = xcd_order(blockIdx.x, a.xcd);
   const int ablk = bid % a.nablk; bid /= a.nablk;
   const int bblk = bid % a.nbblk; bid /= a.nbblk;
@@ -340,127 +354,145 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
   int ldb, bc0;
   if (b0 < a.c1) { Bsrc = a.B1; ldb = a.c1; bc0 = b0; }
   else { Bsrc = a.B2; ldb = a.c2; bc0 = b0 - a.c1; }
-  const int hw = a.h * a.w;
+  const int hw = a.h * W;
 
-  typedef uint4 V;
-  V ra[LA], rb[LB], ra2[LA], rb2[LB];
-  auto gload_to = [&](int st, V *ra, V *rb) __attribute__((always_inline)) {
-    const int p0 = st * 64;                    // first pixel of the stage
-    const int nn = p0 / hw;
-    const int h0 = (p0 - nn * hw) >> a.lw;
+  auto swz_a = [](int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1); };
+  auto swz_b = [](int hy, int hx) {
+    return W == 8 ? (((hx >> 1) & 1) | ((hy & 1) << 1)) : (((hx >> 1) & 1) | (((hx >> 3) & 1) << 1));
+  };
+
+  // ---- the lane's DMA pieces: piece j = wv + 4 i (past the last one: a
+  // duplicate of the previous wave's, the same bytes written twice) ----
+  int doff[NI];                                // source offset from the stage's dy / halo base
+  uint64_t dcls = 0;                           // 4 bits per piece: 1 dy, 2 halo, 4 top row, 8 bottom row
 #pragma unroll
-    for (int i = 0; i < LA; ++i) {
-      const int idx = tid + 256 * i;
-      const int r = idx >> 3, pc = idx & 7;
-      ra[i] = *reinterpret_cast<const V *>(a.A + ((long long)(p0 + r) * a.CA + a0) * 2 + pc * 16);
-    }
-#pragma unroll
-    for (int i = 0; i < LB; ++i) {
-      const int idx = tid + 256 * i;
-      const int r = idx >> 3, pc = idx & 7;
-      V v = {0, 0, 0, 0};
-      if (r < HROWS) {
-        const int hy = r / HW2, hx = r - (r / HW2) * HW2;
-        const int yy = h0 - 1 + hy, xx = hx - 1;
-        if (yy >= 0 && yy < a.h && xx >= 0 && xx < a.w) {
-          const long long sp = ((long long)nn * a.h + yy) * a.w + xx;
-          v = *reinterpret_cast<const V *>(Bsrc + (sp * ldb + bc0) * 2 + pc * 16);
+  for (int i = 0; i < NI; ++i) {
+    int j = wv + 4 * i;
+    if (j >= NJ) j -= 4;
+    const int rl = lane >> 3, p = lane & 7;
+    uint64_t cls = 0;
+    int off = 0;
+    if (j < 8) {
+      const int r = 8 * j + rl;
+      const int c = (((p >> 1) ^ swz_a(r)) << 1) | (p & 1);
+      off = (r * a.CA + a0) * 2 + c * 16;
+      cls = 1;
+    } else {
+      const int rr = 8 * (j - 8) + rl;
+      if (rr < HROWS) {
+        const int hy = rr / HW2, hx = rr - (rr / HW2) * HW2;
+        const int c = (((p >> 1) ^ swz_b(hy, hx)) << 1) | (p & 1);
+        if (hx >= 1 && hx <= W) {
+          off = ((hy - 1) * W + hx - 1) * ldb * 2 + c * 16;
+          cls = hy == 0 ? 4u : (hy == R + 1 ? 8u : 2u);
         }
       }
-      rb[i] = v;
+    }
+    doff[i] = off;
+    dcls |= cls << (4 * i);
+  }
+  const char *zp = rr_zero_page;
+  auto issue = [&](int st, int buf) __attribute__((always_inline)) {
+    const int p0 = st * 64;                    // first pixel of the stage (R whole rows of one image)
+    const int nn = p0 / hw;
+    const int h0 = (p0 - nn * hw) / W;
+    const char *abase = a.A + (long long)p0 * a.CA * 2;
+    const char *bbase = Bsrc + ((long long)(nn * a.h + h0) * W) * ldb * 2 + bc0 * 2;
+    const uint64_t okm = 1u | 2u | (h0 > 0 ? 4u : 0u) | (h0 + R < a.h ? 8u : 0u);   // uniform
+    char *dst = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      int j = wv + 4 * i;
+      if (j >= NJ) j -= 4;                     // (uniform)
+      const char *base = j < 8 ? abase : bbase;
+      const bool ok = ((dcls >> (4 * i)) & okm & 15u) != 0;
+      const char *src = ok ? base + doff[i] : zp;
+      const int d = j < 8 ? j * 1024 : A_BYTES + (j - 8) * 1024;
+      __builtin_amdgcn_global_load_lds((const void *)src, LDS_PTR(dst + d), 16, 0, 0);
     }
   };
-  auto gload = [&](int st) __attribute__((always_inline)) { gload_to(st, ra, rb); };
-  auto swrite_from = [&](int buf, const V *ra, const V *rb) __attribute__((always_inline)) {
-    char *sA = smem + buf * STAGE;
-    char *sB = sA + A_BYTES;
-#pragma unroll
-    for (int i = 0; i < LA; ++i) {
-      const int idx = tid + 256 * i;
-      uint2 *d = reinterpret_cast<uint2 *>(sA + (idx >> 3) * RS + (idx & 7) * 16);
-      d[0] = uint2{ra[i].x, ra[i].y};
-      d[1] = uint2{ra[i].z, ra[i].w};
-    }
-#pragma unroll
-    for (int i = 0; i < LB; ++i) {
-      const int idx = tid + 256 * i;
-      if ((idx >> 3) < HROWS) {
-        uint2 *d = reinterpret_cast<uint2 *>(sB + (idx >> 3) * RS + (idx & 7) * 16);
-        d[0] = uint2{rb[i].x, rb[i].y};
-        d[1] = uint2{rb[i].z, rb[i].w};
-      }
-    }
-  };
-  auto swrite = [&](int buf) __attribute__((always_inline)) { swrite_from(buf, ra, rb); };
 
-  f32x4 acc[MA][MB][9];
+  f32x4 acc[MA][9];
 #pragma unroll
   for (int i = 0; i < MA; ++i)
 #pragma unroll
-    for (int j = 0; j < MB; ++j)
-#pragma unroll
-      for (int t = 0; t < 9; ++t) acc[i][j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // ---- tr-read addresses: bases + compile-time offsets (the swizzle of a dy
+  // row does not change with kk, 32 pixels; of a halo row it depends on the
+  // tap's dx and, at W = 8, flips bit 1 with an odd dy: address bit 6) ----
   const int g = lane >> 4, gi = lane & 15;
   const int q = gi >> 2, pp = gi & 3;
-  const int nst = send - sbeg;
+  const int kl0 = 8 * g + q, kl1 = kl0 + 4;            // the lane's pixel rows at kk = 0
+  const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+  const uint32_t ab0 = kl0 * RS + (swz_a(kl0) << 5) + pp * 8, ab1 = kl1 * RS + (swz_a(kl1) << 5) + pp * 8;
+  uint32_t bb0[3], bb1[3];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) {
+    const int y0 = kl0 / W, x0 = (kl0 & (W - 1)) + dx, y1 = kl1 / W, x1 = (kl1 & (W - 1)) + dx;
+    bb0[dx] = A_BYTES + (y0 * HW2 + x0) * RS + ((wb ^ swz_b(y0, x0)) << 5) + pp * 8;
+    bb1[dx] = A_BYTES + (y1 * HW2 + x1) * RS + ((wb ^ swz_b(y1, x1)) << 5) + pp * 8;
+  }
   auto compute = [&](int buf) __attribute__((always_inline)) {
-    const char *sA = smem + buf * STAGE;
-    const char *sB = sA + A_BYTES;
+    const uint32_t sb = sbase + buf * STAGE;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const int k0 = kk * 32 + 8 * g + q, k1 = k0 + 4;      // this lane's address rows
-      bf16x8 fa[MA];
+      s16x4 fa[MA][2];
+      s16x4 fb[2][2];
 #pragma unroll
       for (int i = 0; i < MA; ++i) {
-        const int col = wa * 16 * MA + i * 16;
-        fa[i] = tr_frag(sA + k0 * RS + col * 2 + pp * 8, sA + k1 * RS + col * 2 + pp * 8);
+        fa[i][0] = tr_read(sb + (ab0 ^ (i << 5)) + kk * 32 * RS);
+        fa[i][1] = tr_read(sb + (ab1 ^ (i << 5)) + kk * 32 * RS);
       }
-      // halo rows of the pixels k0 / k1 at tap (0, 0)
-      const int hr0 = (k0 / W) * HW2 + (k0 & (W - 1));
-      const int hr1 = (k1 / W) * HW2 + (k1 & (W - 1));
+      auto read_b = [&](int t, s16x4 (&o)[2]) __attribute__((always_inline)) {
+        const int dy = t / 3, dx = t % 3;
+        // (kk: 32 pixels further = 32 / W image rows, or 32 columns at W = 64)
+        const uint32_t roff = ((dy + kk * 32 / W) * HW2 + (kk * 32) % W) * RS;
+        const uint32_t flip = (W == 8 && (dy & 1)) ? 64u : 0u;
+        o[0] = tr_read(sb + (bb0[dx] ^ flip) + roff);
+        o[1] = tr_read(sb + (bb1[dx] ^ flip) + roff);
+      };
+      read_b(0, fb[0]);
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const int toff = (t / 3) * HW2 + (t % 3);
-        bf16x8 fb[MB];
-#pragma unroll
-        for (int j = 0; j < MB; ++j) {
-          const int col = wb * 16 * MB + j * 16;
-          fb[j] = tr_frag(sB + (hr0 + toff) * RS + col * 2 + pp * 8,
-                          sB + (hr1 + toff) * RS + col * 2 + pp * 8);
+        if (t + 1 < 9) {
+          read_b(t + 1, fb[(t + 1) & 1]);
+          asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
+        asm volatile("" : "+v"(fb[t & 1][0]), "+v"(fb[t & 1][1]));
+        if (t == 0) {
+#pragma unroll
+          for (int i = 0; i < MA; ++i) asm volatile("" : "+v"(fa[i][0]), "+v"(fa[i][1]));
+        }
+        const bf16x8 b = __builtin_bit_cast(bf16x8, __builtin_shufflevector(fb[t & 1][0], fb[t & 1][1], 0, 1, 2, 3, 4, 5, 6, 7));
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int i = 0; i < MA; ++i)
-#pragma unroll
-          for (int j = 0; j < MB; ++j)
-            acc[i][j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j][t], 0, 0, 0);
+        for (int i = 0; i < MA; ++i) {
+          const bf16x8 av = __builtin_bit_cast(bf16x8, __builtin_shufflevector(fa[i][0], fa[i][1], 0, 1, 2, 3, 4, 5, 6, 7));
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b, acc[i][t], 0, 0, 0);
+        }
         __builtin_amdgcn_s_setprio(0);
       }
     }
   };
-  {
-    // register set (ra2, rb2) holds the odd stages, (ra, rb) the even ones
-    if (nst > 0) {
-      gload(sbeg);
-      swrite(0);
-    }
-    if (nst > 1) gload_to(sbeg + 1, ra2, rb2);
-    if (nst > 2) gload_to(sbeg + 2, ra, rb);
-    __syncthreads();
-    // stage s computes from LDS buffer s & 1 while the registers hold stages
-    // s + 1 (written to the other buffer after the MFMAs) and s + 2 (in flight)
-    auto body = [&](int s, V *xa, V *xb) __attribute__((always_inline)) {
-      compute(s & 1);
-      if (s + 1 < nst) swrite_from((s & 1) ^ 1, xa, xb);
-      if (s + 3 < nst) gload_to(sbeg + s + 3, xa, xb);
-      __syncthreads();
-    };
-    for (int s = 0; s < nst; s += 2) {
-      body(s, ra2, rb2);
-      if (s + 1 < nst) body(s + 1, ra, rb);
-    }
+  // ---- the stage loop: NSTG buffers, stage s + NSTG - 1 in flight while s
+  // computes; per stage every wave issues exactly NI pieces, so "stage s
+  // landed" is vmcnt <= NI x (stages issued after s) ----
+  const int nst = send - sbeg;
+  if (nst > 0) issue(sbeg, 0);
+  if (NSTG == 3 && nst > 1) issue(sbeg + 1, 1);
+  for (int s = 0; s < nst; ++s) {
+    if (NSTG == 3 && s + 1 < nst) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NI) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    // (after the barrier every wave is past compute(s - 1): its buffer is free)
+    if (s + NSTG - 1 < nst) issue(sbeg + s + NSTG - 1, (s + NSTG - 1) % NSTG);
+    compute(s % NSTG);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  constexpr int MB = 1;
+  const int wa = 0;
 
   // partial[split][a / 4][tap][b][a % 4]: the accumulator's own layout (a
   // lane holds 4 consecutive dy channels of one x channel), one 16-B store
@@ -468,16 +500,14 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
   // stores per wave instead of 144 dword ones into 64-B pieces
   // (rr_wgrad_reduce maps the layout back: launch_reduce's alayout)
 #pragma unroll
-  for (int i = 0; i < MA; ++i)
+  for (int i = 0; i < MA; ++i) {
+    const int b = b0 + wb * 16 * MB + gi;
+    const int a4 = (a0 + wa * 16 * MA + i * 16) / 4 + g;
 #pragma unroll
-    for (int j = 0; j < MB; ++j) {
-      const int b = b0 + wb * 16 * MB + j * 16 + gi;
-      const int a4 = (a0 + wa * 16 * MA + i * 16) / 4 + g;
-#pragma unroll
-      for (int t = 0; t < 9; ++t)
-        *reinterpret_cast<f32x4 *>(a.partial + ((((long long)split * (a.CA / 4) + a4) * 9 + t) * a.CB + b) * 4) =
-            acc[i][j][t];
-    }
+    for (int t = 0; t < 9; ++t)
+      *reinterpret_cast<f32x4 *>(a.partial + ((((long long)split * (a.CA / 4) + a4) * 9 + t) * a.CB + b) * 4) =
+          acc[i][t];
+  }
 }
 
 // dw[(a*CB + b)*taps + t] (+)= sum_s partial[s][a][t][b]   (fixed order, 4 chains)
