@@ -22,6 +22,8 @@
 //   bf16: two ds_read_b64_tr_b16 per fragment (4 pixels each), 16x16x32 MFMA
 //   f32 : ds_read_b32 per fragment, 16x16x4 f32 MFMA (exact fp32)
 #include "common.h"
+
+#include <type_traits>
 #include "swgrad.h"
 
 #include <cstdlib>
@@ -318,9 +320,12 @@ struct Halo3Args {
 // columns {x..x+3, x+8..x+11} of one row) or by column bit 1 and row parity
 // (W = 8: columns {x..x+3} of two consecutive rows).  The DMA writes a row's
 // 16-B slots in lane order, so a lane fetches the chunk its slot holds.
-__device__ __forceinline__ s16x4 tr_read(uint32_t addr) {
+template <int N> using ic = std::integral_constant<int, N>;
+
+template <int OFF> __device__ __forceinline__ s16x4 tr_read(uint32_t addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset");
   s16x4 r;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
   return r;
 }
 
@@ -435,28 +440,40 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
   }
   auto compute = [&](int buf) __attribute__((always_inline)) {
     const uint32_t sb = sbase + buf * STAGE;
+    // the stage's read bases (kk and dy are immediate offsets)
+    uint32_t aa[MA][2], ba[2][3][2];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int i = 0; i < MA; ++i) { aa[i][0] = sb + (ab0 ^ (i << 5)); aa[i][1] = sb + (ab1 ^ (i << 5)); }
+#pragma unroll
+    for (int fl = 0; fl < (W == 8 ? 2 : 1); ++fl)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        ba[fl][dx][0] = sb + (bb0[dx] ^ (fl ? 64u : 0u));
+        ba[fl][dx][1] = sb + (bb1[dx] ^ (fl ? 64u : 0u));
+      }
+    auto kloop = [&](auto KKc) __attribute__((always_inline)) {
+      constexpr int kk = decltype(KKc)::value;
       s16x4 fa[MA][2];
       s16x4 fb[2][2];
-#pragma unroll
-      for (int i = 0; i < MA; ++i) {
-        fa[i][0] = tr_read(sb + (ab0 ^ (i << 5)) + kk * 32 * RS);
-        fa[i][1] = tr_read(sb + (ab1 ^ (i << 5)) + kk * 32 * RS);
-      }
-      auto read_b = [&](int t, s16x4 (&o)[2]) __attribute__((always_inline)) {
-        const int dy = t / 3, dx = t % 3;
+      constexpr int AOFF = kk * 32 * RS;
+      fa[0][0] = tr_read<AOFF>(aa[0][0]); fa[0][1] = tr_read<AOFF>(aa[0][1]);
+      fa[1][0] = tr_read<AOFF>(aa[1][0]); fa[1][1] = tr_read<AOFF>(aa[1][1]);
+      fa[2][0] = tr_read<AOFF>(aa[2][0]); fa[2][1] = tr_read<AOFF>(aa[2][1]);
+      fa[3][0] = tr_read<AOFF>(aa[3][0]); fa[3][1] = tr_read<AOFF>(aa[3][1]);
+      auto read_b = [&](auto Tc, s16x4 (&o)[2]) __attribute__((always_inline)) {
+        constexpr int t = decltype(Tc)::value;
+        constexpr int dy = t / 3, dx = t % 3;
         // (kk: 32 pixels further = 32 / W image rows, or 32 columns at W = 64)
-        const uint32_t roff = ((dy + kk * 32 / W) * HW2 + (kk * 32) % W) * RS;
-        const uint32_t flip = (W == 8 && (dy & 1)) ? 64u : 0u;
-        o[0] = tr_read(sb + (bb0[dx] ^ flip) + roff);
-        o[1] = tr_read(sb + (bb1[dx] ^ flip) + roff);
+        constexpr int roff = ((dy + kk * 32 / W) * HW2 + (kk * 32) % W) * RS;
+        constexpr int fl = (W == 8 && (dy & 1)) ? 1 : 0;
+        o[0] = tr_read<roff>(ba[fl][dx][0]);
+        o[1] = tr_read<roff>(ba[fl][dx][1]);
       };
-      read_b(0, fb[0]);
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        if (t + 1 < 9) {
-          read_b(t + 1, fb[(t + 1) & 1]);
+      read_b(ic<0>{}, fb[0]);
+      auto tap = [&](auto Tc) __attribute__((always_inline)) {
+        constexpr int t = decltype(Tc)::value;
+        if constexpr (t + 1 < 9) {
+          read_b(ic<t + 1>{}, fb[(t + 1) & 1]);
           asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
         } else {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -474,8 +491,12 @@ __global__ __launch_bounds__(256, 2) void wgrad3_halo_kernel(Halo3Args a) {
           acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b, acc[i][t], 0, 0, 0);
         }
         __builtin_amdgcn_s_setprio(0);
-      }
-    }
+      };
+      tap(ic<0>{}); tap(ic<1>{}); tap(ic<2>{}); tap(ic<3>{}); tap(ic<4>{});
+      tap(ic<5>{}); tap(ic<6>{}); tap(ic<7>{}); tap(ic<8>{});
+    };
+    kloop(ic<0>{});
+    kloop(ic<1>{});
   };
   // ---- the stage loop: NSTG buffers, stage s + NSTG - 1 in flight while s
   // computes; per stage every wave issues exactly NI pieces, so "stage s
