@@ -1228,6 +1228,31 @@ extern "C" int rr_igemm_ex(const rr_igemm_desc *d, const void *x1, const void *x
   return conv3r_launch(d, a, (hipStream_t)stream);
 }
 
+// conv2's bias + BN-statistics forward with BN1 + PReLU of its input folded
+// in (x1 = t1; the conv reads PReLU(t1 * pre_scale + pre_shift), the bytes
+// rr_affine_act would store): the row-streaming kernel's 64 -> 64 whole-row
+// maps only (rr_igemm_pre_ok)
+extern "C" int rr_igemm_pre_ok(const rr_igemm_desc *d) {
+  return d && d->mode == RR_CONV3X3 && d->act == RR_ACT_NONE && d->has_bias && d->want_stats &&
+                 !d->accumulate && !d->has_mask && !d->c_in2 && stream3_blocks(d, 0) && !stream3_strips(d)
+             ? 1
+             : 0;
+}
+
+extern "C" int rr_igemm_pre(const rr_igemm_desc *d, const void *x1, const void *w, const float *bias,
+                            const float *pre_scale, const float *pre_shift, const float *pre_alpha,
+                            void *y1, float *stats_partial, rr_stream stream) {
+  if (!d || !x1 || !w || !bias || !pre_scale || !pre_shift || !pre_alpha || !y1 || !stats_partial)
+    return RR_EINVAL;
+  if (!rr_igemm_pre_ok(d)) return RR_EUNSUPPORTED;
+  S3Args s{};
+  s.x = (const char *)x1; s.wt = (const char *)w; s.bias = bias; s.y = (char *)y1;
+  s.stats = stats_partial;
+  s.n = d->n; s.h = d->h; s.w = d->w; s.act = d->act;
+  s.pre_s = pre_scale; s.pre_b = pre_shift; s.pre_alpha = pre_alpha;
+  return stream3_launch_pre(d, s, (hipStream_t)stream);
+}
+
 // conv (+ bias) + ReLU + MaxPool2d(2, 2) with the window index, the full-size
 // output never written (the perceptual VGG slice's conv1_2 / conv2_2 + pool,
 // 14:189-196, and every no-backward pool of it): the row-streaming kernel

@@ -30,6 +30,9 @@ struct S3Args {
   // eval epilogues (stream3_launch_ex): PReLU alpha [1], identity residual NHWC bf16
   const float *alpha;
   const char *res;
+  // input transform (stream3_launch_pre): x is the pre-BN t1, the conv reads
+  // PReLU(t1 * pre_s + pre_b) ([64] fp32 each, pre_alpha [1])
+  const float *pre_s, *pre_b, *pre_alpha;
 };
 
 // 0 when the descriptor is not handled by the streaming kernel, else the
@@ -56,6 +59,10 @@ int stream3_launch_sc(const rr_igemm_desc *d, const S3Args &a, hipStream_t st);
 // streaming kernel: stream3_ex_ok() != 0 when it takes *d
 int stream3_ex_ok(const rr_igemm_desc *d);
 int stream3_launch_ex(const rr_igemm_desc *d, const S3Args &a, hipStream_t st);
+// the bias + BN-statistics forward of conv2 with BN1 + PReLU applied to the
+// landed input rows (a.pre_*): RR_EUNSUPPORTED unless the streaming kernel
+// takes *d with whole rows and exactly that flag set
+int stream3_launch_pre(const rr_igemm_desc *d, const S3Args &a, hipStream_t st);
 // "stream3_kernel<64>" / "<32>" (whole rows) or "<s64>" / "<s32>" (column
 // strips) + the suffix
 const char *stream3_name(const rr_igemm_desc *d, const char *suffix);

@@ -93,7 +93,12 @@ constexpr int S3_WG = 256;   // workgroups: one per CU on MI355X (fixed: determi
 // output is stored too (an encoder block's skip tensor); F_PNOIDX: with
 // F_POOL, no window index (nothing runs backward)
 enum : int { F_BIAS = 1, F_STATS = 2, F_RELU = 4, F_ACC = 8, F_MASK = 16, F_BNBWD = 32, F_POOL = 64,
-             F_SC = 128, F_PRELU = 256, F_RES = 512, F_PFULL = 1024, F_PNOIDX = 2048 };
+             F_SC = 128, F_PRELU = 256, F_RES = 512, F_PFULL = 1024, F_PNOIDX = 2048, F_PRE = 4096 };
+// F_PRE: the input is the pre-BN t1 of a ResidualBlock's conv1; every row
+// that lands in the ring is turned into a1 = PReLU(t1 * s + b) in LDS (the
+// bytes rr_affine_act would have written: the same fp32 expression and bf16
+// rounding) before any step reads it -- BN1 + PReLU folded into conv2's
+// forward (14:101-104), the a1 tensor never stored
 
 // chunk swizzle: the 16 pixels of a B read at pixel offset P in {0, 1, 2}
 // mod 16 need distinct (p & 1, chunk ^ swz(p)) pairs with chunks c (outer 8
@@ -220,6 +225,8 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
   constexpr bool SC = (F & F_SC) != 0;
   constexpr bool RES = (F & F_RES) != 0, PRELU = (F & F_PRELU) != 0;
   constexpr bool PFULL = (F & F_PFULL) != 0, PIDX = POOL && !(F & F_PNOIDX);
+  constexpr bool PRE = (F & F_PRE) != 0;
+  static_assert(!PRE || (F == (F_BIAS | F_STATS | F_PRE) && STAG == 0 && !SM), "input transform: the BN-statistics forward");
   static_assert(!SC || (F == F_SC && STAG == 0), "the 1x1 second source: plain dgrad epilogue");
   static_assert(!POOL || ((F & ~(F_BIAS | F_RELU | F_POOL | F_RES | F_PFULL | F_PNOIDX)) == 0 && (F & F_RELU) &&
                           MP % 2 == 0 && W % (8 * MP) == 0), "pool epilogue: bias + ReLU, row-pair blocks");
@@ -289,6 +296,20 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
   // behind a full lgkmcnt wait, until round 6)
   f32x4 biar[(F & F_BIAS) ? MC : 1];
   const float alp = PRELU ? a.alpha[0] : 0.f;   // (resident with the weights: the vmcnt(0) below)
+  // F_PRE: a thread transforms chunks tid + 512 j of a step's new rows, all
+  // at the same ring-row pixel and 16-B slot (512 is a multiple of a row's
+  // W x 8 slots): its 8 channels' (s, b) in registers
+  f32x4 pcs[PRE ? 2 : 1], pcb[PRE ? 2 : 1];
+  float palp = 0.f;
+  if constexpr (PRE) {
+    const int rem = tid % (W * 8);
+    const int px = 1 + (rem >> 3), c = (rem & 7) ^ s3_swz(px & 15);
+    pcs[0] = *reinterpret_cast<const f32x4 *>(a.pre_s + 8 * c);
+    pcs[1] = *reinterpret_cast<const f32x4 *>(a.pre_s + 8 * c + 4);
+    pcb[0] = *reinterpret_cast<const f32x4 *>(a.pre_b + 8 * c);
+    pcb[1] = *reinterpret_cast<const f32x4 *>(a.pre_b + 8 * c + 4);
+    palp = a.pre_alpha[0];
+  }
   if constexpr ((F & F_BIAS) != 0) {
     if (tid < 64) coef[tid] = a.bias[tid];
     __syncthreads();
@@ -662,6 +683,38 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     st_wait += st_b - st_a;
     st_a = st_b;
     const bool comp = cp.kind == S3_COMP;
+    if constexpr (PRE) {
+      // the rows DMA'd for this virtual step (ring slots cslot + 2 + r): a
+      // compute step's image rows y0 + 1 + r, a pre-load's y0 - 1 and y0
+      constexpr int NCH = RPS * W * 8;
+      static_assert(NCH % 512 == 0, "whole chunks per thread");
+#pragma unroll
+      for (int j = 0; j < NCH / 512; ++j) {
+        const int k = tid + 512 * j;
+        const int r = k / (W * 8), rem = k - r * (W * 8);
+        const int px = 1 + (rem >> 3);
+        const int y = comp ? cp.y0 + 1 + r : cp.y0 - RPS + 1 + r;
+        if (y < 0 || y >= H || (!comp && r < RPS - 2)) continue;
+        int sl = cslot + 2 + r;
+        sl = sl >= RING ? sl - RING : sl;
+        const uint32_t addr = sbase + sl * ROWB + px * 128 + (rem & 7) * 16;
+        i32x4 v;
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+        f32x4 lo = unpack4(((u64)(uint32_t)v[1] << 32) | (uint32_t)v[0]);
+        f32x4 hi = unpack4(((u64)(uint32_t)v[3] << 32) | (uint32_t)v[2]);
+        lo = lo * pcs[0] + pcb[0];
+        hi = hi * pcs[1] + pcb[1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          lo[e] = lo[e] > 0.f ? lo[e] : palp * lo[e];
+          hi[e] = hi[e] > 0.f ? hi[e] : palp * hi[e];
+        }
+        const uint2 pl = pack4(lo), ph = pack4(hi);
+        const i32x4 o = i32x4{(int)pl.x, (int)pl.y, (int)ph.x, (int)ph.y};
+        asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(o) : "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
     const int rowg = cp.img * H + cp.y0;
     const long long pix0 = (long long)rowg * IW + cp.xs;
     if (late && pcomp) epilogue(ppix, prowg, pxs);   // its loads were waited for last iteration
@@ -828,6 +881,7 @@ int launch_w(const S3Args &a, int f, int P, hipStream_t st) {
     case F_MASK: launch1<W, 2, F_MASK>(a, P, st); break;
     case F_ACC | F_MASK: launch1<W, 2, F_ACC | F_MASK>(a, P, st); break;
     case F_BNBWD: launch1<W, 2, F_BNBWD>(a, P, st); break;
+    case F_BIAS | F_STATS | F_PRE: launch1<W, 2, F_BIAS | F_STATS | F_PRE, 0>(a, P, st); break;
     // the eval epilogues (stream3_launch_ex), 128-pixel steps
     case F_BIAS | F_PRELU: launch1<W, 2, F_BIAS | F_PRELU, 0>(a, P, st); break;
     case F_BIAS | F_RES | F_RELU: launch1<W, 2, F_BIAS | F_RES | F_RELU, 0>(a, P, st); break;
@@ -1028,6 +1082,17 @@ int stream3_launch_pool(const rr_igemm_desc *d, const S3Args &a0, hipStream_t st
   }
   RR_CHECK_LAUNCH();
   return RR_OK;
+}
+
+int stream3_launch_pre(const rr_igemm_desc *d, const S3Args &a0, hipStream_t st) {
+  if (!stream3_blocks(d, 0) || s3_is_strip(d) || s3_flags(d, false) != (F_BIAS | F_STATS) || !a0.pre_s ||
+      !a0.pre_b || !a0.pre_alpha)
+    return RR_EUNSUPPORTED;
+  S3Args a = a0;
+  a.wld = 64; a.woff = 0; a.w = d->w;
+  const int P = d->n * d->h * d->w;
+  if (d->w == 64) return launch_w<64>(a, F_BIAS | F_STATS | F_PRE, P, st);
+  return launch_w<32>(a, F_BIAS | F_STATS | F_PRE, P, st);
 }
 
 int stream3_launch(const rr_igemm_desc *d, const S3Args &a0, int bnbwd, hipStream_t st) {

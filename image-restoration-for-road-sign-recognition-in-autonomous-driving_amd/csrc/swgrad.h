@@ -14,6 +14,9 @@ struct SWArgs {
   int n, h;                  // w is the template width
   int nwg_ps;                // workgroups per (dy slice, input slice) pair
   int nsteps;                // 128-pixel steps (n h w / 128)
+  // input transform (swgrad_launch_pre): x1 is the pre-BN t1 of a
+  // ResidualBlock's conv1; the kernel reads PReLU(t1 * pre_s + pre_b)
+  const float *pre_s, *pre_b, *pre_alpha;
 };
 
 // nonzero when the descriptor is handled by the streaming kernel
@@ -23,3 +26,7 @@ int swgrad_nsplit(const rr_wgrad_desc *d);
 // launches the streaming kernel into ws (the caller reduces the slabs)
 int swgrad_launch(const rr_wgrad_desc *d, const void *dy, const void *x1, const void *x2, void *ws,
                   hipStream_t st);
+// the same with x1 = t1 and BN1 + PReLU applied to every landed input row
+// ((s, b) of [c_in1] fp32, alpha [1]); single-source inputs only
+int swgrad_launch_pre(const rr_wgrad_desc *d, const void *dy, const void *x1, const float *pre_s,
+                      const float *pre_b, const float *pre_alpha, void *ws, hipStream_t st);

@@ -81,6 +81,7 @@ enum { SW_PRE = 0, SW_COMP = 1 };
 struct SwCur { int kind, n, y0, c; };
 
 typedef short s16x4v __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 // transposed LDS read as inline asm: with LDS-DMA in flight hipcc would put a
 // vmcnt(0) before every visible LDS read; completion is counted by sw_lgkm
@@ -97,7 +98,11 @@ __device__ __forceinline__ void sw_lgkm(int n) {   // n folds to a constant afte
   }
 }
 
-template <int W>
+// PRE: x1 is the pre-BN t1; every input row that lands in the ring becomes
+// a1 = PReLU(t1 * s + b) in LDS (rr_affine_act's fp32 expression and bf16
+// rounding) before any group reads it -- BN1 + PReLU folded into conv2's
+// weight grad (14:101-104), the a1 tensor never stored
+template <int W, bool PRE>
 __global__ __launch_bounds__(512, 2) void swgrad_kernel(SWArgs a) {
   using G = SWGeo<W>;
   constexpr int RPS = G::RPS, ROWB = G::ROWB, RING = G::RING, DYB = G::DYB, DYOFF = G::DYOFF;
@@ -194,6 +199,21 @@ __global__ __launch_bounds__(512, 2) void swgrad_kernel(SWArgs a) {
     for (int dx = 0; dx < 3; ++dx) lb[dx][h] = sbase + lofs(dx + 8 * g + q + 4 * h, wk);
   }
 
+  // PRE: a thread transforms chunks tid + 512 j of a step's input rows, all at
+  // one ring-row pixel and 16-B slot: its 8 channels' (s, b) in registers
+  f32x4 pcs[PRE ? 2 : 1], pcb[PRE ? 2 : 1];
+  float palp = 0.f;
+  if constexpr (PRE) {
+    const int rem = tid % (W * 8);
+    const int px = 1 + (rem >> 3), c = (rem & 7) ^ sw_swz(px & 15);
+    pcs[0] = *reinterpret_cast<const f32x4 *>(a.pre_s + ci0 + 8 * c);
+    pcs[1] = *reinterpret_cast<const f32x4 *>(a.pre_s + ci0 + 8 * c + 4);
+    pcb[0] = *reinterpret_cast<const f32x4 *>(a.pre_b + ci0 + 8 * c);
+    pcb[1] = *reinterpret_cast<const f32x4 *>(a.pre_b + ci0 + 8 * c + 4);
+    palp = a.pre_alpha[0];
+    __builtin_amdgcn_s_waitcnt(0x0F70);        // vmcnt(0): resident before any DMA is in flight
+  }
+
   f32x4 acc[2][9];                              // [co block m][tap]
 #pragma unroll
   for (int m = 0; m < 2; ++m)
@@ -218,6 +238,42 @@ __global__ __launch_bounds__(512, 2) void swgrad_kernel(SWArgs a) {
     constexpr int U = decltype(Uc)::value;
     constexpr int LSEG = (U + D) & 3;           // segment / tile of the step loaded now
     asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((D - 1) * DMAW) : "memory");
+    if constexpr (PRE) {
+      // the step's input rows (segment U): a compute step's image rows
+      // y0 + 1 + r, a pre-load's y0 - 1 and y0 (the rows it reads)
+      constexpr int NCH = RPS * W * 8;
+      static_assert(NCH % 512 == 0, "whole chunks per thread");
+      const bool comp = cp.kind == SW_COMP;
+#pragma unroll
+      for (int j = 0; j < NCH / 512; ++j) {
+        const int k = tid + 512 * j;
+        const int r = k / (W * 8), rem = k - r * (W * 8);
+        const int px = 1 + (rem >> 3);
+        const int y = comp ? cp.y0 + 1 + r : cp.y0 - RPS + 1 + r;
+        if (y < 0 || y >= H || (!comp && r < RPS - 2)) continue;
+        const uint32_t addr = sbase + (U * RPS + r) * ROWB + px * 128 + (rem & 7) * 16;
+        i32x4 v;
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+        f32x4 lo = f32x4{__uint_as_float((uint32_t)v[0] << 16), __uint_as_float((uint32_t)v[0] & 0xffff0000u),
+                         __uint_as_float((uint32_t)v[1] << 16), __uint_as_float((uint32_t)v[1] & 0xffff0000u)};
+        f32x4 hi = f32x4{__uint_as_float((uint32_t)v[2] << 16), __uint_as_float((uint32_t)v[2] & 0xffff0000u),
+                         __uint_as_float((uint32_t)v[3] << 16), __uint_as_float((uint32_t)v[3] & 0xffff0000u)};
+        lo = lo * pcs[0] + pcb[0];
+        hi = hi * pcs[1] + pcb[1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          lo[e] = lo[e] > 0.f ? lo[e] : palp * lo[e];
+          hi[e] = hi[e] > 0.f ? hi[e] : palp * hi[e];
+        }
+        i32x4 o;
+        o[0] = (int)((uint32_t)f32_to_bf16(lo[0]) | ((uint32_t)f32_to_bf16(lo[1]) << 16));
+        o[1] = (int)((uint32_t)f32_to_bf16(lo[2]) | ((uint32_t)f32_to_bf16(lo[3]) << 16));
+        o[2] = (int)((uint32_t)f32_to_bf16(hi[0]) | ((uint32_t)f32_to_bf16(hi[1]) << 16));
+        o[3] = (int)((uint32_t)f32_to_bf16(hi[2]) | ((uint32_t)f32_to_bf16(hi[3]) << 16));
+        asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(o) : "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
     const SwCur lcur = ld;
     const bool llive = ld.c < cend;
     advance(ld);
@@ -348,8 +404,33 @@ int swgrad_launch(const rr_wgrad_desc *d, const void *dy, const void *x1, const 
   a.nwg_ps = SW_WG / S;
   a.nsteps = (int)((long long)d->n * d->h * d->w / 128);
   const dim3 grid(a.nwg_ps * S), block(512);
-  if (d->w == 64) hipLaunchKernelGGL(swgrad_kernel<64>, grid, block, 0, st, a);
-  else hipLaunchKernelGGL(swgrad_kernel<32>, grid, block, 0, st, a);
+  a.pre_s = a.pre_b = a.pre_alpha = nullptr;
+  if (d->w == 64) hipLaunchKernelGGL((swgrad_kernel<64, false>), grid, block, 0, st, a);
+  else hipLaunchKernelGGL((swgrad_kernel<32, false>), grid, block, 0, st, a);
+  RR_CHECK_LAUNCH();
+  return RR_OK;
+}
+
+int swgrad_launch_pre(const rr_wgrad_desc *d, const void *dy, const void *x1, const float *pre_s,
+                      const float *pre_b, const float *pre_alpha, void *ws, hipStream_t st) {
+  if (!swgrad_ok(d) || d->c_in2 || !pre_s || !pre_b || !pre_alpha) return RR_EUNSUPPORTED;
+  const int S = sw_slices(d);
+  SWArgs a;
+  a.dy = (const char *)dy;
+  a.x1 = (const char *)x1;
+  a.x2 = nullptr;
+  a.c1 = d->c_in1;
+  a.c2 = 0;
+  a.cout = d->c_out;
+  a.partial = (float *)ws;
+  a.n = d->n;
+  a.h = d->h;
+  a.nwg_ps = SW_WG / S;
+  a.nsteps = (int)((long long)d->n * d->h * d->w / 128);
+  a.pre_s = pre_s; a.pre_b = pre_b; a.pre_alpha = pre_alpha;
+  const dim3 grid(a.nwg_ps * S), block(512);
+  if (d->w == 64) hipLaunchKernelGGL((swgrad_kernel<64, true>), grid, block, 0, st, a);
+  else hipLaunchKernelGGL((swgrad_kernel<32, true>), grid, block, 0, st, a);
   RR_CHECK_LAUNCH();
   return RR_OK;
 }

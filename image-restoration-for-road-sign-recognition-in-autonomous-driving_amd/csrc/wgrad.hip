@@ -813,6 +813,26 @@ extern "C" int rr_wgrad(const rr_wgrad_desc *d, const void *dy, const void *x1,
   return rr_wgrad_reduce(d, ws, ws_bytes, dw, stream);
 }
 
+extern "C" int rr_wgrad_pre_ok(const rr_wgrad_desc *d) {
+  return d && d->mode == RR_CONV3X3 && !d->c_in2 && !d->accumulate && swgrad_ok(d) ? 1 : 0;
+}
+
+// conv2's weight grad with BN1 + PReLU of its input folded in: x1 is t1 and
+// the kernel reads PReLU(t1 * pre_scale + pre_shift) (the bytes
+// rr_affine_act(t1, pre_scale, pre_shift, pre_alpha) would store); the
+// partial slabs then go through rr_wgrad_reduce
+extern "C" int rr_wgrad_pre(const rr_wgrad_desc *d, const void *dy, const void *x1,
+                            const float *pre_scale, const float *pre_shift, const float *pre_alpha,
+                            float *dw, void *ws, size_t ws_bytes, rr_stream stream) {
+  if (!d || !dy || !x1 || !dw || !pre_scale || !pre_shift || !pre_alpha) return RR_EINVAL;
+  if (!rr_wgrad_pre_ok(d)) return RR_EUNSUPPORTED;
+  const size_t need = rr_wgrad_workspace(d);
+  if (!ws || ws_bytes < need) return RR_EWORKSPACE;
+  const int rc = swgrad_launch_pre(d, dy, x1, pre_scale, pre_shift, pre_alpha, ws, (hipStream_t)stream);
+  if (rc) return rc;
+  return rr_wgrad_reduce(d, ws, ws_bytes, dw, stream);
+}
+
 extern "C" int rr_wgrad_partial(const rr_wgrad_desc *d, const void *dy, const void *x1,
                                 const void *x2, void *ws, size_t ws_bytes, rr_stream stream) {
   if (!d || !dy || !x1) return RR_EINVAL;

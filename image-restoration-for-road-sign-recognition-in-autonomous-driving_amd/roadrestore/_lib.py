@@ -92,6 +92,10 @@ _SIGS = {
     "rr_igemm_pool_kernel_name": (C.c_char_p, [C.POINTER(IgemmDesc)]),
     "rr_igemm_dgrad_sc": (I_, [C.POINTER(IgemmDesc), P_, P_, P_, P_, I_, P_, P_]),
     "rr_igemm_dgrad_sc_kernel_name": (C.c_char_p, [C.POINTER(IgemmDesc), I_]),
+    "rr_igemm_pre_ok": (I_, [C.POINTER(IgemmDesc)]),
+    "rr_igemm_pre": (I_, [C.POINTER(IgemmDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_]),
+    "rr_wgrad_pre_ok": (I_, [C.POINTER(WgradDesc)]),
+    "rr_wgrad_pre": (I_, [C.POINTER(WgradDesc), P_, P_, P_, P_, P_, P_, P_, S_, P_]),
     "rr_wgrad_kernel_name": (C.c_char_p, [C.POINTER(WgradDesc)]),
     "rr_igemm_bnbwd_workspace": (S_, [C.POINTER(IgemmDesc)]),
     "rr_igemm_bnbwd": (I_, [C.POINTER(IgemmDesc), P_, P_, P_, P_, P_, P_, P_, P_, P_, P_, P_]),

@@ -451,6 +451,11 @@ def block_has_shortcut(blk):
     return len(blk.shortcut) > 0
 
 
+# A/B switch: the training-step BN1 + PReLU applied inside conv2's streaming
+# forward and weight grad instead of a separate affine pass over t1 (RR_PATH
+# bn1_fold=0: the pass, as before round 6)
+_FOLD_BN1 = path_flag("bn1_fold", 1) != 0
+
 # A/B switch: eval-mode BN folded into the conv weights (RR_PATH fold_bn=0:
 # conv + separate BN affine passes, as in training)
 _FOLD_BN = path_flag("fold_bn", 1) != 0
@@ -536,9 +541,18 @@ def resblock_forward(blk, x1, x2, n, h, w, wc, dt, training, need_bwd, pool=Fals
     pk1 = wc.conv(c1.weight, dt, dgrad=need_bwd)
     t1, _, st1 = ops.igemm(RR_CONV3X3, x1, x2, n, h, w, pk1[0], cout, bias=c1.bias, stats=training)
     s1, sh1, m1, i1 = _bn_affine(bn1, st1, c1.bias, P, training, need_bwd=need_bwd)
-    a1 = ops.affine_act(t1, s1, sh1, alpha=pr.weight)
     pk2 = wc.conv(c2.weight, dt, dgrad=need_bwd)
-    t2, _, st2 = ops.igemm(RR_CONV3X3, a1, None, n, h, w, pk2[0], cout, bias=c2.bias, stats=training)
+    if _FOLD_BN1 and training and c2.bias is not None and ops.igemm_pre_ok(t1.dtype, n, h, w, cout, cout) and \
+            (not need_bwd or ops.wgrad_pre_ok(t1.dtype, n, h, w, cout, cout)):
+        # BN1 + PReLU applied to conv2's input rows as they land in the
+        # streaming kernels' rings (rr_igemm_pre / rr_wgrad_pre): a1 is never
+        # stored -- bitwise the a1 the affine pass would write
+        a1 = None
+        t2, _, st2 = ops.igemm_pre(t1, n, h, w, pk2[0], cout, c2.bias, s1, sh1, pr.weight)
+    else:
+        a1 = ops.affine_act(t1, s1, sh1, alpha=pr.weight)
+        t2, _, st2 = ops.igemm(RR_CONV3X3, a1, None, n, h, w, pk2[0], cout, bias=c2.bias,
+                               stats=training)
     has_sc = block_has_shortcut(blk)
     # (scale, shift) of bn2 and the shortcut BN as rows of two [2, C] buffers:
     # the backward's recomputed ReLU mask reads them as pairs (no stack copy)
@@ -656,7 +670,11 @@ def resblock_backward(blk, S, g_out, sink, pool=None, convout=None, reduce_side=
                             outs=dict(dgamma0=sink[bn2.weight], dbeta0=sink[bn2.bias]),
                             eval_mode=ev, dbias=(sink[c2.bias], None) if ev else None)
         dt2 = r["dt0"]
-    wgrad(RR_CONV3X3, dt2, S.a1, None, n, h, w, cout, dw=sink[c2.weight])
+    if S.a1 is None:
+        # (the forward folded BN1 + PReLU into conv2: its weight grad reads t1)
+        ops.wgrad_pre(dt2, S.t1, n, h, w, cout, S.s1, S.sh1, pr.weight, dw=sink[c2.weight])
+    else:
+        wgrad(RR_CONV3X3, dt2, S.a1, None, n, h, w, cout, dw=sink[c2.weight])
     outs1 = dict(dgamma0=sink[bn1.weight], dbeta0=sink[bn1.bias], dalpha=sink[pr.weight])
     if FUSE_BNBWD:
         # conv2 dgrad whose epilogue applies the PReLU backward and reduces

@@ -224,6 +224,54 @@ def igemm(mode, x1, x2, n, h, w, wpack, cout, bias=None, act=0, out=None, out2=N
     return out, out2, st
 
 
+def igemm_pre_ok(dtype, n, h, w, cin, cout):
+    """rr_igemm_pre takes conv2's bias + statistics forward on t1 (BN1 + PReLU
+    folded into the input); False on an older A/B build without it"""
+    f = getattr(lib(), "rr_igemm_pre_ok", None)
+    d = IgemmDesc(rr_dtype(dtype), RR_CONV3X3, n, h, w, cin, 0, cout, 0, 0, 0, 1, 0, 1, 0)
+    return bool(f is not None and f(C.byref(d)))
+
+
+def igemm_pre(t1, n, h, w, wpack, cout, bias, pre_scale, pre_shift, pre_alpha):
+    """conv3x3 (+ bias, BN statistics) of a1 = PReLU(t1 * pre_scale + pre_shift)
+    with a1 never stored (rr_igemm_pre): -> (y, None, stats_partial)"""
+    _need_cuda(t1, wpack)
+    d = IgemmDesc(rr_dtype(t1.dtype), RR_CONV3X3, n, h, w, t1.shape[-1], 0, cout, 0, 0, 0, 1, 0, 1, 0)
+    out = torch.empty((n, h, w, cout), dtype=t1.dtype, device=t1.device)
+    st = torch.empty((lib().rr_igemm_stat_blocks(C.byref(d)), cout, 2), dtype=torch.float32,
+                     device=t1.device)
+
+    def launch():
+        lib().check(lib().rr_igemm_pre(C.byref(d), _p(t1), _p(wpack), _p(bias), _p(pre_scale),
+                                       _p(pre_shift), _p(pre_alpha), _p(out), _p(st), stream()),
+                    "rr_igemm_pre")
+    _launch(lambda: igemm_kernel_name(d), 2.0 * n * h * w * cout * 9 * t1.shape[-1], launch,
+            f"fwd m{RR_CONV3X3} {n}x{h}x{w} c{t1.shape[-1]}+0->{cout} pre")
+    return out, None, st
+
+
+def wgrad_pre_ok(dtype, n, h, w, cin, cout):
+    f = getattr(lib(), "rr_wgrad_pre_ok", None)
+    d = WgradDesc(rr_dtype(dtype), RR_CONV3X3, n, h, w, cin, 0, cout, 0)
+    return bool(f is not None and f(C.byref(d)))
+
+
+def wgrad_pre(dy, t1, n, h, w, cout, pre_scale, pre_shift, pre_alpha, dw):
+    """conv2's weight grad on a1 = PReLU(t1 * pre_scale + pre_shift), a1 never
+    stored (rr_wgrad_pre: partial + reduce on the current stream)"""
+    _need_cuda(dy, t1)
+    d = WgradDesc(rr_dtype(dy.dtype), RR_CONV3X3, n, h, w, t1.shape[-1], 0, cout, 0)
+    ws = _ws(lib().rr_wgrad_workspace(C.byref(d)), dy.device)
+
+    def launch():
+        lib().check(lib().rr_wgrad_pre(C.byref(d), _p(dy), _p(t1), _p(pre_scale), _p(pre_shift),
+                                       _p(pre_alpha), _p(dw), _p(ws), ws.numel(), stream()),
+                    "rr_wgrad_pre")
+    _launch(lambda: wgrad_kernel_name(d), 2.0 * cout * t1.shape[-1] * 9 * n * h * w, launch,
+            f"wgrad m{RR_CONV3X3} {n}x{h}x{w} c{t1.shape[-1]}+0->{cout} pre")
+    return dw
+
+
 def wgrad(mode, dy, x1, x2, n, h, w, cout, dw=None, accumulate=False, dw_shape=None,
           reduce_stream=None):
     """Weight grad (fp32, torch layout) of a conv / convT; see rr_wgrad.

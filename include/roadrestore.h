@@ -129,6 +129,20 @@ int rr_igemm_dgrad_sc(const rr_igemm_desc *d, const void *dy, const void *w, con
                       const void *w_sc, int c_sc, void *y, rr_stream stream);
 /* the kernel rr_igemm_dgrad_sc launches for (*d, c_sc), or "unsupported" */
 const char *rr_igemm_dgrad_sc_kernel_name(const rr_igemm_desc *d, int c_sc);
+/* A ResidualBlock's conv2 forward with BatchNorm1 + PReLU of its input folded
+ * in (14:101-104, training): x1 = t1 (conv1's pre-BN output) and the conv
+ * reads a1 = PReLU(t1 * pre_scale[c] + pre_shift[c]) with alpha pre_alpha[0] --
+ * bitwise the bytes rr_affine_act(t1, pre_scale, pre_shift, alpha) would store,
+ * applied to every input row as it lands in the row-streaming kernel's ring,
+ * so a1 is never written.  d: the bias + BN-statistics forward (has_bias,
+ * want_stats, no act / mask / split / accumulate / second source) on the
+ * row-streaming kernel's 64 -> 64 whole-row maps (rr_igemm_pre_ok != 0);
+ * others RR_EUNSUPPORTED (the caller runs rr_affine_act + rr_igemm).
+ * Replaces bn1 + prelu + conv2 of conv_block at 14:99-105. */
+int rr_igemm_pre_ok(const rr_igemm_desc *d);
+int rr_igemm_pre(const rr_igemm_desc *d, const void *x1, const void *w, const float *bias,
+                 const float *pre_scale, const float *pre_shift, const float *pre_alpha,
+                 void *y1, float *stats_partial, rr_stream stream);
 /* number of row blocks the partial stats buffer holds: [blocks][c_out][2] */
 int rr_igemm_stat_blocks(const rr_igemm_desc *d);
 /* The kernel rr_igemm (bnbwd = 0) or rr_igemm_bnbwd (bnbwd = 1) launches for
@@ -186,6 +200,16 @@ int rr_wgrad_partial(const rr_wgrad_desc *d, const void *dy, const void *x1,
                      const void *x2, void *ws, size_t ws_bytes, rr_stream stream);
 int rr_wgrad_reduce(const rr_wgrad_desc *d, const void *ws, size_t ws_bytes, float *dw,
                     rr_stream stream);
+/* conv2's weight grad with BatchNorm1 + PReLU of its input folded in (the
+ * backward of rr_igemm_pre): x1 = t1, the kernel reads PReLU(t1 * pre_scale +
+ * pre_shift) as rr_igemm_pre does; partial launch + rr_wgrad_reduce, bitwise
+ * rr_wgrad on the stored a1.  d: RR_CONV3X3, one source, no accumulate, the
+ * row-streaming weight grad's maps (rr_wgrad_pre_ok != 0); others
+ * RR_EUNSUPPORTED.  Replaces conv_block[3]'s weight grad at 14:99-105. */
+int rr_wgrad_pre_ok(const rr_wgrad_desc *d);
+int rr_wgrad_pre(const rr_wgrad_desc *d, const void *dy, const void *x1, const float *pre_scale,
+                 const float *pre_shift, const float *pre_alpha, float *dw, void *ws,
+                 size_t ws_bytes, rr_stream stream);
 
 /* weight packing (fp32 torch layout -> compute layout/dtype) */
 /* conv [co][ci][k][k] -> fwd [co][k*k][ci] and dgrad [ci][k*k flipped][co].
