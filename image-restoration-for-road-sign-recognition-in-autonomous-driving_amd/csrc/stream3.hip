@@ -643,49 +643,16 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
     lslot = lslot >= RING ? lslot - RING : lslot;
   }
   int cslot = RING - 2;                         // ring slot of the compute step's row y0 - 1
-  // Stagger: waves w and w + 4 share a SIMD.  The "late" half runs the
-  // epilogue of step v - 1 right after the barrier of step v and then the
-  // MFMAs of step v, while the early half runs MFMAs then epilogue of step v:
-  // on every SIMD one wave's epilogue / DMA issue / loop control overlaps
-  // the other's MFMAs, with one barrier per step and no extra registers
-  // (acc of v - 1 is consumed before the MFMAs of v overwrite it).
-  const bool late = STAG && wv >= 4;
-  // vmcnt accounting, ops younger than DMA(v) (issued in iteration v - D):
-  //   early, iteration u: E(u) DMA(u+D) S(u)
-  //     -> (D-1) M + S c(v-D) + (E+S) sum_{v-D<u<v} c(u)
-  //   late, iteration u: S(u-1) E(u) DMA(u+D)
-  //     -> (D-1) M + S sum_{v-D<=u<=v-2} c(u) + E sum_{v-D<u<v} c(u)
-  unsigned hist = 0;                            // bit j: iteration v-1-j computed
-  constexpr unsigned FULL = (1u << D) - 1;
-  constexpr int YE = (D - 1) * DMAW + S + (E + S) * (D - 1);      // steady state, early
-  constexpr int YL = (D - 1) * DMAW + S * (D - 1) + E * (D - 1);  // steady state, late
-  long long ppix = 0;                           // late half: the step whose epilogue is pending
-  int prowg = 0, pxs = 0;
-  bool pcomp = false;
-  [[maybe_unused]] unsigned long long st_a = 0, st_b = 0, st_wait = 0, st_issue = 0, st_mfma = 0, st_epi = 0,
-                                      st_steps = 0, st_t0 = 0, st_t1 = 0;
-  S3_STAMP(st_t0);
-#pragma unroll 1
-  while (cp.c < cend) {
-    S3_STAMP(st_a);
-    if ((hist & FULL) == FULL) {
-      if (late) wait_vm_barrier_c<YL < 63 ? YL : 63>();
-      else wait_vm_barrier_c<YE < 63 ? YE : 63>();
-    } else {
-      const unsigned inner = hist & ((1u << (D - 1)) - 1);          // c(v-1) .. c(v-D+1)
-      const int y = late ? (D - 1) * DMAW + S * __builtin_popcount((hist >> 1) & ((1u << (D - 1)) - 1)) +
-                               E * __builtin_popcount(inner)
-                         : (D - 1) * DMAW + (((hist >> (D - 1)) & 1) ? S : 0) +
-                               (E + S) * __builtin_popcount(inner);
-      wait_vm_barrier(y);
-    }
-    S3_STAMP(st_b);
-    st_wait += st_b - st_a;
-    st_a = st_b;
-    const bool comp = cp.kind == S3_COMP;
+  // F_PRE: BN1 + PReLU of the rows DMA'd for virtual step c (ring slots cs +
+  // 2 + r: a compute step's image rows y0 + 1 + r, a pre-load's y0 - 1 and
+  // y0).  Done one step ahead -- step v + 1's rows at the end of iteration v,
+  // whose barrier waited for DMA(v + 1) instead of DMA(v) -- so the next
+  // iteration's barrier publishes them: no barrier of its own, and the work
+  // overlaps the other waves' MFMAs (no step reads them before: step v's rows
+  // are y0 - 1 .. y0 + RPS)
+  auto pre_rows = [&](const Cur &c, int cs) __attribute__((always_inline)) {
     if constexpr (PRE) {
-      // the rows DMA'd for this virtual step (ring slots cslot + 2 + r): a
-      // compute step's image rows y0 + 1 + r, a pre-load's y0 - 1 and y0
+      const bool cmp = c.kind == S3_COMP;
       constexpr int NCH = RPS * W * 8;
       static_assert(NCH % 512 == 0, "whole chunks per thread");
 #pragma unroll
@@ -693,9 +660,9 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
         const int k = tid + 512 * j;
         const int r = k / (W * 8), rem = k - r * (W * 8);
         const int px = 1 + (rem >> 3);
-        const int y = comp ? cp.y0 + 1 + r : cp.y0 - RPS + 1 + r;
-        if (y < 0 || y >= H || (!comp && r < RPS - 2)) continue;
-        int sl = cslot + 2 + r;
+        const int y = cmp ? c.y0 + 1 + r : c.y0 - RPS + 1 + r;
+        if (y < 0 || y >= H || (!cmp && r < RPS - 2)) continue;
+        int sl = cs + 2 + r;
         sl = sl >= RING ? sl - RING : sl;
         const uint32_t addr = sbase + sl * ROWB + px * 128 + (rem & 7) * 16;
         i32x4 v;
@@ -713,8 +680,65 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
         const i32x4 o = i32x4{(int)pl.x, (int)pl.y, (int)ph.x, (int)ph.y};
         asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(o) : "memory");
       }
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
+  };
+  if constexpr (PRE) {
+    // step 0's rows: its DMA of every wave landed, transformed before the loop
+    wait_vm_barrier_c<(D - 1) * DMAW < 63 ? (D - 1) * DMAW : 63>();
+    pre_rows(cp, cslot);
+  }
+  // Stagger: waves w and w + 4 share a SIMD.  The "late" half runs the
+  // epilogue of step v - 1 right after the barrier of step v and then the
+  // MFMAs of step v, while the early half runs MFMAs then epilogue of step v:
+  // on every SIMD one wave's epilogue / DMA issue / loop control overlaps
+  // the other's MFMAs, with one barrier per step and no extra registers
+  // (acc of v - 1 is consumed before the MFMAs of v overwrite it).
+  const bool late = STAG && wv >= 4;
+  // vmcnt accounting, ops younger than DMA(v) (issued in iteration v - D):
+  //   early, iteration u: E(u) DMA(u+D) S(u)
+  //     -> (D-1) M + S c(v-D) + (E+S) sum_{v-D<u<v} c(u)
+  //   late, iteration u: S(u-1) E(u) DMA(u+D)
+  //     -> (D-1) M + S sum_{v-D<=u<=v-2} c(u) + E sum_{v-D<u<v} c(u)
+  unsigned hist = 0;                            // bit j: iteration v-1-j computed
+  constexpr unsigned FULL = (1u << D) - 1;
+  constexpr int YE = (D - 1) * DMAW + S + (E + S) * (D - 1);      // steady state, early
+  constexpr int YL = (D - 1) * DMAW + S * (D - 1) + E * (D - 1);  // steady state, late
+  // F_PRE waits for DMA(v + 1): (D-2) M + S c(v+1-D) + (E+S) sum_{v+1-D<u<v} c(u)
+  constexpr unsigned FULLP = (1u << (D - 1)) - 1;
+  constexpr int YP = (D - 2) * DMAW + S + (E + S) * (D - 2);
+  long long ppix = 0;                           // late half: the step whose epilogue is pending
+  int prowg = 0, pxs = 0;
+  bool pcomp = false;
+  [[maybe_unused]] unsigned long long st_a = 0, st_b = 0, st_wait = 0, st_issue = 0, st_mfma = 0, st_epi = 0,
+                                      st_steps = 0, st_t0 = 0, st_t1 = 0;
+  S3_STAMP(st_t0);
+#pragma unroll 1
+  while (cp.c < cend) {
+    S3_STAMP(st_a);
+    if constexpr (PRE) {
+      static_assert(D >= 2 && !STAG, "one step ahead");
+      if ((hist & FULLP) == FULLP) {
+        wait_vm_barrier_c<YP < 63 ? YP : 63>();
+      } else {
+        const int y = (D - 2) * DMAW + (((hist >> (D - 2)) & 1) ? S : 0) +
+                      (E + S) * __builtin_popcount(hist & ((1u << (D - 2)) - 1));
+        wait_vm_barrier(y);
+      }
+    } else if ((hist & FULL) == FULL) {
+      if (late) wait_vm_barrier_c<YL < 63 ? YL : 63>();
+      else wait_vm_barrier_c<YE < 63 ? YE : 63>();
+    } else {
+      const unsigned inner = hist & ((1u << (D - 1)) - 1);          // c(v-1) .. c(v-D+1)
+      const int y = late ? (D - 1) * DMAW + S * __builtin_popcount((hist >> 1) & ((1u << (D - 1)) - 1)) +
+                               E * __builtin_popcount(inner)
+                         : (D - 1) * DMAW + (((hist >> (D - 1)) & 1) ? S : 0) +
+                               (E + S) * __builtin_popcount(inner);
+      wait_vm_barrier(y);
+    }
+    S3_STAMP(st_b);
+    st_wait += st_b - st_a;
+    st_a = st_b;
+    const bool comp = cp.kind == S3_COMP;
     const int rowg = cp.img * H + cp.y0;
     const long long pix0 = (long long)rowg * IW + cp.xs;
     if (late && pcomp) epilogue(ppix, prowg, pxs);   // its loads were waited for last iteration
@@ -757,6 +781,13 @@ __global__ __launch_bounds__(512, 2) void stream3_kernel(S3Args a, int nsteps) {
       if (!late) epilogue(pix0, rowg, cp.xs);
       S3_STAMP(st_b);
       st_epi += st_b - st_a;
+    }
+    if constexpr (PRE) {
+      Cur nx = cp;
+      advance(nx);
+      int ncs = cslot + RPS;
+      ncs = ncs >= RING ? ncs - RING : ncs;
+      if (nx.c < cend) pre_rows(nx, ncs);
     }
     ppix = pix0;
     prowg = rowg;
