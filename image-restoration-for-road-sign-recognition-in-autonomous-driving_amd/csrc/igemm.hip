@@ -694,7 +694,7 @@ __global__ __launch_bounds__(NT, (HaloCfg<BC, BP, NT>::OCC)) void igemm3_halo_ke
   // next chunk's halo.  vmcnt retires in issue order, so a wave that loaded
   // the (HBM, long-latency) halo at tap 0 and then waited for its weights
   // two stages later also waited for the halo: the weight prefetch, not the
-  // MFMAs, then set the pace (tools/halo_dbgk.py: without the halo loads the
+  // MFMAs, then set the pace (round-2 halo_dbgk measurement: without the halo loads the
   // K loop ran 9-33% faster).  With separate roles no wave ever waits for a
   // load of the other kind; every wave still runs the same MFMAs.
   // weight/halo role split: measured 3 % faster at BC = 64, W = 32 / 16

@@ -2,10 +2,10 @@
 at the cfg3 shapes (B = 512): fwd (bias + stats) and dgrad, TFLOP/s, for
 every value of an environment switch given on the command line, e.g.
 
-    python tools/ab_conv3r.py RR_CONV3R=1,0 RR_IGEMM_DBG=0,1,4,32
+    python tools/ab_conv3r.py RR_PATH=conv3r=1,conv3r=0
 
-(RR_IGEMM_DBG bits in conv3r, timing only: 1 no epilogue, 4 no DMA in the K
-loop, 16 no weight DMA, 32 no halo DMA; RR_CONV3R_RW=0,1,32 the K loop kind)
+(the library's one run-time knob, RR_PATH, csrc/common.h; the timing-only
+switches of earlier rounds were removed in round 6)
 
 (each NAME=v1,v2,... is swept; the first switch varies fastest; the values
 alternate per layer, ROUNDS times, and each is reported as its median)."""
