@@ -26,6 +26,7 @@ import torch  # noqa: E402
 
 import roadrestore as rr  # noqa: E402
 from roadrestore import imgproc as T, ops  # noqa: E402
+from roadrestore._lib import path_flag  # noqa: E402
 
 
 def main():
@@ -104,7 +105,7 @@ def main():
         "top1_note": "random-init judge: Top-1 collapses to few classes; Top-1 parity with a "
                      "non-degenerate judge is tests/test_models_gpu.py::"
                      "test_inference_pipeline_fp32_end_to_end",
-        "roofline": roof, "bn_folded": os.environ.get("RR_FOLD_BN", "1") != "0",
+        "roofline": roof, "bn_folded": path_flag("fold_bn", 1) != 0,
     }))
 
 

@@ -1,6 +1,6 @@
 """Time the 64 -> 64 channel bf16 3x3 conv at the cfg3 shapes (B=512) through
-rr_igemm: the row-streaming kernel (RR_STREAM3=1) and the tiled halo kernel
-(RR_STREAM3=0), interleaved in one process.  Prints us / TFLOP/s / HBM GB/s
+rr_igemm: the row-streaming kernel (RR_PATH=stream3=1) and the tap-reuse
+kernel (RR_PATH=stream3=0), interleaved in one process.  Prints us / TFLOP/s / HBM GB/s
 (algorithmic bytes: bf16 input + output (+ t or mask / accumulate reads))."""
 import os
 import sys
@@ -14,8 +14,8 @@ from roadrestore._lib import RR_CONV3X3  # noqa: E402
 dev = torch.device("cuda:0")
 B = int(os.environ.get("B", 512))
 reps = int(os.environ.get("REPS", 20))
-variants = os.environ.get("VARIANTS", "1,0").split(",")
-varenv = os.environ.get("VARENV", "RR_STREAM3")     # the env switch the variants set
+variants = os.environ.get("VARIANTS", "stream3=1;stream3=0").split(";")
+varenv = os.environ.get("VARENV", "RR_PATH")        # the env switch the variants set
 only = os.environ.get("CASE")          # e.g. "64:fwd+stats"
 rounds = int(os.environ.get("ROUNDS", 2))
 

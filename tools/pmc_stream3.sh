@@ -1,7 +1,7 @@
 # PMC passes over the streaming conv (tools/bench_stream3.py, one case).
 # usage: bash tools/pmc_stream3.sh [CASE]   (on the GPU box; results in gpurun_out/pmc)
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-export CASE=${1:-64:fwd+stats} VARIANTS=1 ROUNDS=1 REPS=5
+export CASE=${1:-64:fwd+stats} VARIANTS=stream3=1 ROUNDS=1 REPS=5
 rm -rf gpurun_out/pmc; mkdir -p gpurun_out/pmc
 run() { timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $1 --output-format csv -d gpurun_out/pmc/$2 -o p -- python tools/bench_stream3.py > gpurun_out/pmc/$2.log 2>&1; }
 run "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_WAIT_INST_LDS" a && \

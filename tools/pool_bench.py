@@ -51,15 +51,6 @@ def main():
              "maxpool_us": timed(lambda: ops.maxpool2_fwd(y)),
              "fused_us": timed(lambda: ops.igemm_pool(x, n, h, h, pk, c, bias=b)),
              "fused_noidx_us": timed(lambda: ops.igemm_pool(x, n, h, h, pk, c, bias=b, want_idx=False))}
-        if h == 64:
-            # stream3's pool in the other step size (RR_S3_POOL_MP=2 / 4, A/B;
-            # the default is 128-pixel steps)
-            os.environ["RR_S3_POOL_MP"] = "4"
-            r["fused_mp4_us"] = timed(lambda: ops.igemm_pool(x, n, h, h, pk, c, bias=b))
-            y4, i4 = ops.igemm_pool(x, n, h, h, pk, c, bias=b)
-            del os.environ["RR_S3_POOL_MP"]
-            y2, i2 = ops.igemm_pool(x, n, h, h, pk, c, bias=b)
-            r["mp4_equal"] = bool(torch.equal(y4, y2) and torch.equal(i4, i2))
         print(json.dumps(r), flush=True)
 
 
