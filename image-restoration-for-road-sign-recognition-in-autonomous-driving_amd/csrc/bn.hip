@@ -11,6 +11,13 @@
 // (deterministic, no float atomics).
 #include "common.h"
 
+// grid cap of the 8-channel grid-stride elementwise kernels (BN1 + PReLU
+// apply, BN-backward apply): one resident round of 256-thread workgroups, so
+// each workgroup's per-channel coefficient setup is paid once per ~16 rows.
+// Graph-step A/B (profiles/r6zk_abstep_ew_grid.txt, r6zl_*): 2048 vs 4096
+// +0.1-1.0 % in 5 of 6 pairs; 16384 -1 %, one row per thread -5 %.
+#define RR_EW_GRID 2048
+
 namespace {
 
 // ---------------------------------------------------------------------------
@@ -941,7 +948,7 @@ extern "C" int rr_affine_act(int dtype, long long P, int C, const void *x, const
   if ((res_scale == nullptr) != (res_shift == nullptr)) return RR_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   if (C % 8 == 0 && 256 % (C / 8) == 0) {
-    const int grid8 = rr_grid_cap((P * C / 8 + 255) / 256, 4096);
+    const int grid8 = rr_grid_cap((P * C / 8 + 255) / 256, RR_EW_GRID);
     if (dtype == RR_BF16)
       hipLaunchKernelGGL(affine_act8_kernel<bf16_t>, dim3(grid8), dim3(256), 0, st, P, C,
                          (const bf16_t *)x, scale, shift, alpha, (const bf16_t *)res, res_scale,
@@ -1130,7 +1137,7 @@ extern "C" int rr_bn_bwd_apply(const rr_bnbwd_desc *d, const void *g, const void
   const BnBwd a = make_bnbwd(d, g, aux, aff_s, aff_b, alpha, t0, mean0, invstd0, t1, mean1, invstd1);
   hipStream_t st = (hipStream_t)stream;
   if (d->C % 8 == 0 && 256 % (d->C / 8) == 0) {
-    const int grid8 = rr_grid_cap((d->P * d->C / 8 + 255) / 256, 4096);
+    const int grid8 = rr_grid_cap((d->P * d->C / 8 + 255) / 256, RR_EW_GRID);
 #define RR_APP8(TT, M, N, GM) hipLaunchKernelGGL((bn_bwd_apply8_kernel<TT, M, N, GM>), dim3(grid8), dim3(256), 0, st, a, coef, (TT *)dt0, (TT *)dt1, (TT *)gm_out)
 #define RR_APP8_M(TT, M)                                                        \
     if (d->nbn == 1) { if (gm_out) RR_APP8(TT, M, 1, true); else RR_APP8(TT, M, 1, false); } \
@@ -1175,7 +1182,7 @@ extern "C" int rr_bn_bwd_apply_convout(const rr_bnbwd_desc *d, int h, int w, con
   if (cout != 3) return RR_EUNSUPPORTED;
   BnBwd a = make_bnbwd(d, nullptr, nullptr, aff_s, aff_b, nullptr, t0, mean0, invstd0, t1, mean1, invstd1);
   a.h = h; a.w = w; a.cody = dy; a.cow = wt;
-  const int grid8 = rr_grid_cap((d->P * d->C / 8 + 255) / 256, 4096);
+  const int grid8 = rr_grid_cap((d->P * d->C / 8 + 255) / 256, RR_EW_GRID);
   hipStream_t st = (hipStream_t)stream;
   if (d->dtype == RR_BF16)
     hipLaunchKernelGGL((bn_bwd_apply8_kernel<bf16_t, 4, 2, false, true>), dim3(grid8), dim3(256), 0, st, a, coef,
